@@ -1,0 +1,213 @@
+#!/usr/bin/env python3
+"""DAD train-step throughput on MI355X (BASELINE.json metric).
+
+One "step" = the full fused DAD step on one clean + one noisy batch per GPU:
+3 encoder passes (student-clean, teacher-weak, student-strong) with in-kernel weak/strong
+augmentation, CE + masked KL + class-aware ECDA/MMD, DACP mask, analytic backward,
+global-norm clip + Adam + teacher EMA (+ one RCCL all-reduce of the grads for N > 1).
+Post-warm-up epoch 60 (full loss weights) with a confident synthetic teacher, so the KL and
+ECDA terms are active.  Inputs are resident in HBM before timing.
+
+    python bench.py [--gpus N --steps K --warmup W --precision bf16|fp32]
+    torchrun --nproc-per-node N bench.py --gpus N ...          (one process per GPU)
+
+Prints ONE JSON line (rank 0).
+"""
+import argparse
+import importlib
+import json
+import math
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+PKG = importlib.import_module(
+    "robust-speech-emotion-recognition-via-dynamic-asymmetric-distillation-in-noisy-environments_amd")
+
+METRIC = "utterances/sec (DAD train step) batch=64 at 1/2/4/8 MI355X; loss parity"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+BF16_PEAK_TFLOPS = 2500.0      # dense bf16 MFMA
+FP32_PEAK_TFLOPS = 157.3       # f32 MFMA == f32 vector rate
+
+
+def init_model_weights(model, seed, margin=5.0):
+    """nn.Linear-range W1/b1 and a classifier aligned with class prototypes (confident teacher)."""
+    g = torch.Generator().manual_seed(seed)
+    P = torch.randn(4, 768, generator=g, dtype=torch.float64) * 2.0
+    k1 = 1.0 / math.sqrt(768)
+    W1 = (torch.rand(256, 768, generator=g, dtype=torch.float64) * 2 - 1) * k1
+    b1 = (torch.rand(256, generator=g, dtype=torch.float64) * 2 - 1) * k1
+    mu = torch.relu(P @ W1.T + b1)
+    dirs = mu - mu.mean(0, keepdim=True)
+    dirs = dirs / dirs.norm(dim=1, keepdim=True)
+    proj = mu @ dirs.T
+    gap = float(np.mean([float(proj[c, c] - torch.cat([proj[c, :c], proj[c, c + 1:]]).max()) for c in range(4)]))
+    W2 = dirs * (margin / gap)
+    b2 = torch.zeros(4, dtype=torch.float64)
+    flat = torch.cat([W1.reshape(-1), b1, W2.reshape(-1), b2]).float()
+    with torch.no_grad():
+        model.student_flat.copy_(flat)
+        model.teacher_flat.copy_(flat)
+    return P.float()
+
+
+def make_batches(P, n, B, T, seed, device, snr_db=5.0):
+    """n (clean, noisy) batch pairs, all frames valid (BASELINE.md §3 inputs)."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    Pd = P.to(device)
+    out = []
+    for i in range(n):
+        yc = (torch.arange(B, device=device) + i) % 4
+        yn = (yc + 1) % 4
+        xc = Pd[yc][:, None, :] + 0.5 * torch.randn(B, T, 768, generator=g, device=device)
+        sig = (0.5 + 10 ** (-snr_db / 20)) * (0.5 + 2.0 * torch.rand(B, 1, 1, generator=g, device=device))
+        xn = Pd[yn][:, None, :] + sig * torch.randn(B, T, 768, generator=g, device=device)
+        pad = torch.zeros(B, T, dtype=torch.bool, device=device)
+        out.append(({"net_input": {"feats": xc.contiguous(), "padding_mask": pad}, "labels": yc},
+                    {"net_input": {"feats": xn.contiguous(), "padding_mask": pad}, "labels": yn}))
+    return out
+
+
+def cpu_baseline(B, T, steps, epoch):
+    """The NumPy oracle (CPU restatement of the reference step) on this host's cores."""
+    from oracle import dad_oracle, synth
+    try:
+        import threadpoolctl
+        info = threadpoolctl.threadpool_info()
+        cores = max([i.get("num_threads", 1) for i in info if i.get("user_api") == "blas"] or [1])
+    except Exception:
+        cores = os.cpu_count() or 1
+    cfg = dad_oracle.make_cfg("iemocap")
+    W1, b1, W2, b2, _ = synth.init_weights(0)
+    orc = dad_oracle.DADOracle(W1, b1, W2, b2, cfg)
+    rng = np.random.default_rng(0)
+    times = []
+    for k in range(steps + 1):
+        inp = synth.make_step_inputs(0, k, B, T, ragged=False)
+        inp = {n: inp[n] for n in ("xc", "mc", "yc", "xn", "mn", "yn")}    # draws sampled inside (like randn)
+        t0 = time.perf_counter()
+        orc.step(inp, epoch, rng=rng)
+        times.append(time.perf_counter() - t0)
+    med = statistics.median(times[1:])
+    return {"value": B / med, "unit": "utterances/s", "cores": int(cores), "kind": "port",
+            "sample": "%d steps (after 1 warm-up) of the NumPy oracle DAD step, B=%d T=%d epoch %d incl. "
+                      "noise sampling; median %.3f s/step" % (steps, B, T, epoch, med)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--frames", type=int, default=300)
+    ap.add_argument("--epoch", type=int, default=60)
+    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--fp32-steps", type=int, default=10, help="also time the FP32 parity mode (N=1)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+    PKG.lib()
+    B, T = args.batch, args.frames
+
+    model = PKG.SSRLModel().to(dev)
+    P = init_model_weights(model, seed=0)
+    comm = PKG.DPComm.from_torch_distributed() if world > 1 else None
+    step = PKG.DADStep(model, flavor="iemocap", precision=args.precision, rng="counter", seed=1000 + rank, comm=comm)
+    data = make_batches(P, 4, B, T, seed=17 + rank, device=dev)
+    torch.cuda.synchronize()
+
+    def run(n, events=None):
+        step.kernel_events = events
+        for i in range(n):
+            c, nb = data[i % len(data)]
+            step.step(c, nb, args.epoch)
+        step.kernel_events = None
+
+    run(args.warmup)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    events = []
+    t0 = time.perf_counter()
+    run(args.steps, events)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    losses = {k: float(v) for k, v in step.losses().items()}
+    msum = float(step.outputs(B, B)["msum"])
+    enc_ms = statistics.mean(a.elapsed_time(b) for a, b in events)
+
+    fp32 = None
+    if rank == 0 and world == 1 and args.fp32_steps > 0 and args.precision == "bf16":
+        s32 = PKG.DADStep(model, flavor="iemocap", precision="fp32", rng="counter", seed=5)
+        for i in range(3):
+            s32.step(data[i % 4][0], data[i % 4][1], args.epoch)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for i in range(args.fp32_steps):
+            s32.step(data[i % 4][0], data[i % 4][1], args.epoch)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t1) / args.fp32_steps
+        fp32 = {"value": B / dt, "ms_per_step": dt * 1e3, "dtype": "f32"}
+
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+    ms = elapsed / args.steps * 1e3
+    value = B * world * args.steps / elapsed
+    rows = B * T
+    enc_bytes = 2 * rows * 768 * 4                      # clean + noisy fp32 features, read once
+    enc_gbs = enc_bytes / (enc_ms * 1e-3) / 1e9
+    flops = 2 * 768 * 256 * (2 * rows + 3 * rows)       # 5 encoder-sized contractions / step
+    peak_tf = BF16_PEAK_TFLOPS if args.precision == "bf16" else FP32_PEAK_TFLOPS
+    t_roof = max(flops / (peak_tf * 1e12), enc_bytes / (HBM_PEAK_GBS * 1e9))
+    line = {
+        "metric": METRIC, "value": value, "unit": "utterances/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": args.precision, "data": "synthetic",
+        "config": {"workload": "IEMOCAP DAD train step (configs[1]): batch=64/GPU, T=300x768 synthetic "
+                               "emotion2vec-shaped features, post-warm-up epoch %d (CE+KL+ECDA active), "
+                               "counter-RNG augmentation in-kernel" % args.epoch,
+                   "global_batch": B * world, "per_gpu_batch": B, "seq_len": T, "feature_dim": 768,
+                   "parallelism": "dp%d" % world},
+        "roofline": {"bound": "hbm", "kernel": "dad_encode_%s" % args.precision, "achieved": enc_gbs,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": enc_gbs / HBM_PEAK_GBS, "traffic": None,
+                     "avg_launch_ms": enc_ms, "algorithmic_bytes_per_launch": enc_bytes},
+        "step_roofline": {"t_roof_us": t_roof * 1e6, "t_step_us": ms * 1e3, "frac": t_roof / (ms * 1e-3),
+                          "flops_per_step": flops, "bytes_per_step": enc_bytes, "mfma_peak_tflops": peak_tf},
+        "losses_last_step": losses, "mask_sum_last_step": msum,
+    }
+    if fp32 is not None:
+        line["fp32_mode"] = fp32
+    if world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(B, T, args.cpu_steps, args.epoch)
+    print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,207 @@
+/*
+ * dad.h — C ABI of the MI355X-native DAD (Dynamic Asymmetric Distillation) train step.
+ *
+ * The reference (TMZZ22331/Robust-Speech-Emotion-Recognition-via-Dynamic-Asymmetric-
+ * Distillation-in-Noisy-Environments) is pure Python/PyTorch with no FFI; its operator
+ * surface for the hot path is the Python object API listed in SURVEY.md §8(b).  Each
+ * entry point below names the reference interface it replaces (I/ = IEMOCAP/DAD-train-
+ * IEMOCAP/, identical in CASIA/ and EMODB/ up to the differences resolved by dad_config).
+ *
+ * Conventions:
+ *   - every pointer is a DEVICE pointer owned by the caller (PyTorch tensors in the
+ *     Python host layer); sizes are explicit; no allocation, no host synchronisation,
+ *     enqueue-only on `stream` (a hipStream_t), graph-capturable;
+ *   - return 0 on success, a hipError_t value, or a DAD_E_* code; no exceptions cross;
+ *   - reentrant across streams; not thread-safe on one shared state.
+ *   - fixed model dims: INPUT_DIM 768, HIDDEN_DIM 256, NUM_CLASSES 4 (I/config.py:54-56).
+ */
+#ifndef DAD_ABI_H_
+#define DAD_ABI_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DAD_ABI_VERSION 1
+
+/* error codes (besides hipError_t values) */
+#define DAD_OK 0
+#define DAD_E_ARG 1001        /* null pointer / invalid scalar */
+#define DAD_E_SHAPE 1002      /* B/T out of the supported range */
+#define DAD_E_COMM 1003       /* RCCL failure */
+#define DAD_E_UNSUPPORTED 1004
+
+#define DAD_INPUT_DIM 768
+#define DAD_HIDDEN_DIM 256
+#define DAD_NUM_CLASSES 4
+#define DAD_MAX_BATCH 1024
+/* flat parameter vector [W1 (256x768) | b1 (256) | W2 (4x256) | b2 (4)] — the student
+ * (or teacher) half of SSRLModel.parameters() (I/model.py:101-122) */
+#define DAD_NPARAM (256 * 768 + 256 + 4 * 256 + 4)
+/* per-step extras appended to the gradient buffer so ONE all-reduce carries them:
+ * [0,4) DACP floored thresholds tau' (mean over ranks), [4,8) per-class certainty
+ * sums, [8,12) per-class counts, [12,16) losses (total, ce, kl, ecda) */
+#define DAD_GRAD_EXTRA 16
+#define DAD_GRAD_FLOATS (DAD_NPARAM + DAD_GRAD_EXTRA)
+/* persistent DACPManager state (I/utils.py:384-398): [0,4) tau (ema_thresholds),
+ * [4,8) Q (class_quality_scores), [8,12) epoch score sums, [12,16) epoch counts,
+ * [16,20) calibrated anchors */
+#define DAD_DACP_FLOATS 20
+#define DAD_NORM_BLOCKS 256
+
+/* per-step outputs ("tail" buffer): header then per-sample arrays */
+#define DAD_TAIL_HDR 64
+#define DAD_T_TOTAL 0
+#define DAD_T_CE 1
+#define DAD_T_KL 2
+#define DAD_T_ECDA 3
+#define DAD_T_SCL 4           /* always 0: C/train_CASIA.py:442, E/train_emodb.py:404 */
+#define DAD_T_MSUM 5
+#define DAD_T_CLIPNORM 6
+#define DAD_T_CLIPCOEF 7
+#define DAD_T_W 8             /* [4] DACP class weights W_c */
+#define DAD_T_TAU_BEFORE 12   /* [4] */
+#define DAD_T_TAU_AFTER 16    /* [4] */
+#define DAD_T_FLOORED 20      /* [4] */
+#define DAD_T_ECDA_TERM 24    /* [4] att_c * (mmd_c + gamma comp_c + delta rep) */
+#define DAD_T_ECDA_GATE 28    /* [4] */
+#define DAD_T_KL_ON 32
+#define DAD_T_ECDA_ON 33
+#define DAD_T_TAU_HAT 40      /* [4] batch quantile thresholds */
+/* after the header (noisy batch, Bn rows): score[Bn], pred[Bn] (as float), mask[Bn], q[Bn][4] */
+#define DAD_TAIL_FLOATS(Bn) (DAD_TAIL_HDR + (Bn) * (3 + DAD_NUM_CLASSES))
+
+enum dad_precision { DAD_PREC_FP32 = 0, DAD_PREC_BF16 = 1 };
+enum dad_rng_mode { DAD_RNG_EXPLICIT = 0, DAD_RNG_COUNTER = 1 };
+
+/* Every scalar the step reads from the reference's config module, resolved by the host
+ * at CALL time (the reference re-reads config inside the functions, I/utils.py:410,567,
+ * and the ablation runners mutate it between runs, I/run_granular_ablations.py:25-30).
+ * Float scalars are the float32 values torch would use for the python-float operands. */
+typedef struct dad_config {
+  int32_t B, T;                 /* clean batch: utterances, padded frames (batch max length) */
+  int32_t Bn, Tn;               /* noisy batch (collated independently, I/train.py:479-483) */
+  int32_t precision;            /* dad_precision */
+  int32_t rng_mode;             /* dad_rng_mode */
+  uint64_t seed, counter;       /* counter-RNG key material (counter = global step) */
+  int32_t warmup;               /* epoch < WARMUP_EPOCHS: CE only, no EMA (I/train.py:402,491) */
+  int32_t use_dacp;             /* DACP vs fixed threshold (I/train.py:414-420) */
+  int32_t ecda_on;              /* USE_ECDA && weight_ecda > 0 (I/train.py:450) */
+  int32_t use_entropy;          /* USE_ENTROPY_IN_SCORE (I/utils.py:415) */
+  int32_t class_aware;          /* USE_CLASS_AWARE_MMD (I/utils.py:579) */
+  int32_t dp_world;             /* ranks whose grads are all-reduced (1 = single GPU) */
+  float w_kl, w_ecda;           /* update_loss_weights (I/train.py:380-395) */
+  float dacp_gamma;             /* quantile level gamma_e (I/utils.py:471-473) */
+  float dacp_k, dacp_lambda, dacp_alpha, dacp_one_m_alpha;
+  float fixed_thr;              /* FIXED_CONFIDENCE_THRESHOLD */
+  float ecda_att_lambda, ecda_gamma, ecda_delta;
+  float ls_eps;                 /* label smoothing (I/train.py:364) */
+  float p_drop, drop_scale;     /* classifier dropout p, float32(1)/float32(1-p) */
+  float feat_p;                 /* strong-aug feature dropout rate (I/utils.py:325,343) */
+  float weak_std, strong_std;
+  int32_t mask_len, start_hi;   /* int(Tn*ratio), max(1, Tn-mask_len+1) (I/utils.py:365,370) */
+  int32_t clip;                 /* GRADIENT_CLIPPING */
+  float max_norm;
+  float lr_step_size;           /* lr / (1 - beta1^t)      (torch Adam single-tensor) */
+  float bc2_sqrt;               /* sqrt(1 - beta2^t) */
+  float beta1, one_m_beta1, beta2, one_m_beta2, adam_eps, weight_decay;
+  float ema_m, ema_one_m;       /* EMA_MOMENTUM, 1-EMA_MOMENTUM (I/model.py:219) */
+  float dacp_beta, dacp_one_m_beta;   /* epoch-end quality smoothing (I/utils.py:433-436) */
+  int32_t splits;               /* weight-gradient split-K factor (0 = auto) */
+  int32_t reserved[5];
+} dad_config;
+
+/* One clean + one noisy collated batch (I/dataload_noisy.py:124-129 format). */
+typedef struct dad_batch {
+  const float* xc;              /* [B][T][768] clean features */
+  const uint8_t* mc;            /* [B][T] padding mask, 1 = pad */
+  const int64_t* yc;            /* [B] clean labels */
+  const float* xn;              /* [Bn][Tn][768] noisy features */
+  const uint8_t* mn;            /* [Bn][Tn] */
+  /* DAD_RNG_EXPLICIT only (parity mode; NULL otherwise): the reference's six draws */
+  const float* nw;              /* [Bn][Tn][768] randn for weak aug */
+  const float* ns;              /* [Bn][Tn][768] randn for strong aug */
+  const float* u;               /* [768] rand for feature dropout */
+  const int64_t* start;         /* [Bn] temporal-mask starts */
+  const uint8_t* keep1;         /* [B][256] classifier dropout keep mask, clean pass */
+  const uint8_t* keep2;         /* [Bn][256] classifier dropout keep mask, strong pass */
+} dad_batch;
+
+/* Persistent training state, all caller-owned device buffers. */
+typedef struct dad_state {
+  float* student;               /* [DAD_NPARAM] */
+  float* teacher;               /* [DAD_NPARAM] */
+  float* exp_avg;               /* [DAD_NPARAM] Adam m */
+  float* exp_avg_sq;            /* [DAD_NPARAM] Adam v */
+  float* grad;                  /* [DAD_GRAD_FLOATS] grads (+extras); the DP all-reduce buffer */
+  uint16_t* w1bf_student;       /* [256*768] bf16 shadow of student W1 */
+  uint16_t* w1bf_teacher;       /* [256*768] bf16 shadow of teacher W1 */
+  float* dacp;                  /* [DAD_DACP_FLOATS] */
+  float* tail;                  /* [DAD_TAIL_FLOATS(Bn)] per-step outputs */
+  float* emb;                   /* [B+2*Bn][256] e_clean [B], e_teacher [Bn], e_strong [Bn] */
+  float* logits;                /* [B+2*Bn][4]   z_clean, z_teacher, z_strong */
+} dad_state;
+
+/* --- sizing ------------------------------------------------------------------------ */
+size_t dad_param_count(void);
+int dad_workspace_bytes(const dad_config* cfg, size_t* bytes);
+const char* dad_error_string(int code);
+
+/* --- fused train step ---------------------------------------------------------------
+ * Replaces the body of Trainer.train_epoch's loop (I/train.py:484-492):
+ *   train_step (I/train.py:397-471) + backward + clip_grad_norm_ + Adam.step + update_teacher_ema.
+ * dad_step_compute: encoder passes, losses, DACP mask, analytic backward -> state->grad.
+ * dad_step_apply:   global-norm clip, Adam (L2 decay), teacher EMA, DACP state commit,
+ *                   bf16 shadow refresh.  A DP caller all-reduces state->grad in between.
+ * dad_step = compute + apply (single GPU). */
+int dad_step_compute(const dad_config* cfg, const dad_batch* batch, const dad_state* st,
+                     void* workspace, void* stream);
+/* dad_step_compute = dad_step_encode (the fused augmentation + three encoder GEMMs +
+ * pooling partials, one launch) followed by dad_step_backward (pool, losses, DACP,
+ * ECDA, analytic backward, weight gradient, reduction); split so callers can time the
+ * encoder launch on their stream. */
+int dad_step_encode(const dad_config* cfg, const dad_batch* batch, const dad_state* st,
+                    void* workspace, void* stream);
+int dad_step_backward(const dad_config* cfg, const dad_batch* batch, const dad_state* st,
+                      void* workspace, void* stream);
+int dad_step_apply(const dad_config* cfg, const dad_state* st, void* workspace, void* stream);
+int dad_step(const dad_config* cfg, const dad_batch* batch, const dad_state* st,
+             void* workspace, void* stream);
+
+/* DACPManager.update_class_quality_scores_epoch (I/utils.py:430-447) */
+int dad_epoch_end(const dad_config* cfg, const dad_state* st, void* stream);
+/* refresh the bf16 shadows of W1 after the caller changed student/teacher params
+ * (e.g. load_complete_pretrained_weights, I/model.py:143-198) */
+int dad_refresh_shadow(const dad_state* st, void* stream);
+
+/* SSRLModel.update_teacher_ema (I/model.py:211-223) over flat [W1|b1|W2|b2] vectors:
+ * teacher = teacher*ema_m + student*ema_one_m (n floats) */
+int dad_teacher_ema(const float* student, float* teacher, size_t n, float ema_m, float ema_one_m, void* stream);
+
+/* --- modular operators (the SSRLModel / utils.py surface) --------------------------
+ * Emotion2VecEncoder.forward (I/model.py:18-41): e[B][256] = masked mean of ReLU(x W1^T + b1).
+ * workspace: dad_encoder_workspace_bytes(B, T). */
+size_t dad_encoder_workspace_bytes(int B, int T);
+int dad_encoder_forward(const float* x, const uint8_t* pad, int B, int T, const float* w1,
+                        const float* b1, float* e_out, int precision, void* workspace, void* stream);
+/* backward of the above w.r.t. W1, b1 given de[B][256] (autograd of I/model.py:28-36);
+ * recomputes the ReLU pattern; dw1 [256][768], db1 [256] are overwritten. */
+int dad_encoder_backward(const float* x, const uint8_t* pad, int B, int T, const float* w1,
+                         const float* b1, const float* de, float* dw1, float* db1,
+                         void* workspace, void* stream);
+
+/* --- data-parallel gradient exchange (RCCL over xGMI) ------------------------------ */
+int dad_comm_unique_id_bytes(void);
+int dad_comm_get_unique_id(void* id_out);
+int dad_comm_init(void** comm, int nranks, const void* id, int rank);
+/* in-place SUM all-reduce of state->grad (DAD_GRAD_FLOATS floats) on `stream` */
+int dad_comm_allreduce_grad(void* comm, const dad_state* st, void* stream);
+int dad_comm_destroy(void* comm);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DAD_ABI_H_ */

@@ -450,7 +450,7 @@ class DADOracle:
                 s = q.max(1).astype(F32)
                 pred = q.argmax(1)
                 maskf = (s >= F32(cfg["FIXED_CONFIDENCE_THRESHOLD"])).astype(np.float64)
-                w = np.ones(B, F32)
+                w = np.ones(len(s), F32)          # torch.ones_like(mask): noisy batch size
                 ecda_mask = maskf.astype(F32)
             es, act_s, vlen_s = encoder_forward(xs, mn, W1, b1)
             zs, ds = self._cls(es, W2, b2, inp["keep2"], p)

@@ -1,0 +1,132 @@
+"""ctypes binding of the C ABI in include/dad.h (libdad_hip.so).
+
+The structures below mirror dad.h field for field.  Loading fails loudly: there is no
+Python or PyTorch fallback for any operator of the step.
+"""
+import ctypes
+import os
+
+from . import _build
+
+c_float_p = ctypes.POINTER(ctypes.c_float)
+
+DAD_NPARAM = 256 * 768 + 256 + 4 * 256 + 4
+DAD_GRAD_EXTRA = 16
+DAD_GRAD_FLOATS = DAD_NPARAM + DAD_GRAD_EXTRA
+DAD_DACP_FLOATS = 20
+DAD_TAIL_HDR = 64
+DAD_MAX_BATCH = 1024
+PREC_FP32, PREC_BF16 = 0, 1
+RNG_EXPLICIT, RNG_COUNTER = 0, 1
+
+# tail header slots (dad.h DAD_T_*)
+T_TOTAL, T_CE, T_KL, T_ECDA, T_SCL, T_MSUM, T_CLIPNORM, T_CLIPCOEF = range(8)
+T_W, T_TAU_BEFORE, T_TAU_AFTER, T_FLOORED, T_ECDA_TERM, T_ECDA_GATE = 8, 12, 16, 20, 24, 28
+T_KL_ON, T_ECDA_ON, T_TAU_HAT = 32, 33, 40
+
+
+def tail_floats(bn):
+    return DAD_TAIL_HDR + bn * 7
+
+
+class DadConfig(ctypes.Structure):
+    _fields_ = [
+        ("B", ctypes.c_int32), ("T", ctypes.c_int32), ("Bn", ctypes.c_int32), ("Tn", ctypes.c_int32),
+        ("precision", ctypes.c_int32), ("rng_mode", ctypes.c_int32),
+        ("seed", ctypes.c_uint64), ("counter", ctypes.c_uint64),
+        ("warmup", ctypes.c_int32), ("use_dacp", ctypes.c_int32), ("ecda_on", ctypes.c_int32),
+        ("use_entropy", ctypes.c_int32), ("class_aware", ctypes.c_int32), ("dp_world", ctypes.c_int32),
+        ("w_kl", ctypes.c_float), ("w_ecda", ctypes.c_float), ("dacp_gamma", ctypes.c_float),
+        ("dacp_k", ctypes.c_float), ("dacp_lambda", ctypes.c_float), ("dacp_alpha", ctypes.c_float),
+        ("dacp_one_m_alpha", ctypes.c_float), ("fixed_thr", ctypes.c_float),
+        ("ecda_att_lambda", ctypes.c_float), ("ecda_gamma", ctypes.c_float), ("ecda_delta", ctypes.c_float),
+        ("ls_eps", ctypes.c_float), ("p_drop", ctypes.c_float), ("drop_scale", ctypes.c_float),
+        ("feat_p", ctypes.c_float), ("weak_std", ctypes.c_float), ("strong_std", ctypes.c_float),
+        ("mask_len", ctypes.c_int32), ("start_hi", ctypes.c_int32), ("clip", ctypes.c_int32),
+        ("max_norm", ctypes.c_float), ("lr_step_size", ctypes.c_float), ("bc2_sqrt", ctypes.c_float),
+        ("beta1", ctypes.c_float), ("one_m_beta1", ctypes.c_float), ("beta2", ctypes.c_float),
+        ("one_m_beta2", ctypes.c_float), ("adam_eps", ctypes.c_float), ("weight_decay", ctypes.c_float),
+        ("ema_m", ctypes.c_float), ("ema_one_m", ctypes.c_float),
+        ("dacp_beta", ctypes.c_float), ("dacp_one_m_beta", ctypes.c_float),
+        ("splits", ctypes.c_int32), ("reserved", ctypes.c_int32 * 5),
+    ]
+
+
+class DadBatch(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in
+                ("xc", "mc", "yc", "xn", "mn", "nw", "ns", "u", "start", "keep1", "keep2")]
+
+
+class DadState(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in
+                ("student", "teacher", "exp_avg", "exp_avg_sq", "grad", "w1bf_student", "w1bf_teacher",
+                 "dacp", "tail", "emb", "logits")]
+
+
+# exported symbols (must match include/dad.h); tests check every one is present
+EXPORTS = {
+    "dad_param_count": (ctypes.c_size_t, []),
+    "dad_workspace_bytes": (ctypes.c_int, [ctypes.POINTER(DadConfig), ctypes.POINTER(ctypes.c_size_t)]),
+    "dad_error_string": (ctypes.c_char_p, [ctypes.c_int]),
+    "dad_step_compute": (ctypes.c_int, [ctypes.POINTER(DadConfig), ctypes.POINTER(DadBatch),
+                                        ctypes.POINTER(DadState), ctypes.c_void_p, ctypes.c_void_p]),
+    "dad_step_encode": (ctypes.c_int, [ctypes.POINTER(DadConfig), ctypes.POINTER(DadBatch),
+                                       ctypes.POINTER(DadState), ctypes.c_void_p, ctypes.c_void_p]),
+    "dad_step_backward": (ctypes.c_int, [ctypes.POINTER(DadConfig), ctypes.POINTER(DadBatch),
+                                         ctypes.POINTER(DadState), ctypes.c_void_p, ctypes.c_void_p]),
+    "dad_step_apply": (ctypes.c_int, [ctypes.POINTER(DadConfig), ctypes.POINTER(DadState),
+                                      ctypes.c_void_p, ctypes.c_void_p]),
+    "dad_step": (ctypes.c_int, [ctypes.POINTER(DadConfig), ctypes.POINTER(DadBatch), ctypes.POINTER(DadState),
+                                ctypes.c_void_p, ctypes.c_void_p]),
+    "dad_epoch_end": (ctypes.c_int, [ctypes.POINTER(DadConfig), ctypes.POINTER(DadState), ctypes.c_void_p]),
+    "dad_refresh_shadow": (ctypes.c_int, [ctypes.POINTER(DadState), ctypes.c_void_p]),
+    "dad_teacher_ema": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_float,
+                                       ctypes.c_float, ctypes.c_void_p]),
+    "dad_encoder_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int, ctypes.c_int]),
+    "dad_encoder_forward": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                           ctypes.c_void_p, ctypes.c_void_p]),
+    "dad_encoder_backward": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "dad_comm_unique_id_bytes": (ctypes.c_int, []),
+    "dad_comm_get_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
+    "dad_comm_init": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_void_p, ctypes.c_int]),
+    "dad_comm_allreduce_grad": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(DadState), ctypes.c_void_p]),
+    "dad_comm_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+}
+
+_LIB = None
+
+
+class DadError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libdad_hip.so (in-tree).  Raises if it is missing: build it with _build.build()."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    path = _build.LIB_PATH
+    if not os.path.exists(path):
+        raise DadError("libdad_hip.so not built (%s); run __graft_entry__.build() or "
+                       "python -m <pkg>._build" % path)
+    L = ctypes.CDLL(path)
+    for name, (res, args) in EXPORTS.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = L
+    return L
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = lib().dad_error_string(rc)
+        raise DadError("%s failed: %s (%d)" % (what, msg.decode() if msg else "?", rc))
+
+
+def ptr(t):
+    """Device pointer of a tensor (or None)."""
+    return None if t is None else ctypes.c_void_p(t.data_ptr())

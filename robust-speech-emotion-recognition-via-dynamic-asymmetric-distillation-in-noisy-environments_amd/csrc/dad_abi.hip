@@ -1,0 +1,386 @@
+// Host side of the C ABI (include/dad.h): argument validation, workspace carving and the
+// kernel sequence of one DAD step.  Enqueue-only: no allocation, no synchronisation.
+#include <string.h>
+
+#include "dad_common.h"
+#include "dad_kernels.h"
+
+namespace {
+
+#define DAD_TRY(expr)                           \
+  do {                                          \
+    hipError_t e_ = (expr);                     \
+    if (e_ != hipSuccess) return (int)e_;       \
+  } while (0)
+
+inline int check_cfg(const dad_config* c) {
+  if (!c) return DAD_E_ARG;
+  if (c->B < 1 || c->B > DAD_MAX_BATCH || c->T < 1) return DAD_E_SHAPE;
+  if (c->Bn < 0 || c->Bn > DAD_MAX_BATCH || c->Tn < 0) return DAD_E_SHAPE;
+  if (!c->warmup && (c->Bn < 1 || c->Tn < 1)) return DAD_E_SHAPE;
+  if (c->precision != DAD_PREC_FP32 && c->precision != DAD_PREC_BF16) return DAD_E_ARG;
+  if (c->rng_mode != DAD_RNG_EXPLICIT && c->rng_mode != DAD_RNG_COUNTER) return DAD_E_ARG;
+  if (c->dp_world < 1) return DAD_E_ARG;
+  return DAD_OK;
+}
+
+inline DadGeom geom_of(const dad_config* c) { return dad_geom(c->B, c->T, c->Bn, c->Tn); }
+
+inline int splits_of(const dad_config* c) {
+  return c->splits > 0 ? c->splits : dad_auto_splits(geom_of(c), c->precision, c->warmup);
+}
+
+inline int max_splits_of(const dad_config* c) {
+  // the workspace is sized for the largest split count any step with this geometry may use
+  return c->splits > 0 ? c->splits : dad_auto_splits(geom_of(c), c->precision, 0);
+}
+
+template <typename T>
+inline T* ws_ptr(void* ws, size_t off) {
+  return reinterpret_cast<T*>(reinterpret_cast<char*>(ws) + off);
+}
+
+struct Keys {
+  uint32_t weak, strong, feat, tstart, drop1, drop2;
+};
+
+inline Keys keys_of(const dad_config* c) {
+  Keys k;
+  k.weak = dad_stream_key(c->seed, c->counter, DAD_RNG_WEAK);
+  k.strong = dad_stream_key(c->seed, c->counter, DAD_RNG_STRONG);
+  k.feat = dad_stream_key(c->seed, c->counter, DAD_RNG_FEAT);
+  k.tstart = dad_stream_key(c->seed, c->counter, DAD_RNG_TSTART);
+  k.drop1 = dad_stream_key(c->seed, c->counter, DAD_RNG_DROP1);
+  k.drop2 = dad_stream_key(c->seed, c->counter, DAD_RNG_DROP2);
+  return k;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t dad_param_count(void) { return DAD_NPARAM; }
+
+const char* dad_error_string(int code) {
+  switch (code) {
+    case DAD_OK: return "ok";
+    case DAD_E_ARG: return "DAD_E_ARG: invalid argument";
+    case DAD_E_SHAPE: return "DAD_E_SHAPE: unsupported batch/sequence shape";
+    case DAD_E_COMM: return "DAD_E_COMM: RCCL failure";
+    case DAD_E_UNSUPPORTED: return "DAD_E_UNSUPPORTED";
+    default: return hipGetErrorString((hipError_t)code);
+  }
+}
+
+int dad_workspace_bytes(const dad_config* cfg, size_t* bytes) {
+  int rc = check_cfg(cfg);
+  if (rc) return rc;
+  if (!bytes) return DAD_E_ARG;
+  *bytes = dad_ws_layout(geom_of(cfg), max_splits_of(cfg), cfg->precision).bytes;
+  return DAD_OK;
+}
+
+}  // extern "C"
+
+static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const dad_state* st, void* workspace,
+                               void* stream_, bool do_encode, bool do_backward) {
+  int rc = check_cfg(cfg);
+  if (rc) return rc;
+  if (!bt || !st || !workspace) return DAD_E_ARG;
+  if (!bt->xc || !bt->mc || !bt->yc || !st->student || !st->teacher || !st->grad || !st->dacp || !st->tail ||
+      !st->emb || !st->logits || !st->w1bf_student || !st->w1bf_teacher)
+    return DAD_E_ARG;
+  if (!cfg->warmup && (!bt->xn || !bt->mn)) return DAD_E_ARG;
+  const bool explicit_rng = cfg->rng_mode == DAD_RNG_EXPLICIT;
+  if (explicit_rng && cfg->p_drop > 0.0f && (!bt->keep1 || (!cfg->warmup && !bt->keep2))) return DAD_E_ARG;
+  if (explicit_rng && !cfg->warmup && (!bt->nw || !bt->ns || !bt->u || !bt->start)) return DAD_E_ARG;
+  hipStream_t stream = (hipStream_t)stream_;
+  const DadGeom G = geom_of(cfg);
+  const int Bn = cfg->warmup ? 0 : G.Bn;
+  const int splits = splits_of(cfg);
+  if (splits > max_splits_of(cfg)) return DAD_E_ARG;
+  const DadWs L = dad_ws_layout(G, max_splits_of(cfg), cfg->precision);
+  const Keys k = keys_of(cfg);
+  float* part_sum = ws_ptr<float>(workspace, L.part_sum);
+  float* part_cnt = ws_ptr<float>(workspace, L.part_cnt);
+  uint32_t* bits = ws_ptr<uint32_t>(workspace, L.bits);
+  float* vlen = ws_ptr<float>(workspace, L.vlen);
+  float* ge = ws_ptr<float>(workspace, L.ge);
+  float* wpart = ws_ptr<float>(workspace, L.wpart);
+  float* normpart = ws_ptr<float>(workspace, L.normpart);
+  float* ecda_scratch = ws_ptr<float>(workspace, L.ecda);
+  __bf16* xs_bf16 = ws_ptr<__bf16>(workspace, L.xs_bf16);
+  const bool bf16 = cfg->precision == DAD_PREC_BF16;
+
+  // 1. fused augmentation + encoder GEMMs + pooling partials
+  DadEncodeArgs ea;
+  memset(&ea, 0, sizeof(ea));
+  ea.g = G; ea.warmup = cfg->warmup;
+  ea.mask_len = cfg->mask_len; ea.start_hi = cfg->start_hi;
+  ea.xc = bt->xc; ea.mc = bt->mc; ea.xn = bt->xn; ea.mn = bt->mn;
+  ea.w1_student = st->student + DAD_OFF_W1; ea.b1_student = st->student + DAD_OFF_B1;
+  ea.w1_teacher = st->teacher + DAD_OFF_W1; ea.b1_teacher = st->teacher + DAD_OFF_B1;
+  ea.w1bf_student = reinterpret_cast<const __bf16*>(st->w1bf_student);
+  ea.w1bf_teacher = reinterpret_cast<const __bf16*>(st->w1bf_teacher);
+  if (explicit_rng) { ea.nw = bt->nw; ea.ns = bt->ns; ea.u = bt->u; ea.start = bt->start; }
+  ea.key_weak = k.weak; ea.key_strong = k.strong; ea.key_feat = k.feat; ea.key_tstart = k.tstart;
+  ea.weak_std = cfg->weak_std; ea.strong_std = cfg->strong_std; ea.feat_p = cfg->feat_p;
+  ea.part_sum = part_sum; ea.part_cnt = part_cnt; ea.bits = bits; ea.xs_bf16 = xs_bf16;
+  const int nwaves = G.Bc * G.ncc + Bn * G.ncn;
+  const dim3 egrid((nwaves + 3) / 4);
+  if (do_encode) {
+    if (bf16) hipLaunchKernelGGL(dad_encode_bf16, egrid, dim3(256), 0, stream, ea);
+    else hipLaunchKernelGGL(dad_encode_f32, egrid, dim3(256), 0, stream, ea);
+    DAD_TRY(hipGetLastError());
+  }
+  if (!do_backward) return DAD_OK;
+
+  // 2. pooled embeddings + classifier logits
+  DadPoolArgs pa;
+  memset(&pa, 0, sizeof(pa));
+  pa.g = G; pa.warmup = cfg->warmup;
+  pa.mc = bt->mc; pa.mn = bt->mn; pa.part_sum = part_sum;
+  pa.student = st->student; pa.teacher = st->teacher;
+  if (explicit_rng) { pa.keep1 = bt->keep1; pa.keep2 = bt->keep2; }
+  pa.key_drop1 = k.drop1; pa.key_drop2 = k.drop2;
+  pa.p_drop = cfg->p_drop; pa.drop_scale = cfg->drop_scale;
+  pa.emb = st->emb; pa.vlen = vlen; pa.logits = st->logits;
+  hipLaunchKernelGGL(dad_pool, dim3(G.Bc + Bn), dim3(256), 0, stream, pa);
+  DAD_TRY(hipGetLastError());
+
+  // 3. losses, DACP mask, analytic backward to dL/de and the classifier grads
+  DadTailArgs ta;
+  memset(&ta, 0, sizeof(ta));
+  ta.cfg = *cfg; ta.yc = bt->yc; ta.logits = st->logits; ta.emb = st->emb; ta.student = st->student;
+  if (explicit_rng) { ta.keep1 = bt->keep1; ta.keep2 = bt->keep2; }
+  ta.key_drop1 = k.drop1; ta.key_drop2 = k.drop2;
+  ta.dacp = st->dacp; ta.tailf = st->tail; ta.ge = ge; ta.grad = st->grad;
+  hipLaunchKernelGGL(dad_tail, dim3(1), dim3(256), 0, stream, ta);
+  DAD_TRY(hipGetLastError());
+
+  // 4. ECDA (class-aware MMD + compactness + repulsion) and its embedding grads
+  if (!cfg->warmup) {
+    DadEcdaArgs ca;
+    memset(&ca, 0, sizeof(ca));
+    ca.cfg = *cfg; ca.yc = bt->yc; ca.emb = st->emb; ca.tailf = st->tail;
+    ca.tail_terms = st->tail + DAD_T_ECDA_TERM; ca.ge = ge; ca.scratch = ecda_scratch;
+    hipLaunchKernelGGL(dad_ecda, dim3(DAD_C), dim3(256), 0, stream, ca);
+    DAD_TRY(hipGetLastError());
+  }
+
+  // 5. encoder weight gradient (split-K partial slabs)
+  DadWgradArgs wa;
+  memset(&wa, 0, sizeof(wa));
+  wa.g = G; wa.warmup = cfg->warmup; wa.splits = splits;
+  wa.mask_len = cfg->mask_len; wa.start_hi = cfg->start_hi;
+  wa.xc = bt->xc; wa.xn = bt->xn;
+  if (explicit_rng) { wa.ns = bt->ns; wa.u = bt->u; wa.start = bt->start; }
+  wa.key_strong = k.strong; wa.key_feat = k.feat; wa.key_tstart = k.tstart;
+  wa.strong_std = cfg->strong_std; wa.feat_p = cfg->feat_p;
+  wa.bits = bits; wa.ge = ge; wa.vlen = vlen; wa.xs_bf16 = xs_bf16; wa.wpart = wpart;
+  if (bf16) hipLaunchKernelGGL(dad_wgrad_bf16, dim3(6 * splits), dim3(256), 0, stream, wa);
+  else hipLaunchKernelGGL(dad_wgrad_f32, dim3(6 * splits), dim3(256), 0, stream, wa);
+  DAD_TRY(hipGetLastError());
+
+  // 6. reduce partials -> dW1, db1; loss totals; squared-norm partials (single GPU)
+  DadReduceArgs ra;
+  memset(&ra, 0, sizeof(ra));
+  ra.g = G; ra.splits = splits; ra.warmup = cfg->warmup;
+  ra.want_norm = cfg->dp_world == 1;
+  ra.w_kl = cfg->w_kl; ra.w_ecda = cfg->w_ecda;
+  ra.wpart = wpart; ra.ge = ge; ra.vlen = vlen; ra.part_cnt = part_cnt; ra.tailf = st->tail;
+  ra.grad = st->grad; ra.normpart = normpart;
+  hipLaunchKernelGGL(dad_reduce, dim3(193), dim3(256), 0, stream, ra);
+  DAD_TRY(hipGetLastError());
+  return DAD_OK;
+}
+
+extern "C" {
+
+int dad_step_compute(const dad_config* cfg, const dad_batch* bt, const dad_state* st, void* workspace,
+                     void* stream) {
+  return step_compute_phases(cfg, bt, st, workspace, stream, true, true);
+}
+
+int dad_step_encode(const dad_config* cfg, const dad_batch* bt, const dad_state* st, void* workspace,
+                    void* stream) {
+  return step_compute_phases(cfg, bt, st, workspace, stream, true, false);
+}
+
+int dad_step_backward(const dad_config* cfg, const dad_batch* bt, const dad_state* st, void* workspace,
+                      void* stream) {
+  return step_compute_phases(cfg, bt, st, workspace, stream, false, true);
+}
+
+int dad_step_apply(const dad_config* cfg, const dad_state* st, void* workspace, void* stream_) {
+  int rc = check_cfg(cfg);
+  if (rc) return rc;
+  if (!st || !workspace) return DAD_E_ARG;
+  hipStream_t stream = (hipStream_t)stream_;
+  const DadWs L = dad_ws_layout(geom_of(cfg), max_splits_of(cfg), cfg->precision);
+  float* normpart = ws_ptr<float>(workspace, L.normpart);
+  const int nblk = (DAD_NPARAM + 1023) / 1024;
+  int nnorm = 193;
+  if (cfg->dp_world > 1) {
+    hipLaunchKernelGGL(dad_norm, dim3(nblk), dim3(256), 0, stream, st->grad, normpart, 1.0f / (float)cfg->dp_world);
+    DAD_TRY(hipGetLastError());
+    nnorm = nblk;
+  }
+  DadOptimArgs oa;
+  memset(&oa, 0, sizeof(oa));
+  oa.cfg = *cfg;
+  oa.student = st->student; oa.teacher = st->teacher; oa.exp_avg = st->exp_avg; oa.exp_avg_sq = st->exp_avg_sq;
+  oa.grad = st->grad;
+  oa.w1bf_student = reinterpret_cast<__bf16*>(st->w1bf_student);
+  oa.w1bf_teacher = reinterpret_cast<__bf16*>(st->w1bf_teacher);
+  oa.dacp = st->dacp; oa.tailf = st->tail; oa.normpart = normpart; oa.nnorm = nnorm;
+  hipLaunchKernelGGL(dad_optim, dim3(nblk), dim3(256), 0, stream, oa);
+  DAD_TRY(hipGetLastError());
+  return DAD_OK;
+}
+
+int dad_step(const dad_config* cfg, const dad_batch* batch, const dad_state* st, void* workspace, void* stream) {
+  int rc = dad_step_compute(cfg, batch, st, workspace, stream);
+  if (rc) return rc;
+  return dad_step_apply(cfg, st, workspace, stream);
+}
+
+int dad_epoch_end(const dad_config* cfg, const dad_state* st, void* stream_) {
+  if (!cfg || !st || !st->dacp) return DAD_E_ARG;
+  hipLaunchKernelGGL(dad_epoch_end_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream_, st->dacp, cfg->dacp_beta,
+                     cfg->dacp_one_m_beta);
+  DAD_TRY(hipGetLastError());
+  return DAD_OK;
+}
+
+int dad_refresh_shadow(const dad_state* st, void* stream_) {
+  if (!st || !st->student || !st->teacher || !st->w1bf_student || !st->w1bf_teacher) return DAD_E_ARG;
+  hipLaunchKernelGGL(dad_shadow_kernel, dim3((DAD_H * DAD_D + 255) / 256), dim3(256), 0, (hipStream_t)stream_,
+                     st->student, st->teacher, reinterpret_cast<__bf16*>(st->w1bf_student),
+                     reinterpret_cast<__bf16*>(st->w1bf_teacher));
+  DAD_TRY(hipGetLastError());
+  return DAD_OK;
+}
+
+// ----------------------------------------------------------------- modular encoder ops
+size_t dad_encoder_workspace_bytes(int B, int T) {
+  if (B < 1 || T < 1) return 0;
+  const DadGeom g = dad_geom(B, T, 0, 0);
+  return dad_ws_layout(g, dad_auto_splits(g, DAD_PREC_FP32, 1), DAD_PREC_FP32).bytes;
+}
+
+}  // extern "C"
+
+namespace {
+
+__global__ __launch_bounds__(256) void dad_embed_kernel(const float* part_sum, const uint8_t* pad, int B, int T,
+                                                        int nchunk, float* vlen, float* e_out) {
+  (void)B;
+  __shared__ float red[4];
+  const int b = blockIdx.x, h = threadIdx.x;
+  float l = 0.0f;
+  for (int t = h; t < T; t += 256) l += pad[(size_t)b * T + t] == 0 ? 1.0f : 0.0f;
+  l = dad_wave_sum(l);
+  if ((h & 63) == 0) red[h >> 6] = l;
+  __syncthreads();
+  const float len = ((red[0] + red[1]) + red[2]) + red[3];
+  float s = 0.0f;
+  for (int c = 0; c < nchunk; ++c) s += part_sum[((size_t)b * nchunk + c) * DAD_H + h];
+  e_out[(size_t)b * DAD_H + h] = s / fmaxf(len, 1.0f);
+  if (h == 0 && vlen) vlen[b] = len;
+}
+
+__global__ __launch_bounds__(256) void dad_w1bf_kernel(const float* w, __bf16* out) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < (size_t)DAD_H * DAD_D) out[i] = (__bf16)w[i];
+}
+
+int encoder_forward_impl(const float* x, const uint8_t* pad, int B, int T, const float* w1, const float* b1,
+                         int precision, void* workspace, hipStream_t stream, const DadWs& L, float* vlen_out,
+                         float* e_out) {
+  __bf16* w1bf = ws_ptr<__bf16>(workspace, L.w1bf);
+  if (precision == DAD_PREC_BF16) {
+    hipLaunchKernelGGL(dad_w1bf_kernel, dim3((DAD_H * DAD_D + 255) / 256), dim3(256), 0, stream, w1, w1bf);
+    DAD_TRY(hipGetLastError());
+  }
+  const DadGeom G = dad_geom(B, T, 0, 0);
+  DadEncodeArgs ea;
+  memset(&ea, 0, sizeof(ea));
+  ea.g = G; ea.warmup = 1;
+  ea.xc = x; ea.mc = pad; ea.w1_student = w1; ea.b1_student = b1; ea.w1bf_student = w1bf;
+  ea.part_sum = ws_ptr<float>(workspace, L.part_sum);
+  ea.part_cnt = ws_ptr<float>(workspace, L.part_cnt);
+  ea.bits = ws_ptr<uint32_t>(workspace, L.bits);
+  const dim3 egrid((B * G.ncc + 3) / 4);
+  if (precision == DAD_PREC_BF16) hipLaunchKernelGGL(dad_encode_bf16, egrid, dim3(256), 0, stream, ea);
+  else hipLaunchKernelGGL(dad_encode_f32, egrid, dim3(256), 0, stream, ea);
+  DAD_TRY(hipGetLastError());
+  if (e_out) {
+    hipLaunchKernelGGL(dad_embed_kernel, dim3(B), dim3(256), 0, stream, ea.part_sum, pad, B, T, G.ncc, vlen_out,
+                       e_out);
+    DAD_TRY(hipGetLastError());
+  }
+  return DAD_OK;
+}
+
+__global__ __launch_bounds__(256) void dad_embed_len_kernel(const uint8_t* pad, int B, int T, float* vlen) {
+  __shared__ float red[4];
+  const int b = blockIdx.x, h = threadIdx.x;
+  float l = 0.0f;
+  for (int t = h; t < T; t += 256) l += pad[(size_t)b * T + t] == 0 ? 1.0f : 0.0f;
+  l = dad_wave_sum(l);
+  if ((h & 63) == 0) red[h >> 6] = l;
+  __syncthreads();
+  if (h == 0) vlen[b] = ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+}  // namespace
+
+extern "C" {
+
+int dad_encoder_forward(const float* x, const uint8_t* pad, int B, int T, const float* w1, const float* b1,
+                        float* e_out, int precision, void* workspace, void* stream) {
+  if (!x || !pad || !w1 || !b1 || !e_out || !workspace) return DAD_E_ARG;
+  if (B < 1 || B > DAD_MAX_BATCH || T < 1) return DAD_E_SHAPE;
+  if (precision != DAD_PREC_FP32 && precision != DAD_PREC_BF16) return DAD_E_ARG;
+  const DadGeom G = dad_geom(B, T, 0, 0);
+  const DadWs L = dad_ws_layout(G, dad_auto_splits(G, DAD_PREC_FP32, 1), DAD_PREC_FP32);
+  return encoder_forward_impl(x, pad, B, T, w1, b1, precision, workspace, (hipStream_t)stream, L,
+                              ws_ptr<float>(workspace, L.vlen), e_out);
+}
+
+int dad_encoder_backward(const float* x, const uint8_t* pad, int B, int T, const float* w1, const float* b1,
+                         const float* de, float* dw1, float* db1, void* workspace, void* stream_) {
+  if (!x || !pad || !w1 || !b1 || !de || !dw1 || !db1 || !workspace) return DAD_E_ARG;
+  if (B < 1 || B > DAD_MAX_BATCH || T < 1) return DAD_E_SHAPE;
+  hipStream_t stream = (hipStream_t)stream_;
+  const DadGeom G = dad_geom(B, T, 0, 0);
+  const int splits = dad_auto_splits(G, DAD_PREC_FP32, 1);
+  const DadWs L = dad_ws_layout(G, splits, DAD_PREC_FP32);
+  float* vlen = ws_ptr<float>(workspace, L.vlen);
+  // recompute the ReLU'/valid bits and per-slab active counts (FP32 forward)
+  int rc = encoder_forward_impl(x, pad, B, T, w1, b1, DAD_PREC_FP32, workspace, stream, L, nullptr, nullptr);
+  if (rc) return rc;
+  hipLaunchKernelGGL(dad_embed_len_kernel, dim3(B), dim3(256), 0, stream, pad, B, T, vlen);
+  DAD_TRY(hipGetLastError());
+  DadWgradArgs wa;
+  memset(&wa, 0, sizeof(wa));
+  wa.g = G; wa.warmup = 1; wa.splits = splits;
+  wa.xc = x; wa.bits = ws_ptr<uint32_t>(workspace, L.bits); wa.ge = de; wa.vlen = vlen;
+  wa.wpart = ws_ptr<float>(workspace, L.wpart);
+  hipLaunchKernelGGL(dad_wgrad_f32, dim3(6 * splits), dim3(256), 0, stream, wa);
+  DAD_TRY(hipGetLastError());
+  float* gflat = ws_ptr<float>(workspace, L.gflat);
+  DadReduceArgs ra;
+  memset(&ra, 0, sizeof(ra));
+  ra.g = G; ra.splits = splits; ra.warmup = 1; ra.want_norm = 0;
+  ra.wpart = wa.wpart; ra.ge = de; ra.vlen = vlen; ra.part_cnt = ws_ptr<float>(workspace, L.part_cnt);
+  ra.tailf = nullptr; ra.grad = gflat; ra.normpart = ws_ptr<float>(workspace, L.normpart);
+  hipLaunchKernelGGL(dad_reduce, dim3(193), dim3(256), 0, stream, ra);
+  DAD_TRY(hipGetLastError());
+  DAD_TRY(hipMemcpyAsync(dw1, gflat + DAD_OFF_W1, sizeof(float) * DAD_H * DAD_D, hipMemcpyDeviceToDevice, stream));
+  DAD_TRY(hipMemcpyAsync(db1, gflat + DAD_OFF_B1, sizeof(float) * DAD_H, hipMemcpyDeviceToDevice, stream));
+  return DAD_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,181 @@
+// Shared device-side definitions for the DAD train-step kernels (gfx950 / CDNA4).
+//
+// Layout contract (see DESIGN.md "Data layout in HBM"):
+//   features   f32 [B][T][768] row-major (the reference collator's padded layout,
+//              I/dataload_noisy.py:111-129), padding mask u8 [B][T] (1 = pad)
+//   W1         f32 [256][768] (nn.Linear weight, I/model.py:13), bf16 shadow [256][768]
+//   rows are processed in 32-row "slabs" that never cross an utterance: slab (b, c)
+//   covers frames 32c .. 32c+31 of utterance b (frames >= T are masked).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/dad.h"
+
+#define DAD_D 768
+#define DAD_H 256
+#define DAD_C 4
+#define DAD_SLAB 32
+#define DAD_HT (DAD_H / 32)      // 32-wide h tiles
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int dad_nchunk(int T) { return (T + DAD_SLAB - 1) / DAD_SLAB; }
+
+// ---------------------------------------------------------------------------------
+// Counter-based RNG (production mode).  Each random value is a pure function of
+// (seed, step counter, stream, element index), so the weight-gradient kernel can
+// regenerate the strong augmentation instead of storing it.  Per value: the
+// "lowbias32" integer mixer (two 32-bit multiplies) with the 32-bit stream key
+// injected between its two rounds, so different streams are different bijections of
+// the element index (not shifted copies of one sequence).  The stream key is derived
+// on the host from (seed, counter, stream) with splitmix64 (dad_stream_key).
+// Philox4x32-10 costs ~40 quarter-rate multiplies per 4 outputs, which made the
+// augmentation VALU-bound ("RNG").
+enum DadStream {
+  DAD_RNG_WEAK = 1,      // teacher weak-aug noise      (I/utils.py:330)
+  DAD_RNG_STRONG = 2,    // student strong-aug noise    (I/utils.py:338)
+  DAD_RNG_FEAT = 3,      // feature-dropout uniforms    (I/utils.py:343)
+  DAD_RNG_TSTART = 4,    // temporal mask start         (I/utils.py:370)
+  DAD_RNG_DROP1 = 5,     // classifier dropout, clean   (I/train.py:400)
+  DAD_RNG_DROP2 = 6,     // classifier dropout, strong  (I/train.py:440)
+};
+
+__host__ __device__ __forceinline__ uint32_t dad_rng32(uint32_t i, uint32_t key) {
+  uint32_t x = i;
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= key;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+static inline uint32_t dad_stream_key(uint64_t seed, uint64_t counter, uint32_t stream) {
+  uint64_t z = seed * 0x9E3779B97F4A7C15ull + counter * 0xD1B54A32D192ED03ull + (uint64_t)stream * 0xABC98388FB8FAC03ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (uint32_t)(z ^ (z >> 32));
+}
+
+// uniform in (0, 1]  (24-bit resolution)
+__device__ __forceinline__ float dad_u01_open0(uint32_t h) {
+  return (float)((h >> 8) + 1u) * (1.0f / 16777216.0f);
+}
+// uniform in [0, 1)
+__device__ __forceinline__ float dad_u01(uint32_t h) { return (float)(h >> 8) * (1.0f / 16777216.0f); }
+
+// Two standard normals from two hashes (Box-Muller; v_log/v_sqrt/v_sin/v_cos).
+__device__ __forceinline__ void dad_box_muller(uint32_t h0, uint32_t h1, float& z0, float& z1) {
+  float u1 = dad_u01_open0(h0);
+  float u2 = dad_u01(h1);
+  float r = __builtin_amdgcn_sqrtf(-1.38629436112f * __builtin_amdgcn_logf(u1));  // -2 ln u1
+  z0 = r * __builtin_amdgcn_cosf(u2);   // v_cos_f32 takes revolutions: cos(2*pi*u2)
+  z1 = r * __builtin_amdgcn_sinf(u2);
+}
+
+// 4 normals for elements (row, d..d+3) of a [rows][768] tensor in stream `key`.
+__device__ __forceinline__ f32x4 dad_normal4(uint32_t key, uint32_t row, uint32_t d) {
+  uint32_t i = row * (uint32_t)DAD_D + d;
+  f32x4 z;
+  float a, b, c, e;
+  dad_box_muller(dad_rng32(i, key), dad_rng32(i + 1u, key), a, b);
+  dad_box_muller(dad_rng32(i + 2u, key), dad_rng32(i + 3u, key), c, e);
+  z[0] = a; z[1] = b; z[2] = c; z[3] = e;
+  return z;
+}
+
+__device__ __forceinline__ float dad_uniform_at(uint32_t key, uint32_t idx) {
+  return dad_u01(dad_rng32(idx, key));
+}
+
+// ---------------------------------------------------------------------------------
+// wave helpers (wave64)
+__device__ __forceinline__ float dad_wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double dad_wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float dad_wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Row index inside a 32x32 MFMA accumulator tile for (register r, lane half kh):
+// C/D layout of v_mfma_f32_32x32x{2f32,16bf16}: col = lane&31, row = (r&3)+8*(r>>2)+4*(lane>>5).
+__device__ __forceinline__ int dad_acc_row(int r, int kh) { return (r & 3) + 8 * (r >> 2) + 4 * kh; }
+
+// ---------------------------------------------------------------------------------
+// Batch geometry: the clean and noisy batches are collated independently by the reference
+// (I/train.py:479-483), so their utterance counts and padded lengths differ in general.
+struct DadGeom {
+  int Bc, Tc, ncc, tpc;   // clean: utterances, frames, 32-row slabs per utterance, padded frames
+  int Bn, Tn, ncn, tpn;   // noisy (Bn = 0 during warm-up when no noisy batch is used)
+};
+
+static inline __host__ __device__ DadGeom dad_geom(int Bc, int Tc, int Bn, int Tn) {
+  DadGeom g;
+  g.Bc = Bc; g.Tc = Tc; g.ncc = (Tc + DAD_SLAB - 1) / DAD_SLAB; g.tpc = g.ncc * DAD_SLAB;
+  g.Bn = Bn; g.Tn = Tn > 0 ? Tn : 1; g.ncn = (g.Tn + DAD_SLAB - 1) / DAD_SLAB; g.tpn = g.ncn * DAD_SLAB;
+  return g;
+}
+
+// Workspace layout (bytes), shared by host and device.  All offsets 256-B aligned.
+//   slab-indexed buffers: clean slabs [0, Bc*ncc), noisy slabs after them.
+struct DadWs {
+  size_t part_sum;   // f32 [Bc*ncc + 2*Bn*ncn][H]  per-slab pooled ReLU sums (clean | teacher-weak | strong)
+  size_t part_cnt;   // f32 [Bc*ncc + Bn*ncn][H]    per-slab active-row counts (clean | strong)
+  size_t bits;       // u32 [Bc*tpc + Bn*tpn][8]    ReLU' & valid bits per row and 32-wide h tile
+  size_t vlen;       // f32 [Bc + Bn]               valid lengths (clean | noisy)
+  size_t ge;         // f32 [Bc + Bn][H]            dL/de_clean | dL/de_strong
+  size_t wpart;      // f32 [S][H][D]               split-K weight-gradient partial slabs
+  size_t normpart;   // f32 [DAD_NORM_BLOCKS]       squared-norm partials
+  size_t ecda;       // f32 [C][Bc+Bn][Bc+Bn]       ECDA pairwise scratch for large member sets
+  size_t xs_bf16;    // bf16 [Bn][Tn][768]          BF16 mode: strong-augmented input (wgrad operand)
+  size_t w1bf;       // bf16 [H][D]                 modular encoder ops: bf16 copy of W1
+  size_t gflat;      // f32 [DAD_GRAD_FLOATS]       modular encoder backward: scratch grad vector
+  size_t bytes;
+  int splits;
+};
+
+static inline size_t dad_align(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// weight-gradient split-K factor: enough workgroups to cover the chip (6 column blocks
+// per split), bounded by the number of 32-row slabs.
+static inline int dad_auto_splits(const DadGeom& g, int precision, int warmup) {
+  const int total = g.Bc * g.ncc + (warmup ? 0 : g.Bn * g.ncn);
+  const int target = precision == DAD_PREC_BF16 ? 43 : 64;
+  return total < target ? total : target;
+}
+
+static inline DadWs dad_ws_layout(const DadGeom& g, int splits, int precision) {
+  DadWs w;
+  const size_t nsc = (size_t)g.Bc * g.ncc, nsn = (size_t)g.Bn * g.ncn;
+  const size_t nb = (size_t)g.Bc + g.Bn;
+  size_t off = 0;
+  w.splits = splits;
+  w.part_sum = off; off = dad_align(off + sizeof(float) * (nsc + 2 * nsn) * DAD_H);
+  w.part_cnt = off; off = dad_align(off + sizeof(float) * (nsc + nsn) * DAD_H);
+  w.bits = off;     off = dad_align(off + sizeof(uint32_t) * ((size_t)g.Bc * g.tpc + (size_t)g.Bn * g.tpn) * DAD_HT);
+  w.vlen = off;     off = dad_align(off + sizeof(float) * nb);
+  w.ge = off;       off = dad_align(off + sizeof(float) * nb * DAD_H);
+  w.wpart = off;    off = dad_align(off + sizeof(float) * (size_t)splits * DAD_H * DAD_D);
+  w.normpart = off; off = dad_align(off + sizeof(float) * DAD_NORM_BLOCKS);
+  w.ecda = off;     off = dad_align(off + sizeof(float) * DAD_C * nb * nb);
+  w.xs_bf16 = off;  off = dad_align(off + (precision == DAD_PREC_BF16 ? 2 * (size_t)g.Bn * g.Tn * DAD_D : 0));
+  w.w1bf = off;     off = dad_align(off + 2 * (size_t)DAD_H * DAD_D);
+  w.gflat = off;    off = dad_align(off + sizeof(float) * DAD_GRAD_FLOATS);
+  w.bytes = off;
+  return w;
+}

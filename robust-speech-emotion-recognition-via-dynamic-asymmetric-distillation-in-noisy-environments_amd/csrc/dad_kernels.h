@@ -1,0 +1,101 @@
+// Kernel argument blocks and entry points (internal to libdad_hip.so).
+#pragma once
+#include "dad_common.h"
+
+struct DadEncodeArgs {
+  DadGeom g;
+  int warmup, mask_len, start_hi;
+  const float* xc; const uint8_t* mc;
+  const float* xn; const uint8_t* mn;
+  const float* w1_student; const float* b1_student;
+  const float* w1_teacher; const float* b1_teacher;
+  const __bf16* w1bf_student; const __bf16* w1bf_teacher;
+  // explicit draws (parity mode) or NULL -> counter RNG
+  const float* nw; const float* ns; const float* u; const int64_t* start;
+  uint32_t key_weak, key_strong, key_feat, key_tstart;
+  float weak_std, strong_std, feat_p;
+  float* part_sum; float* part_cnt; uint32_t* bits;
+  __bf16* xs_bf16;          // BF16 mode: strong-augmented input as fed to the MFMA (for wgrad)
+};
+
+struct DadPoolArgs {
+  DadGeom g;
+  int warmup;
+  const uint8_t* mc; const uint8_t* mn;
+  const float* part_sum;
+  const float* student; const float* teacher;     // flat params (W2/b2 used)
+  const uint8_t* keep1; const uint8_t* keep2;     // explicit dropout masks or NULL
+  uint32_t key_drop1, key_drop2;
+  float p_drop, drop_scale;
+  float* emb; float* vlen; float* logits;
+};
+
+struct DadTailArgs {
+  dad_config cfg;
+  const int64_t* yc;
+  const float* logits; const float* emb;
+  const float* student;
+  const uint8_t* keep1; const uint8_t* keep2;
+  uint32_t key_drop1, key_drop2;
+  float* dacp;            // persistent DACP state (read; committed by the optimizer kernel)
+  float* tailf;           // per-step outputs (see DAD_TAIL_* in dad.h)
+  float* ge;              // [Bc+Bn][H] dL/de
+  float* grad;            // flat grads (W2, b2 written here) + extras
+};
+
+struct DadEcdaArgs {
+  dad_config cfg;
+  const int64_t* yc;
+  const float* emb;
+  const float* tailf;
+  float* tail_terms;      // per-class loss terms
+  float* ge;
+  float* scratch;         // global fallback for large member sets
+};
+
+struct DadWgradArgs {
+  DadGeom g;
+  int warmup, splits, mask_len, start_hi;
+  const float* xc; const float* xn;
+  const float* ns; const float* u; const int64_t* start;
+  uint32_t key_strong, key_feat, key_tstart;
+  float strong_std, feat_p;
+  const uint32_t* bits; const float* ge; const float* vlen;
+  const __bf16* xs_bf16;
+  float* wpart;
+};
+
+struct DadReduceArgs {
+  DadGeom g;
+  int splits, warmup, want_norm;
+  float w_kl, w_ecda;
+  const float* wpart; const float* ge; const float* vlen; const float* part_cnt;
+  const float* tailf;
+  float* grad; float* normpart;
+};
+
+struct DadOptimArgs {
+  dad_config cfg;
+  float* student; float* teacher; float* exp_avg; float* exp_avg_sq;
+  float* grad; __bf16* w1bf_student; __bf16* w1bf_teacher;
+  float* dacp; float* tailf; const float* normpart; int nnorm;
+};
+
+__global__ void dad_encode_f32(DadEncodeArgs a);
+__global__ void dad_encode_bf16(DadEncodeArgs a);
+__global__ void dad_pool(DadPoolArgs a);
+__global__ void dad_tail(DadTailArgs a);
+__global__ void dad_ecda(DadEcdaArgs a);
+__global__ void dad_wgrad_f32(DadWgradArgs a);
+__global__ void dad_wgrad_bf16(DadWgradArgs a);
+__global__ void dad_reduce(DadReduceArgs a);
+__global__ void dad_norm(float* grad, float* normpart, float inv_world);
+__global__ void dad_optim(DadOptimArgs a);
+__global__ void dad_epoch_end_kernel(float* dacp, float beta, float one_m_beta);
+__global__ void dad_shadow_kernel(const float* student, const float* teacher, __bf16* ws, __bf16* wt);
+
+// offsets inside the flat parameter vector [W1 | b1 | W2 | b2]
+#define DAD_OFF_W1 0
+#define DAD_OFF_B1 (DAD_H * DAD_D)
+#define DAD_OFF_W2 (DAD_OFF_B1 + DAD_H)
+#define DAD_OFF_B2 (DAD_OFF_W2 + DAD_C * DAD_H)

@@ -1,0 +1,285 @@
+// Fused encoder forward for the DAD step (one launch covers all three encoder passes).
+//
+// Replaces, per step (I/train.py:399,406-410,439):
+//   student_encoder(clean)                         Emotion2VecEncoder.forward, I/model.py:18-41
+//   teacher_encoder(weak_augment(noisy))           + DataAugmentation.weak_augment, I/utils.py:328-331
+//   student_encoder(strong_augment(noisy))         + strong_augment/_apply_temporal_masking, I/utils.py:333-375
+//
+// Work unit = one wave = one 32-row slab (utterance b, frames 32c..32c+31) x all 256 hidden
+// units.  A noisy slab is read from HBM once and feeds BOTH the teacher (weak aug, teacher W1)
+// and the student (strong aug, student W1) GEMMs.  The epilogue adds the bias, applies ReLU
+// and the padding mask and reduces over the slab's frames, so the [B,T,256] activation never
+// reaches HBM; it emits per-slab pooled sums, per-slab active counts (for d b1) and the
+// ReLU'-and-valid bit mask the weight-gradient kernel consumes.
+//
+// Precision modes:  FP32 -> v_mfma_f32_32x32x2_f32 (exact f32 FMA chain; parity mode)
+//                   BF16 -> v_mfma_f32_32x32x16_bf16 on the augmented tile rounded to bf16
+//                           and the bf16 shadow of W1 (fp32 accumulate; throughput mode)
+#include "dad_common.h"
+#include "dad_kernels.h"
+
+namespace {
+
+struct EncodeGeom {
+  int b, c, noisy, T, nc;
+  size_t sum_slab;     // slab index into part_sum for the (first) branch of this wave
+  size_t row0;         // global row of frame 0 of this utterance ([b][T] layout)
+};
+
+// waves [0, Bn*ncn) are noisy slabs (when not warming up), the rest clean slabs
+__device__ __forceinline__ EncodeGeom encode_geom(const DadEncodeArgs& a, int wid) {
+  EncodeGeom e;
+  const DadGeom& g = a.g;
+  const int nnoisy = a.warmup ? 0 : g.Bn * g.ncn;
+  e.noisy = wid < nnoisy;
+  const int slab = e.noisy ? wid : wid - nnoisy;
+  e.nc = e.noisy ? g.ncn : g.ncc;
+  e.T = e.noisy ? g.Tn : g.Tc;
+  e.b = slab / e.nc;
+  e.c = slab - e.b * e.nc;
+  e.sum_slab = e.noisy ? (size_t)g.Bc * g.ncc + slab : (size_t)slab;
+  e.row0 = (size_t)e.b * e.T;
+  return e;
+}
+
+// Temporal-mask start for utterance b (I/utils.py:370: randint(0, max(1, Tmax-mlen+1))).
+__device__ __forceinline__ int tmask_start(const DadEncodeArgs& a, int b) {
+  if (a.start) return (int)a.start[b];
+  uint32_t h = dad_rng32((uint32_t)b, a.key_tstart);
+  return (int)(((uint64_t)h * (uint64_t)a.start_hi) >> 32);
+}
+
+// Feature-dropout keep flag for channel d (I/utils.py:343: rand(D) > dropout_rate).
+__device__ __forceinline__ float feat_keep(const DadEncodeArgs& a, int d) {
+  float u = a.u ? a.u[d] : dad_uniform_at(a.key_feat, (uint32_t)d);
+  return u > a.feat_p ? 1.0f : 0.0f;
+}
+
+__device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+
+// Augment 4 consecutive channels d..d+3 of row (b, t): weak and strong variants.
+// Op order mirrors the reference: noise*std then add; *feature mask; temporal zero.
+__device__ __forceinline__ void augment4(const DadEncodeArgs& a, f32x4 x, int grow, int d, bool tzero,
+                                         f32x4& xw, f32x4& xs) {
+  f32x4 nw, ns;
+  if (a.nw) {
+    nw = ld4(a.nw + (size_t)grow * DAD_D + d);
+    ns = ld4(a.ns + (size_t)grow * DAD_D + d);
+  } else {
+    nw = dad_normal4(a.key_weak, (uint32_t)grow, (uint32_t)d);
+    ns = dad_normal4(a.key_strong, (uint32_t)grow, (uint32_t)d);
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float w = nw[e] * a.weak_std;
+    xw[e] = x[e] + w;
+    float s = ns[e] * a.strong_std;
+    float v = (x[e] + s) * feat_keep(a, d + e);
+    xs[e] = tzero ? 0.0f : v;
+  }
+}
+
+// Pool one 32x256 accumulator set: bias + ReLU + padding mask + sum over the slab rows.
+// sum_slab / cnt_slab index part_sum / part_cnt; bits_row (< 0: no bits) is the first
+// row of this slab in the bits buffer.
+__device__ __forceinline__ void encode_epilogue(const DadEncodeArgs& a, const f32x16* acc, const float* bias,
+                                                size_t sum_slab, long cnt_slab, long bits_row, uint32_t vbits,
+                                                uint32_t* lds_bits) {
+  const int lane = threadIdx.x & 63;
+  const int j = lane & 31, kh = lane >> 5;
+  const bool want_bits = bits_row >= 0;
+#pragma unroll
+  for (int ht = 0; ht < DAD_HT; ++ht) {
+    const int h = ht * 32 + j;
+    const float bh = bias[h];
+    float s = 0.0f, n = 0.0f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = dad_acc_row(r, kh);
+      const bool v = (vbits >> row) & 1u;
+      const float pre = acc[ht][r] + bh;
+      const bool act = v && pre > 0.0f;
+      s += act ? pre : 0.0f;
+      n += act ? 1.0f : 0.0f;
+      if (want_bits) {
+        const uint64_t m = __ballot(act);
+        if (lane == 0) {
+          const int row0 = dad_acc_row(r, 0);
+          lds_bits[row0 * DAD_HT + ht] = (uint32_t)m;
+          lds_bits[(row0 + 4) * DAD_HT + ht] = (uint32_t)(m >> 32);
+        }
+      }
+    }
+    s += __shfl_xor(s, 32, 64);
+    n += __shfl_xor(n, 32, 64);
+    if (kh == 0) {
+      a.part_sum[sum_slab * DAD_H + h] = s;
+      if (cnt_slab >= 0) a.part_cnt[(size_t)cnt_slab * DAD_H + h] = n;
+    }
+  }
+  if (want_bits) {
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): lane 0's LDS writes landed
+    __builtin_amdgcn_wave_barrier();
+    // 32 rows x 8 words = 1 KB per slab, stored contiguously: 16 B per lane
+    const uint4 w = reinterpret_cast<const uint4*>(lds_bits)[lane];
+    reinterpret_cast<uint4*>(a.bits + (size_t)bits_row * DAD_HT)[lane] = w;
+  }
+}
+
+// epilogues of one wave: clean -> (clean sums, clean counts, clean bits);
+// noisy -> teacher sums (no grads), then strong sums/counts/bits
+__device__ __forceinline__ void encode_finish(const DadEncodeArgs& a, const EncodeGeom& e, const f32x16* acc0,
+                                              const f32x16* acc1, uint32_t vbits, uint32_t* lb) {
+  const DadGeom& g = a.g;
+  if (!e.noisy) {
+    encode_epilogue(a, acc0, a.b1_student, e.sum_slab, (long)e.sum_slab,
+                    (long)e.b * g.tpc + (long)e.c * DAD_SLAB, vbits, lb);
+  } else {
+    const size_t nslab_n = (size_t)g.Bn * g.ncn;
+    const size_t local = e.sum_slab - (size_t)g.Bc * g.ncc;
+    encode_epilogue(a, acc0, a.b1_teacher, e.sum_slab, -1, -1, vbits, lb);
+    encode_epilogue(a, acc1, a.b1_student, e.sum_slab + nslab_n, (long)((size_t)g.Bc * g.ncc + local),
+                    (long)g.Bc * g.tpc + (long)e.b * g.tpn + (long)e.c * DAD_SLAB, vbits, lb);
+  }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------- FP32 (parity mode)
+__global__ __launch_bounds__(256) void dad_encode_f32(DadEncodeArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds_bits_all[4][DAD_SLAB * DAD_HT];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int wid = blockIdx.x * 4 + wv;
+  if (wid >= (a.warmup ? 0 : a.g.Bn * a.g.ncn) + a.g.Bc * a.g.ncc) return;
+  const EncodeGeom g = encode_geom(a, wid);
+  const int i = lane & 31, kh = lane >> 5;
+  const int t = g.c * DAD_SLAB + i;
+  const bool tin = t < g.T;
+  const int grow = (int)g.row0 + (tin ? t : 0);
+  const uint8_t* pad = g.noisy ? a.mn : a.mc;
+  const bool valid = tin && pad[g.row0 + t] == 0;
+  const uint32_t vbits = (uint32_t)__ballot(valid);
+  const float* X = (g.noisy ? a.xn : a.xc) + (size_t)grow * DAD_D;
+  bool tzero = false;
+  if (g.noisy && a.mask_len > 0) {
+    const int st = tmask_start(a, g.b);
+    tzero = t >= st && t < st + a.mask_len;
+  }
+  // B operands: student W1 (clean + strong), teacher W1 (weak)
+  const float* Ws = a.w1_student + (size_t)i * DAD_D + 4 * kh;
+  const float* Wt = a.w1_teacher + (size_t)i * DAD_D + 4 * kh;
+
+  f32x16 acc0[DAD_HT], acc1[DAD_HT];
+#pragma unroll
+  for (int ht = 0; ht < DAD_HT; ++ht) {
+    acc0[ht] = f32x16{};
+    acc1[ht] = f32x16{};
+  }
+  // k ordering: step (d0, e, kh) uses channel d0 + 4*kh + e for BOTH operands
+  if (!g.noisy) {
+    for (int d0 = 0; d0 < DAD_D; d0 += 8) {
+      const f32x4 x = tin ? ld4(X + d0 + 4 * kh) : f32x4{};
+#pragma unroll
+      for (int ht = 0; ht < DAD_HT; ++ht) {
+        const f32x4 w = ld4(Ws + (size_t)ht * 32 * DAD_D + d0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc0[ht] = __builtin_amdgcn_mfma_f32_32x32x2f32(x[e], w[e], acc0[ht], 0, 0, 0);
+      }
+    }
+  } else {
+    for (int d0 = 0; d0 < DAD_D; d0 += 8) {
+      const int d = d0 + 4 * kh;
+      const f32x4 x = tin ? ld4(X + d) : f32x4{};
+      f32x4 xw, xs;
+      augment4(a, x, grow, d, tzero, xw, xs);
+#pragma unroll
+      for (int ht = 0; ht < DAD_HT; ++ht) {
+        const f32x4 wt = ld4(Wt + (size_t)ht * 32 * DAD_D + d0);
+        const f32x4 ws = ld4(Ws + (size_t)ht * 32 * DAD_D + d0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          acc0[ht] = __builtin_amdgcn_mfma_f32_32x32x2f32(xw[e], wt[e], acc0[ht], 0, 0, 0);
+          acc1[ht] = __builtin_amdgcn_mfma_f32_32x32x2f32(xs[e], ws[e], acc1[ht], 0, 0, 0);
+        }
+      }
+    }
+  }
+  encode_finish(a, g, acc0, acc1, vbits, lds_bits_all[wv]);
+}
+
+// ------------------------------------------------------------ BF16 (throughput mode)
+__device__ __forceinline__ bf16x8 to_bf16x8(f32x4 lo, f32x4 hi) {
+  bf16x8 r;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    r[e] = (__bf16)lo[e];
+    r[e + 4] = (__bf16)hi[e];
+  }
+  return r;
+}
+
+__global__ __launch_bounds__(256) void dad_encode_bf16(DadEncodeArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds_bits_all[4][DAD_SLAB * DAD_HT];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int wid = blockIdx.x * 4 + wv;
+  if (wid >= (a.warmup ? 0 : a.g.Bn * a.g.ncn) + a.g.Bc * a.g.ncc) return;
+  const EncodeGeom g = encode_geom(a, wid);
+  const int i = lane & 31, kh = lane >> 5;
+  const int t = g.c * DAD_SLAB + i;
+  const bool tin = t < g.T;
+  const int grow = (int)g.row0 + (tin ? t : 0);
+  const uint8_t* pad = g.noisy ? a.mn : a.mc;
+  const bool valid = tin && pad[g.row0 + t] == 0;
+  const uint32_t vbits = (uint32_t)__ballot(valid);
+  const float* X = (g.noisy ? a.xn : a.xc) + (size_t)grow * DAD_D + 8 * kh;
+  bool tzero = false;
+  if (g.noisy && a.mask_len > 0) {
+    const int st = tmask_start(a, g.b);
+    tzero = t >= st && t < st + a.mask_len;
+  }
+  // bf16 fragments: lane (row/col i, half kh) holds k = 8*kh .. 8*kh+7 of the 16-deep step
+  const bf16x8* Ws = reinterpret_cast<const bf16x8*>(a.w1bf_student + (size_t)i * DAD_D + 8 * kh);
+  const bf16x8* Wt = reinterpret_cast<const bf16x8*>(a.w1bf_teacher + (size_t)i * DAD_D + 8 * kh);
+  constexpr int HT_STRIDE = 32 * DAD_D / 8;   // bf16x8 elements between h tiles
+  f32x16 acc0[DAD_HT], acc1[DAD_HT];
+#pragma unroll
+  for (int ht = 0; ht < DAD_HT; ++ht) {
+    acc0[ht] = f32x16{};
+    acc1[ht] = f32x16{};
+  }
+  if (!g.noisy) {
+    for (int d0 = 0; d0 < DAD_D; d0 += 16) {
+      f32x4 lo = tin ? ld4(X + d0) : f32x4{};
+      f32x4 hi = tin ? ld4(X + d0 + 4) : f32x4{};
+      const bf16x8 xa = to_bf16x8(lo, hi);
+#pragma unroll
+      for (int ht = 0; ht < DAD_HT; ++ht) {
+        const bf16x8 w = Ws[ht * HT_STRIDE + d0 / 8];
+        acc0[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa, w, acc0[ht], 0, 0, 0);
+      }
+    }
+  } else {
+    for (int d0 = 0; d0 < DAD_D; d0 += 16) {
+      const int d = d0 + 8 * kh;
+      f32x4 lo = tin ? ld4(X + d0) : f32x4{};
+      f32x4 hi = tin ? ld4(X + d0 + 4) : f32x4{};
+      f32x4 wlo, whi, slo, shi;
+      augment4(a, lo, grow, d, tzero, wlo, slo);
+      augment4(a, hi, grow, d + 4, tzero, whi, shi);
+      const bf16x8 xw = to_bf16x8(wlo, whi);
+      const bf16x8 xs = to_bf16x8(slo, shi);
+      if (tin) *reinterpret_cast<bf16x8*>(a.xs_bf16 + (size_t)grow * DAD_D + d) = xs;
+#pragma unroll
+      for (int ht = 0; ht < DAD_HT; ++ht) {
+        const bf16x8 wt = Wt[ht * HT_STRIDE + d0 / 8];
+        const bf16x8 ws = Ws[ht * HT_STRIDE + d0 / 8];
+        acc0[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xw, wt, acc0[ht], 0, 0, 0);
+        acc1[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xs, ws, acc1[ht], 0, 0, 0);
+      }
+    }
+  }
+  encode_finish(a, g, acc0, acc1, vbits, lds_bits_all[wv]);
+}

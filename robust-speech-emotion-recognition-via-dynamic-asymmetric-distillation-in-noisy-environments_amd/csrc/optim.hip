@@ -1,0 +1,109 @@
+// Parameter update: global-norm clip + Adam (L2 weight decay) + teacher EMA + DACP commit.
+//
+//   torch.nn.utils.clip_grad_norm_(model.parameters(), MAX_GRAD_NORM)   I/train.py:487-488
+//   optim.Adam(weight_decay=1e-5).step()  (single-tensor algorithm)       I/train.py:362,489
+//   SSRLModel.update_teacher_ema()         (post-warm-up only)           I/model.py:211-223
+//   DACPManager state: ema_thresholds EMA + epoch score collection        I/utils.py:485-505
+//
+// One elementwise pass over the flat [W1|b1|W2|b2] vectors; every block re-derives the
+// clip coefficient from the same squared-norm partials in the same order, so the result
+// is identical across blocks (and across data-parallel ranks).  The bf16 shadows of W1
+// used by the BF16 forward are refreshed in the same pass.
+#include "dad_common.h"
+#include "dad_kernels.h"
+
+__global__ __launch_bounds__(256) void dad_optim(DadOptimArgs a) {
+  __shared__ float coef_s;
+  const dad_config& cfg = a.cfg;
+  const int tid = threadIdx.x;
+  if (tid < 64) {
+    double s = 0.0;
+    for (int k = tid; k < a.nnorm; k += 64) s += (double)a.normpart[k];
+    s = dad_wave_sum_d(s);
+    if (tid == 0) {
+      const float norm = (float)sqrt(s);
+      float coef = 1.0f;
+      if (cfg.clip) coef = fminf(cfg.max_norm / (norm + 1e-6f), 1.0f);
+      coef_s = coef;
+      if (blockIdx.x == 0) {
+        a.tailf[DAD_T_CLIPNORM] = norm;
+        a.tailf[DAD_T_CLIPCOEF] = coef;
+        const float* ex = a.grad + DAD_NPARAM;
+        a.tailf[DAD_T_TOTAL] = ex[12];
+      }
+    }
+  }
+  // DACP state commit (thresholds were computed against the pre-step state by dad_tail;
+  // with data parallelism the floored thresholds are the rank mean)
+  if (blockIdx.x == 0 && tid < DAD_C && !cfg.warmup && cfg.use_dacp) {
+    const float* ex = a.grad + DAD_NPARAM;
+    float* d = a.dacp;
+    d[tid] = cfg.dacp_alpha * d[tid] + cfg.dacp_one_m_alpha * ex[tid];
+    d[8 + tid] += ex[4 + tid];
+    d[12 + tid] += ex[8 + tid];
+  }
+  __syncthreads();
+  const float coef = coef_s;
+  const size_t n0 = (size_t)blockIdx.x * 1024;
+  for (int k = 0; k < 4; ++k) {
+    const size_t i = n0 + (size_t)k * 256 + tid;
+    if (i >= DAD_NPARAM) break;
+    float g = a.grad[i] * coef;
+    float p = a.student[i];
+    g = g + cfg.weight_decay * p;                               // grad.add(param, alpha=wd)
+    float m = a.exp_avg[i];
+    m = m + cfg.one_m_beta1 * (g - m);                          // exp_avg.lerp_(grad, 1-beta1)
+    float v = a.exp_avg_sq[i];
+    v = v * cfg.beta2 + cfg.one_m_beta2 * g * g;                // mul_(beta2).addcmul_(g, g, 1-beta2)
+    const float denom = sqrtf(v) / cfg.bc2_sqrt + cfg.adam_eps;
+    p = p + (-cfg.lr_step_size) * (m / denom);                  // addcdiv_(m, denom, -step_size)
+    a.exp_avg[i] = m;
+    a.exp_avg_sq[i] = v;
+    a.student[i] = p;
+    float t = a.teacher[i];
+    if (!cfg.warmup) {
+      t = t * cfg.ema_m + p * cfg.ema_one_m;
+      a.teacher[i] = t;
+    }
+    if (i < (size_t)DAD_H * DAD_D) {
+      a.w1bf_student[i] = (__bf16)p;
+      a.w1bf_teacher[i] = (__bf16)t;
+    }
+  }
+}
+
+// DACPManager.update_class_quality_scores_epoch (I/utils.py:430-447)
+__global__ void dad_epoch_end_kernel(float* dacp, float beta, float one_m_beta) {
+  const int c = threadIdx.x;
+  if (c >= DAD_C) return;
+  const float n = dacp[12 + c];
+  const float cur = n > 0.0f ? dacp[8 + c] / n : dacp[4 + c];
+  dacp[4 + c] = beta * dacp[4 + c] + one_m_beta * cur;
+  dacp[8 + c] = 0.0f;
+  dacp[12 + c] = 0.0f;
+}
+
+__global__ __launch_bounds__(256) void dad_shadow_kernel(const float* student, const float* teacher, __bf16* ws,
+                                                         __bf16* wt) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < (size_t)DAD_H * DAD_D) {
+    ws[i] = (__bf16)student[i];
+    wt[i] = (__bf16)teacher[i];
+  }
+}
+
+__global__ __launch_bounds__(256) void dad_ema_kernel(const float* student, float* teacher, size_t n, float m,
+                                                      float one_m) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) teacher[i] = teacher[i] * m + student[i] * one_m;
+}
+
+extern "C" int dad_teacher_ema(const float* student, float* teacher, size_t n, float ema_m, float ema_one_m,
+                               void* stream) {
+  if (!student || !teacher) return DAD_E_ARG;
+  if (n == 0) return DAD_OK;
+  hipLaunchKernelGGL(dad_ema_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, student,
+                     teacher, n, ema_m, ema_one_m);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? DAD_OK : (int)e;
+}

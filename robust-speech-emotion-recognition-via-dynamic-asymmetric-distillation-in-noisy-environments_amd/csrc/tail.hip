@@ -1,0 +1,611 @@
+// The small "tail" of the DAD step: pooling finalisation + classifier forward, the losses,
+// the DACP mask and the analytic backward down to dL/de (the per-utterance embedding grads).
+//
+//   dad_pool  (grid B)   : e = sum(slab partials)/max(1,len)       I/model.py:35-36
+//                          logits = W2 (dropout(e)) + b2            I/model.py:54-64
+//   dad_tail  (1 block)  : CE(label smoothing), softmax, certainty, DACP thresholds and
+//                          mask, masked KL, classifier backward     I/train.py:397-471,
+//                                                                   I/utils.py:400-507
+//   dad_ecda  (grid C)   : ECDALoss forward + backward, one workgroup per class
+//                                                                   I/utils.py:510-652
+//
+// Numerics: float32 with torch's op order where the result feeds a discrete decision
+// (softmax -> certainty -> quantile -> EMA threshold -> mask); double accumulators for
+// the batch sums.  The per-class set sizes are data dependent; everything is decided on
+// device (no host sync), so the step is graph-capturable.
+#include "dad_common.h"
+#include "dad_kernels.h"
+
+#define TAIL_THREADS 256
+
+__device__ __forceinline__ float block_sum_f(float v, float* red) {
+  v = dad_wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  float s = 0.0f;
+  const int nw = blockDim.x >> 6;
+  for (int k = 0; k < nw; ++k) s += red[k];
+  return s;
+}
+
+__device__ __forceinline__ double block_sum_d(double v, double* red) {
+  v = dad_wave_sum_d(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  double s = 0.0;
+  const int nw = blockDim.x >> 6;
+  for (int k = 0; k < nw; ++k) s += red[k];
+  return s;
+}
+
+__device__ __forceinline__ float keep_value(const uint8_t* keep, uint32_t key, int b, int h, float p, float scale) {
+  if (p <= 0.0f) return 1.0f;
+  bool k;
+  if (keep) k = keep[(size_t)b * DAD_H + h] != 0;
+  else k = dad_uniform_at(key, (uint32_t)(b * DAD_H + h)) >= p;
+  return k ? scale : 0.0f;
+}
+
+// ------------------------------------------------------------------------------ pool
+// blocks [0, Bc): clean utterances; blocks [Bc, Bc+Bn): noisy utterances (teacher + strong)
+__global__ __launch_bounds__(256) void dad_pool(DadPoolArgs a) {
+  __shared__ float red[8];
+  __shared__ float zred[8][4];
+  const DadGeom& g = a.g;
+  const int blk = blockIdx.x, h = threadIdx.x;
+  const int w = h >> 6, l = h & 63;
+  const bool noisy = blk >= g.Bc;
+  const int b = noisy ? blk - g.Bc : blk;
+  const int T = noisy ? g.Tn : g.Tc;
+  const uint8_t* pad = noisy ? a.mn : a.mc;
+  // valid length (I/model.py:35: (1-mask).sum(dim=1))
+  float len = 0.0f;
+  for (int t = h; t < T; t += 256) len += pad[(size_t)b * T + t] == 0 ? 1.0f : 0.0f;
+  len = block_sum_f(len, red);
+  if (h == 0) a.vlen[blk] = len;
+  const float* W2s = a.student + DAD_OFF_W2;
+  const float* b2s = a.student + DAD_OFF_B2;
+  const float* W2t = a.teacher + DAD_OFF_W2;
+  const float* b2t = a.teacher + DAD_OFF_B2;
+  const size_t nsc = (size_t)g.Bc * g.ncc, nsn = (size_t)g.Bn * g.ncn;
+  const int nbr = noisy ? 2 : 1;
+  float zp[2][4];
+  for (int k = 0; k < nbr; ++k) {
+    // part_sum slab base and embedding row of this (branch, utterance)
+    size_t slab0;
+    int nc, erow;
+    if (!noisy) { slab0 = (size_t)b * g.ncc; nc = g.ncc; erow = b; }
+    else if (k == 0) { slab0 = nsc + (size_t)b * g.ncn; nc = g.ncn; erow = g.Bc + b; }              // teacher
+    else { slab0 = nsc + nsn + (size_t)b * g.ncn; nc = g.ncn; erow = g.Bc + g.Bn + b; }           // strong
+    float s = 0.0f;
+    for (int c = 0; c < nc; ++c) s += a.part_sum[(slab0 + c) * DAD_H + h];
+    const float e = s / fmaxf(len, 1.0f);
+    a.emb[(size_t)erow * DAD_H + h] = e;
+    float d;
+    const bool teacher = noisy && k == 0;
+    if (!noisy) d = e * keep_value(a.keep1, a.key_drop1, b, h, a.p_drop, a.drop_scale);
+    else if (!teacher) d = e * keep_value(a.keep2, a.key_drop2, b, h, a.p_drop, a.drop_scale);
+    else d = e;   // teacher classifier: dropout p = 0 (I/model.py:121)
+    const float* W2 = teacher ? W2t : W2s;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) zp[k][c] = dad_wave_sum(W2[c * DAD_H + h] * d);
+  }
+  if (l == 0)
+    for (int k = 0; k < nbr; ++k)
+      for (int c = 0; c < 4; ++c) zred[k * 4 + c][w] = zp[k][c];
+  __syncthreads();
+  if (h < nbr * 4) {
+    const int k = h >> 2, c = h & 3;
+    const bool teacher = noisy && k == 0;
+    const float dot = ((zred[h][0] + zred[h][1]) + zred[h][2]) + zred[h][3];
+    const float bias = teacher ? b2t[c] : b2s[c];
+    const int erow = !noisy ? b : (k == 0 ? g.Bc + b : g.Bc + g.Bn + b);
+    a.logits[(size_t)erow * DAD_C + c] = dot + bias;
+  }
+}
+
+// ------------------------------------------------------------------------------ tail
+__global__ __launch_bounds__(TAIL_THREADS) void dad_tail(DadTailArgs a) {
+  const dad_config& cfg = a.cfg;
+  const int B = cfg.B;                       // clean utterances
+  const int Bn = cfg.warmup ? 0 : cfg.Bn;    // noisy utterances
+  const int tid = threadIdx.x;
+  __shared__ double dred[8];
+  __shared__ float fred[8];
+  __shared__ float gz[2][DAD_MAX_BATCH][DAD_C];       // dL/dz clean, strong
+  __shared__ float sq[DAD_MAX_BATCH][DAD_C];          // teacher probs
+  __shared__ float ss[DAD_MAX_BATCH];                 // certainty scores
+  __shared__ int sp[DAD_MAX_BATCH];                   // pseudo labels
+  __shared__ float sm[DAD_MAX_BATCH];                 // mask
+  __shared__ float srt[DAD_C][DAD_MAX_BATCH];         // per-class sorted scores
+  __shared__ int ncls[DAD_C];
+  __shared__ float tau_new[DAD_C];
+  __shared__ float sflag[4];
+
+  float* tf = a.tailf;
+  float* extras = a.grad + DAD_NPARAM;
+  const float* z0 = a.logits;
+  const float* z1 = a.logits + (size_t)B * DAD_C;
+  const float* z2 = a.logits + (size_t)(B + Bn) * DAD_C;
+  const float eps = cfg.ls_eps;
+
+  // ---- supervised CE with label smoothing on the clean logits (I/train.py:364,400)
+  double ce_part = 0.0;
+  for (int b = tid; b < B; b += TAIL_THREADS) {
+    float z[4], m = -INFINITY;
+    for (int c = 0; c < 4; ++c) { z[c] = z0[b * 4 + c]; m = fmaxf(m, z[c]); }
+    float se = 0.0f;
+    for (int c = 0; c < 4; ++c) se += expf(z[c] - m);
+    const float lse = m + logf(se);
+    const int y = (int)a.yc[b];
+    float lsum = 0.0f;
+    for (int c = 0; c < 4; ++c) {
+      const float ls = z[c] - lse;
+      lsum += ls;
+      const float p = expf(ls);
+      gz[0][b][c] = (p - (c == y ? 1.0f - eps : 0.0f) - eps * 0.25f) / (float)B;
+    }
+    ce_part += -(1.0 - (double)eps) * (double)(z[y] - lse) - (double)eps * 0.25 * (double)lsum;
+  }
+  const double ce = block_sum_d(ce_part, dred) / (double)B;
+
+  float kl = 0.0f, msum = 0.0f;
+  int kl_on = 0;
+  if (!cfg.warmup) {
+    // ---- teacher probs (I/train.py:409-410) and certainty (I/utils.py:400-428)
+    for (int b = tid; b < Bn; b += TAIL_THREADS) {
+      float z[4], m = -INFINITY;
+      for (int c = 0; c < 4; ++c) { z[c] = z1[b * 4 + c]; m = fmaxf(m, z[c]); }
+      float e[4], se = 0.0f;
+      for (int c = 0; c < 4; ++c) { e[c] = expf(z[c] - m); se += e[c]; }
+      float q[4], mx = -1.0f;
+      int pred = 0;
+      for (int c = 0; c < 4; ++c) {
+        q[c] = e[c] / se;
+        sq[b][c] = q[c];
+        if (q[c] > mx) { mx = q[c]; pred = c; }
+      }
+      float s = mx;
+      if (cfg.use_dacp && cfg.use_entropy) {
+        float ent = 0.0f;
+        for (int c = 0; c < 4; ++c) ent += q[c] * log2f(q[c] + 1e-8f);
+        ent = -ent;
+        s = mx * (1.0f - ent / 2.0f);   // log2(NUM_CLASSES) = 2
+      }
+      ss[b] = s;
+      sp[b] = pred;
+    }
+    if (tid < DAD_C) ncls[tid] = 0;
+    __syncthreads();
+    if (cfg.use_dacp) {
+      // ---- DACPManager.calculate_mask (I/utils.py:449-507)
+      const float* Q = a.dacp + 4;
+      const float* tau = a.dacp;
+      const float* anchors = a.dacp + 16;
+      // per-class order statistics: rank of each score inside its pseudo-label class
+      for (int b = tid; b < Bn; b += TAIL_THREADS) {
+        const int c = sp[b];
+        const float s = ss[b];
+        int rank = 0;
+        for (int k = 0; k < Bn; ++k) {
+          if (sp[k] != c) continue;
+          const float o = ss[k];
+          rank += (o < s || (o == s && k < b)) ? 1 : 0;
+        }
+        srt[c][rank] = s;
+        atomicAdd(&ncls[c], 1);
+      }
+      __syncthreads();
+      if (tid < DAD_C) {
+        const int c = tid;
+        const float qmean = (((Q[0] + Q[1]) + Q[2]) + Q[3]) / 4.0f;
+        const float wc = 1.0f / (1.0f + expf(-(cfg.dacp_k * (Q[c] - qmean))));
+        const int n = ncls[c];
+        float that;
+        if (n > 0) {
+          // torch.quantile(linear): rank = q*(n-1) in f32, lerp(below, above, rank-floor)
+          const float rank = cfg.dacp_gamma * (float)(n - 1);
+          const int lo = (int)rank;
+          const int hi = (int)ceilf(rank);
+          const float wgt = rank - (float)lo;
+          const float vlo = srt[c][lo], vhi = srt[c][hi];
+          that = wgt < 0.5f ? vlo + wgt * (vhi - vlo) : vhi - (vhi - vlo) * (1.0f - wgt);
+        } else {
+          that = tau[c];
+        }
+        const float adj = cfg.dacp_lambda * (wc - 0.5f);
+        const float fl = fmaxf(that + adj, anchors[c]);
+        const float tn = cfg.dacp_alpha * tau[c] + cfg.dacp_one_m_alpha * fl;
+        tau_new[c] = tn;
+        tf[DAD_T_W + c] = wc;
+        tf[DAD_T_TAU_BEFORE + c] = tau[c];
+        tf[DAD_T_TAU_AFTER + c] = tn;
+        tf[DAD_T_FLOORED + c] = fl;
+        tf[DAD_T_TAU_HAT + c] = that;
+        extras[0 + c] = fl;
+      }
+      __syncthreads();
+      for (int b = tid; b < Bn; b += TAIL_THREADS) sm[b] = ss[b] >= tau_new[sp[b]] ? 1.0f : 0.0f;
+      // epoch statistics for update_class_quality_scores_epoch (I/utils.py:503-505)
+      if (tid < DAD_C) {
+        double s = 0.0;
+        int n = 0;
+        for (int b = 0; b < Bn; ++b)
+          if (sp[b] == tid) { s += ss[b]; ++n; }
+        extras[4 + tid] = (float)s;
+        extras[8 + tid] = (float)n;
+      }
+    } else {
+      // fixed threshold (I/train.py:417-420): mask = float(max prob >= thr), weights = ones
+      for (int b = tid; b < Bn; b += TAIL_THREADS) sm[b] = ss[b] >= cfg.fixed_thr ? 1.0f : 0.0f;
+      if (tid < DAD_C) {
+        tf[DAD_T_W + tid] = 1.0f;
+        extras[0 + tid] = 0.0f;
+        extras[4 + tid] = 0.0f;
+        extras[8 + tid] = 0.0f;
+      }
+    }
+    __syncthreads();
+    float mpart = 0.0f;
+    for (int b = tid; b < Bn; b += TAIL_THREADS) mpart += sm[b];
+    msum = block_sum_f(mpart, fred);
+    kl_on = msum > 1.0f;   // I/train.py:444 (mask.sum().item() > 1)
+    // ---- masked consistency KL(q || p_student) (I/train.py:445-447) + its logit grad
+    double kl_part = 0.0;
+    const float denom = msum + 1e-8f;
+    for (int b = tid; b < Bn; b += TAIL_THREADS) {
+      float z[4], m = -INFINITY;
+      for (int c = 0; c < 4; ++c) { z[c] = z2[b * 4 + c]; m = fmaxf(m, z[c]); }
+      float se = 0.0f;
+      for (int c = 0; c < 4; ++c) se += expf(z[c] - m);
+      const float lse = m + logf(se);
+      float klb = 0.0f;
+      for (int c = 0; c < 4; ++c) {
+        const float q = sq[b][c];
+        const float ls = z[c] - lse;
+        klb += q > 0.0f ? q * (logf(q) - ls) : 0.0f;
+        gz[1][b][c] = kl_on ? cfg.w_kl * sm[b] * (expf(ls) - q) / denom : 0.0f;
+      }
+      kl_part += (double)(klb * sm[b]);
+    }
+    const double kls = block_sum_d(kl_part, dred);
+    kl = kl_on ? (float)(kls / (double)denom) : 0.0f;
+  }
+  // ---- per-sample outputs (noisy batch) for inspection / ECDA
+  for (int b = tid; b < Bn; b += TAIL_THREADS) {
+    tf[DAD_TAIL_HDR + b] = ss[b];
+    tf[DAD_TAIL_HDR + Bn + b] = (float)sp[b];
+    tf[DAD_TAIL_HDR + 2 * Bn + b] = sm[b];
+    for (int c = 0; c < 4; ++c) tf[DAD_TAIL_HDR + 3 * Bn + b * 4 + c] = sq[b][c];
+  }
+  if (tid == 0) {
+    tf[DAD_T_CE] = (float)ce;
+    tf[DAD_T_KL] = kl;
+    tf[DAD_T_SCL] = 0.0f;
+    tf[DAD_T_MSUM] = msum;
+    tf[DAD_T_KL_ON] = (float)kl_on;
+    tf[DAD_T_ECDA_ON] = (kl_on && cfg.ecda_on) ? 1.0f : 0.0f;
+    for (int c = 0; c < 4; ++c) { tf[DAD_T_ECDA_TERM + c] = 0.0f; tf[DAD_T_ECDA_GATE + c] = 0.0f; }
+  }
+  __syncthreads();
+  // ---- classifier backward (nn.Linear + nn.Dropout, I/model.py:62-63), both passes
+  const int h = tid;   // TAIL_THREADS == H
+  const float* W2 = a.student + DAD_OFF_W2;
+  const float w2h[4] = {W2[h], W2[DAD_H + h], W2[2 * DAD_H + h], W2[3 * DAD_H + h]};
+  const float* e0 = a.emb;
+  const float* e2 = a.emb + (size_t)(B + Bn) * DAD_H;
+  double gw[4] = {0, 0, 0, 0};
+  for (int b = 0; b < B; ++b) {
+    const float k1 = keep_value(a.keep1, a.key_drop1, b, h, cfg.p_drop, cfg.drop_scale);
+    const float d0 = e0[(size_t)b * DAD_H + h] * k1;
+    float g0 = 0.0f;
+    for (int c = 0; c < 4; ++c) {
+      gw[c] += (double)gz[0][b][c] * d0;
+      g0 += w2h[c] * gz[0][b][c];
+    }
+    a.ge[(size_t)b * DAD_H + h] = g0 * k1;
+  }
+  for (int b = 0; b < Bn; ++b) {
+    const float k2 = keep_value(a.keep2, a.key_drop2, b, h, cfg.p_drop, cfg.drop_scale);
+    const float d2 = e2[(size_t)b * DAD_H + h] * k2;
+    float g2 = 0.0f;
+    for (int c = 0; c < 4; ++c) {
+      gw[c] += (double)gz[1][b][c] * d2;
+      g2 += w2h[c] * gz[1][b][c];
+    }
+    a.ge[(size_t)(B + b) * DAD_H + h] = g2 * k2;
+  }
+  for (int c = 0; c < 4; ++c) a.grad[DAD_OFF_W2 + c * DAD_H + h] = (float)gw[c];
+  if (tid < 4) {
+    double s = 0.0;
+    for (int b = 0; b < B; ++b) s += (double)gz[0][b][tid];
+    for (int b = 0; b < Bn; ++b) s += (double)gz[1][b][tid];
+    a.grad[DAD_OFF_B2 + tid] = (float)s;
+  }
+}
+
+// ------------------------------------------------------------------------------ ECDA
+// One workgroup per class (I/utils.py:601-632 loop body); the global-MMD ablation
+// (I/utils.py:633-650) runs in workgroup 0.  Each workgroup only writes the embedding
+// grads of ITS class members (clean: label == c, noisy: masked & pseudo-label == c), so
+// no atomics are needed and the result is deterministic.
+#define ECDA_THREADS 256
+#define ECDA_NZ 80           // members staged in LDS (n <= 80); larger sets read global
+
+struct EcdaSmem {
+  float z[ECDA_NZ * DAD_H];
+  float dm[ECDA_NZ * ECDA_NZ];
+  int idx[2 * DAD_MAX_BATCH];     // member list: [0,ns) clean rows, [ns,n) noisy rows
+  float wt[2 * DAD_MAX_BATCH];    // member weights
+  float cent[DAD_C][DAD_H];
+  float rowc[2 * DAD_MAX_BATCH];  // sum_b Csym[a][b]
+  double dred[8];
+  float fred[8];
+  int cnt_clean[DAD_C], cnt_noisy[DAD_C];
+};
+
+// mmd = t_ss + t_tt - 2 t_st of _gaussian_kernel (I/utils.py:521-563) over members
+// idx[0..ns) (clean embeddings) and idx[ns..n) (strong embeddings), plus grads
+// `scale * d mmd / dz` added into ge.  Returns mmd (valid in all threads).
+__device__ float ecda_mmd(EcdaSmem& S, const float* emb_c, const float* emb_s, float* ge_c, float* ge_s,
+                          int ns, int n, float* scratch, float scale) {
+  const int tid = threadIdx.x;
+  const bool staged = n <= ECDA_NZ;
+  // stage Z
+  if (staged) {
+    for (int k = tid; k < n * DAD_H; k += ECDA_THREADS) {
+      const int a = k / DAD_H, hh = k - a * DAD_H;
+      const float* src = a < ns ? emb_c : emb_s;
+      S.z[k] = src[(size_t)S.idx[a] * DAD_H + hh];
+    }
+  }
+  __syncthreads();
+  float* D = staged ? S.dm : scratch;
+  auto zrow = [&](int a) -> const float* {
+    return staged ? &S.z[a * DAD_H] : ((a < ns ? emb_c : emb_s) + (size_t)S.idx[a] * DAD_H);
+  };
+  // pairwise squared distances (I/utils.py:533-537)
+  double part = 0.0;
+  for (int p = tid; p < n * n; p += ECDA_THREADS) {
+    const int i = p / n, j = p - i * n;
+    float d = 0.0f;
+    if (i != j) {
+      const float* zi = zrow(i);
+      const float* zj = zrow(j);
+      for (int hh = 0; hh < DAD_H; ++hh) {
+        const float df = zj[hh] - zi[hh];
+        d += df * df;
+      }
+    }
+    D[p] = d;
+    part += d;
+  }
+  const double sumD = [&] {
+    double v = dad_wave_sum_d(part);
+    __syncthreads();
+    if ((tid & 63) == 0) S.dred[tid >> 6] = v;
+    __syncthreads();
+    double s = 0.0;
+    for (int k = 0; k < ECDA_THREADS / 64; ++k) s += S.dred[k];
+    return s;
+  }();
+  // detached bandwidth (I/utils.py:540-544): sum(D)/(n^2-n) / mul^(num//2), x mul^i
+  float bw = (n > 1) ? (float)(sumD / (double)(n * n - n)) : 1.0f;
+  bw = bw / 4.0f;
+  float bws[5];
+  for (int m = 0; m < 5; ++m) bws[m] = bw * (float)(1 << m) + 1e-8f;
+  // weight normalisers (I/utils.py:552-557)
+  double wsum_t = 0.0;
+  for (int a = ns; a < n; ++a) wsum_t += S.wt[a];
+  const float Wss = (float)ns * (float)ns + 1e-8f;
+  const float Wtt = (float)(wsum_t * wsum_t) + 1e-8f;
+  const float Wst = (float)((double)ns * wsum_t) + 1e-8f;
+  // terms and coefficients C_ij = dmmd/dK_ij * dK_ij/dD_ij (stored over D)
+  double tss = 0.0, ttt = 0.0, tst = 0.0;
+  for (int p = tid; p < n * n; p += ECDA_THREADS) {
+    const int i = p / n, j = p - i * n;
+    const float d = D[p];
+    float K = 0.0f, dK = 0.0f;
+    for (int m = 0; m < 5; ++m) {
+      const float e = expf(-d / bws[m]);
+      K += e;
+      dK -= e / bws[m];
+    }
+    float coef;
+    if (i < ns && j < ns) { tss += K; coef = 1.0f / Wss; }
+    else if (i >= ns && j >= ns) { const float ww = S.wt[i] * S.wt[j]; ttt += (double)K * ww; coef = ww / Wtt; }
+    else if (i < ns) { tst += (double)K * S.wt[j]; coef = -2.0f * S.wt[j] / Wst; }
+    else coef = 0.0f;   // the T x S block is not used by t_st
+    D[p] = coef * dK;
+  }
+  double red3[3] = {tss, ttt, tst};
+  for (int r = 0; r < 3; ++r) {
+    double v = dad_wave_sum_d(red3[r]);
+    __syncthreads();
+    if ((tid & 63) == 0) S.dred[tid >> 6] = v;
+    __syncthreads();
+    double s = 0.0;
+    for (int k = 0; k < ECDA_THREADS / 64; ++k) s += S.dred[k];
+    red3[r] = s;
+  }
+  const float mmd = (float)(red3[0] / Wss + red3[1] / Wtt - 2.0 * (red3[2] / Wst));
+  __syncthreads();
+  // symmetrise: Csym_ij = C_ij + C_ji (read-only pass into rowc + second buffer-free form)
+  for (int i = tid; i < n; i += ECDA_THREADS) {
+    float r = 0.0f;
+    for (int j = 0; j < n; ++j) r += D[i * n + j] + D[j * n + i];
+    S.rowc[i] = r;
+  }
+  __syncthreads();
+  // dZ_i = 2 * (rowc_i * z_i - sum_j Csym_ij z_j)
+  for (int k = tid; k < n * DAD_H; k += ECDA_THREADS) {
+    const int i = k / DAD_H, hh = k - i * DAD_H;
+    float acc = 0.0f;
+    for (int j = 0; j < n; ++j) acc += (D[i * n + j] + D[j * n + i]) * zrow(j)[hh];
+    const float g = 2.0f * (S.rowc[i] * zrow(i)[hh] - acc);
+    float* dst = (i < ns ? ge_c : ge_s) + (size_t)S.idx[i] * DAD_H + hh;
+    *dst += scale * g;
+  }
+  __syncthreads();
+  return mmd;
+}
+
+__global__ __launch_bounds__(ECDA_THREADS) void dad_ecda(DadEcdaArgs a) {
+  __shared__ EcdaSmem S;
+  const dad_config& cfg = a.cfg;
+  const int B = cfg.B, Bn = cfg.Bn;
+  const int c = blockIdx.x, tid = threadIdx.x;
+  const float* tf = a.tailf;
+  if (tf[DAD_T_ECDA_ON] == 0.0f) return;
+  const float* score = tf + DAD_TAIL_HDR;
+  const float* predf = tf + DAD_TAIL_HDR + Bn;
+  const float* mask = tf + DAD_TAIL_HDR + 2 * Bn;
+  const float* emb_c = a.emb;
+  const float* emb_s = a.emb + (size_t)(B + Bn) * DAD_H;
+  float* ge_c = a.ge;
+  float* ge_s = a.ge + (size_t)B * DAD_H;
+  float* scratch = a.scratch + (size_t)c * (B + Bn) * (B + Bn);
+  const float wscale = cfg.w_ecda;
+
+  if (!cfg.class_aware) {
+    // global MMD ablation: all clean vs all masked noisy, unit weights (I/utils.py:633-650)
+    if (c != 0) return;
+    if (tid == 0) {
+      int n = 0;
+      for (int b = 0; b < B; ++b) { S.idx[n] = b; S.wt[n] = 1.0f; ++n; }
+      const int ns = n;
+      for (int b = 0; b < Bn; ++b)
+        if (mask[b] > 0.0f) { S.idx[n] = b; S.wt[n] = 1.0f; ++n; }
+      S.cnt_clean[0] = ns;
+      S.cnt_noisy[0] = n - ns;
+    }
+    __syncthreads();
+    const int ns = S.cnt_clean[0], nt = S.cnt_noisy[0];
+    if (ns >= 2 && nt >= 2) {
+      const float mmd = ecda_mmd(S, emb_c, emb_s, ge_c, ge_s, ns, ns + nt, scratch, wscale);
+      if (tid == 0) { a.tail_terms[0] = mmd; a.tail_terms[DAD_T_ECDA_GATE - DAD_T_ECDA_TERM] = 1.0f; }
+    }
+    return;
+  }
+
+  // class-aware path.  In fixed-threshold mode class_weights_wce = ones(B) (I/train.py:420)
+  // so the loop runs over range(B): only classes < min(B, C) can have members.
+  const int ncls = cfg.use_dacp ? DAD_C : (Bn < DAD_C ? Bn : DAD_C);
+  if (c >= ncls) return;
+  // membership counts and noisy centroids of every class (needed for repulsion)
+  if (tid < DAD_C) {
+    int nc = 0, nn = 0;
+    if (tid < ncls) {
+      for (int b = 0; b < B; ++b) nc += a.yc[b] == tid;
+      for (int b = 0; b < Bn; ++b) nn += ((int)predf[b] == tid && mask[b] > 0.0f);
+    }
+    S.cnt_clean[tid] = nc;
+    S.cnt_noisy[tid] = nn;
+  }
+  __syncthreads();
+  {
+    const int hh = tid;
+    for (int k = 0; k < DAD_C; ++k) {
+      float s = 0.0f;
+      if (S.cnt_noisy[k] > 0)
+        for (int b = 0; b < Bn; ++b)
+          if ((int)predf[b] == k && mask[b] > 0.0f) s += emb_s[(size_t)b * DAD_H + hh];
+      S.cent[k][hh] = S.cnt_noisy[k] > 0 ? s / (float)S.cnt_noisy[k] : 0.0f;
+    }
+  }
+  __syncthreads();
+  // class attention (I/utils.py:597-599) over the ncls class weights
+  const float* w = tf + DAD_T_W;
+  float wmean = 0.0f, att_c;
+  float att[DAD_C];
+  if (cfg.use_dacp) {
+    wmean = (((w[0] + w[1]) + w[2]) + w[3]) / 4.0f;
+    for (int k = 0; k < DAD_C; ++k) att[k] = expf(cfg.ecda_att_lambda * (wmean - w[k]));
+  } else {
+    for (int k = 0; k < DAD_C; ++k) att[k] = 1.0f;
+  }
+  att_c = att[c];
+  // repulsion over valid centroids (I/utils.py:582-595)
+  int nvalid = 0;
+  for (int k = 0; k < ncls; ++k) nvalid += S.cnt_noisy[k] > 0;
+  float rep = 0.0f;
+  const int npairs = nvalid * (nvalid - 1) / 2;
+  // pairwise centroid distances: computed by wave 0 lanes, small (<= 6 pairs)
+  __shared__ float pdist[DAD_C][DAD_C];
+  if (tid < DAD_C * DAD_C) {
+    const int p = tid / DAD_C, q = tid % DAD_C;
+    float d = 0.0f;
+    if (p < ncls && q < ncls && S.cnt_noisy[p] > 0 && S.cnt_noisy[q] > 0 && p != q) {
+      for (int hh = 0; hh < DAD_H; ++hh) {
+        const float df = S.cent[p][hh] - S.cent[q][hh];
+        d += df * df;
+      }
+      d = sqrtf(d);
+    }
+    pdist[p][q] = d;
+  }
+  __syncthreads();
+  if (nvalid > 1) {
+    float s = 0.0f;
+    for (int p = 0; p < ncls; ++p)
+      for (int q = p + 1; q < ncls; ++q)
+        if (S.cnt_noisy[p] > 0 && S.cnt_noisy[q] > 0) s += pdist[p][q];
+    rep = -s / (float)npairs;
+  }
+  int gated[DAD_C];
+  float rep_coef = 0.0f;
+  for (int k = 0; k < DAD_C; ++k) {
+    gated[k] = k < ncls && S.cnt_clean[k] >= 2 && S.cnt_noisy[k] >= 2;   // I/utils.py:609-610
+    if (gated[k]) rep_coef += att[k] * cfg.ecda_delta;
+  }
+  // repulsion grads for this class's noisy members
+  if (nvalid > 1 && S.cnt_noisy[c] > 0 && rep_coef != 0.0f) {
+    const int hh = tid;
+    float g = 0.0f;
+    for (int q = 0; q < ncls; ++q) {
+      if (q == c || S.cnt_noisy[q] == 0) continue;
+      const float nd = pdist[c][q];
+      if (nd > 0.0f) g += (S.cent[c][hh] - S.cent[q][hh]) / nd;
+    }
+    g = -g / (float)npairs / (float)S.cnt_noisy[c];
+    for (int b = 0; b < Bn; ++b)
+      if ((int)predf[b] == c && mask[b] > 0.0f) ge_s[(size_t)b * DAD_H + hh] += wscale * rep_coef * g;
+  }
+  __syncthreads();
+  if (!gated[c]) return;
+  // members of class c
+  if (tid == 0) {
+    int n = 0;
+    for (int b = 0; b < B; ++b)
+      if (a.yc[b] == c) { S.idx[n] = b; S.wt[n] = 1.0f; ++n; }
+    for (int b = 0; b < Bn; ++b)
+      if ((int)predf[b] == c && mask[b] > 0.0f) { S.idx[n] = b; S.wt[n] = score[b]; ++n; }
+  }
+  __syncthreads();
+  const int ns = S.cnt_clean[c], nt = S.cnt_noisy[c];
+  const float mmd = ecda_mmd(S, emb_c, emb_s, ge_c, ge_s, ns, ns + nt, scratch, wscale * att_c);
+  // compactness (I/utils.py:614-616): mean_j ||z_j - mu||^2, grad (2/nt)(z_j - mu)
+  float cpart = 0.0f;
+  for (int k = tid; k < nt * DAD_H; k += ECDA_THREADS) {
+    const int j = k / DAD_H, hh = k - j * DAD_H;
+    const int b = S.idx[ns + j];
+    const float df = emb_s[(size_t)b * DAD_H + hh] - S.cent[c][hh];
+    cpart += df * df;
+    ge_s[(size_t)b * DAD_H + hh] += wscale * att_c * cfg.ecda_gamma * (2.0f / (float)nt) * df;
+  }
+  float comp = dad_wave_sum(cpart);
+  __syncthreads();
+  if ((tid & 63) == 0) S.fred[tid >> 6] = comp;
+  __syncthreads();
+  comp = 0.0f;
+  for (int k = 0; k < ECDA_THREADS / 64; ++k) comp += S.fred[k];
+  comp /= (float)nt;
+  if (tid == 0) {
+    a.tail_terms[c] = att_c * (mmd + cfg.ecda_gamma * comp + cfg.ecda_delta * rep);
+    a.tail_terms[DAD_T_ECDA_GATE - DAD_T_ECDA_TERM + c] = 1.0f;
+  }
+}

@@ -1,0 +1,323 @@
+// Encoder weight gradient: dW1 = sum_rows G[row]^T x[row],  G = relu'(pre) * valid * dL/de_b / len_b
+// (autograd of pre_net + ReLU + masked mean pool, I/model.py:28-36, for the clean branch
+// (I/train.py:399) and the strong-augmented noisy branch (I/train.py:439)).
+//
+// K = rows (B*T per branch) is long and the output (256x768) small, so the reduction is
+// split over `splits` row ranges; each workgroup writes one f32 partial slab, and
+// dad_reduce sums them in a fixed order (deterministic, no float atomics).
+// G is rebuilt on the fly from the ReLU' bit mask written by the forward and the
+// per-(utterance, h) scale dL/de / len.  The strong branch's augmented input is
+//   FP32: regenerated exactly (same counter-RNG function, or re-read explicit noise);
+//   BF16: re-read from the bf16 copy the forward stored (the exact MFMA operand it used).
+#include "dad_common.h"
+#include "dad_kernels.h"
+
+namespace {
+
+__device__ __forceinline__ float wg_normal1(uint32_t key, uint32_t idx) {
+  float z0, z1;
+  const uint32_t base = idx & ~1u;
+  dad_box_muller(dad_rng32(base, key), dad_rng32(base | 1u, key), z0, z1);
+  return (idx & 1u) ? z1 : z0;
+}
+
+__device__ __forceinline__ int wg_tstart(const DadWgradArgs& a, int b) {
+  if (a.start) return (int)a.start[b];
+  const uint32_t h = dad_rng32((uint32_t)b, a.key_tstart);
+  return (int)(((uint64_t)h * (uint64_t)a.start_hi) >> 32);
+}
+
+__device__ __forceinline__ float wg_featkeep(const DadWgradArgs& a, int d) {
+  const float u = a.u ? a.u[d] : dad_uniform_at(a.key_feat, (uint32_t)d);
+  return u > a.feat_p ? 1.0f : 0.0f;
+}
+
+// slab s of the weight-gradient row list: clean slabs first, then strong (noisy) slabs
+struct SlabIdx {
+  int br, b, c, T;
+  int erow;          // row of ge / vlen (clean b, or Bc + b)
+  size_t row0;       // [b][T] row of frame 0
+  size_t bits_row;   // first row of this slab in the bits buffer
+};
+__device__ __forceinline__ SlabIdx wg_slab(const DadWgradArgs& a, int s) {
+  const DadGeom& g = a.g;
+  const int nsc = g.Bc * g.ncc;
+  SlabIdx r;
+  r.br = s >= nsc;
+  const int rem = r.br ? s - nsc : s;
+  const int nc = r.br ? g.ncn : g.ncc;
+  r.b = rem / nc;
+  r.c = rem - r.b * nc;
+  r.T = r.br ? g.Tn : g.Tc;
+  r.erow = r.br ? g.Bc + r.b : r.b;
+  r.row0 = (size_t)r.b * r.T;
+  r.bits_row = r.br ? (size_t)g.Bc * g.tpc + (size_t)r.b * g.tpn + (size_t)r.c * DAD_SLAB
+                    : (size_t)r.b * g.tpc + (size_t)r.c * DAD_SLAB;
+  return r;
+}
+
+__device__ __forceinline__ int wg_total(const DadWgradArgs& a) {
+  return a.g.Bc * a.g.ncc + (a.warmup ? 0 : a.g.Bn * a.g.ncn);
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------- FP32 (parity mode)
+// grid = 6 column blocks x splits; wave = 32 columns x 256 rows of dW1.
+// v_mfma_f32_32x32x2_f32: A[i=h][k] = G[row k][h], B[k][j=d] = x[row k][d] (k = 2 rows).
+__global__ __launch_bounds__(256) void dad_wgrad_f32(DadWgradArgs a) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int dblk = blockIdx.x % 6, split = blockIdx.x / 6;
+  const int d0 = (dblk * 4 + wv) * 32;
+  const int i = lane & 31, kh = lane >> 5;
+  const int total = wg_total(a);
+  const int per = (total + a.splits - 1) / a.splits;
+  const int s0 = split * per;
+  const int s1 = min(total, s0 + per);
+  f32x16 acc[DAD_HT];
+#pragma unroll
+  for (int ht = 0; ht < DAD_HT; ++ht) acc[ht] = f32x16{};
+  const int d = d0 + i;
+  for (int s = s0; s < s1; ++s) {
+    const SlabIdx q = wg_slab(a, s);
+    const float* X = q.br ? a.xn : a.xc;
+    const float len = fmaxf(a.vlen[q.erow], 1.0f);
+    float scale[DAD_HT];
+#pragma unroll
+    for (int ht = 0; ht < DAD_HT; ++ht) scale[ht] = a.ge[(size_t)q.erow * DAD_H + ht * 32 + i] / len;
+    int st = 0;
+    float fkeep = 1.0f;
+    if (q.br) {
+      st = a.mask_len > 0 ? wg_tstart(a, q.b) : 0;
+      fkeep = wg_featkeep(a, d);
+    }
+    const uint32_t* bw = a.bits + q.bits_row * DAD_HT;
+    for (int rr = 0; rr < DAD_SLAB; rr += 2) {
+      if (q.c * DAD_SLAB + rr >= q.T) break;
+      const int t = q.c * DAD_SLAB + rr + kh;
+      const bool tin = t < q.T;
+      const size_t grow = q.row0 + (tin ? t : 0);
+      float x = tin ? X[grow * DAD_D + d] : 0.0f;
+      if (q.br && tin) {
+        const float n = a.ns ? a.ns[grow * DAD_D + d] : wg_normal1(a.key_strong, (uint32_t)(grow * DAD_D + d));
+        const float sn = n * a.strong_std;
+        x = (x + sn) * fkeep;
+        if (a.mask_len > 0 && t >= st && t < st + a.mask_len) x = 0.0f;
+      }
+      const uint4 w0 = *reinterpret_cast<const uint4*>(bw + (rr + kh) * DAD_HT);
+      const uint4 w1 = *reinterpret_cast<const uint4*>(bw + (rr + kh) * DAD_HT + 4);
+      const uint32_t wds[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+      for (int ht = 0; ht < DAD_HT; ++ht) {
+        const float g = ((wds[ht] >> i) & 1u) ? scale[ht] : 0.0f;
+        acc[ht] = __builtin_amdgcn_mfma_f32_32x32x2f32(g, x, acc[ht], 0, 0, 0);
+      }
+    }
+  }
+  float* out = a.wpart + (size_t)split * DAD_H * DAD_D;
+#pragma unroll
+  for (int ht = 0; ht < DAD_HT; ++ht)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) out[(size_t)(ht * 32 + dad_acc_row(r, kh)) * DAD_D + d] = acc[ht][r];
+}
+
+// ------------------------------------------------------------ BF16 (throughput mode)
+// grid = 6 column blocks (128 d) x splits; workgroup tile 256 h x 128 d; wave w owns
+// h tiles {2w, 2w+1} x d tiles 0..3 (8 accumulators).  Per 32-row slab the workgroup
+// stages x (bf16, [32][128]) and G (bf16, [32][256]) row-major in LDS and the waves read
+// k-major fragments with ds_read_b64_tr_b16 (k = rows).  Row pitches are padded by 64 B
+// so the four rows of a transposed read land on disjoint bank quarters.
+#define WG_XP 160   // Xt row pitch (bf16 elements) = 320 B
+#define WG_GP 288   // Gt row pitch (bf16 elements) = 576 B
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+__device__ __forceinline__ bf16x8 tr_frag(const __bf16* tile, int pitch, int rowbase, int colbase) {
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4, li = lane & 15;
+  const int q = li >> 2, p = li & 3;
+  const int col = colbase + 16 * (g & 1) + 4 * p;
+  const int row = rowbase + 8 * (g >> 1) + q;
+  const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + row * pitch + col));
+  const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + (row + 4) * pitch + col));
+  bf16x8 r;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    r[e] = __builtin_bit_cast(__bf16, (short)v0[e]);
+    r[e + 4] = __builtin_bit_cast(__bf16, (short)v1[e]);
+  }
+  return r;
+}
+
+__global__ __launch_bounds__(256, 2) void dad_wgrad_bf16(DadWgradArgs a) {
+  __shared__ __attribute__((aligned(16))) __bf16 Xt[DAD_SLAB * WG_XP];
+  __shared__ __attribute__((aligned(16))) __bf16 Gt[DAD_SLAB * WG_GP];
+  __shared__ float sc[DAD_H];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wv = tid >> 6;
+  const int kh = lane >> 5;
+  const int dblk = blockIdx.x % 6, split = blockIdx.x / 6;
+  const int dbase = dblk * 128;
+  const int total = wg_total(a);
+  const int per = (total + a.splits - 1) / a.splits;
+  const int s0 = split * per;
+  const int s1 = min(total, s0 + per);
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[m][n] = f32x16{};
+
+  for (int s = s0; s < s1; ++s) {
+    const SlabIdx q = wg_slab(a, s);
+    __syncthreads();   // previous slab's fragment reads are done
+    sc[tid] = a.ge[(size_t)q.erow * DAD_H + tid] / fmaxf(a.vlen[q.erow], 1.0f);
+    // x tile: 32 rows x 128 columns
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int row = (tid >> 5) + 8 * m;
+      const int col = (tid & 31) * 4;
+      const int t = q.c * DAD_SLAB + row;
+      bf16x4 v;
+      if (t < q.T) {
+        const size_t off = (q.row0 + t) * DAD_D + dbase + col;
+        if (q.br == 0) {
+          const f32x4 x = *reinterpret_cast<const f32x4*>(a.xc + off);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = (__bf16)x[e];
+        } else {
+          v = *reinterpret_cast<const bf16x4*>(a.xs_bf16 + off);
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = (__bf16)0.0f;
+      }
+      *reinterpret_cast<bf16x4*>(&Xt[row * WG_XP + col]) = v;
+    }
+    __syncthreads();   // sc visible
+    {
+      const int row = tid >> 3, hq = tid & 7;
+      const uint32_t word = a.bits[(q.bits_row + row) * DAD_HT + hq];
+#pragma unroll
+      for (int g8 = 0; g8 < 4; ++g8) {
+        bf16x8 gv;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int hh = hq * 32 + g8 * 8 + e;
+          gv[e] = (__bf16)(((word >> (g8 * 8 + e)) & 1u) ? sc[hh] : 0.0f);
+        }
+        *reinterpret_cast<bf16x8*>(&Gt[row * WG_GP + hq * 32 + g8 * 8]) = gv;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[2], bf[4];
+#pragma unroll
+      for (int m = 0; m < 2; ++m) af[m] = tr_frag(Gt, WG_GP, 16 * ks, 32 * (2 * wv + m));
+#pragma unroll
+      for (int n = 0; n < 4; ++n) bf[n] = tr_frag(Xt, WG_XP, 16 * ks, 32 * n);
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[m], bf[n], acc[m][n], 0, 0, 0);
+    }
+  }
+  float* out = a.wpart + (size_t)split * DAD_H * DAD_D;
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int h = (2 * wv + m) * 32 + dad_acc_row(r, kh);
+        const int d = dbase + 32 * n + (lane & 31);
+        out[(size_t)h * DAD_D + d] = acc[m][n][r];
+      }
+}
+
+// ---------------------------------------------------------------- reduce + squared norms
+// blocks [0,192): dW1 = sum_s wpart[s] (fixed order) + squared-norm partial;
+// block 192: db1 = sum_b (dL/de_b / len_b) * active_count_b, the W2/b2 norm partial and
+// the loss totals (I/train.py:462-466).
+__global__ __launch_bounds__(256) void dad_reduce(DadReduceArgs a) {
+  __shared__ double red[4];
+  const int tid = threadIdx.x;
+  double sq = 0.0;
+  if (blockIdx.x < 192) {
+    const size_t e0 = (size_t)blockIdx.x * 1024 + (size_t)tid * 4;
+    f32x4 s = f32x4{};
+    for (int k = 0; k < a.splits; ++k) s += *reinterpret_cast<const f32x4*>(a.wpart + (size_t)k * DAD_H * DAD_D + e0);
+    *reinterpret_cast<f32x4*>(a.grad + DAD_OFF_W1 + e0) = s;
+    for (int e = 0; e < 4; ++e) sq += (double)s[e] * s[e];
+  } else {
+    const int h = tid;
+    const DadGeom& g = a.g;
+    double gb = 0.0;
+    const int nb = g.Bc + (a.warmup ? 0 : g.Bn);
+    for (int r = 0; r < nb; ++r) {
+      // row r of ge/vlen: clean utterance r, or strong utterance r - Bc
+      const bool strong = r >= g.Bc;
+      const int nc = strong ? g.ncn : g.ncc;
+      const size_t slab0 = strong ? (size_t)g.Bc * g.ncc + (size_t)(r - g.Bc) * g.ncn : (size_t)r * g.ncc;
+      const float sc = a.ge[(size_t)r * DAD_H + h] / fmaxf(a.vlen[r], 1.0f);
+      float cnt = 0.0f;
+      for (int c = 0; c < nc; ++c) cnt += a.part_cnt[(slab0 + c) * DAD_H + h];
+      gb += (double)sc * cnt;
+    }
+    const float db1 = (float)gb;
+    a.grad[DAD_OFF_B1 + h] = db1;
+    sq = (double)db1 * db1;
+    if (!a.tailf) return;   // modular encoder backward: W1/b1 only
+    for (int c = 0; c < 4; ++c) {
+      const float g = a.grad[DAD_OFF_W2 + c * DAD_H + h];
+      sq += (double)g * g;
+    }
+    if (h < 4) {
+      const float g = a.grad[DAD_OFF_B2 + h];
+      sq += (double)g * g;
+    }
+    if (h == 0) {
+      const float* tf = a.tailf;
+      const float ecda = ((tf[DAD_T_ECDA_TERM] + tf[DAD_T_ECDA_TERM + 1]) + tf[DAD_T_ECDA_TERM + 2]) +
+                         tf[DAD_T_ECDA_TERM + 3];
+      const float ce = tf[DAD_T_CE], kl = tf[DAD_T_KL];
+      float* ex = a.grad + DAD_NPARAM;
+      ex[12] = ce + a.w_kl * kl + a.w_ecda * ecda;
+      ex[13] = ce;
+      ex[14] = kl;
+      ex[15] = ecda;
+    }
+  }
+  if (!a.want_norm) return;
+  double v = dad_wave_sum_d(sq);
+  if ((tid & 63) == 0) red[tid >> 6] = v;
+  __syncthreads();
+  if (tid == 0) a.normpart[blockIdx.x] = (float)(((red[0] + red[1]) + red[2]) + red[3]);
+}
+
+// Data-parallel path: after the SUM all-reduce, average (grads, thresholds, losses) and
+// recompute the squared-norm partials over the averaged gradient.
+__global__ __launch_bounds__(256) void dad_norm(float* grad, float* normpart, float inv) {
+  __shared__ double red[4];
+  const int tid = threadIdx.x;
+  double sq = 0.0;
+  const size_t n0 = (size_t)blockIdx.x * 1024;
+  for (int k = 0; k < 4; ++k) {
+    const size_t e = n0 + (size_t)k * 256 + tid;
+    if (e < DAD_NPARAM) {
+      const float g = grad[e] * inv;
+      grad[e] = g;
+      sq += (double)g * g;
+    }
+  }
+  if (blockIdx.x == 0 && tid < DAD_GRAD_EXTRA) {
+    float* ex = grad + DAD_NPARAM;
+    if (tid < 4 || tid >= 12) ex[tid] *= inv;   // thresholds and losses are means; sums stay sums
+  }
+  double v = dad_wave_sum_d(sq);
+  if ((tid & 63) == 0) red[tid >> 6] = v;
+  __syncthreads();
+  if (tid == 0) normpart[blockIdx.x] = (float)(((red[0] + red[1]) + red[2]) + red[3]);
+}

@@ -1,0 +1,53 @@
+"""Data-parallel gradient exchange: one RCCL all-reduce per step over xGMI.
+
+The reference is single-device (I/train.py:58).  Each rank runs the full DAD step on its
+own clean+noisy shard; `dad_step_compute` leaves [grads | DACP tau', score sums, counts |
+losses] in one flat buffer, this module SUM-all-reduces it in place on the step's stream
+(RCCL, called through the C ABI so the collective is part of the enqueued step), and
+`dad_step_apply` averages and applies it identically on every rank.
+The RCCL communicator is bootstrapped by broadcasting rank 0's ncclUniqueId over the
+already-initialised torch.distributed process group.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+
+
+class DPComm:
+    def __init__(self, rank, world, comm_handle=None):
+        self.rank, self.world = int(rank), int(world)
+        self._comm = comm_handle
+
+    @classmethod
+    def from_torch_distributed(cls, group=None):
+        import torch.distributed as dist
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        if world == 1:
+            return cls(rank, world, None)
+        L = _lib.lib()
+        n = L.dad_comm_unique_id_bytes()
+        buf = (ctypes.c_uint8 * n)()
+        if rank == 0:
+            _lib.check(L.dad_comm_get_unique_id(buf), "dad_comm_get_unique_id")
+        t = torch.tensor(list(bytes(buf)), dtype=torch.uint8)
+        backend = dist.get_backend(group)
+        if backend == "nccl":
+            t = t.cuda()
+        dist.broadcast(t, src=0, group=group)
+        raw = bytes(t.cpu().tolist())
+        idbuf = (ctypes.c_uint8 * n).from_buffer_copy(raw)
+        handle = ctypes.c_void_p()
+        _lib.check(L.dad_comm_init(ctypes.byref(handle), world, idbuf, rank), "dad_comm_init")
+        return cls(rank, world, handle)
+
+    def allreduce_grad(self, state_struct, stream):
+        if self.world == 1:
+            return
+        _lib.check(_lib.lib().dad_comm_allreduce_grad(self._comm, state_struct, stream), "dad_comm_allreduce_grad")
+
+    def close(self):
+        if self._comm is not None:
+            _lib.lib().dad_comm_destroy(self._comm)
+            self._comm = None

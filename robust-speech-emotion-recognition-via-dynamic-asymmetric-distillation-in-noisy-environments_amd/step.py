@@ -1,0 +1,262 @@
+"""The fused DAD train step: one C-ABI call sequence per step, all decisions on device.
+
+`DADStep.step(clean_batch, noisy_batch, epoch)` replaces the body of the reference's
+`train_epoch` loop (I/train.py:484-492):
+
+    optimizer.zero_grad(); losses = train_step(clean, noisy, epoch)      # I/train.py:397-471
+    losses['total_loss'].backward(); clip_grad_norm_(...); optimizer.step()
+    if not warm-up: model.update_teacher_ema()
+
+with the same batch dicts (`{'net_input': {'feats', 'padding_mask'}, 'labels'}`,
+I/dataload_noisy.py:124-129) and the same returned loss dict keys.  The step keeps the
+Adam moments, the DACP state (`DACPManager`: ema_thresholds, class_quality_scores, epoch
+score statistics) and every scratch buffer on the device; nothing is synchronised with the
+host, so losses come back as 0-d device tensors.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from .config import ConfigView, dad_config_for
+
+PRECISIONS = {"fp32": _lib.PREC_FP32, "bf16": _lib.PREC_BF16}
+
+
+def _dev_batch(batch, device, labels=True):
+    ni = batch["net_input"]
+    x = ni["feats"].to(device=device, dtype=torch.float32, non_blocking=True).contiguous()
+    pm = ni.get("padding_mask")
+    if pm is None:
+        pad = torch.zeros(x.shape[0], x.shape[1], dtype=torch.uint8, device=device)
+    else:
+        pad = pm.to(device=device, dtype=torch.bool, non_blocking=True).contiguous().view(torch.uint8)
+    y = None
+    if labels:
+        y = batch["labels"].to(device=device, dtype=torch.int64, non_blocking=True).contiguous()
+    if x.dim() != 3 or x.shape[2] != 768:
+        raise ValueError("feats must be [B, T, 768], got %s" % (tuple(x.shape),))
+    return x, pad, y
+
+
+class DADStep:
+    """Owns the device state of the DAD step around an `SSRLModel`.
+
+    Args:
+        model: `SSRLModel` (already on the target cuda device).
+        cfg: reference-style config module / dict / object (read at every step), or None.
+        flavor: 'iemocap' | 'casia' | 'emodb' (which ablation switches are honoured).
+        precision: 'fp32' (exact-f32 MFMA, parity mode) or 'bf16' (bf16 MFMA, fp32 accumulate).
+        rng: 'counter' (in-kernel counter-based RNG) or 'explicit' (draws passed to step()).
+        seed: counter-RNG seed.
+        comm: optional `dist.DPComm` for data-parallel gradient averaging.
+    """
+
+    def __init__(self, model, cfg=None, flavor=None, precision="fp32", rng="counter", seed=0, comm=None,
+                 anchors=None, splits=0):
+        self.model = model
+        self.view = cfg if isinstance(cfg, ConfigView) else ConfigView(cfg, flavor=flavor)
+        self.device = model.student_flat.device
+        if self.device.type != "cuda":
+            raise RuntimeError("DADStep needs the model on an MI355X ('cuda') device")
+        self.precision = PRECISIONS[precision]
+        self.rng_mode = _lib.RNG_COUNTER if rng == "counter" else _lib.RNG_EXPLICIT
+        self.seed = int(seed)
+        self.comm = comm
+        self.splits = int(splits)
+        dev = self.device
+        P = _lib.DAD_NPARAM
+        self.exp_avg = torch.zeros(P, device=dev)
+        self.exp_avg_sq = torch.zeros(P, device=dev)
+        self.grad = torch.zeros(_lib.DAD_GRAD_FLOATS, device=dev)
+        self.w1bf_student = torch.empty(256 * 768, dtype=torch.bfloat16, device=dev)
+        self.w1bf_teacher = torch.empty(256 * 768, dtype=torch.bfloat16, device=dev)
+        # DACPManager state (I/utils.py:384-398): tau=0.5, Q=0.5, epoch sums, anchors
+        self.dacp = torch.zeros(_lib.DAD_DACP_FLOATS, device=dev)
+        self.dacp[0:4] = 0.5
+        self.dacp[4:8] = 0.5
+        if anchors is not None:
+            self.set_anchors(anchors)
+        self.adam_step = 0
+        self.global_step = 0
+        self._ws = None
+        self._bufs = {}
+        self.kernel_events = None     # list -> (start, end) events around each encoder launch
+        self.refresh_shadow()
+
+    # ----------------------------------------------------------------------------- state
+    @property
+    def ema_thresholds(self):
+        return self.dacp[0:4]
+
+    @property
+    def class_quality_scores(self):
+        return self.dacp[4:8]
+
+    @property
+    def calibrated_anchors(self):
+        return self.dacp[16:20]
+
+    def set_anchors(self, anchors):
+        """`calibrated_anchors` input of DACPManager.calculate_mask (I/train.py:317-357)."""
+        a = torch.as_tensor(anchors, dtype=torch.float32).to(self.device)
+        self.dacp[16:20].copy_(a)
+
+    def refresh_shadow(self):
+        """Re-derive the bf16 W1 shadows after the caller changed the model's parameters."""
+        st = self._state_struct(0)
+        _lib.check(_lib.lib().dad_refresh_shadow(st, self._stream()), "dad_refresh_shadow")
+
+    def state_dict(self):
+        return {"exp_avg": self.exp_avg.clone(), "exp_avg_sq": self.exp_avg_sq.clone(),
+                "adam_step": self.adam_step, "global_step": self.global_step, "dacp": self.dacp.clone()}
+
+    def load_state_dict(self, sd):
+        self.exp_avg.copy_(sd["exp_avg"])
+        self.exp_avg_sq.copy_(sd["exp_avg_sq"])
+        self.adam_step = int(sd["adam_step"])
+        self.global_step = int(sd.get("global_step", 0))
+        self.dacp.copy_(sd["dacp"])
+
+    # ---------------------------------------------------------------------------- buffers
+    def _stream(self):
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def _buffers_for(self, Bc, Bn):
+        key = (Bc, Bn)
+        b = self._bufs.get(key)
+        if b is None:
+            dev = self.device
+            nb = Bc + 2 * Bn
+            b = {"tail": torch.zeros(_lib.tail_floats(max(Bn, 1)), device=dev),
+                 "emb": torch.zeros(max(nb, 1), 256, device=dev),
+                 "logits": torch.zeros(max(nb, 1), 4, device=dev)}
+            self._bufs[key] = b
+        return b
+
+    def _state_struct(self, Bn, Bc=None):
+        m = self.model
+        s = _lib.DadState()
+        s.student = m.student_flat.data_ptr()
+        s.teacher = m.teacher_flat.data_ptr()
+        s.exp_avg = self.exp_avg.data_ptr()
+        s.exp_avg_sq = self.exp_avg_sq.data_ptr()
+        s.grad = self.grad.data_ptr()
+        s.w1bf_student = self.w1bf_student.data_ptr()
+        s.w1bf_teacher = self.w1bf_teacher.data_ptr()
+        s.dacp = self.dacp.data_ptr()
+        if Bc is not None:
+            b = self._buffers_for(Bc, Bn)
+            s.tail, s.emb, s.logits = b["tail"].data_ptr(), b["emb"].data_ptr(), b["logits"].data_ptr()
+            self._last = b
+        return s
+
+    def _workspace(self, cfg):
+        nbytes = ctypes.c_size_t(0)
+        _lib.check(_lib.lib().dad_workspace_bytes(cfg, ctypes.byref(nbytes)), "dad_workspace_bytes")
+        need = int(nbytes.value)
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+        return self._ws
+
+    # ------------------------------------------------------------------------------- step
+    def make_config(self, Bc, Tc, Bn, Tn, epoch, lr=None, adam_step=None):
+        return dad_config_for(self.view, Bc, Tc, Bn, Tn, epoch,
+                              adam_step if adam_step is not None else self.adam_step + 1, lr=lr,
+                              precision=self.precision, rng_mode=self.rng_mode, seed=self.seed,
+                              counter=self.global_step,
+                              dp_world=self.comm.world if self.comm is not None else 1, splits=self.splits)
+
+    def step(self, clean_batch, noisy_batch, epoch, lr=None, draws=None):
+        """One full training step; returns the reference's loss dict as 0-d device tensors."""
+        dev = self.device
+        xc, mc, yc = _dev_batch(clean_batch, dev)
+        warm = epoch < self.view.WARMUP_EPOCHS
+        if noisy_batch is not None:
+            xn, mn, _ = _dev_batch(noisy_batch, dev, labels=False)
+            Bn, Tn = xn.shape[0], xn.shape[1]
+        elif warm:
+            xn = mn = None
+            Bn, Tn = 0, 0
+        else:
+            raise ValueError("post-warm-up steps need a noisy batch")
+        Bc, Tc = xc.shape[0], xc.shape[1]
+        cfg = self.make_config(Bc, Tc, Bn, Tn, epoch, lr=lr)
+        bt = _lib.DadBatch()
+        bt.xc, bt.mc, bt.yc = xc.data_ptr(), mc.data_ptr(), yc.data_ptr()
+        if xn is not None:
+            bt.xn, bt.mn = xn.data_ptr(), mn.data_ptr()
+        keep = []
+        if self.rng_mode == _lib.RNG_EXPLICIT:
+            if draws is None:
+                raise ValueError("rng='explicit' needs the step's draws")
+            dd = {}
+            for k in ("nw", "ns", "u"):
+                if draws.get(k) is not None:
+                    dd[k] = torch.as_tensor(draws[k]).to(dev, torch.float32).contiguous()
+            if draws.get("start") is not None:
+                dd["start"] = torch.as_tensor(draws["start"]).to(dev, torch.int64).contiguous()
+            for k in ("keep1", "keep2"):
+                if draws.get(k) is not None:
+                    dd[k] = torch.as_tensor(draws[k]).to(dev, torch.bool).contiguous().view(torch.uint8)
+            for k, v in dd.items():
+                setattr(bt, k, v.data_ptr())
+            keep.append(dd)
+        st = self._state_struct(Bn, Bc)
+        ws = self._workspace(cfg)
+        stream = self._stream()
+        L = _lib.lib()
+        ev = self.kernel_events
+        if ev is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        _lib.check(L.dad_step_encode(cfg, bt, st, _lib.ptr(ws), stream), "dad_step_encode")
+        if ev is not None:
+            e1.record()
+            ev.append((e0, e1))
+        _lib.check(L.dad_step_backward(cfg, bt, st, _lib.ptr(ws), stream), "dad_step_backward")
+        if self.comm is not None and self.comm.world > 1:
+            self.comm.allreduce_grad(st, stream)
+        _lib.check(L.dad_step_apply(cfg, st, _lib.ptr(ws), stream), "dad_step_apply")
+        self.adam_step += 1
+        self.global_step += 1
+        self._keepalive = (xc, mc, yc, xn, mn, keep)
+        return self.losses()
+
+    def losses(self):
+        """Loss dict of the last step (keys of I/train.py:468-470 + scl_loss for CASIA/EMODB)."""
+        t = self._last["tail"]
+        g = self.grad[_lib.DAD_NPARAM + 12:_lib.DAD_NPARAM + 16]
+        out = {"total_loss": g[0].clone(), "supervised_ce_loss": g[1].clone(),
+               "consistency_loss": g[2].clone(), "ecda_loss": g[3].clone()}
+        if self.view.flavor in ("casia", "emodb"):
+            out["scl_loss"] = t[_lib.T_SCL].clone()
+        return out
+
+    def outputs(self, Bc=None, Bn=None):
+        """Per-step intermediates (device tensors) of the last step, for inspection/tests."""
+        b = self._last
+        t = b["tail"]
+        nb = (b["emb"].shape[0])
+        if Bc is None:
+            raise ValueError("pass Bc, Bn")
+        H = _lib.DAD_TAIL_HDR
+        return {
+            "e_clean": b["emb"][:Bc], "e_teacher": b["emb"][Bc:Bc + Bn], "e_strong": b["emb"][Bc + Bn:Bc + 2 * Bn],
+            "z_clean": b["logits"][:Bc], "z_teacher": b["logits"][Bc:Bc + Bn],
+            "z_strong": b["logits"][Bc + Bn:Bc + 2 * Bn],
+            "score": t[H:H + Bn], "pred": t[H + Bn:H + 2 * Bn], "mask": t[H + 2 * Bn:H + 3 * Bn],
+            "q": t[H + 3 * Bn:H + 7 * Bn].view(Bn, 4) if Bn else t[H:H],
+            "w": t[_lib.T_W:_lib.T_W + 4], "tau_before": t[_lib.T_TAU_BEFORE:_lib.T_TAU_BEFORE + 4],
+            "tau_after": t[_lib.T_TAU_AFTER:_lib.T_TAU_AFTER + 4],
+            "ecda_terms": t[_lib.T_ECDA_TERM:_lib.T_ECDA_TERM + 4],
+            "clip_norm": t[_lib.T_CLIPNORM], "clip_coef": t[_lib.T_CLIPCOEF], "msum": t[_lib.T_MSUM],
+            "grad": self.grad[:_lib.DAD_NPARAM], "nb": nb,
+        }
+
+    def epoch_end(self):
+        """DACPManager.update_class_quality_scores_epoch (I/utils.py:430-447), on device."""
+        cfg = self.make_config(1, 1, 1, 1, self.view.WARMUP_EPOCHS)
+        st = self._state_struct(0)
+        _lib.check(_lib.lib().dad_epoch_end(cfg, st, self._stream()), "dad_epoch_end")
+

@@ -1,0 +1,77 @@
+"""C-ABI library checks that need no GPU: the shared library loads, exports every entry
+point include/dad.h declares, and the ctypes mirrors have the C layout."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+import dadpkg
+
+ROOT = dadpkg.ROOT
+HEADER = os.path.join(ROOT, "include", "dad.h")
+
+
+def _declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\**\s+\**(dad_[a-z_0-9]+)\s*\(", src, flags=re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    p = dadpkg.pkg()
+    p.build(verbose=False)
+    L = p.lib()
+    names = _declared_functions()
+    assert len(names) >= 15, names
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+    # the ctypes binding table covers exactly the header's entry points
+    assert sorted(p._lib.EXPORTS) == names
+
+
+def test_host_only_queries():
+    p = dadpkg.pkg()
+    L = p.lib()
+    assert L.dad_param_count() == 256 * 768 + 256 + 4 * 256 + 4
+    cfg = p.dad_config_for(p.ConfigView(flavor="iemocap"), 64, 300, 64, 300, 60, 1)
+    n = ctypes.c_size_t(0)
+    assert L.dad_workspace_bytes(cfg, ctypes.byref(n)) == 0
+    assert n.value > 0
+    bad = p.dad_config_for(p.ConfigView(flavor="iemocap"), 64, 300, 64, 300, 60, 1)
+    bad.B = 0
+    assert L.dad_workspace_bytes(bad, ctypes.byref(n)) == 1002       # DAD_E_SHAPE
+    assert L.dad_error_string(1001).decode().startswith("DAD_E_ARG")
+    assert L.dad_encoder_workspace_bytes(8, 20) > 0
+
+
+def test_ctypes_structs_match_c_layout(tmp_path):
+    """Compile a C probe against include/dad.h and compare sizeof/offsetof with ctypes."""
+    p = dadpkg.pkg()
+    fields = {"dad_config": p._lib.DadConfig, "dad_batch": p._lib.DadBatch, "dad_state": p._lib.DadState}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "dad.h"', "int main(void){"]
+    for cname, cls in fields.items():
+        lines.append('printf("%s %%zu\\n", sizeof(%s));' % (cname, cname))
+        for f in cls._fields_:
+            lines.append('printf("%s.%s %%zu\\n", offsetof(%s, %s));' % (cname, f[0], cname, f[0]))
+    lines.append("return 0;}")
+    c = tmp_path / "probe.c"
+    c.write_text("\n".join(lines))
+    exe = tmp_path / "probe"
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(c), "-o", str(exe)])
+    out = dict(l.split() for l in subprocess.check_output([str(exe)]).decode().splitlines())
+    for cname, cls in fields.items():
+        assert int(out[cname]) == ctypes.sizeof(cls), cname
+        for f in cls._fields_:
+            assert int(out["%s.%s" % (cname, f[0])]) == getattr(cls, f[0]).offset, (cname, f[0])
+
+
+def test_no_oracle_import_in_product():
+    pkgdir = os.path.join(ROOT, dadpkg.PKG_NAME)
+    for dp, _, fs in os.walk(pkgdir):
+        for f in fs:
+            if f.endswith((".py", ".hip", ".h", ".cpp")):
+                txt = open(os.path.join(dp, f)).read()
+                assert "oracle" not in re.findall(r"(?:import|from)\s+(oracle)\b", txt), f
+                assert "/root/reference" not in txt, f

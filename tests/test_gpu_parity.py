@@ -1,0 +1,193 @@
+"""Parity of the fused HIP step (through the C ABI) with the reference goldens and the oracle.
+
+Every golden step is an independent state transition from a seeded state (see
+tests/golden/gen_golden.py); the HIP step starts from the same state with the same
+injected draws (rng='explicit') in FP32 mode (exact-f32 MFMA).  Tolerance: 1e-4 relative
+to the tensor's max magnitude (the north_star's loss/logit bound) for every float; the
+DACP mask and pseudo-labels bit-exact.  BF16 mode is checked against the oracle with a
+bf16-appropriate tolerance.
+"""
+import numpy as np
+import pytest
+import torch
+
+import goldens
+import gpu_harness as gh
+from oracle import dad_oracle, synth
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+
+
+def _cmp_loss(a, b, what):
+    assert abs(a - b) <= TOL * max(1.0, abs(b)), (what, a, b)
+
+
+@pytest.mark.parametrize("name", goldens.variants())
+def test_fused_step_matches_reference_goldens(name):
+    d, spec, cfg = goldens.load(name)
+    step = gh.make_step(cfg, anchors=d["anchors"])
+    orc = dad_oracle.DADOracle(*goldens.problem(spec), cfg, anchors=d["anchors"])
+    idx = d["w1_index"]
+    for s, epoch in goldens.schedule(d):
+        p = "s%d_" % s
+        st = goldens.state(spec, s)
+        gh.load_state(step, st)
+        orc.load_state(st)
+        inp = goldens.step_inputs(spec, s)
+        lr = float(d[p + "lr"])
+        o = gh.run_step(step, inp, epoch, lr=lr)
+        r = orc.step(inp, epoch, lr=lr)
+        for k in ("total_loss", "supervised_ce_loss", "consistency_loss", "ecda_loss"):
+            _cmp_loss(o[k], float(d[p + k]), (name, s, k))
+        assert gh.rel(o["z_clean"], d[p + "z_clean"]) < TOL, (name, s)
+        assert gh.rel(o["e_clean"], d[p + "e_clean"]) < TOL, (name, s)
+        if p + "z_strong" in d:
+            assert gh.rel(o["z_strong"], d[p + "z_strong"]) < TOL, (name, s)
+            assert gh.rel(o["z_teacher"], d[p + "z_teacher"]) < TOL, (name, s)
+            assert gh.rel(o["e_strong"], d[p + "e_strong"]) < TOL, (name, s)
+            assert gh.rel(o["e_teacher"], d[p + "e_teacher"]) < TOL, (name, s)
+            np.testing.assert_array_equal(o["pred"], np.argmax(d[p + "z_teacher"], 1))
+        if p + "mask" in d:
+            np.testing.assert_array_equal(o["mask"], d[p + "mask"])
+            assert gh.rel(o["score"], d[p + "score"]) < TOL
+            np.testing.assert_allclose(o["tau_after"], d[p + "tau_after"], atol=1e-6)
+            np.testing.assert_allclose(o["w"], d[p + "w"], atol=1e-6)
+            np.testing.assert_allclose(o["dacp"][0:4], d[p + "tau_after"], atol=1e-6)   # committed
+        elif p + "z_strong" in d:                                                      # fixed threshold
+            np.testing.assert_array_equal(o["mask"], r["mask"])
+        _cmp_loss(float(o["clip_norm"]), float(d[p + "clip_norm"]), (name, s, "clip_norm"))
+        coef = float(o["clip_coef"])
+        g = [x * np.float32(coef) for x in o["grads"]]
+        assert gh.rel(g[0].reshape(-1)[idx], d[p + "gW1c_s"]) < TOL, (name, s, "gW1")
+        assert gh.rel(g[1], d[p + "gb1c"]) < TOL, (name, s, "gb1")
+        assert gh.rel(g[2], d[p + "gW2c"]) < TOL, (name, s, "gW2")
+        assert gh.rel(g[3], d[p + "gb2c"]) < TOL, (name, s, "gb2")
+        # full tensors against the oracle (pre-clip grads)
+        for a, b_ in zip(o["grads"], r["grads"]):
+            assert gh.rel(a, b_) < TOL, (name, s, "full grads")
+        for who in ("s", "t"):
+            prm = o["student"] if who == "s" else o["teacher"]
+            assert gh.rel(prm[0].reshape(-1)[idx], d[p + who + "W1_s"]) < TOL
+            assert gh.rel(prm[1], d[p + who + "b1"]) < TOL
+            assert gh.rel(prm[2], d[p + who + "W2"]) < TOL
+            assert gh.rel(prm[3], d[p + who + "b2"]) < TOL
+        assert gh.rel(o["student"][0], r["student"][0]) < TOL
+        assert gh.rel(o["teacher"][0], r["teacher"][0]) < TOL
+        assert gh.rel(o["exp_avg"][1], d[p + "exp_avg_b1"]) < TOL
+        assert gh.rel(o["exp_avg_sq"][2], d[p + "exp_avg_sq_W2"]) < TOL
+    # epoch-end quality update over the post-warm-up steps' certainty statistics
+    n = int(d["epoch_end_after_step"])
+    with torch.no_grad():
+        step.dacp[4:8].copy_(torch.from_numpy(goldens.state(spec, n)["Q"]))
+    np.testing.assert_array_equal(step.dacp[12:16].cpu().numpy(), d["epoch_end_counts"])
+    step.epoch_end()
+    np.testing.assert_allclose(step.dacp[4:8].cpu().numpy(), d["epoch_end_Q"], atol=2e-6)
+    assert float(step.dacp[8:16].abs().sum()) == 0.0
+
+
+def _problem(B, T, seed=5, Bn=None, Tn=None, ragged=True, snr=5.0):
+    """Inputs with independent clean/noisy geometry (the reference collates them separately)."""
+    Bn = B if Bn is None else Bn
+    Tn = T if Tn is None else Tn
+    _, _, _, _, P = synth.init_weights(seed)
+    xc, mc, yc = synth.make_batch(P, seed * 11 + 1, B, T, ragged=ragged)
+    xn, mn, yn = synth.make_batch(P, seed * 11 + 2, Bn, Tn, snr_db=snr, noisy=True, ragged=ragged, label_shift=1)
+    dr = synth.make_draws(seed * 11 + 3, Bn, Tn)
+    dr["keep1"] = synth.make_draws(seed * 11 + 4, B, 1)["keep1"]
+    return dict(xc=xc, mc=mc, yc=yc, xn=xn, mn=mn, yn=yn, **dr)
+
+
+EDGE = [
+    dict(B=1, T=1, Bn=2, Tn=3),          # smallest shapes, gates closed
+    dict(B=5, T=33, Bn=7, Tn=31),        # slab boundary crossings, Bc != Bn, Tc != Tn
+    dict(B=16, T=64, Bn=16, Tn=64),      # exact slab multiples
+    dict(B=12, T=45, Bn=20, Tn=70, ragged=False),
+    dict(B=64, T=40, Bn=64, Tn=40),
+]
+
+
+@pytest.mark.parametrize("geom", EDGE, ids=lambda g: "B%dT%d_Bn%dTn%d" % (g["B"], g["T"], g["Bn"], g["Tn"]))
+@pytest.mark.parametrize("flavor", ["iemocap", "casia_ecda"])
+def test_fused_step_edge_geometries_match_oracle(geom, flavor):
+    if flavor == "casia_ecda":
+        cfg = dad_oracle.make_cfg("casia", USE_ECDA=True)
+    else:
+        cfg = dad_oracle.make_cfg("iemocap")
+    g = dict(geom)
+    ragged = g.pop("ragged", True)
+    inp = _problem(ragged=ragged, **g)
+    st = synth.make_state(3, 1)
+    step = gh.make_step(cfg)
+    orc = dad_oracle.DADOracle(*synth.init_weights(3)[:4], cfg)
+    for epoch in (0, 60):
+        gh.load_state(step, st)
+        orc.load_state(st)
+        o = gh.run_step(step, inp, epoch)
+        r = orc.step(inp, epoch)
+        for k in ("total_loss", "supervised_ce_loss", "consistency_loss", "ecda_loss"):
+            _cmp_loss(o[k], r[k], (geom, epoch, k))
+        assert gh.rel(o["z_clean"], r["z_clean"]) < TOL
+        if epoch >= 30:
+            assert gh.rel(o["z_strong"], r["z_strong"]) < TOL
+            np.testing.assert_array_equal(o["mask"], r["mask"])
+        for a, b_ in zip(o["grads"], r["grads"]):
+            assert gh.rel(a, b_) < TOL, (geom, epoch)
+        assert gh.rel(o["student"][0], r["student"][0]) < TOL
+
+
+def test_bf16_step_close_to_oracle():
+    """BF16 MFMA mode: embeddings/logits within bf16 rounding of the fp32 oracle."""
+    cfg = dad_oracle.make_cfg("iemocap")
+    inp = _problem(B=32, T=96, seed=9)
+    st = synth.make_state(9, 2)
+    step = gh.make_step(cfg, precision="bf16")
+    orc = dad_oracle.DADOracle(*synth.init_weights(9)[:4], cfg)
+    gh.load_state(step, st)
+    orc.load_state(st)
+    o = gh.run_step(step, inp, 60)
+    r = orc.step(inp, 60)
+    assert gh.rel(o["e_clean"], r["e_clean"]) < 2e-2
+    assert gh.rel(o["z_clean"], r["z_clean"]) < 2e-2
+    assert gh.rel(o["z_strong"], r["z_strong"]) < 2e-2
+    assert abs(o["supervised_ce_loss"] - r["supervised_ce_loss"]) < 2e-2 * max(1, abs(r["supervised_ce_loss"]))
+    # gradient direction agrees (bf16 operands, fp32 accumulate)
+    g1 = np.concatenate([x.reshape(-1) for x in o["grads"]]).astype(np.float64)
+    g2 = np.concatenate([x.reshape(-1) for x in r["grads"]]).astype(np.float64)
+    if np.array_equal(o["mask"], r["mask"]):
+        cos = g1 @ g2 / (np.linalg.norm(g1) * np.linalg.norm(g2))
+        assert cos > 0.99, cos
+
+
+def test_modular_encoder_matches_torch_fp32():
+    """Emotion2VecEncoder forward/backward (HIP) vs a plain PyTorch fp32 reference of the op."""
+    import dadpkg
+    p = dadpkg.pkg()
+    torch.manual_seed(0)
+    m = p.SSRLModel().cuda()
+    B, T = 6, 37
+    x = torch.randn(B, T, 768, device="cuda")
+    pad = torch.zeros(B, T, dtype=torch.bool, device="cuda")
+    pad[1, 20:] = True
+    pad[4, 5:] = True
+    enc = m.student_encoder
+    e = enc(x, pad)
+    W = enc.pre_net.weight.detach().clone().requires_grad_(True)
+    b = enc.pre_net.bias.detach().clone().requires_grad_(True)
+    h = torch.relu(x @ W.T + b) * (~pad).unsqueeze(-1).float()
+    ref = h.sum(1) / (~pad).float().sum(1, keepdim=True).clamp(min=1.0)
+    assert gh.rel(e.detach().cpu(), ref.detach().cpu()) < 1e-5
+    g = torch.randn(B, 256, device="cuda")
+    (e * g).sum().backward()
+    (ref * g).sum().backward()
+    assert gh.rel(enc.pre_net.weight.grad.cpu(), W.grad.cpu()) < 1e-5
+    assert gh.rel(enc.pre_net.bias.grad.cpu(), b.grad.cpu()) < 1e-5
+    # predict / get_embeddings (eval path) and the teacher EMA entry point
+    logits = m.predict(x, pad)
+    assert logits.shape == (B, 4)
+    t0 = m.teacher_flat.clone()
+    with torch.no_grad():
+        m.student_flat.add_(1.0)
+    m.update_teacher_ema()
+    exp = t0 * np.float32(0.99) + m.student_flat * np.float32(1.0 - 0.99)
+    assert gh.rel(m.teacher_flat.cpu(), exp.cpu()) < 1e-6
