@@ -404,7 +404,7 @@ class DADOracle:
             inp = dict(inp)
             H = W1.shape[0]
             inp["keep1"] = rng.random((B, H), dtype=np.float32) >= p
-            inp["keep2"] = rng.random((B, H), dtype=np.float32) >= p
+            inp["keep2"] = rng.random((inp["xn"].shape[0], H), dtype=np.float32) >= p
 
         # ---- clean supervised branch (I/train.py:398-403)
         ec, act_c, vlen_c = encoder_forward(xc, mc, W1, b1)
@@ -427,12 +427,12 @@ class DADOracle:
             xn, mn = inp["xn"], inp["mn"]
             if "nw" not in inp:
                 inp = dict(inp)
-                T, D = xn.shape[1], xn.shape[2]
+                Bn, T, D = xn.shape
                 inp["nw"] = rng.standard_normal(xn.shape, dtype=np.float32)
                 inp["ns"] = rng.standard_normal(xn.shape, dtype=np.float32)
                 inp["u"] = rng.random(D, dtype=np.float32)
                 mlen = int(T * cfg["TEMPORAL_MASK_RATIO"])
-                inp["start"] = rng.integers(0, max(1, T - mlen + 1), size=B)
+                inp["start"] = rng.integers(0, max(1, T - mlen + 1), size=Bn)
             xw = weak_augment(xn, inp["nw"], cfg["WEAK_NOISE_STD"])
             xs = strong_augment(xn, inp["ns"], inp["u"], inp["start"], cfg["STRONG_NOISE_STD"],
                                 p, cfg["TEMPORAL_MASK_RATIO"])
@@ -457,7 +457,7 @@ class DADOracle:
             out.update(e_teacher=et, z_teacher=zt, q=q, score=s, pred=pred, mask=maskf.astype(F32),
                        e_strong=es, z_strong=zs)
             ges = np.zeros_like(es, dtype=np.float64)
-            gzs = np.zeros((B, C))
+            gzs = np.zeros((xn.shape[0], C))
             msum = maskf.sum()
             if msum > 1:                                  # I/train.py:444
                 qd = q.astype(np.float64)

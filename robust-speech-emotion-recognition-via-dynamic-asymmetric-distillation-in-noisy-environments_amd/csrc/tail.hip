@@ -434,21 +434,17 @@ __device__ float ecda_mmd(EcdaSmem& S, const float* emb_c, const float* emb_s, f
   }
   const float mmd = (float)(red3[0] / Wss + red3[1] / Wtt - 2.0 * (red3[2] / Wst));
   __syncthreads();
-  // symmetrise: Csym_ij = C_ij + C_ji (read-only pass into rowc + second buffer-free form)
-  for (int i = tid; i < n; i += ECDA_THREADS) {
-    float r = 0.0f;
-    for (int j = 0; j < n; ++j) r += D[i * n + j] + D[j * n + i];
-    S.rowc[i] = r;
-  }
+  // dZ_i = 2 * sum_j Csym_ij (z_i - z_j),  Csym_ij = C_ij + C_ji  (the autograd form of
+  // d/dz of ||z_i - z_j||^2; summing the differences avoids the cancellation of
+  // rowsum(C) z_i - C z for near-identical same-class embeddings)
   __syncthreads();
-  // dZ_i = 2 * (rowc_i * z_i - sum_j Csym_ij z_j)
   for (int k = tid; k < n * DAD_H; k += ECDA_THREADS) {
     const int i = k / DAD_H, hh = k - i * DAD_H;
+    const float zi = zrow(i)[hh];
     float acc = 0.0f;
-    for (int j = 0; j < n; ++j) acc += (D[i * n + j] + D[j * n + i]) * zrow(j)[hh];
-    const float g = 2.0f * (S.rowc[i] * zrow(i)[hh] - acc);
+    for (int j = 0; j < n; ++j) acc += (D[i * n + j] + D[j * n + i]) * (zi - zrow(j)[hh]);
     float* dst = (i < ns ? ge_c : ge_s) + (size_t)S.idx[i] * DAD_H + hh;
-    *dst += scale * g;
+    *dst += scale * (2.0f * acc);
   }
   __syncthreads();
   return mmd;

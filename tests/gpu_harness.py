@@ -72,3 +72,51 @@ def rel(a, b):
     if a.size == 0:
         return 0.0
     return float(np.max(np.abs(a - b)) / max(1e-6, float(np.max(np.abs(b)))))
+
+
+def close_grad(a, b, what, tol_norm=1e-4, tol_elem=1e-3):
+    """Gradient / parameter check: Frobenius-relative <= tol_norm and max-relative <= tol_elem.
+
+    The ReLU' pattern is a discrete decision: a pre-activation that rounds to ~0 can
+    take the other sign on a different (equally valid) fp32 summation order, moving one
+    row's contribution in one hidden unit's gradient row.  With ~1e6 decisions per
+    branch per step that happens about once per B=64 step; it is visible elementwise but
+    not in the norm, so gradients/parameters use a norm bound plus a looser elementwise one.
+    """
+    a = np.asarray(a, np.float64).reshape(-1)
+    b = np.asarray(b, np.float64).reshape(-1)
+    if a.size == 0:
+        return
+    rn = float(np.linalg.norm(a - b) / max(1e-12, float(np.linalg.norm(b))))
+    if not rn < tol_norm:
+        raise AssertionError("%s: norm-rel %.3e (tol %.1e)" % (what, rn, tol_norm))
+    close(a, b, tol_elem, what + " [elementwise]")
+
+
+def close(a, b, tol, what):
+    """Max-relative check with a diagnostic message (index, values) on failure."""
+    a = np.asarray(a, np.float64).reshape(-1)
+    b = np.asarray(b, np.float64).reshape(-1)
+    if a.size == 0:
+        return
+    err = np.abs(a - b)
+    r = float(err.max() / max(1e-6, float(np.abs(b).max())))
+    if not r < tol:
+        i = int(err.argmax())
+        raise AssertionError("%s: rel %.3e (tol %.1e) at %d: got %.9g want %.9g; max|want| %.6g; "
+                             "n_bad(>tol) %d/%d" % (what, r, tol, i, a[i], b[i], np.abs(b).max(),
+                                                    int((err > tol * np.abs(b).max()).sum()), a.size))
+
+
+def ws_ge(step, Bc, Tc, Bn, Tn):
+    """dL/de rows [Bc+Bn][256] from the step's workspace (mirror of dad_ws_layout)."""
+    al = lambda x: (x + 255) & ~255
+    ncc, ncn = (Tc + 31) // 32, (Tn + 31) // 32
+    tpc, tpn = ncc * 32, ncn * 32
+    off = 0
+    off = al(off + 4 * (Bc * ncc + 2 * Bn * ncn) * 256)      # part_sum
+    off = al(off + 4 * (Bc * ncc + Bn * ncn) * 256)          # part_cnt
+    off = al(off + 4 * (Bc * tpc + Bn * tpn) * 8)            # bits
+    off = al(off + 4 * (Bc + Bn))                            # vlen
+    ws = step._ws
+    return ws[off:off + 4 * (Bc + Bn) * 256].view(torch.float32).view(Bc + Bn, 256).cpu().numpy()
