@@ -143,6 +143,7 @@ typedef struct dad_state {
   float* tail;                  /* [DAD_TAIL_FLOATS(Bn)] per-step outputs */
   float* emb;                   /* [B+2*Bn][256] e_clean [B], e_teacher [Bn], e_strong [Bn] */
   float* logits;                /* [B+2*Bn][4]   z_clean, z_teacher, z_strong */
+  float* losses;                /* [4] (optional) total, ce, kl, ecda of this step (rank mean) */
 } dad_state;
 
 /* --- sizing ------------------------------------------------------------------------ */

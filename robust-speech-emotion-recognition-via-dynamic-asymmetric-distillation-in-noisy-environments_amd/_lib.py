@@ -60,7 +60,7 @@ class DadBatch(ctypes.Structure):
 class DadState(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in
                 ("student", "teacher", "exp_avg", "exp_avg_sq", "grad", "w1bf_student", "w1bf_teacher",
-                 "dacp", "tail", "emb", "logits")]
+                 "dacp", "tail", "emb", "logits", "losses")]
 
 
 # exported symbols (must match include/dad.h); tests check every one is present

@@ -105,6 +105,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   float* part_cnt = ws_ptr<float>(workspace, L.part_cnt);
   uint32_t* bits = ws_ptr<uint32_t>(workspace, L.bits);
   float* vlen = ws_ptr<float>(workspace, L.vlen);
+  float* cnt_tot = ws_ptr<float>(workspace, L.cnt_tot);
   float* ge = ws_ptr<float>(workspace, L.ge);
   float* wpart = ws_ptr<float>(workspace, L.wpart);
   float* normpart = ws_ptr<float>(workspace, L.normpart);
@@ -128,8 +129,10 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   ea.part_sum = part_sum; ea.part_cnt = part_cnt; ea.bits = bits; ea.xs_bf16 = xs_bf16;
   const int nwaves = G.Bc * G.ncc + Bn * G.ncn;
   const dim3 egrid((nwaves + 3) / 4);
+  // bf16: 8-wave workgroups, 4 noisy slabs (teacher + student waves) or 8 clean slabs each
+  const dim3 egrid_bf16((Bn * G.ncn + 3) / 4 + (G.Bc * G.ncc + 7) / 8);
   if (do_encode) {
-    if (bf16) hipLaunchKernelGGL(dad_encode_bf16, egrid, dim3(256), 0, stream, ea);
+    if (bf16) hipLaunchKernelGGL(dad_encode_bf16, egrid_bf16, dim3(512), 0, stream, ea);
     else hipLaunchKernelGGL(dad_encode_f32, egrid, dim3(256), 0, stream, ea);
     DAD_TRY(hipGetLastError());
   }
@@ -145,6 +148,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   pa.key_drop1 = k.drop1; pa.key_drop2 = k.drop2;
   pa.p_drop = cfg->p_drop; pa.drop_scale = cfg->drop_scale;
   pa.emb = st->emb; pa.vlen = vlen; pa.logits = st->logits;
+  pa.part_cnt = part_cnt; pa.cnt_tot = cnt_tot;
   hipLaunchKernelGGL(dad_pool, dim3(G.Bc + Bn), dim3(256), 0, stream, pa);
   DAD_TRY(hipGetLastError());
 
@@ -155,7 +159,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   if (explicit_rng) { ta.keep1 = bt->keep1; ta.keep2 = bt->keep2; }
   ta.key_drop1 = k.drop1; ta.key_drop2 = k.drop2;
   ta.dacp = st->dacp; ta.tailf = st->tail; ta.ge = ge; ta.grad = st->grad;
-  hipLaunchKernelGGL(dad_tail, dim3(1), dim3(256), 0, stream, ta);
+  hipLaunchKernelGGL(dad_tail, dim3(1), dim3(1024), 0, stream, ta);
   DAD_TRY(hipGetLastError());
 
   // 4. ECDA (class-aware MMD + compactness + repulsion) and its embedding grads
@@ -188,7 +192,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   ra.g = G; ra.splits = splits; ra.warmup = cfg->warmup;
   ra.want_norm = cfg->dp_world == 1;
   ra.w_kl = cfg->w_kl; ra.w_ecda = cfg->w_ecda;
-  ra.wpart = wpart; ra.ge = ge; ra.vlen = vlen; ra.part_cnt = part_cnt; ra.tailf = st->tail;
+  ra.wpart = wpart; ra.ge = ge; ra.vlen = vlen; ra.cnt_tot = cnt_tot; ra.tailf = st->tail;
   ra.grad = st->grad; ra.normpart = normpart;
   hipLaunchKernelGGL(dad_reduce, dim3(193), dim3(256), 0, stream, ra);
   DAD_TRY(hipGetLastError());
@@ -234,6 +238,7 @@ int dad_step_apply(const dad_config* cfg, const dad_state* st, void* workspace, 
   oa.w1bf_student = reinterpret_cast<__bf16*>(st->w1bf_student);
   oa.w1bf_teacher = reinterpret_cast<__bf16*>(st->w1bf_teacher);
   oa.dacp = st->dacp; oa.tailf = st->tail; oa.normpart = normpart; oa.nnorm = nnorm;
+  oa.losses_out = st->losses;
   hipLaunchKernelGGL(dad_optim, dim3(nblk), dim3(256), 0, stream, oa);
   DAD_TRY(hipGetLastError());
   return DAD_OK;
@@ -312,7 +317,8 @@ int encoder_forward_impl(const float* x, const uint8_t* pad, int B, int T, const
   ea.part_cnt = ws_ptr<float>(workspace, L.part_cnt);
   ea.bits = ws_ptr<uint32_t>(workspace, L.bits);
   const dim3 egrid((B * G.ncc + 3) / 4);
-  if (precision == DAD_PREC_BF16) hipLaunchKernelGGL(dad_encode_bf16, egrid, dim3(256), 0, stream, ea);
+  if (precision == DAD_PREC_BF16)
+    hipLaunchKernelGGL(dad_encode_bf16, dim3((B * G.ncc + 7) / 8), dim3(512), 0, stream, ea);
   else hipLaunchKernelGGL(dad_encode_f32, egrid, dim3(256), 0, stream, ea);
   DAD_TRY(hipGetLastError());
   if (e_out) {
@@ -323,7 +329,8 @@ int encoder_forward_impl(const float* x, const uint8_t* pad, int B, int T, const
   return DAD_OK;
 }
 
-__global__ __launch_bounds__(256) void dad_embed_len_kernel(const uint8_t* pad, int B, int T, float* vlen) {
+__global__ __launch_bounds__(256) void dad_embed_len_kernel(const uint8_t* pad, int B, int T, int nchunk,
+                                                            const float* part_cnt, float* vlen, float* cnt_tot) {
   __shared__ float red[4];
   const int b = blockIdx.x, h = threadIdx.x;
   float l = 0.0f;
@@ -332,6 +339,9 @@ __global__ __launch_bounds__(256) void dad_embed_len_kernel(const uint8_t* pad, 
   if ((h & 63) == 0) red[h >> 6] = l;
   __syncthreads();
   if (h == 0) vlen[b] = ((red[0] + red[1]) + red[2]) + red[3];
+  float cnt = 0.0f;
+  for (int c = 0; c < nchunk; ++c) cnt += part_cnt[((size_t)b * nchunk + c) * DAD_H + h];
+  cnt_tot[(size_t)b * DAD_H + h] = cnt;
 }
 
 }  // namespace
@@ -361,7 +371,9 @@ int dad_encoder_backward(const float* x, const uint8_t* pad, int B, int T, const
   // recompute the ReLU'/valid bits and per-slab active counts (FP32 forward)
   int rc = encoder_forward_impl(x, pad, B, T, w1, b1, DAD_PREC_FP32, workspace, stream, L, nullptr, nullptr);
   if (rc) return rc;
-  hipLaunchKernelGGL(dad_embed_len_kernel, dim3(B), dim3(256), 0, stream, pad, B, T, vlen);
+  float* cnt_tot = ws_ptr<float>(workspace, L.cnt_tot);
+  hipLaunchKernelGGL(dad_embed_len_kernel, dim3(B), dim3(256), 0, stream, pad, B, T, G.ncc,
+                     ws_ptr<float>(workspace, L.part_cnt), vlen, cnt_tot);
   DAD_TRY(hipGetLastError());
   DadWgradArgs wa;
   memset(&wa, 0, sizeof(wa));
@@ -374,7 +386,7 @@ int dad_encoder_backward(const float* x, const uint8_t* pad, int B, int T, const
   DadReduceArgs ra;
   memset(&ra, 0, sizeof(ra));
   ra.g = G; ra.splits = splits; ra.warmup = 1; ra.want_norm = 0;
-  ra.wpart = wa.wpart; ra.ge = de; ra.vlen = vlen; ra.part_cnt = ws_ptr<float>(workspace, L.part_cnt);
+  ra.wpart = wa.wpart; ra.ge = de; ra.vlen = vlen; ra.cnt_tot = cnt_tot;
   ra.tailf = nullptr; ra.grad = gflat; ra.normpart = ws_ptr<float>(workspace, L.normpart);
   hipLaunchKernelGGL(dad_reduce, dim3(193), dim3(256), 0, stream, ra);
   DAD_TRY(hipGetLastError());

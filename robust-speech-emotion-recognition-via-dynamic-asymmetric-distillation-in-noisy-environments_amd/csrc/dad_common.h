@@ -138,6 +138,7 @@ struct DadWs {
   size_t part_cnt;   // f32 [Bc*ncc + Bn*ncn][H]    per-slab active-row counts (clean | strong)
   size_t bits;       // u32 [Bc*tpc + Bn*tpn][8]    ReLU' & valid bits per row and 32-wide h tile
   size_t vlen;       // f32 [Bc + Bn]               valid lengths (clean | noisy)
+  size_t cnt_tot;    // f32 [Bc + Bn][H]            active-row counts per utterance (clean | strong)
   size_t ge;         // f32 [Bc + Bn][H]            dL/de_clean | dL/de_strong
   size_t wpart;      // f32 [S][H][D]               split-K weight-gradient partial slabs
   size_t normpart;   // f32 [DAD_NORM_BLOCKS]       squared-norm partials
@@ -169,6 +170,7 @@ static inline DadWs dad_ws_layout(const DadGeom& g, int splits, int precision) {
   w.part_cnt = off; off = dad_align(off + sizeof(float) * (nsc + nsn) * DAD_H);
   w.bits = off;     off = dad_align(off + sizeof(uint32_t) * ((size_t)g.Bc * g.tpc + (size_t)g.Bn * g.tpn) * DAD_HT);
   w.vlen = off;     off = dad_align(off + sizeof(float) * nb);
+  w.cnt_tot = off;  off = dad_align(off + sizeof(float) * nb * DAD_H);
   w.ge = off;       off = dad_align(off + sizeof(float) * nb * DAD_H);
   w.wpart = off;    off = dad_align(off + sizeof(float) * (size_t)splits * DAD_H * DAD_D);
   w.normpart = off; off = dad_align(off + sizeof(float) * DAD_NORM_BLOCKS);

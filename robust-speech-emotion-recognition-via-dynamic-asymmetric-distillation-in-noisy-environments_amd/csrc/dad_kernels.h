@@ -28,6 +28,7 @@ struct DadPoolArgs {
   uint32_t key_drop1, key_drop2;
   float p_drop, drop_scale;
   float* emb; float* vlen; float* logits;
+  const float* part_cnt; float* cnt_tot;
 };
 
 struct DadTailArgs {
@@ -69,7 +70,7 @@ struct DadReduceArgs {
   DadGeom g;
   int splits, warmup, want_norm;
   float w_kl, w_ecda;
-  const float* wpart; const float* ge; const float* vlen; const float* part_cnt;
+  const float* wpart; const float* ge; const float* vlen; const float* cnt_tot;
   const float* tailf;
   float* grad; float* normpart;
 };
@@ -79,6 +80,7 @@ struct DadOptimArgs {
   float* student; float* teacher; float* exp_avg; float* exp_avg_sq;
   float* grad; __bf16* w1bf_student; __bf16* w1bf_teacher;
   float* dacp; float* tailf; const float* normpart; int nnorm;
+  float* losses_out;
 };
 
 __global__ void dad_encode_f32(DadEncodeArgs a);

@@ -210,6 +210,62 @@ __global__ __launch_bounds__(256) void dad_encode_f32(DadEncodeArgs a) {
 }
 
 // ------------------------------------------------------------ BF16 (throughput mode)
+// One wave = one GEMM on one 32-row slab: 32 rows x 256 hidden units x K=768 with
+// v_mfma_f32_32x32x16_bf16 (8 accumulator tiles = 128 VGPRs -> 2 waves per SIMD).
+// Workgroup = 8 waves sharing W1 through LDS:
+//   noisy workgroup: 4 slabs; waves 0-3 teacher (weak aug, teacher W1), waves 4-7 student
+//                    (strong aug, student W1) on the SAME slabs, so the second read of a
+//                    slab's rows hits the CU's L1/L2 instead of HBM;
+//   clean workgroup: 8 slabs, student W1.
+// W1 streams through a double-buffered LDS ring in 32-column chunks ([256 h][4 x 16 B],
+// 16-B chunk position XOR-swizzled by (h>>2)&3 so the ds_read_b128 B-fragment reads of
+// 16 consecutive rows are bank-conflict free); x is prefetched two chunks ahead in
+// registers (8 KB in flight per wave) and augmented + rounded to bf16 in registers.
+#define ENC_WAVES 8
+#define ENC_KC 32
+#define ENC_NCH (DAD_D / ENC_KC)
+#define ENC_WCHUNK_BYTES (DAD_H * ENC_KC * 2)   // 16 KB per weight per chunk
+
+struct Bf16Geom {
+  int kind;        // 0 clean-student, 1 noisy-teacher (weak), 2 noisy-student (strong), -1 idle
+  int b, c, T;
+  size_t row0, sum_slab;
+  long cnt_slab, bits_row;
+};
+
+__device__ __forceinline__ Bf16Geom bf16_geom(const DadEncodeArgs& a, int& noisy_wg) {
+  const DadGeom& g = a.g;
+  const int wv = threadIdx.x >> 6;
+  const int nsn = a.warmup ? 0 : g.Bn * g.ncn;
+  const int nwg_n = (nsn + 3) / 4;
+  Bf16Geom e;
+  noisy_wg = (int)blockIdx.x < nwg_n;
+  int slab;
+  if (noisy_wg) {
+    slab = blockIdx.x * 4 + (wv & 3);
+    e.kind = slab < nsn ? (wv < 4 ? 1 : 2) : -1;
+  } else {
+    slab = (blockIdx.x - nwg_n) * 8 + wv;
+    e.kind = slab < g.Bc * g.ncc ? 0 : -1;
+  }
+  if (e.kind < 0) { e.b = e.c = 0; e.T = 1; e.row0 = 0; e.sum_slab = 0; e.cnt_slab = -1; e.bits_row = -1; return e; }
+  const int nc = e.kind == 0 ? g.ncc : g.ncn;
+  e.T = e.kind == 0 ? g.Tc : g.Tn;
+  e.b = slab / nc;
+  e.c = slab - e.b * nc;
+  e.row0 = (size_t)e.b * e.T;
+  const size_t nsc = (size_t)g.Bc * g.ncc;
+  if (e.kind == 0) {
+    e.sum_slab = slab; e.cnt_slab = slab; e.bits_row = (long)e.b * g.tpc + (long)e.c * DAD_SLAB;
+  } else if (e.kind == 1) {
+    e.sum_slab = nsc + slab; e.cnt_slab = -1; e.bits_row = -1;
+  } else {
+    e.sum_slab = nsc + (size_t)g.Bn * g.ncn + slab; e.cnt_slab = (long)(nsc + slab);
+    e.bits_row = (long)g.Bc * g.tpc + (long)e.b * g.tpn + (long)e.c * DAD_SLAB;
+  }
+  return e;
+}
+
 __device__ __forceinline__ bf16x8 to_bf16x8(f32x4 lo, f32x4 hi) {
   bf16x8 r;
 #pragma unroll
@@ -220,66 +276,150 @@ __device__ __forceinline__ bf16x8 to_bf16x8(f32x4 lo, f32x4 hi) {
   return r;
 }
 
-__global__ __launch_bounds__(256) void dad_encode_bf16(DadEncodeArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds_bits_all[4][DAD_SLAB * DAD_HT];
-  const int lane = threadIdx.x & 63;
-  const int wv = threadIdx.x >> 6;
-  const int wid = blockIdx.x * 4 + wv;
-  if (wid >= (a.warmup ? 0 : a.g.Bn * a.g.ncn) + a.g.Bc * a.g.ncc) return;
-  const EncodeGeom g = encode_geom(a, wid);
+// stage one 32-column chunk of (one or two) bf16 W1 matrices: global -> registers
+struct WStage {
+  uint4 v[2][2];
+};
+__device__ __forceinline__ void w_load(WStage& w, const __bf16* W0, const __bf16* W1, int ch, bool two) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int item = tid + q * 512;               // 1024 16-B pieces per matrix per chunk
+    const int h = item >> 2, c = item & 3;
+    const size_t off = (size_t)h * DAD_D + ch * ENC_KC + 8 * c;
+    w.v[0][q] = *reinterpret_cast<const uint4*>(W0 + off);
+    if (two) w.v[1][q] = *reinterpret_cast<const uint4*>(W1 + off);
+  }
+}
+__device__ __forceinline__ void w_store(const WStage& w, char* buf, bool two) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int item = tid + q * 512;
+    const int h = item >> 2, c = item & 3;
+    const int pos = c ^ ((h >> 2) & 3);
+    *reinterpret_cast<uint4*>(buf + h * 64 + pos * 16) = w.v[0][q];
+    if (two) *reinterpret_cast<uint4*>(buf + ENC_WCHUNK_BYTES + h * 64 + pos * 16) = w.v[1][q];
+  }
+}
+
+struct XChunk {
+  f32x4 v[2][2];    // [k-step][lo/hi]: lane (row r, half kh) holds columns 16ks + 8kh .. +7
+};
+__device__ __forceinline__ void x_load(XChunk& x, const float* row, bool tin, int ch, int kh) {
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const int d = ch * ENC_KC + 16 * ks + 8 * kh;
+    x.v[ks][0] = tin ? *reinterpret_cast<const f32x4*>(row + d) : f32x4{};
+    x.v[ks][1] = tin ? *reinterpret_cast<const f32x4*>(row + d + 4) : f32x4{};
+  }
+}
+
+__global__ __launch_bounds__(512, 1) void dad_encode_bf16(DadEncodeArgs a) {
+  __shared__ __attribute__((aligned(16))) char wbuf[2][2 * ENC_WCHUNK_BYTES];
+  __shared__ __attribute__((aligned(16))) uint32_t lds_bits_all[ENC_WAVES][DAD_SLAB * DAD_HT];
+  __shared__ float featkeep[DAD_D];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int i = lane & 31, kh = lane >> 5;
-  const int t = g.c * DAD_SLAB + i;
-  const bool tin = t < g.T;
-  const int grow = (int)g.row0 + (tin ? t : 0);
-  const uint8_t* pad = g.noisy ? a.mn : a.mc;
-  const bool valid = tin && pad[g.row0 + t] == 0;
+  int noisy_wg;
+  const Bf16Geom e = bf16_geom(a, noisy_wg);
+  const bool two = noisy_wg;
+  const __bf16* W0 = noisy_wg ? a.w1bf_teacher : a.w1bf_student;   // buffer half 0
+  const __bf16* W1 = a.w1bf_student;                               // buffer half 1 (noisy only)
+  // strong-aug feature keep flags for all 768 channels (I/utils.py:343), once per workgroup
+  if (noisy_wg)
+    for (int d = threadIdx.x; d < DAD_D; d += 512) featkeep[d] = feat_keep(a, d);
+  // per-wave row state
+  const bool active = e.kind >= 0;
+  const int t = e.c * DAD_SLAB + i;
+  const bool tin = active && t < e.T;
+  const int grow = (int)e.row0 + (tin ? t : 0);
+  bool valid = false;
+  if (tin) valid = (e.kind == 0 ? a.mc : a.mn)[e.row0 + t] == 0;
   const uint32_t vbits = (uint32_t)__ballot(valid);
-  const float* X = (g.noisy ? a.xn : a.xc) + (size_t)grow * DAD_D + 8 * kh;
+  const float* xrow = (e.kind == 0 ? a.xc : a.xn) + (size_t)grow * DAD_D;
   bool tzero = false;
-  if (g.noisy && a.mask_len > 0) {
-    const int st = tmask_start(a, g.b);
+  if (e.kind == 2 && a.mask_len > 0) {
+    const int st = tmask_start(a, e.b);
     tzero = t >= st && t < st + a.mask_len;
   }
-  // bf16 fragments: lane (row/col i, half kh) holds k = 8*kh .. 8*kh+7 of the 16-deep step
-  const bf16x8* Ws = reinterpret_cast<const bf16x8*>(a.w1bf_student + (size_t)i * DAD_D + 8 * kh);
-  const bf16x8* Wt = reinterpret_cast<const bf16x8*>(a.w1bf_teacher + (size_t)i * DAD_D + 8 * kh);
-  constexpr int HT_STRIDE = 32 * DAD_D / 8;   // bf16x8 elements between h tiles
-  f32x16 acc0[DAD_HT], acc1[DAD_HT];
+  const int wsel = (two && wv >= 4) ? ENC_WCHUNK_BYTES : 0;   // student half of a noisy workgroup
+
+  f32x16 acc[DAD_HT];
 #pragma unroll
-  for (int ht = 0; ht < DAD_HT; ++ht) {
-    acc0[ht] = f32x16{};
-    acc1[ht] = f32x16{};
-  }
-  if (!g.noisy) {
-    for (int d0 = 0; d0 < DAD_D; d0 += 16) {
-      f32x4 lo = tin ? ld4(X + d0) : f32x4{};
-      f32x4 hi = tin ? ld4(X + d0 + 4) : f32x4{};
-      const bf16x8 xa = to_bf16x8(lo, hi);
+  for (int ht = 0; ht < DAD_HT; ++ht) acc[ht] = f32x16{};
+
+  // prologue: W chunk 0 -> LDS, x chunks 0 and 1 -> registers
+  WStage ws;
+  w_load(ws, W0, W1, 0, two);
+  XChunk xa, xb;
+  x_load(xa, xrow, tin, 0, kh);
+  x_load(xb, xrow, tin, 1, kh);
+  w_store(ws, wbuf[0], two);
+  __syncthreads();
+
+  auto compute = [&](int ch, const XChunk& x) {
+    const char* wb = wbuf[ch & 1] + wsel;
 #pragma unroll
-      for (int ht = 0; ht < DAD_HT; ++ht) {
-        const bf16x8 w = Ws[ht * HT_STRIDE + d0 / 8];
-        acc0[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa, w, acc0[ht], 0, 0, 0);
+    for (int ks = 0; ks < 2; ++ks) {
+      const int d = ch * ENC_KC + 16 * ks + 8 * kh;
+      f32x4 lo = x.v[ks][0], hi = x.v[ks][1];
+      if (e.kind == 1 || e.kind == 2) {
+        f32x4 nlo, nhi;
+        const bool strong = e.kind == 2;
+        if (a.nw) {
+          const float* src = (strong ? a.ns : a.nw) + (size_t)grow * DAD_D + d;
+          nlo = *reinterpret_cast<const f32x4*>(src);
+          nhi = *reinterpret_cast<const f32x4*>(src + 4);
+        } else {
+          const uint32_t key = strong ? a.key_strong : a.key_weak;
+          nlo = dad_normal4(key, (uint32_t)grow, (uint32_t)d);
+          nhi = dad_normal4(key, (uint32_t)grow, (uint32_t)(d + 4));
+        }
+        const float sd = strong ? a.strong_std : a.weak_std;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          // op order of the reference: noise*std, add; then feature mask; then temporal zero
+          float v0 = lo[q] + nlo[q] * sd;
+          float v1 = hi[q] + nhi[q] * sd;
+          if (strong) {
+            v0 = tzero ? 0.0f : v0 * featkeep[d + q];
+            v1 = tzero ? 0.0f : v1 * featkeep[d + 4 + q];
+          }
+          lo[q] = v0;
+          hi[q] = v1;
+        }
+      }
+      const bf16x8 xa8 = to_bf16x8(lo, hi);
+      if (e.kind == 2 && tin) *reinterpret_cast<bf16x8*>(a.xs_bf16 + (size_t)grow * DAD_D + d) = xa8;
+      if (active) {
+        const int c16 = ks * 2 + kh;
+#pragma unroll
+        for (int ht = 0; ht < DAD_HT; ++ht) {
+          const int h = ht * 32 + i;
+          const bf16x8 w = *reinterpret_cast<const bf16x8*>(wb + h * 64 + ((c16 ^ ((h >> 2) & 3)) * 16));
+          acc[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa8, w, acc[ht], 0, 0, 0);
+        }
       }
     }
-  } else {
-    for (int d0 = 0; d0 < DAD_D; d0 += 16) {
-      const int d = d0 + 8 * kh;
-      f32x4 lo = tin ? ld4(X + d0) : f32x4{};
-      f32x4 hi = tin ? ld4(X + d0 + 4) : f32x4{};
-      f32x4 wlo, whi, slo, shi;
-      augment4(a, lo, grow, d, tzero, wlo, slo);
-      augment4(a, hi, grow, d + 4, tzero, whi, shi);
-      const bf16x8 xw = to_bf16x8(wlo, whi);
-      const bf16x8 xs = to_bf16x8(slo, shi);
-      if (tin) *reinterpret_cast<bf16x8*>(a.xs_bf16 + (size_t)grow * DAD_D + d) = xs;
-#pragma unroll
-      for (int ht = 0; ht < DAD_HT; ++ht) {
-        const bf16x8 wt = Wt[ht * HT_STRIDE + d0 / 8];
-        const bf16x8 ws = Ws[ht * HT_STRIDE + d0 / 8];
-        acc0[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xw, wt, acc0[ht], 0, 0, 0);
-        acc1[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xs, ws, acc1[ht], 0, 0, 0);
-      }
-    }
+  };
+
+  for (int ch = 0; ch < ENC_NCH; ch += 2) {
+    // chunk ch: x in xa, W in wbuf[0]
+    if (ch + 1 < ENC_NCH) w_load(ws, W0, W1, ch + 1, two);
+    compute(ch, xa);
+    if (ch + 2 < ENC_NCH) x_load(xa, xrow, tin, ch + 2, kh);
+    if (ch + 1 < ENC_NCH) w_store(ws, wbuf[1], two);
+    __syncthreads();
+    if (ch + 1 >= ENC_NCH) break;
+    // chunk ch+1: x in xb, W in wbuf[1]
+    if (ch + 2 < ENC_NCH) w_load(ws, W0, W1, ch + 2, two);
+    compute(ch + 1, xb);
+    if (ch + 3 < ENC_NCH) x_load(xb, xrow, tin, ch + 3, kh);
+    if (ch + 2 < ENC_NCH) w_store(ws, wbuf[0], two);
+    __syncthreads();
   }
-  encode_finish(a, g, acc0, acc1, vbits, lds_bits_all[wv]);
+  if (!active) return;
+  const float* bias = e.kind == 1 ? a.b1_teacher : a.b1_student;
+  encode_epilogue(a, acc, bias, e.sum_slab, e.cnt_slab, e.bits_row, vbits, lds_bits_all[wv]);
 }

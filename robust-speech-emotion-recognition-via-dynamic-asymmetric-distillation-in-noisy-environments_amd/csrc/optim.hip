@@ -30,6 +30,8 @@ __global__ __launch_bounds__(256) void dad_optim(DadOptimArgs a) {
         a.tailf[DAD_T_CLIPCOEF] = coef;
         const float* ex = a.grad + DAD_NPARAM;
         a.tailf[DAD_T_TOTAL] = ex[12];
+        if (a.losses_out)
+          for (int k = 0; k < 4; ++k) a.losses_out[k] = ex[12 + k];
       }
     }
   }

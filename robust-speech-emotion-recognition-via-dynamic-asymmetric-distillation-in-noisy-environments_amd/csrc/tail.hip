@@ -16,7 +16,7 @@
 #include "dad_common.h"
 #include "dad_kernels.h"
 
-#define TAIL_THREADS 256
+#define TAIL_THREADS 1024
 
 __device__ __forceinline__ float block_sum_f(float v, float* red) {
   v = dad_wave_sum(v);
@@ -85,6 +85,13 @@ __global__ __launch_bounds__(256) void dad_pool(DadPoolArgs a) {
     for (int c = 0; c < nc; ++c) s += a.part_sum[(slab0 + c) * DAD_H + h];
     const float e = s / fmaxf(len, 1.0f);
     a.emb[(size_t)erow * DAD_H + h] = e;
+    if (k == nbr - 1) {
+      // active-row count per (utterance, h) of the branch that gets a gradient (clean / strong)
+      const size_t cslab0 = noisy ? nsc + (size_t)b * g.ncn : (size_t)b * g.ncc;
+      float cnt = 0.0f;
+      for (int c = 0; c < nc; ++c) cnt += a.part_cnt[(cslab0 + c) * DAD_H + h];
+      a.cnt_tot[(size_t)(noisy ? g.Bc + b : b) * DAD_H + h] = cnt;
+    }
     float d;
     const bool teacher = noisy && k == 0;
     if (!noisy) d = e * keep_value(a.keep1, a.key_drop1, b, h, a.p_drop, a.drop_scale);
@@ -114,8 +121,9 @@ __global__ __launch_bounds__(TAIL_THREADS) void dad_tail(DadTailArgs a) {
   const int B = cfg.B;                       // clean utterances
   const int Bn = cfg.warmup ? 0 : cfg.Bn;    // noisy utterances
   const int tid = threadIdx.x;
-  __shared__ double dred[8];
-  __shared__ float fred[8];
+  __shared__ double dred[16];
+  __shared__ float fred[16];
+  __shared__ float gwp[4][DAD_C][DAD_H];              // classifier weight-grad partials
   __shared__ float gz[2][DAD_MAX_BATCH][DAD_C];       // dL/dz clean, strong
   __shared__ float sq[DAD_MAX_BATCH][DAD_C];          // teacher probs
   __shared__ float ss[DAD_MAX_BATCH];                 // certainty scores
@@ -292,34 +300,42 @@ __global__ __launch_bounds__(TAIL_THREADS) void dad_tail(DadTailArgs a) {
     for (int c = 0; c < 4; ++c) { tf[DAD_T_ECDA_TERM + c] = 0.0f; tf[DAD_T_ECDA_GATE + c] = 0.0f; }
   }
   __syncthreads();
-  // ---- classifier backward (nn.Linear + nn.Dropout, I/model.py:62-63), both passes
-  const int h = tid;   // TAIL_THREADS == H
+  // ---- classifier backward (nn.Linear + nn.Dropout, I/model.py:62-63), both passes.
+  // thread (h, q): hidden unit h, utterances b = q mod 4 (independent loads, 4-way split)
+  const int h = tid & (DAD_H - 1), qg = tid >> 8;
   const float* W2 = a.student + DAD_OFF_W2;
   const float w2h[4] = {W2[h], W2[DAD_H + h], W2[2 * DAD_H + h], W2[3 * DAD_H + h]};
   const float* e0 = a.emb;
   const float* e2 = a.emb + (size_t)(B + Bn) * DAD_H;
-  double gw[4] = {0, 0, 0, 0};
-  for (int b = 0; b < B; ++b) {
+  float gw[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  for (int b = qg; b < B; b += 4) {
     const float k1 = keep_value(a.keep1, a.key_drop1, b, h, cfg.p_drop, cfg.drop_scale);
     const float d0 = e0[(size_t)b * DAD_H + h] * k1;
     float g0 = 0.0f;
+#pragma unroll
     for (int c = 0; c < 4; ++c) {
-      gw[c] += (double)gz[0][b][c] * d0;
+      gw[c] += gz[0][b][c] * d0;
       g0 += w2h[c] * gz[0][b][c];
     }
     a.ge[(size_t)b * DAD_H + h] = g0 * k1;
   }
-  for (int b = 0; b < Bn; ++b) {
+  for (int b = qg; b < Bn; b += 4) {
     const float k2 = keep_value(a.keep2, a.key_drop2, b, h, cfg.p_drop, cfg.drop_scale);
     const float d2 = e2[(size_t)b * DAD_H + h] * k2;
     float g2 = 0.0f;
+#pragma unroll
     for (int c = 0; c < 4; ++c) {
-      gw[c] += (double)gz[1][b][c] * d2;
+      gw[c] += gz[1][b][c] * d2;
       g2 += w2h[c] * gz[1][b][c];
     }
     a.ge[(size_t)(B + b) * DAD_H + h] = g2 * k2;
   }
-  for (int c = 0; c < 4; ++c) a.grad[DAD_OFF_W2 + c * DAD_H + h] = (float)gw[c];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) gwp[qg][c][h] = gw[c];
+  __syncthreads();
+  if (qg == 0)
+    for (int c = 0; c < 4; ++c)
+      a.grad[DAD_OFF_W2 + c * DAD_H + h] = ((gwp[0][c][h] + gwp[1][c][h]) + gwp[2][c][h]) + gwp[3][c][h];
   if (tid < 4) {
     double s = 0.0;
     for (int b = 0; b < B; ++b) s += (double)gz[0][b][tid];
@@ -346,7 +362,39 @@ struct EcdaSmem {
   double dred[8];
   float fred[8];
   int cnt_clean[DAD_C], cnt_noisy[DAD_C];
+  int lab[DAD_MAX_BATCH];         // clean labels
+  int prd[DAD_MAX_BATCH];         // noisy pseudo-labels, -1 where not masked in
+  float scr[DAD_MAX_BATCH];       // noisy certainty scores
+  int wcount[ECDA_THREADS / 64];
+  int nmem;
 };
+
+// Ordered block-wide compaction: appends every i in [0, n) with flag(i) to S.idx (and
+// weight(i) to S.wt) after position `base`, in ascending i.  Returns the new length.
+template <typename Flag, typename Wgt>
+__device__ int ecda_compact(EcdaSmem& S, int n, int base, Flag flag, Wgt weight) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int c0 = 0; c0 < n; c0 += ECDA_THREADS) {
+    const int i = c0 + tid;
+    const bool f = i < n && flag(i);
+    const uint64_t bal = __ballot(f);
+    if (lane == 0) S.wcount[w] = __popcll(bal);
+    __syncthreads();
+    int pre = 0, tot = 0;
+    for (int k = 0; k < ECDA_THREADS / 64; ++k) {
+      if (k < w) pre += S.wcount[k];
+      tot += S.wcount[k];
+    }
+    if (f) {
+      const int pos = base + pre + __popcll(bal & ((1ull << lane) - 1ull));
+      S.idx[pos] = i;
+      S.wt[pos] = weight(i);
+    }
+    base += tot;
+    __syncthreads();
+  }
+  return base;
+}
 
 // mmd = t_ss + t_tt - 2 t_st of _gaussian_kernel (I/utils.py:521-563) over members
 // idx[0..ns) (clean embeddings) and idx[ns..n) (strong embeddings), plus grads
@@ -452,6 +500,7 @@ __device__ float ecda_mmd(EcdaSmem& S, const float* emb_c, const float* emb_s, f
 
 __global__ __launch_bounds__(ECDA_THREADS) void dad_ecda(DadEcdaArgs a) {
   __shared__ EcdaSmem S;
+  __shared__ float pdist[DAD_C][DAD_C];
   const dad_config& cfg = a.cfg;
   const int B = cfg.B, Bn = cfg.Bn;
   const int c = blockIdx.x, tid = threadIdx.x;
@@ -466,72 +515,69 @@ __global__ __launch_bounds__(ECDA_THREADS) void dad_ecda(DadEcdaArgs a) {
   float* ge_s = a.ge + (size_t)B * DAD_H;
   float* scratch = a.scratch + (size_t)c * (B + Bn) * (B + Bn);
   const float wscale = cfg.w_ecda;
+  // stage per-sample metadata (masked-out noisy samples get pseudo-label -1)
+  for (int b = tid; b < B; b += ECDA_THREADS) S.lab[b] = (int)a.yc[b];
+  for (int b = tid; b < Bn; b += ECDA_THREADS) {
+    S.prd[b] = mask[b] > 0.0f ? (int)predf[b] : -1;   // noisy_mask>thr re-cast: I/utils.py:573-576
+    S.scr[b] = score[b];
+  }
+  if (tid < DAD_C) { S.cnt_clean[tid] = 0; S.cnt_noisy[tid] = 0; }
+  __syncthreads();
 
   if (!cfg.class_aware) {
     // global MMD ablation: all clean vs all masked noisy, unit weights (I/utils.py:633-650)
     if (c != 0) return;
-    if (tid == 0) {
-      int n = 0;
-      for (int b = 0; b < B; ++b) { S.idx[n] = b; S.wt[n] = 1.0f; ++n; }
-      const int ns = n;
-      for (int b = 0; b < Bn; ++b)
-        if (mask[b] > 0.0f) { S.idx[n] = b; S.wt[n] = 1.0f; ++n; }
-      S.cnt_clean[0] = ns;
-      S.cnt_noisy[0] = n - ns;
-    }
-    __syncthreads();
-    const int ns = S.cnt_clean[0], nt = S.cnt_noisy[0];
+    int n = ecda_compact(S, B, 0, [](int) { return true; }, [](int) { return 1.0f; });
+    const int ns = n;
+    n = ecda_compact(S, Bn, n, [&](int i) { return S.prd[i] >= 0; }, [](int) { return 1.0f; });
+    const int nt = n - ns;
     if (ns >= 2 && nt >= 2) {
-      const float mmd = ecda_mmd(S, emb_c, emb_s, ge_c, ge_s, ns, ns + nt, scratch, wscale);
+      const float mmd = ecda_mmd(S, emb_c, emb_s, ge_c, ge_s, ns, n, scratch, wscale);
       if (tid == 0) { a.tail_terms[0] = mmd; a.tail_terms[DAD_T_ECDA_GATE - DAD_T_ECDA_TERM] = 1.0f; }
     }
     return;
   }
 
-  // class-aware path.  In fixed-threshold mode class_weights_wce = ones(B) (I/train.py:420)
-  // so the loop runs over range(B): only classes < min(B, C) can have members.
+  // class-aware path.  In fixed-threshold mode class_weights_wce = ones(Bn) (I/train.py:420)
+  // so the loop runs over range(Bn): only classes < min(Bn, C) can have members.
   const int ncls = cfg.use_dacp ? DAD_C : (Bn < DAD_C ? Bn : DAD_C);
   if (c >= ncls) return;
-  // membership counts and noisy centroids of every class (needed for repulsion)
-  if (tid < DAD_C) {
-    int nc = 0, nn = 0;
-    if (tid < ncls) {
-      for (int b = 0; b < B; ++b) nc += a.yc[b] == tid;
-      for (int b = 0; b < Bn; ++b) nn += ((int)predf[b] == tid && mask[b] > 0.0f);
-    }
-    S.cnt_clean[tid] = nc;
-    S.cnt_noisy[tid] = nn;
-  }
+  for (int b = tid; b < B; b += ECDA_THREADS)
+    if (S.lab[b] >= 0 && S.lab[b] < ncls) atomicAdd(&S.cnt_clean[S.lab[b]], 1);
+  for (int b = tid; b < Bn; b += ECDA_THREADS)
+    if (S.prd[b] >= 0 && S.prd[b] < ncls) atomicAdd(&S.cnt_noisy[S.prd[b]], 1);
   __syncthreads();
+  // noisy centroids of every class in one pass (needed for the repulsion term)
   {
     const int hh = tid;
-    for (int k = 0; k < DAD_C; ++k) {
-      float s = 0.0f;
-      if (S.cnt_noisy[k] > 0)
-        for (int b = 0; b < Bn; ++b)
-          if ((int)predf[b] == k && mask[b] > 0.0f) s += emb_s[(size_t)b * DAD_H + hh];
-      S.cent[k][hh] = S.cnt_noisy[k] > 0 ? s / (float)S.cnt_noisy[k] : 0.0f;
+    float cs[DAD_C] = {0.0f, 0.0f, 0.0f, 0.0f};
+    // unconditional, unrolled loads: a data-dependent skip here serialised one global-load
+    // latency per utterance
+#pragma unroll 8
+    for (int b = 0; b < Bn; ++b) {
+      const int pk = S.prd[b];
+      const float e = emb_s[(size_t)b * DAD_H + hh];
+#pragma unroll
+      for (int k = 0; k < DAD_C; ++k) cs[k] += pk == k ? e : 0.0f;
     }
+#pragma unroll
+    for (int k = 0; k < DAD_C; ++k) S.cent[k][hh] = S.cnt_noisy[k] > 0 ? cs[k] / (float)S.cnt_noisy[k] : 0.0f;
   }
   __syncthreads();
-  // class attention (I/utils.py:597-599) over the ncls class weights
+  // class attention (I/utils.py:597-599)
   const float* w = tf + DAD_T_W;
-  float wmean = 0.0f, att_c;
   float att[DAD_C];
   if (cfg.use_dacp) {
-    wmean = (((w[0] + w[1]) + w[2]) + w[3]) / 4.0f;
+    const float wmean = (((w[0] + w[1]) + w[2]) + w[3]) / 4.0f;
     for (int k = 0; k < DAD_C; ++k) att[k] = expf(cfg.ecda_att_lambda * (wmean - w[k]));
   } else {
     for (int k = 0; k < DAD_C; ++k) att[k] = 1.0f;
   }
-  att_c = att[c];
+  const float att_c = att[c];
   // repulsion over valid centroids (I/utils.py:582-595)
   int nvalid = 0;
   for (int k = 0; k < ncls; ++k) nvalid += S.cnt_noisy[k] > 0;
-  float rep = 0.0f;
   const int npairs = nvalid * (nvalid - 1) / 2;
-  // pairwise centroid distances: computed by wave 0 lanes, small (<= 6 pairs)
-  __shared__ float pdist[DAD_C][DAD_C];
   if (tid < DAD_C * DAD_C) {
     const int p = tid / DAD_C, q = tid % DAD_C;
     float d = 0.0f;
@@ -545,45 +591,41 @@ __global__ __launch_bounds__(ECDA_THREADS) void dad_ecda(DadEcdaArgs a) {
     pdist[p][q] = d;
   }
   __syncthreads();
+  float rep = 0.0f;
   if (nvalid > 1) {
-    float s = 0.0f;
+    float sp = 0.0f;
     for (int p = 0; p < ncls; ++p)
       for (int q = p + 1; q < ncls; ++q)
-        if (S.cnt_noisy[p] > 0 && S.cnt_noisy[q] > 0) s += pdist[p][q];
-    rep = -s / (float)npairs;
+        if (S.cnt_noisy[p] > 0 && S.cnt_noisy[q] > 0) sp += pdist[p][q];
+    rep = -sp / (float)npairs;
   }
-  int gated[DAD_C];
+  bool gated[DAD_C];
   float rep_coef = 0.0f;
   for (int k = 0; k < DAD_C; ++k) {
     gated[k] = k < ncls && S.cnt_clean[k] >= 2 && S.cnt_noisy[k] >= 2;   // I/utils.py:609-610
     if (gated[k]) rep_coef += att[k] * cfg.ecda_delta;
   }
-  // repulsion grads for this class's noisy members
+  // repulsion grads for this class's noisy members (d rep / d mu_c, then 1/n_c per member)
   if (nvalid > 1 && S.cnt_noisy[c] > 0 && rep_coef != 0.0f) {
     const int hh = tid;
-    float g = 0.0f;
+    float gsum = 0.0f;
     for (int q = 0; q < ncls; ++q) {
       if (q == c || S.cnt_noisy[q] == 0) continue;
       const float nd = pdist[c][q];
-      if (nd > 0.0f) g += (S.cent[c][hh] - S.cent[q][hh]) / nd;
+      if (nd > 0.0f) gsum += (S.cent[c][hh] - S.cent[q][hh]) / nd;
     }
-    g = -g / (float)npairs / (float)S.cnt_noisy[c];
+    const float gval = wscale * rep_coef * (-gsum / (float)npairs / (float)S.cnt_noisy[c]);
     for (int b = 0; b < Bn; ++b)
-      if ((int)predf[b] == c && mask[b] > 0.0f) ge_s[(size_t)b * DAD_H + hh] += wscale * rep_coef * g;
+      if (S.prd[b] == c) ge_s[(size_t)b * DAD_H + hh] += gval;
   }
   __syncthreads();
   if (!gated[c]) return;
-  // members of class c
-  if (tid == 0) {
-    int n = 0;
-    for (int b = 0; b < B; ++b)
-      if (a.yc[b] == c) { S.idx[n] = b; S.wt[n] = 1.0f; ++n; }
-    for (int b = 0; b < Bn; ++b)
-      if ((int)predf[b] == c && mask[b] > 0.0f) { S.idx[n] = b; S.wt[n] = score[b]; ++n; }
-  }
-  __syncthreads();
-  const int ns = S.cnt_clean[c], nt = S.cnt_noisy[c];
-  const float mmd = ecda_mmd(S, emb_c, emb_s, ge_c, ge_s, ns, ns + nt, scratch, wscale * att_c);
+  // members of class c: clean (label c, weight 1) then masked noisy (pseudo-label c, weight = score)
+  int n = ecda_compact(S, B, 0, [&](int i) { return S.lab[i] == c; }, [](int) { return 1.0f; });
+  const int ns = n;
+  n = ecda_compact(S, Bn, n, [&](int i) { return S.prd[i] == c; }, [&](int i) { return S.scr[i]; });
+  const int nt = n - ns;
+  const float mmd = ecda_mmd(S, emb_c, emb_s, ge_c, ge_s, ns, n, scratch, wscale * att_c);
   // compactness (I/utils.py:614-616): mean_j ||z_j - mu||^2, grad (2/nt)(z_j - mu)
   float cpart = 0.0f;
   for (int k = tid; k < nt * DAD_H; k += ECDA_THREADS) {

@@ -150,10 +150,123 @@ __device__ __forceinline__ bf16x8 tr_frag(const __bf16* tile, int pitch, int row
   return r;
 }
 
-__global__ __launch_bounds__(256, 2) void dad_wgrad_bf16(DadWgradArgs a) {
+// Per-thread registers for one slab in flight: 4 rows x 4 columns of x (fp32 clean rows or
+// the encoder's bf16 strong rows), one ReLU' bits word and the dL/de row scale.  Loads are
+// unconditional (row index clamped into the utterance) so the compiler can keep several
+// slabs outstanding with partial vmcnt waits; out-of-range rows are zeroed when staged.
+template <int BR> struct XRaw { using T = f32x4; };
+template <> struct XRaw<1> { using T = bf16x4; };
+template <int BR> struct SlabRegs {
+  typename XRaw<BR>::T x[4];
+  uint32_t word;
+  float ge, len;
+  int nvalid;
+};
+
+template <int BR>
+__device__ __forceinline__ void wg_load(const DadWgradArgs& a, int s, int dbase, SlabRegs<BR>& r) {
+  const DadGeom& g = a.g;
+  const int tid = threadIdx.x;
+  const int nc = BR ? g.ncn : g.ncc, T = BR ? g.Tn : g.Tc;
+  const int b = s / nc, c = s - b * nc;
+  const int erow = BR ? g.Bc + b : b;
+  const size_t bits_row = BR ? (size_t)g.Bc * g.tpc + (size_t)b * g.tpn + (size_t)c * DAD_SLAB
+                             : (size_t)b * g.tpc + (size_t)c * DAD_SLAB;
+  r.nvalid = T - c * DAD_SLAB;
+  const int col = (tid & 31) * 4;
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int t = min(c * DAD_SLAB + (tid >> 5) + 8 * m, T - 1);
+    const size_t off = ((size_t)b * T + t) * DAD_D + dbase + col;
+    if constexpr (BR == 0) r.x[m] = *reinterpret_cast<const f32x4*>(a.xc + off);
+    else r.x[m] = *reinterpret_cast<const bf16x4*>(a.xs_bf16 + off);
+  }
+  r.word = a.bits[(bits_row + (tid >> 3)) * DAD_HT + (tid & 7)];
+  r.ge = a.ge[(size_t)erow * DAD_H + tid];
+  r.len = a.vlen[erow];
+}
+
+template <int BR>
+__device__ __forceinline__ void wg_stage(const SlabRegs<BR>& r, __bf16* Xt, __bf16* Gt, float* sc) {
+  const int tid = threadIdx.x;
+  const int col = (tid & 31) * 4;
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const bool ok = (tid >> 5) + 8 * m < r.nvalid;
+    bf16x4 v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = ok ? (__bf16)r.x[m][e] : (__bf16)0.0f;
+    *reinterpret_cast<bf16x4*>(&Xt[((tid >> 5) + 8 * m) * WG_XP + col]) = v;
+  }
+  sc[tid] = r.ge / fmaxf(r.len, 1.0f);
+  __syncthreads();
+  const int row = tid >> 3, hq = tid & 7;
+  const f32x4* sv = reinterpret_cast<const f32x4*>(sc + hq * 32);
+#pragma unroll
+  for (int g8 = 0; g8 < 4; ++g8) {
+    const f32x4 lo = sv[2 * g8], hi = sv[2 * g8 + 1];
+    bf16x8 gv;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      gv[e] = (__bf16)(((r.word >> (g8 * 8 + e)) & 1u) ? lo[e] : 0.0f);
+      gv[e + 4] = (__bf16)(((r.word >> (g8 * 8 + e + 4)) & 1u) ? hi[e] : 0.0f);
+    }
+    *reinterpret_cast<bf16x8*>(&Gt[row * WG_GP + hq * 32 + g8 * 8]) = gv;
+  }
+}
+
+__device__ __forceinline__ void wg_compute(const __bf16* Xt, const __bf16* Gt, int wv, f32x16 (&acc)[2][4]) {
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    bf16x8 af[2], bfr[4];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) af[m] = tr_frag(Gt, WG_GP, 16 * ks, 32 * (2 * wv + m));
+#pragma unroll
+    for (int n = 0; n < 4; ++n) bfr[n] = tr_frag(Xt, WG_XP, 16 * ks, 32 * n);
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[m], bfr[n], acc[m][n], 0, 0, 0);
+  }
+}
+
+// slabs [lo, hi) of one branch; three slabs in flight in registers while the current one
+// is in LDS (the grid is ~one workgroup per CU, so memory-level parallelism has to come
+// from inside the workgroup)
+template <int BR>
+__device__ __forceinline__ void wg_phase(const DadWgradArgs& a, int lo, int hi, int dbase, __bf16* Xt, __bf16* Gt,
+                                         float* sc, f32x16 (&acc)[2][4]) {
+  if (lo >= hi) return;
+  const int wv = threadIdx.x >> 6;
+  SlabRegs<BR> r0, r1, r2;
+  wg_load<BR>(a, lo, dbase, r0);
+  if (lo + 1 < hi) wg_load<BR>(a, lo + 1, dbase, r1);
+  if (lo + 2 < hi) wg_load<BR>(a, lo + 2, dbase, r2);
+  for (int s = lo; s < hi; s += 3) {
+    __syncthreads();                 // previous compute finished reading Xt/Gt/sc
+    wg_stage<BR>(r0, Xt, Gt, sc);
+    if (s + 3 < hi) wg_load<BR>(a, s + 3, dbase, r0);
+    __syncthreads();
+    wg_compute(Xt, Gt, wv, acc);
+    if (s + 1 >= hi) break;
+    __syncthreads();
+    wg_stage<BR>(r1, Xt, Gt, sc);
+    if (s + 4 < hi) wg_load<BR>(a, s + 4, dbase, r1);
+    __syncthreads();
+    wg_compute(Xt, Gt, wv, acc);
+    if (s + 2 >= hi) break;
+    __syncthreads();
+    wg_stage<BR>(r2, Xt, Gt, sc);
+    if (s + 5 < hi) wg_load<BR>(a, s + 5, dbase, r2);
+    __syncthreads();
+    wg_compute(Xt, Gt, wv, acc);
+  }
+}
+
+__global__ __launch_bounds__(256, 1) void dad_wgrad_bf16(DadWgradArgs a) {
   __shared__ __attribute__((aligned(16))) __bf16 Xt[DAD_SLAB * WG_XP];
   __shared__ __attribute__((aligned(16))) __bf16 Gt[DAD_SLAB * WG_GP];
-  __shared__ float sc[DAD_H];
+  __shared__ __attribute__((aligned(16))) float sc[DAD_H];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wv = tid >> 6;
   const int kh = lane >> 5;
@@ -163,67 +276,14 @@ __global__ __launch_bounds__(256, 2) void dad_wgrad_bf16(DadWgradArgs a) {
   const int per = (total + a.splits - 1) / a.splits;
   const int s0 = split * per;
   const int s1 = min(total, s0 + per);
+  const int nsc = a.g.Bc * a.g.ncc;
   f32x16 acc[2][4];
 #pragma unroll
   for (int m = 0; m < 2; ++m)
 #pragma unroll
     for (int n = 0; n < 4; ++n) acc[m][n] = f32x16{};
-
-  for (int s = s0; s < s1; ++s) {
-    const SlabIdx q = wg_slab(a, s);
-    __syncthreads();   // previous slab's fragment reads are done
-    sc[tid] = a.ge[(size_t)q.erow * DAD_H + tid] / fmaxf(a.vlen[q.erow], 1.0f);
-    // x tile: 32 rows x 128 columns
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const int row = (tid >> 5) + 8 * m;
-      const int col = (tid & 31) * 4;
-      const int t = q.c * DAD_SLAB + row;
-      bf16x4 v;
-      if (t < q.T) {
-        const size_t off = (q.row0 + t) * DAD_D + dbase + col;
-        if (q.br == 0) {
-          const f32x4 x = *reinterpret_cast<const f32x4*>(a.xc + off);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = (__bf16)x[e];
-        } else {
-          v = *reinterpret_cast<const bf16x4*>(a.xs_bf16 + off);
-        }
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = (__bf16)0.0f;
-      }
-      *reinterpret_cast<bf16x4*>(&Xt[row * WG_XP + col]) = v;
-    }
-    __syncthreads();   // sc visible
-    {
-      const int row = tid >> 3, hq = tid & 7;
-      const uint32_t word = a.bits[(q.bits_row + row) * DAD_HT + hq];
-#pragma unroll
-      for (int g8 = 0; g8 < 4; ++g8) {
-        bf16x8 gv;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int hh = hq * 32 + g8 * 8 + e;
-          gv[e] = (__bf16)(((word >> (g8 * 8 + e)) & 1u) ? sc[hh] : 0.0f);
-        }
-        *reinterpret_cast<bf16x8*>(&Gt[row * WG_GP + hq * 32 + g8 * 8]) = gv;
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 af[2], bf[4];
-#pragma unroll
-      for (int m = 0; m < 2; ++m) af[m] = tr_frag(Gt, WG_GP, 16 * ks, 32 * (2 * wv + m));
-#pragma unroll
-      for (int n = 0; n < 4; ++n) bf[n] = tr_frag(Xt, WG_XP, 16 * ks, 32 * n);
-#pragma unroll
-      for (int m = 0; m < 2; ++m)
-#pragma unroll
-        for (int n = 0; n < 4; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[m], bf[n], acc[m][n], 0, 0, 0);
-    }
-  }
+  wg_phase<0>(a, s0, min(s1, nsc), dbase, Xt, Gt, sc, acc);
+  wg_phase<1>(a, max(s0, nsc) - nsc, s1 - nsc, dbase, Xt, Gt, sc, acc);
   float* out = a.wpart + (size_t)split * DAD_H * DAD_D;
 #pragma unroll
   for (int m = 0; m < 2; ++m)
@@ -252,20 +312,21 @@ __global__ __launch_bounds__(256) void dad_reduce(DadReduceArgs a) {
     *reinterpret_cast<f32x4*>(a.grad + DAD_OFF_W1 + e0) = s;
     for (int e = 0; e < 4; ++e) sq += (double)s[e] * s[e];
   } else {
+    // db1[h] = sum_r dL/de[r][h] / max(1, len_r) * active_count[r][h]  (independent loads, 4 chains)
     const int h = tid;
     const DadGeom& g = a.g;
-    double gb = 0.0;
     const int nb = g.Bc + (a.warmup ? 0 : g.Bn);
-    for (int r = 0; r < nb; ++r) {
-      // row r of ge/vlen: clean utterance r, or strong utterance r - Bc
-      const bool strong = r >= g.Bc;
-      const int nc = strong ? g.ncn : g.ncc;
-      const size_t slab0 = strong ? (size_t)g.Bc * g.ncc + (size_t)(r - g.Bc) * g.ncn : (size_t)r * g.ncc;
-      const float sc = a.ge[(size_t)r * DAD_H + h] / fmaxf(a.vlen[r], 1.0f);
-      float cnt = 0.0f;
-      for (int c = 0; c < nc; ++c) cnt += a.part_cnt[(slab0 + c) * DAD_H + h];
-      gb += (double)sc * cnt;
+    float acc4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    int r = 0;
+    for (; r + 4 <= nb; r += 4) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int rr = r + u;
+        acc4[u] += a.ge[(size_t)rr * DAD_H + h] / fmaxf(a.vlen[rr], 1.0f) * a.cnt_tot[(size_t)rr * DAD_H + h];
+      }
     }
+    for (; r < nb; ++r) acc4[0] += a.ge[(size_t)r * DAD_H + h] / fmaxf(a.vlen[r], 1.0f) * a.cnt_tot[(size_t)r * DAD_H + h];
+    const double gb = ((double)acc4[0] + acc4[1]) + ((double)acc4[2] + acc4[3]);
     const float db1 = (float)gb;
     a.grad[DAD_OFF_B1 + h] = db1;
     sq = (double)db1 * db1;

@@ -203,6 +203,8 @@ class DADStep:
                 setattr(bt, k, v.data_ptr())
             keep.append(dd)
         st = self._state_struct(Bn, Bc)
+        self._loss_vec = torch.empty(4, device=dev)          # written by the optimizer kernel
+        st.losses = self._loss_vec.data_ptr()
         ws = self._workspace(cfg)
         stream = self._stream()
         L = _lib.lib()
@@ -225,12 +227,10 @@ class DADStep:
 
     def losses(self):
         """Loss dict of the last step (keys of I/train.py:468-470 + scl_loss for CASIA/EMODB)."""
-        t = self._last["tail"]
-        g = self.grad[_lib.DAD_NPARAM + 12:_lib.DAD_NPARAM + 16]
-        out = {"total_loss": g[0].clone(), "supervised_ce_loss": g[1].clone(),
-               "consistency_loss": g[2].clone(), "ecda_loss": g[3].clone()}
+        g = self._loss_vec       # fresh per step: no copy kernels, no host sync
+        out = {"total_loss": g[0], "supervised_ce_loss": g[1], "consistency_loss": g[2], "ecda_loss": g[3]}
         if self.view.flavor in ("casia", "emodb"):
-            out["scl_loss"] = t[_lib.T_SCL].clone()
+            out["scl_loss"] = torch.zeros((), device=self.device)   # always 0 (C/train_CASIA.py:442)
         return out
 
     def outputs(self, Bc=None, Bn=None):

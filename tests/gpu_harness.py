@@ -118,5 +118,6 @@ def ws_ge(step, Bc, Tc, Bn, Tn):
     off = al(off + 4 * (Bc * ncc + Bn * ncn) * 256)          # part_cnt
     off = al(off + 4 * (Bc * tpc + Bn * tpn) * 8)            # bits
     off = al(off + 4 * (Bc + Bn))                            # vlen
+    off = al(off + 4 * (Bc + Bn) * 256)                      # cnt_tot
     ws = step._ws
     return ws[off:off + 4 * (Bc + Bn) * 256].view(torch.float32).view(Bc + Bn, 256).cpu().numpy()
