@@ -26,33 +26,44 @@ def _newest(paths):
     return max(os.path.getmtime(p) for p in paths)
 
 
-def _compile(src):
-    obj = os.path.join(OBJ_DIR, os.path.splitext(src)[0] + ".o")
+def lib_path(variant=None):
+    """Diagnostic builds (e.g. DAD_PROBE_* kernels) live beside the product library."""
+    return LIB_PATH if not variant else os.path.join(LIB_DIR, "libdad_hip_%s.so" % variant)
+
+
+def _compile(src, variant=None, extra=()):
+    odir = OBJ_DIR if not variant else os.path.join(OBJ_DIR, variant)
+    obj = os.path.join(odir, os.path.splitext(src)[0] + ".o")
     deps = [os.path.join(CSRC, src)] + [os.path.join(CSRC, h) for h in HEADERS]
     if os.path.exists(obj) and os.path.getmtime(obj) >= _newest(deps):
         return obj
-    cmd = [HIPCC] + CFLAGS + ["-c", os.path.join(CSRC, src), "-o", obj]
+    cmd = [HIPCC] + CFLAGS + list(extra) + ["-c", os.path.join(CSRC, src), "-o", obj]
     r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     if r.returncode != 0:
         raise RuntimeError("hipcc failed for %s:\n%s" % (src, r.stdout))
     return obj
 
 
-def build(verbose=True):
-    """Compile (incrementally) and link; returns the library path."""
-    os.makedirs(OBJ_DIR, exist_ok=True)
+def build(verbose=True, variant=None, extra=()):
+    """Compile (incrementally) and link; returns the library path.
+
+    variant/extra: a diagnostic build with extra compiler flags into lib/libdad_hip_<variant>.so
+    (loaded only when DAD_LIB_VARIANT names it; the product library is never replaced).
+    """
+    path = lib_path(variant)
+    os.makedirs(OBJ_DIR if not variant else os.path.join(OBJ_DIR, variant), exist_ok=True)
     os.makedirs(LIB_DIR, exist_ok=True)
     jobs = min(len(SOURCES), int(os.environ.get("MAX_JOBS", "8")))
     with concurrent.futures.ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(_compile, SOURCES))
-    if not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < _newest(objs):
-        cmd = [HIPCC, "-shared", "-o", LIB_PATH] + objs + ["-L" + os.path.join(ROCM, "lib"), "-lrccl"]
+        objs = list(ex.map(lambda s: _compile(s, variant, extra), SOURCES))
+    if not os.path.exists(path) or os.path.getmtime(path) < _newest(objs):
+        cmd = [HIPCC, "-shared", "-o", path] + objs + ["-L" + os.path.join(ROCM, "lib"), "-lrccl"]
         r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
         if r.returncode != 0:
             raise RuntimeError("link failed:\n%s" % r.stdout)
     if verbose:
-        print("built", LIB_PATH)
-    return LIB_PATH
+        print("built", path)
+    return path
 
 
 if __name__ == "__main__":

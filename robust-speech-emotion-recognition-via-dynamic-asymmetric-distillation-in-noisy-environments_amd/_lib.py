@@ -108,7 +108,7 @@ def lib():
     global _LIB
     if _LIB is not None:
         return _LIB
-    path = _build.LIB_PATH
+    path = _build.lib_path(os.environ.get("DAD_LIB_VARIANT") or None)
     if not os.path.exists(path):
         raise DadError("libdad_hip.so not built (%s); run __graft_entry__.build() or "
                        "python -m <pkg>._build" % path)

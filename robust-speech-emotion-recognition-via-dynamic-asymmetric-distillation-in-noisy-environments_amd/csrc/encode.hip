@@ -224,6 +224,7 @@ __global__ __launch_bounds__(256) void dad_encode_f32(DadEncodeArgs a) {
 #define ENC_WAVES 8
 #define ENC_KC 32
 #define ENC_NCH (DAD_D / ENC_KC)
+static_assert(ENC_NCH % 2 == 0 && ENC_NCH >= 4, "bf16 encoder pipeline assumes an even chunk count");
 #define ENC_WCHUNK_BYTES (DAD_H * ENC_KC * 2)   // 16 KB per weight per chunk
 
 struct Bf16Geom {
@@ -235,7 +236,7 @@ struct Bf16Geom {
 
 __device__ __forceinline__ Bf16Geom bf16_geom(const DadEncodeArgs& a, int& noisy_wg) {
   const DadGeom& g = a.g;
-  const int wv = threadIdx.x >> 6;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: scalar branches
   const int nsn = a.warmup ? 0 : g.Bn * g.ncn;
   const int nwg_n = (nsn + 3) / 4;
   Bf16Geom e;
@@ -278,56 +279,67 @@ __device__ __forceinline__ bf16x8 to_bf16x8(f32x4 lo, f32x4 hi) {
 
 // stage one 32-column chunk of (one or two) bf16 W1 matrices: global -> registers
 struct WStage {
-  uint4 v[2][2];
+  u32x4 v[2][2];
 };
-__device__ __forceinline__ void w_load(WStage& w, const __bf16* W0, const __bf16* W1, int ch, bool two) {
+template <bool TWO>
+__device__ __forceinline__ void w_load(WStage& w, const __bf16* W0, const __bf16* W1, int ch) {
   const int tid = threadIdx.x;
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int item = tid + q * 512;               // 1024 16-B pieces per matrix per chunk
     const int h = item >> 2, c = item & 3;
     const size_t off = (size_t)h * DAD_D + ch * ENC_KC + 8 * c;
-    w.v[0][q] = *reinterpret_cast<const uint4*>(W0 + off);
-    if (two) w.v[1][q] = *reinterpret_cast<const uint4*>(W1 + off);
+    w.v[0][q] = *reinterpret_cast<const u32x4*>(W0 + off);
+    if constexpr (TWO) w.v[1][q] = *reinterpret_cast<const u32x4*>(W1 + off);
   }
 }
-__device__ __forceinline__ void w_store(const WStage& w, char* buf, bool two) {
+template <bool TWO>
+__device__ __forceinline__ void w_store(const WStage& w, char* buf) {
   const int tid = threadIdx.x;
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int item = tid + q * 512;
     const int h = item >> 2, c = item & 3;
     const int pos = c ^ ((h >> 2) & 3);
-    *reinterpret_cast<uint4*>(buf + h * 64 + pos * 16) = w.v[0][q];
-    if (two) *reinterpret_cast<uint4*>(buf + ENC_WCHUNK_BYTES + h * 64 + pos * 16) = w.v[1][q];
+    *reinterpret_cast<u32x4*>(buf + h * 64 + pos * 16) = w.v[0][q];
+    if constexpr (TWO) *reinterpret_cast<u32x4*>(buf + ENC_WCHUNK_BYTES + h * 64 + pos * 16) = w.v[1][q];
   }
 }
 
 struct XChunk {
   f32x4 v[2][2];    // [k-step][lo/hi]: lane (row r, half kh) holds columns 16ks + 8kh .. +7
 };
-__device__ __forceinline__ void x_load(XChunk& x, const float* row, bool tin, int ch, int kh) {
+// unconditional: rows past the utterance read its frame 0 (row clamped by the caller) and
+// are discarded by the epilogue's valid mask, so no per-lane branch splits the vmcnt chain
+__device__ __forceinline__ void x_load(XChunk& x, const float* row, int ch, int kh) {
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
     const int d = ch * ENC_KC + 16 * ks + 8 * kh;
-    x.v[ks][0] = tin ? *reinterpret_cast<const f32x4*>(row + d) : f32x4{};
-    x.v[ks][1] = tin ? *reinterpret_cast<const f32x4*>(row + d + 4) : f32x4{};
+#ifdef DAD_PROBE_NOX
+    x.v[ks][0] = f32x4{(float)d, 1.0f, 2.0f, 3.0f};
+    x.v[ks][1] = f32x4{(float)kh, 1.0f, 2.0f, 3.0f};
+    (void)row;
+#else
+    x.v[ks][0] = *reinterpret_cast<const f32x4*>(row + d);
+    x.v[ks][1] = *reinterpret_cast<const f32x4*>(row + d + 4);
+#endif
   }
 }
 
-__global__ __launch_bounds__(512, 1) void dad_encode_bf16(DadEncodeArgs a) {
-  __shared__ __attribute__((aligned(16))) char wbuf[2][2 * ENC_WCHUNK_BYTES];
-  __shared__ __attribute__((aligned(16))) uint32_t lds_bits_all[ENC_WAVES][DAD_SLAB * DAD_HT];
-  __shared__ float featkeep[DAD_D];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+// NOISE: 0 = counter RNG in-kernel, 1 = explicit noise tensors (parity mode draws)
+// TWO: noisy workgroup (teacher + student weights, waves 0-3 weak / 4-7 strong) vs clean
+template <int NOISE, bool TWO>
+__device__ __forceinline__ void encode_bf16_body(const DadEncodeArgs& a, char (*wbuf)[2 * ENC_WCHUNK_BYTES],
+                                                 uint32_t (*lds_bits_all)[DAD_SLAB * DAD_HT], float* featkeep) {
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int i = lane & 31, kh = lane >> 5;
   int noisy_wg;
-  const Bf16Geom e = bf16_geom(a, noisy_wg);
-  const bool two = noisy_wg;
-  const __bf16* W0 = noisy_wg ? a.w1bf_teacher : a.w1bf_student;   // buffer half 0
+  Bf16Geom e = bf16_geom(a, noisy_wg);
+  e.kind = __builtin_amdgcn_readfirstlane(e.kind);
+  const __bf16* W0 = TWO ? a.w1bf_teacher : a.w1bf_student;        // buffer half 0
   const __bf16* W1 = a.w1bf_student;                               // buffer half 1 (noisy only)
   // strong-aug feature keep flags for all 768 channels (I/utils.py:343), once per workgroup
-  if (noisy_wg)
+  if constexpr (TWO)
     for (int d = threadIdx.x; d < DAD_D; d += 512) featkeep[d] = feat_keep(a, d);
   // per-wave row state
   const bool active = e.kind >= 0;
@@ -338,25 +350,21 @@ __global__ __launch_bounds__(512, 1) void dad_encode_bf16(DadEncodeArgs a) {
   if (tin) valid = (e.kind == 0 ? a.mc : a.mn)[e.row0 + t] == 0;
   const uint32_t vbits = (uint32_t)__ballot(valid);
   const float* xrow = (e.kind == 0 ? a.xc : a.xn) + (size_t)grow * DAD_D;
+  const float* nrow = NOISE ? (e.kind == 2 ? a.ns : a.nw) + (size_t)grow * DAD_D : nullptr;
   bool tzero = false;
   if (e.kind == 2 && a.mask_len > 0) {
     const int st = tmask_start(a, e.b);
     tzero = t >= st && t < st + a.mask_len;
   }
-  const int wsel = (two && wv >= 4) ? ENC_WCHUNK_BYTES : 0;   // student half of a noisy workgroup
+  const int wsel = (TWO && wv >= 4) ? ENC_WCHUNK_BYTES : 0;   // student half of a noisy workgroup
+  const bool noisy_kind = TWO && (e.kind == 1 || e.kind == 2);
+  const bool strong = TWO && e.kind == 2;
+  const uint32_t key = strong ? a.key_strong : a.key_weak;
+  const float sd = strong ? a.strong_std : a.weak_std;
 
   f32x16 acc[DAD_HT];
 #pragma unroll
   for (int ht = 0; ht < DAD_HT; ++ht) acc[ht] = f32x16{};
-
-  // prologue: W chunk 0 -> LDS, x chunks 0 and 1 -> registers
-  WStage ws;
-  w_load(ws, W0, W1, 0, two);
-  XChunk xa, xb;
-  x_load(xa, xrow, tin, 0, kh);
-  x_load(xb, xrow, tin, 1, kh);
-  w_store(ws, wbuf[0], two);
-  __syncthreads();
 
   auto compute = [&](int ch, const XChunk& x) {
     const char* wb = wbuf[ch & 1] + wsel;
@@ -364,62 +372,95 @@ __global__ __launch_bounds__(512, 1) void dad_encode_bf16(DadEncodeArgs a) {
     for (int ks = 0; ks < 2; ++ks) {
       const int d = ch * ENC_KC + 16 * ks + 8 * kh;
       f32x4 lo = x.v[ks][0], hi = x.v[ks][1];
-      if (e.kind == 1 || e.kind == 2) {
+      if (noisy_kind) {
         f32x4 nlo, nhi;
-        const bool strong = e.kind == 2;
-        if (a.nw) {
-          const float* src = (strong ? a.ns : a.nw) + (size_t)grow * DAD_D + d;
-          nlo = *reinterpret_cast<const f32x4*>(src);
-          nhi = *reinterpret_cast<const f32x4*>(src + 4);
+        if constexpr (NOISE) {
+          nlo = *reinterpret_cast<const f32x4*>(nrow + d);
+          nhi = *reinterpret_cast<const f32x4*>(nrow + d + 4);
         } else {
-          const uint32_t key = strong ? a.key_strong : a.key_weak;
+#ifdef DAD_PROBE_NORNG
+          nlo = f32x4{}; nhi = f32x4{};
+#else
           nlo = dad_normal4(key, (uint32_t)grow, (uint32_t)d);
           nhi = dad_normal4(key, (uint32_t)grow, (uint32_t)(d + 4));
+#endif
         }
-        const float sd = strong ? a.strong_std : a.weak_std;
+        // feature keep flags read unconditionally (a per-lane tzero guard made them branches)
+        f32x4 fk_lo = f32x4{1.0f, 1.0f, 1.0f, 1.0f}, fk_hi = fk_lo;
+        if (strong) {
+          fk_lo = *reinterpret_cast<const f32x4*>(featkeep + d);
+          fk_hi = *reinterpret_cast<const f32x4*>(featkeep + d + 4);
+        }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           // op order of the reference: noise*std, add; then feature mask; then temporal zero
           float v0 = lo[q] + nlo[q] * sd;
           float v1 = hi[q] + nhi[q] * sd;
           if (strong) {
-            v0 = tzero ? 0.0f : v0 * featkeep[d + q];
-            v1 = tzero ? 0.0f : v1 * featkeep[d + 4 + q];
+            v0 = tzero ? 0.0f : v0 * fk_lo[q];
+            v1 = tzero ? 0.0f : v1 * fk_hi[q];
           }
           lo[q] = v0;
           hi[q] = v1;
         }
       }
       const bf16x8 xa8 = to_bf16x8(lo, hi);
-      if (e.kind == 2 && tin) *reinterpret_cast<bf16x8*>(a.xs_bf16 + (size_t)grow * DAD_D + d) = xa8;
+      if (strong && tin) *reinterpret_cast<bf16x8*>(a.xs_bf16 + (size_t)grow * DAD_D + d) = xa8;
       if (active) {
         const int c16 = ks * 2 + kh;
 #pragma unroll
         for (int ht = 0; ht < DAD_HT; ++ht) {
           const int h = ht * 32 + i;
           const bf16x8 w = *reinterpret_cast<const bf16x8*>(wb + h * 64 + ((c16 ^ ((h >> 2) & 3)) * 16));
+#ifdef DAD_PROBE_NOMFMA
+          acc[ht][0] += (float)xa8[0] * (float)w[0];
+#else
           acc[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa8, w, acc[ht], 0, 0, 0);
+#endif
         }
       }
     }
   };
 
+  // prologue: W chunk 0 -> LDS; W chunks 1, 2 and x chunks 0, 1 in flight in registers
+  WStage wa, wb_;
+  XChunk xa, xb;
+  w_load<TWO>(wa, W0, W1, 0);
+  w_load<TWO>(wb_, W0, W1, 1);
+  x_load(xa, xrow, 0, kh);
+  x_load(xb, xrow, 1, kh);
+  w_store<TWO>(wa, wbuf[0]);
+  w_load<TWO>(wa, W0, W1, 2);
+  __syncthreads();
+
+  // chunk ch: x in xa, W in wbuf[0]; W(ch+1) in wb_, W(ch+2) in wa.  ENC_NCH is even.
+  // Every prefetch is issued unconditionally (chunk index clamped: the tail re-reads the
+  // last, L2-hot chunk): a conditional load leaves the two paths with different pending
+  // counts and the compiler then merges them into a full vmcnt(0) drain every chunk.
+  const int last = ENC_NCH - 1;
   for (int ch = 0; ch < ENC_NCH; ch += 2) {
-    // chunk ch: x in xa, W in wbuf[0]
-    if (ch + 1 < ENC_NCH) w_load(ws, W0, W1, ch + 1, two);
     compute(ch, xa);
-    if (ch + 2 < ENC_NCH) x_load(xa, xrow, tin, ch + 2, kh);
-    if (ch + 1 < ENC_NCH) w_store(ws, wbuf[1], two);
+    x_load(xa, xrow, min(ch + 2, last), kh);
+    w_store<TWO>(wb_, wbuf[1]);
+    w_load<TWO>(wb_, W0, W1, min(ch + 3, last));
     __syncthreads();
-    if (ch + 1 >= ENC_NCH) break;
-    // chunk ch+1: x in xb, W in wbuf[1]
-    if (ch + 2 < ENC_NCH) w_load(ws, W0, W1, ch + 2, two);
     compute(ch + 1, xb);
-    if (ch + 3 < ENC_NCH) x_load(xb, xrow, tin, ch + 3, kh);
-    if (ch + 2 < ENC_NCH) w_store(ws, wbuf[0], two);
+    x_load(xb, xrow, min(ch + 3, last), kh);
+    w_store<TWO>(wa, wbuf[0]);            // past the end: overwrites a buffer nobody reads again
+    w_load<TWO>(wa, W0, W1, min(ch + 4, last));
     __syncthreads();
   }
   if (!active) return;
   const float* bias = e.kind == 1 ? a.b1_teacher : a.b1_student;
   encode_epilogue(a, acc, bias, e.sum_slab, e.cnt_slab, e.bits_row, vbits, lds_bits_all[wv]);
+}
+
+__global__ __launch_bounds__(512, 1) void dad_encode_bf16(DadEncodeArgs a) {
+  __shared__ __attribute__((aligned(16))) char wbuf[2][2 * ENC_WCHUNK_BYTES];
+  __shared__ __attribute__((aligned(16))) uint32_t lds_bits_all[ENC_WAVES][DAD_SLAB * DAD_HT];
+  __shared__ __attribute__((aligned(16))) float featkeep[DAD_D];
+  const int nsn = a.warmup ? 0 : a.g.Bn * a.g.ncn;
+  if ((int)blockIdx.x >= (nsn + 3) / 4) encode_bf16_body<0, false>(a, wbuf, lds_bits_all, featkeep);
+  else if (a.nw) encode_bf16_body<1, true>(a, wbuf, lds_bits_all, featkeep);
+  else encode_bf16_body<0, true>(a, wbuf, lds_bits_all, featkeep);
 }

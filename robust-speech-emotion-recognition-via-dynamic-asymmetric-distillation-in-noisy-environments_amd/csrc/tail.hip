@@ -353,12 +353,11 @@ __global__ __launch_bounds__(TAIL_THREADS) void dad_tail(DadTailArgs a) {
 #define ECDA_NZ 80           // members staged in LDS (n <= 80); larger sets read global
 
 struct EcdaSmem {
-  float z[ECDA_NZ * DAD_H];
-  float dm[ECDA_NZ * ECDA_NZ];
+  float z[ECDA_NZ * DAD_H];       // staged member embeddings (before that: centroid partials)
+  float dm[ECDA_NZ * ECDA_NZ];    // pairwise distances, then symmetric MMD coefficients
   int idx[2 * DAD_MAX_BATCH];     // member list: [0,ns) clean rows, [ns,n) noisy rows
   float wt[2 * DAD_MAX_BATCH];    // member weights
   float cent[DAD_C][DAD_H];
-  float rowc[2 * DAD_MAX_BATCH];  // sum_b Csym[a][b]
   double dred[8];
   float fred[8];
   int cnt_clean[DAD_C], cnt_noisy[DAD_C];
@@ -366,8 +365,27 @@ struct EcdaSmem {
   int prd[DAD_MAX_BATCH];         // noisy pseudo-labels, -1 where not masked in
   float scr[DAD_MAX_BATCH];       // noisy certainty scores
   int wcount[ECDA_THREADS / 64];
-  int nmem;
 };
+
+__device__ __forceinline__ double ecda_block_sum_d(EcdaSmem& S, double v) {
+  v = dad_wave_sum_d(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) S.dred[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int k = 0; k < ECDA_THREADS / 64; ++k) s += S.dred[k];
+  return s;
+}
+
+__device__ __forceinline__ float ecda_block_sum_f(EcdaSmem& S, float v) {
+  v = dad_wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) S.fred[threadIdx.x >> 6] = v;
+  __syncthreads();
+  float s = 0.0f;
+  for (int k = 0; k < ECDA_THREADS / 64; ++k) s += S.fred[k];
+  return s;
+}
 
 // Ordered block-wide compaction: appends every i in [0, n) with flag(i) to S.idx (and
 // weight(i) to S.wt) after position `base`, in ascending i.  Returns the new length.
@@ -396,51 +414,62 @@ __device__ int ecda_compact(EcdaSmem& S, int n, int base, Flag flag, Wgt weight)
   return base;
 }
 
-// mmd = t_ss + t_tt - 2 t_st of _gaussian_kernel (I/utils.py:521-563) over members
-// idx[0..ns) (clean embeddings) and idx[ns..n) (strong embeddings), plus grads
-// `scale * d mmd / dz` added into ge.  Returns mmd (valid in all threads).
-__device__ float ecda_mmd(EcdaSmem& S, const float* emb_c, const float* emb_s, float* ge_c, float* ge_s,
-                          int ns, int n, float* scratch, float scale) {
-  const int tid = threadIdx.x;
-  const bool staged = n <= ECDA_NZ;
-  // stage Z
-  if (staged) {
-    for (int k = tid; k < n * DAD_H; k += ECDA_THREADS) {
-      const int a = k / DAD_H, hh = k - a * DAD_H;
-      const float* src = a < ns ? emb_c : emb_s;
-      S.z[k] = src[(size_t)S.idx[a] * DAD_H + hh];
+// Member embeddings: staged in LDS when n <= ECDA_NZ, read from global otherwise.
+struct EcdaRows {
+  const float* emb_c;
+  const float* emb_s;
+  const EcdaSmem* S;
+  int ns;
+  bool staged;
+  __device__ __forceinline__ const float* row(int a) const {
+    return staged ? &S->z[a * DAD_H] : ((a < ns ? emb_c : emb_s) + (size_t)S->idx[a] * DAD_H);
+  }
+};
+
+__device__ __forceinline__ void ecda_stage(EcdaSmem& S, const EcdaRows& R, int n) {
+  if (R.staged) {
+#pragma unroll 4
+    for (int k = threadIdx.x; k < n * (DAD_H / 4); k += ECDA_THREADS) {
+      const int a = k / (DAD_H / 4), q = k - a * (DAD_H / 4);
+      const float* src = (a < R.ns ? R.emb_c : R.emb_s) + (size_t)S.idx[a] * DAD_H;
+      reinterpret_cast<f32x4*>(S.z)[k] = reinterpret_cast<const f32x4*>(src)[q];
     }
   }
   __syncthreads();
-  float* D = staged ? S.dm : scratch;
-  auto zrow = [&](int a) -> const float* {
-    return staged ? &S.z[a * DAD_H] : ((a < ns ? emb_c : emb_s) + (size_t)S.idx[a] * DAD_H);
-  };
-  // pairwise squared distances (I/utils.py:533-537)
+}
+
+// mmd = t_ss + t_tt - 2 t_st of _gaussian_kernel (I/utils.py:521-563) over members
+// [0, ns) (clean embeddings) and [ns, n) (strong embeddings).  Leaves the symmetric
+// coefficient matrix Csym = dmmd/dD + (dmmd/dD)^T in D, so that
+// dmmd/dz_i = 2 sum_j Csym_ij (z_i - z_j).  Returns mmd (valid in all threads).
+__device__ float ecda_mmd_coef(EcdaSmem& S, const EcdaRows& R, int n, float* D) {
+  const int tid = threadIdx.x;
+  const int ns = R.ns;
+  // pairwise squared distances (I/utils.py:533-537).  Lane reads float4 (q + i + j) mod 64
+  // of both rows: consecutive pairs hit different LDS banks, and (i, j) / (j, i) sum in the
+  // same order, so D stays exactly symmetric.
   double part = 0.0;
   for (int p = tid; p < n * n; p += ECDA_THREADS) {
     const int i = p / n, j = p - i * n;
     float d = 0.0f;
     if (i != j) {
-      const float* zi = zrow(i);
-      const float* zj = zrow(j);
-      for (int hh = 0; hh < DAD_H; ++hh) {
-        const float df = zj[hh] - zi[hh];
-        d += df * df;
+      const f32x4* zi = reinterpret_cast<const f32x4*>(R.row(i));
+      const f32x4* zj = reinterpret_cast<const f32x4*>(R.row(j));
+      const int rot = (i + j) & 63;
+#pragma unroll 8
+      for (int q = 0; q < DAD_H / 4; ++q) {
+        const int qq = (q + rot) & 63;
+        const f32x4 df = zj[qq] - zi[qq];
+        d += df[0] * df[0];
+        d += df[1] * df[1];
+        d += df[2] * df[2];
+        d += df[3] * df[3];
       }
     }
     D[p] = d;
     part += d;
   }
-  const double sumD = [&] {
-    double v = dad_wave_sum_d(part);
-    __syncthreads();
-    if ((tid & 63) == 0) S.dred[tid >> 6] = v;
-    __syncthreads();
-    double s = 0.0;
-    for (int k = 0; k < ECDA_THREADS / 64; ++k) s += S.dred[k];
-    return s;
-  }();
+  const double sumD = ecda_block_sum_d(S, part);
   // detached bandwidth (I/utils.py:540-544): sum(D)/(n^2-n) / mul^(num//2), x mul^i
   float bw = (n > 1) ? (float)(sumD / (double)(n * n - n)) : 1.0f;
   bw = bw / 4.0f;
@@ -470,32 +499,69 @@ __device__ float ecda_mmd(EcdaSmem& S, const float* emb_c, const float* emb_s, f
     else coef = 0.0f;   // the T x S block is not used by t_st
     D[p] = coef * dK;
   }
-  double red3[3] = {tss, ttt, tst};
-  for (int r = 0; r < 3; ++r) {
-    double v = dad_wave_sum_d(red3[r]);
-    __syncthreads();
-    if ((tid & 63) == 0) S.dred[tid >> 6] = v;
-    __syncthreads();
-    double s = 0.0;
-    for (int k = 0; k < ECDA_THREADS / 64; ++k) s += S.dred[k];
-    red3[r] = s;
-  }
-  const float mmd = (float)(red3[0] / Wss + red3[1] / Wtt - 2.0 * (red3[2] / Wst));
-  __syncthreads();
-  // dZ_i = 2 * sum_j Csym_ij (z_i - z_j),  Csym_ij = C_ij + C_ji  (the autograd form of
-  // d/dz of ||z_i - z_j||^2; summing the differences avoids the cancellation of
-  // rowsum(C) z_i - C z for near-identical same-class embeddings)
-  __syncthreads();
-  for (int k = tid; k < n * DAD_H; k += ECDA_THREADS) {
-    const int i = k / DAD_H, hh = k - i * DAD_H;
-    const float zi = zrow(i)[hh];
-    float acc = 0.0f;
-    for (int j = 0; j < n; ++j) acc += (D[i * n + j] + D[j * n + i]) * (zi - zrow(j)[hh]);
-    float* dst = (i < ns ? ge_c : ge_s) + (size_t)S.idx[i] * DAD_H + hh;
-    *dst += scale * (2.0f * acc);
+  tss = ecda_block_sum_d(S, tss);
+  ttt = ecda_block_sum_d(S, ttt);
+  tst = ecda_block_sum_d(S, tst);
+  const float mmd = (float)(tss / Wss + ttt / Wtt - 2.0 * (tst / Wst));
+  // symmetrise in place (each unordered pair owned by one thread)
+  for (int p = tid; p < n * n; p += ECDA_THREADS) {
+    const int i = p / n, j = p - i * n;
+    if (i < j) {
+      const float v = D[i * n + j] + D[j * n + i];
+      D[i * n + j] = v;
+      D[j * n + i] = v;
+    }
   }
   __syncthreads();
   return mmd;
+}
+
+// Embedding grads of the members, one column (hh = tid) per thread, eight member rows per
+// batch: the eight read-modify-write loads of ge are issued together (the rows are
+// distinct, but the compiler cannot prove it, so a plain loop would serialise them):
+//   g = mmd_scale * 2 sum_j Csym_ij (z_i - z_j)            (all members, if D)
+//     + comp_scale * (z_i - mu_c) + rep_g                    (noisy members)
+// comp_part accumulates sum ||z_i - mu_c||^2 over noisy members (when cent).
+__device__ void ecda_member_grads(const EcdaSmem& S, const EcdaRows& R, int n, const float* D, float mmd_scale,
+                                  const float* cent, float comp_scale, float rep_g, float* ge_c, float* ge_s,
+                                  float& comp_part) {
+  const int hh = threadIdx.x;
+  const int ns = R.ns;
+  for (int m0 = 0; m0 < n; m0 += 8) {
+    float old[8];
+    float* dst[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int m = m0 + u;
+      dst[u] = nullptr;
+      if (m < n) {
+        dst[u] = (m < ns ? ge_c : ge_s) + (size_t)S.idx[m] * DAD_H + hh;
+        old[u] = *dst[u];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int m = m0 + u;
+      if (m >= n) break;
+      float g = 0.0f;
+      float zi = 0.0f;
+      if (D || cent) zi = R.row(m)[hh];
+      if (D) {
+        float acc = 0.0f;
+        for (int j = 0; j < n; ++j) acc += D[m * n + j] * (zi - R.row(j)[hh]);
+        g = mmd_scale * (2.0f * acc);
+      }
+      if (m >= ns) {
+        if (cent) {
+          const float df = zi - cent[hh];
+          comp_part += df * df;
+          g += comp_scale * df;
+        }
+        g += rep_g;
+      }
+      *dst[u] = old[u] + g;
+    }
+  }
 }
 
 __global__ __launch_bounds__(ECDA_THREADS) void dad_ecda(DadEcdaArgs a) {
@@ -532,7 +598,12 @@ __global__ __launch_bounds__(ECDA_THREADS) void dad_ecda(DadEcdaArgs a) {
     n = ecda_compact(S, Bn, n, [&](int i) { return S.prd[i] >= 0; }, [](int) { return 1.0f; });
     const int nt = n - ns;
     if (ns >= 2 && nt >= 2) {
-      const float mmd = ecda_mmd(S, emb_c, emb_s, ge_c, ge_s, ns, n, scratch, wscale);
+      const EcdaRows R{emb_c, emb_s, &S, ns, n <= ECDA_NZ};
+      float* D = R.staged ? S.dm : scratch;
+      ecda_stage(S, R, n);
+      const float mmd = ecda_mmd_coef(S, R, n, D);
+      float unused = 0.0f;
+      ecda_member_grads(S, R, n, D, wscale, nullptr, 0.0f, 0.0f, ge_c, ge_s, unused);
       if (tid == 0) { a.tail_terms[0] = mmd; a.tail_terms[DAD_T_ECDA_GATE - DAD_T_ECDA_TERM] = 1.0f; }
     }
     return;
@@ -546,22 +617,31 @@ __global__ __launch_bounds__(ECDA_THREADS) void dad_ecda(DadEcdaArgs a) {
     if (S.lab[b] >= 0 && S.lab[b] < ncls) atomicAdd(&S.cnt_clean[S.lab[b]], 1);
   for (int b = tid; b < Bn; b += ECDA_THREADS)
     if (S.prd[b] >= 0 && S.prd[b] < ncls) atomicAdd(&S.cnt_noisy[S.prd[b]], 1);
-  __syncthreads();
-  // noisy centroids of every class in one pass (needed for the repulsion term)
+  // noisy centroids of every class (needed for the repulsion term): four utterance groups
+  // x 64 float4 columns, all loads of a group in flight, partials combined in fixed order
   {
-    const int hh = tid;
-    float cs[DAD_C] = {0.0f, 0.0f, 0.0f, 0.0f};
-    // unconditional, unrolled loads: a data-dependent skip here serialised one global-load
-    // latency per utterance
-#pragma unroll 8
-    for (int b = 0; b < Bn; ++b) {
-      const int pk = S.prd[b];
-      const float e = emb_s[(size_t)b * DAD_H + hh];
+    float* part = S.z;   // [4 groups][C][H], before the members are staged
+    const int g = tid >> 6, q = tid & 63;
+    f32x4 cs[DAD_C];
 #pragma unroll
-      for (int k = 0; k < DAD_C; ++k) cs[k] += pk == k ? e : 0.0f;
+    for (int k = 0; k < DAD_C; ++k) cs[k] = f32x4{};
+#pragma unroll 16
+    for (int b = g; b < Bn; b += 4) {
+      const int pk = S.prd[b];
+      const f32x4 e = reinterpret_cast<const f32x4*>(emb_s + (size_t)b * DAD_H)[q];
+#pragma unroll
+      for (int k = 0; k < DAD_C; ++k) cs[k] += pk == k ? e : f32x4{};
     }
 #pragma unroll
-    for (int k = 0; k < DAD_C; ++k) S.cent[k][hh] = S.cnt_noisy[k] > 0 ? cs[k] / (float)S.cnt_noisy[k] : 0.0f;
+    for (int k = 0; k < DAD_C; ++k) reinterpret_cast<f32x4*>(part + (g * DAD_C + k) * DAD_H)[q] = cs[k];
+    __syncthreads();
+    const int hh = tid;
+#pragma unroll
+    for (int k = 0; k < DAD_C; ++k) {
+      const float sk = ((part[(0 * DAD_C + k) * DAD_H + hh] + part[(1 * DAD_C + k) * DAD_H + hh]) +
+                        part[(2 * DAD_C + k) * DAD_H + hh]) + part[(3 * DAD_C + k) * DAD_H + hh];
+      S.cent[k][hh] = S.cnt_noisy[k] > 0 ? sk / (float)S.cnt_noisy[k] : 0.0f;
+    }
   }
   __syncthreads();
   // class attention (I/utils.py:597-599)
@@ -605,8 +685,10 @@ __global__ __launch_bounds__(ECDA_THREADS) void dad_ecda(DadEcdaArgs a) {
     gated[k] = k < ncls && S.cnt_clean[k] >= 2 && S.cnt_noisy[k] >= 2;   // I/utils.py:609-610
     if (gated[k]) rep_coef += att[k] * cfg.ecda_delta;
   }
-  // repulsion grads for this class's noisy members (d rep / d mu_c, then 1/n_c per member)
-  if (nvalid > 1 && S.cnt_noisy[c] > 0 && rep_coef != 0.0f) {
+  // repulsion grad of this class's noisy members (d rep / d mu_c, then 1/n_c per member)
+  const bool rep_on = nvalid > 1 && S.cnt_noisy[c] > 0 && rep_coef != 0.0f;
+  float rep_g = 0.0f;
+  if (rep_on) {
     const int hh = tid;
     float gsum = 0.0f;
     for (int q = 0; q < ncls; ++q) {
@@ -614,34 +696,29 @@ __global__ __launch_bounds__(ECDA_THREADS) void dad_ecda(DadEcdaArgs a) {
       const float nd = pdist[c][q];
       if (nd > 0.0f) gsum += (S.cent[c][hh] - S.cent[q][hh]) / nd;
     }
-    const float gval = wscale * rep_coef * (-gsum / (float)npairs / (float)S.cnt_noisy[c]);
-    for (int b = 0; b < Bn; ++b)
-      if (S.prd[b] == c) ge_s[(size_t)b * DAD_H + hh] += gval;
+    rep_g = wscale * rep_coef * (-gsum / (float)npairs / (float)S.cnt_noisy[c]);
   }
-  __syncthreads();
-  if (!gated[c]) return;
-  // members of class c: clean (label c, weight 1) then masked noisy (pseudo-label c, weight = score)
-  int n = ecda_compact(S, B, 0, [&](int i) { return S.lab[i] == c; }, [](int) { return 1.0f; });
+  if (!gated[c] && !rep_on) return;
+  // members of class c: clean (label c, weight 1) then masked noisy (pseudo-label c, weight = score);
+  // a class below the gate only needs its noisy members (repulsion)
+  int n = gated[c] ? ecda_compact(S, B, 0, [&](int i) { return S.lab[i] == c; }, [](int) { return 1.0f; }) : 0;
   const int ns = n;
   n = ecda_compact(S, Bn, n, [&](int i) { return S.prd[i] == c; }, [&](int i) { return S.scr[i]; });
   const int nt = n - ns;
-  const float mmd = ecda_mmd(S, emb_c, emb_s, ge_c, ge_s, ns, n, scratch, wscale * att_c);
+  const EcdaRows R{emb_c, emb_s, &S, ns, n <= ECDA_NZ};
+  float* D = nullptr;
+  float mmd = 0.0f;
+  if (gated[c]) {
+    D = R.staged ? S.dm : scratch;
+    ecda_stage(S, R, n);
+    mmd = ecda_mmd_coef(S, R, n, D);
+  }
   // compactness (I/utils.py:614-616): mean_j ||z_j - mu||^2, grad (2/nt)(z_j - mu)
   float cpart = 0.0f;
-  for (int k = tid; k < nt * DAD_H; k += ECDA_THREADS) {
-    const int j = k / DAD_H, hh = k - j * DAD_H;
-    const int b = S.idx[ns + j];
-    const float df = emb_s[(size_t)b * DAD_H + hh] - S.cent[c][hh];
-    cpart += df * df;
-    ge_s[(size_t)b * DAD_H + hh] += wscale * att_c * cfg.ecda_gamma * (2.0f / (float)nt) * df;
-  }
-  float comp = dad_wave_sum(cpart);
-  __syncthreads();
-  if ((tid & 63) == 0) S.fred[tid >> 6] = comp;
-  __syncthreads();
-  comp = 0.0f;
-  for (int k = 0; k < ECDA_THREADS / 64; ++k) comp += S.fred[k];
-  comp /= (float)nt;
+  ecda_member_grads(S, R, n, D, wscale * att_c, gated[c] ? S.cent[c] : nullptr,
+                    wscale * att_c * cfg.ecda_gamma * (2.0f / (float)nt), rep_g, ge_c, ge_s, cpart);
+  if (!gated[c]) return;
+  const float comp = ecda_block_sum_f(S, cpart) / (float)nt;
   if (tid == 0) {
     a.tail_terms[c] = att_c * (mmd + cfg.ecda_gamma * comp + cfg.ecda_delta * rep);
     a.tail_terms[DAD_T_ECDA_GATE - DAD_T_ECDA_TERM + c] = 1.0f;

@@ -158,7 +158,7 @@ template <int BR> struct XRaw { using T = f32x4; };
 template <> struct XRaw<1> { using T = bf16x4; };
 template <int BR> struct SlabRegs {
   typename XRaw<BR>::T x[4];
-  uint32_t word;
+  uint32_t word[4];   // ReLU' bits of rows (tid>>5)+8m, hidden units 8*(tid&31) .. +7 in byte (tid&3)
   float ge, len;
   int nvalid;
 };
@@ -181,7 +181,8 @@ __device__ __forceinline__ void wg_load(const DadWgradArgs& a, int s, int dbase,
     if constexpr (BR == 0) r.x[m] = *reinterpret_cast<const f32x4*>(a.xc + off);
     else r.x[m] = *reinterpret_cast<const bf16x4*>(a.xs_bf16 + off);
   }
-  r.word = a.bits[(bits_row + (tid >> 3)) * DAD_HT + (tid & 7)];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) r.word[m] = a.bits[(bits_row + (tid >> 5) + 8 * m) * DAD_HT + ((tid & 31) >> 2)];
   r.ge = a.ge[(size_t)erow * DAD_H + tid];
   r.len = a.vlen[erow];
 }
@@ -200,18 +201,20 @@ __device__ __forceinline__ void wg_stage(const SlabRegs<BR>& r, __bf16* Xt, __bf
   }
   sc[tid] = r.ge / fmaxf(r.len, 1.0f);
   __syncthreads();
-  const int row = tid >> 3, hq = tid & 7;
-  const f32x4* sv = reinterpret_cast<const f32x4*>(sc + hq * 32);
+  // G rows: 32 consecutive lanes write one 512-B row (conflict-free ds_write_b128)
+  const int c16 = tid & 31;
+  const f32x4 lo = reinterpret_cast<const f32x4*>(sc)[2 * c16];
+  const f32x4 hi = reinterpret_cast<const f32x4*>(sc)[2 * c16 + 1];
 #pragma unroll
-  for (int g8 = 0; g8 < 4; ++g8) {
-    const f32x4 lo = sv[2 * g8], hi = sv[2 * g8 + 1];
+  for (int m = 0; m < 4; ++m) {
+    const uint32_t byte = r.word[m] >> ((c16 & 3) * 8);
     bf16x8 gv;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      gv[e] = (__bf16)(((r.word >> (g8 * 8 + e)) & 1u) ? lo[e] : 0.0f);
-      gv[e + 4] = (__bf16)(((r.word >> (g8 * 8 + e + 4)) & 1u) ? hi[e] : 0.0f);
+      gv[e] = (__bf16)(((byte >> e) & 1u) ? lo[e] : 0.0f);
+      gv[e + 4] = (__bf16)(((byte >> (e + 4)) & 1u) ? hi[e] : 0.0f);
     }
-    *reinterpret_cast<bf16x8*>(&Gt[row * WG_GP + hq * 32 + g8 * 8]) = gv;
+    *reinterpret_cast<bf16x8*>(&Gt[((tid >> 5) + 8 * m) * WG_GP + c16 * 8]) = gv;
   }
 }
 
@@ -239,25 +242,28 @@ __device__ __forceinline__ void wg_phase(const DadWgradArgs& a, int lo, int hi, 
   if (lo >= hi) return;
   const int wv = threadIdx.x >> 6;
   SlabRegs<BR> r0, r1, r2;
+  // prefetches are unconditional (slab index clamped to the last one): conditional loads
+  // make the compiler merge the paths' pending counts into a vmcnt(0) drain
+  const int last = hi - 1;
   wg_load<BR>(a, lo, dbase, r0);
-  if (lo + 1 < hi) wg_load<BR>(a, lo + 1, dbase, r1);
-  if (lo + 2 < hi) wg_load<BR>(a, lo + 2, dbase, r2);
+  wg_load<BR>(a, min(lo + 1, last), dbase, r1);
+  wg_load<BR>(a, min(lo + 2, last), dbase, r2);
   for (int s = lo; s < hi; s += 3) {
     __syncthreads();                 // previous compute finished reading Xt/Gt/sc
     wg_stage<BR>(r0, Xt, Gt, sc);
-    if (s + 3 < hi) wg_load<BR>(a, s + 3, dbase, r0);
+    wg_load<BR>(a, min(s + 3, last), dbase, r0);
     __syncthreads();
     wg_compute(Xt, Gt, wv, acc);
     if (s + 1 >= hi) break;
     __syncthreads();
     wg_stage<BR>(r1, Xt, Gt, sc);
-    if (s + 4 < hi) wg_load<BR>(a, s + 4, dbase, r1);
+    wg_load<BR>(a, min(s + 4, last), dbase, r1);
     __syncthreads();
     wg_compute(Xt, Gt, wv, acc);
     if (s + 2 >= hi) break;
     __syncthreads();
     wg_stage<BR>(r2, Xt, Gt, sc);
-    if (s + 5 < hi) wg_load<BR>(a, s + 5, dbase, r2);
+    wg_load<BR>(a, min(s + 5, last), dbase, r2);
     __syncthreads();
     wg_compute(Xt, Gt, wv, acc);
   }
