@@ -171,6 +171,11 @@ int dad_step_backward(const dad_config* cfg, const dad_batch* batch, const dad_s
 int dad_step_apply(const dad_config* cfg, const dad_state* st, void* workspace, void* stream);
 int dad_step(const dad_config* cfg, const dad_batch* batch, const dad_state* st,
              void* workspace, void* stream);
+/* Trainer.train_step alone (I/train.py:397-471) for callers that keep their own
+ * backward/clip/optimizer/EMA (I/train.py:486-492): after dad_step_compute, commits the
+ * DACP state update of calculate_mask (I/utils.py:485-505) and writes st->losses; the
+ * pre-clip gradient of total_loss stays in st->grad (rank mean when dp_world > 1). */
+int dad_step_commit(const dad_config* cfg, const dad_state* st, void* workspace, void* stream);
 
 /* DACPManager.update_class_quality_scores_epoch (I/utils.py:430-447) */
 int dad_epoch_end(const dad_config* cfg, const dad_state* st, void* stream);

@@ -383,11 +383,17 @@ class DADOracle:
             d = (e * (keep.astype(F32) / F32(1 - p)).astype(F32)).astype(F32)
         return (d @ W2.T + b2).astype(F32), d
 
-    def step(self, inp, epoch, lr=None, rng=None):
+    def step(self, inp, epoch, lr=None, rng=None, allreduce=None, world=1):
         """One step on inputs ``inp`` (oracle/synth.make_step_inputs layout).
 
         If the injected draws are absent, they are sampled from ``rng`` (numpy Generator):
         that is the CPU-baseline mode, timing the same work the reference's step does.
+
+        Data parallel (the build's DP contract): ``allreduce(vec)`` returns
+        the SUM over ``world`` ranks of a float64 vector [grads | floored tau' | score-sum
+        deltas | count deltas | losses].  Each rank's mask/losses are the reference on its own
+        shard; the update uses the rank-mean gradient, the committed thresholds are
+        alpha*tau + (1-alpha)*mean(tau'), and the epoch score statistics are summed.
         """
         cfg = self.cfg
         use_dacp, use_ecda, use_entropy, class_aware = effective_switches(cfg)
@@ -442,6 +448,7 @@ class DADOracle:
             q = softmax(zt).astype(F32)
             if use_dacp:
                 tau_before = self.dacp.tau.copy()
+                sums_before = (self.dacp.score_sum.copy(), self.dacp.score_cnt.copy())
                 mask, s, pred, w, floored = dacp_mask(self.dacp, q, epoch, self.anchors, cfg, use_entropy)
                 out.update(tau_before=tau_before, tau_after=self.dacp.tau.copy(), w=w, floored=floored)
                 maskf = mask.astype(np.float64)
@@ -490,6 +497,29 @@ class DADOracle:
         grads = [gW1, gb1, gW2.astype(F32), gb2.astype(F32)]
         total = ce + w_kl * kl + w_ecda * ecda
         out.update(consistency_loss=kl, ecda_loss=ecda, total_loss=total, grads=[g.copy() for g in grads])
+        if allreduce is not None and world > 1:
+            dacp_on = use_dacp and not warm
+            Cn = len(self.dacp.tau)
+            fl = np.asarray(out["floored"], np.float64) if dacp_on else np.zeros(Cn)
+            dsum = (self.dacp.score_sum - sums_before[0]) if dacp_on else np.zeros(Cn)
+            dcnt = (self.dacp.score_cnt - sums_before[1]).astype(np.float64) if dacp_on else np.zeros(Cn)
+            vec = np.concatenate([g.astype(np.float64).reshape(-1) for g in grads] +
+                                 [fl, dsum, dcnt, np.array([total, ce, kl, ecda], np.float64)])
+            vec = np.asarray(allreduce(vec), np.float64)
+            o, new = 0, []
+            for g in grads:
+                new.append((vec[o:o + g.size] / world).astype(F32).reshape(g.shape))
+                o += g.size
+            grads = new
+            if dacp_on:
+                a = cfg["DACP_THRESHOLD_SMOOTHING_ALPHA"]
+                mean_fl = (vec[o:o + Cn] / world).astype(F32)
+                self.dacp.tau = (F32(a) * tau_before + F32(1 - a) * mean_fl).astype(F32)
+                self.dacp.score_sum = sums_before[0] + vec[o + Cn:o + 2 * Cn]
+                self.dacp.score_cnt = sums_before[1] + np.rint(vec[o + 2 * Cn:o + 3 * Cn]).astype(np.int64)
+                out["tau_committed"] = self.dacp.tau.copy()
+            out["losses_mean"] = vec[o + 3 * Cn:o + 3 * Cn + 4] / world
+            out["grads_mean"] = [g.copy() for g in grads]
 
         # ---- clip_grad_norm_ (I/train.py:487-488)
         norms = [np.sqrt(np.sum(g.astype(np.float64) ** 2)) for g in grads]

@@ -13,9 +13,9 @@ from . import _build, _lib
 from .config import FLAVOR_DEFAULTS, ConfigView, dad_config_for
 from .model import EmotionClassifier, Emotion2VecEncoder, SSRLModel
 from .step import DADStep
-from .dist import DPComm
+from .dist import DPComm, ProcessGroupComm
 
-__all__ = ["SSRLModel", "Emotion2VecEncoder", "EmotionClassifier", "DADStep", "DPComm", "ConfigView",
+__all__ = ["SSRLModel", "Emotion2VecEncoder", "EmotionClassifier", "DADStep", "DPComm", "ProcessGroupComm", "ConfigView",
            "dad_config_for", "FLAVOR_DEFAULTS", "build", "lib"]
 
 

@@ -78,6 +78,8 @@ EXPORTS = {
                                       ctypes.c_void_p, ctypes.c_void_p]),
     "dad_step": (ctypes.c_int, [ctypes.POINTER(DadConfig), ctypes.POINTER(DadBatch), ctypes.POINTER(DadState),
                                 ctypes.c_void_p, ctypes.c_void_p]),
+    "dad_step_commit": (ctypes.c_int, [ctypes.POINTER(DadConfig), ctypes.POINTER(DadState),
+                                       ctypes.c_void_p, ctypes.c_void_p]),
     "dad_epoch_end": (ctypes.c_int, [ctypes.POINTER(DadConfig), ctypes.POINTER(DadState), ctypes.c_void_p]),
     "dad_refresh_shadow": (ctypes.c_int, [ctypes.POINTER(DadState), ctypes.c_void_p]),
     "dad_teacher_ema": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_float,

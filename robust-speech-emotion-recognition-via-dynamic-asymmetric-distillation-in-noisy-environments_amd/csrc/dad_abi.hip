@@ -244,6 +244,23 @@ int dad_step_apply(const dad_config* cfg, const dad_state* st, void* workspace, 
   return DAD_OK;
 }
 
+int dad_step_commit(const dad_config* cfg, const dad_state* st, void* workspace, void* stream_) {
+  int rc = check_cfg(cfg);
+  if (rc) return rc;
+  if (!st || !st->grad || !st->dacp || !st->tail || !workspace) return DAD_E_ARG;
+  hipStream_t stream = (hipStream_t)stream_;
+  if (cfg->dp_world > 1) {
+    const DadWs L = dad_ws_layout(geom_of(cfg), max_splits_of(cfg), cfg->precision);
+    const int nblk = (DAD_NPARAM + 1023) / 1024;
+    hipLaunchKernelGGL(dad_norm, dim3(nblk), dim3(256), 0, stream, st->grad, ws_ptr<float>(workspace, L.normpart),
+                       1.0f / (float)cfg->dp_world);
+    DAD_TRY(hipGetLastError());
+  }
+  hipLaunchKernelGGL(dad_commit_kernel, dim3(1), dim3(64), 0, stream, *cfg, st->grad, st->dacp, st->tail, st->losses);
+  DAD_TRY(hipGetLastError());
+  return DAD_OK;
+}
+
 int dad_step(const dad_config* cfg, const dad_batch* batch, const dad_state* st, void* workspace, void* stream) {
   int rc = dad_step_compute(cfg, batch, st, workspace, stream);
   if (rc) return rc;

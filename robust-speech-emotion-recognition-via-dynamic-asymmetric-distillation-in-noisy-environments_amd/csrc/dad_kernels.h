@@ -93,6 +93,7 @@ __global__ void dad_wgrad_bf16(DadWgradArgs a);
 __global__ void dad_reduce(DadReduceArgs a);
 __global__ void dad_norm(float* grad, float* normpart, float inv_world);
 __global__ void dad_optim(DadOptimArgs a);
+__global__ void dad_commit_kernel(dad_config cfg, const float* grad, float* dacp, float* tailf, float* losses_out);
 __global__ void dad_epoch_end_kernel(float* dacp, float beta, float one_m_beta);
 __global__ void dad_shadow_kernel(const float* student, const float* teacher, __bf16* ws, __bf16* wt);
 

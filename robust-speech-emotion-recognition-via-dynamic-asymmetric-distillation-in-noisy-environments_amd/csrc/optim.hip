@@ -12,6 +12,28 @@
 #include "dad_common.h"
 #include "dad_kernels.h"
 
+// DACP state commit (thresholds were computed against the pre-step state by dad_tail;
+// with data parallelism the floored thresholds are the rank mean): tau EMA and the epoch
+// score collection of calculate_mask (I/utils.py:485-505).  Threads 0..C-1.
+__device__ __forceinline__ void dacp_commit(const dad_config& cfg, const float* grad, float* d, int tid) {
+  if (tid < DAD_C && !cfg.warmup && cfg.use_dacp) {
+    const float* ex = grad + DAD_NPARAM;
+    d[tid] = cfg.dacp_alpha * d[tid] + cfg.dacp_one_m_alpha * ex[tid];
+    d[8 + tid] += ex[4 + tid];
+    d[12 + tid] += ex[8 + tid];
+  }
+}
+
+// train_step without the update (the caller runs clip / optimizer.step / EMA itself,
+// I/train.py:486-492): commit the DACP state and publish this step's losses.
+__global__ void dad_commit_kernel(dad_config cfg, const float* grad, float* dacp, float* tailf, float* losses_out) {
+  const int tid = threadIdx.x;
+  const float* ex = grad + DAD_NPARAM;
+  if (tid == 0) tailf[DAD_T_TOTAL] = ex[12];
+  if (losses_out && tid < 4) losses_out[tid] = ex[12 + tid];
+  dacp_commit(cfg, grad, dacp, tid);
+}
+
 __global__ __launch_bounds__(256) void dad_optim(DadOptimArgs a) {
   __shared__ float coef_s;
   const dad_config& cfg = a.cfg;
@@ -35,15 +57,7 @@ __global__ __launch_bounds__(256) void dad_optim(DadOptimArgs a) {
       }
     }
   }
-  // DACP state commit (thresholds were computed against the pre-step state by dad_tail;
-  // with data parallelism the floored thresholds are the rank mean)
-  if (blockIdx.x == 0 && tid < DAD_C && !cfg.warmup && cfg.use_dacp) {
-    const float* ex = a.grad + DAD_NPARAM;
-    float* d = a.dacp;
-    d[tid] = cfg.dacp_alpha * d[tid] + cfg.dacp_one_m_alpha * ex[tid];
-    d[8 + tid] += ex[4 + tid];
-    d[12 + tid] += ex[8 + tid];
-  }
+  if (blockIdx.x == 0) dacp_commit(cfg, a.grad, a.dacp, tid);
   __syncthreads();
   const float coef = coef_s;
   const size_t n0 = (size_t)blockIdx.x * 1024;

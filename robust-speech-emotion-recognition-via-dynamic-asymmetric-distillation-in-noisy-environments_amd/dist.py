@@ -42,7 +42,7 @@ class DPComm:
         _lib.check(L.dad_comm_init(ctypes.byref(handle), world, idbuf, rank), "dad_comm_init")
         return cls(rank, world, handle)
 
-    def allreduce_grad(self, state_struct, stream):
+    def allreduce_grad(self, state_struct, stream, grad=None):
         if self.world == 1:
             return
         _lib.check(_lib.lib().dad_comm_allreduce_grad(self._comm, state_struct, stream), "dad_comm_allreduce_grad")
@@ -51,3 +51,29 @@ class DPComm:
         if self._comm is not None:
             _lib.lib().dad_comm_destroy(self._comm)
             self._comm = None
+
+
+class ProcessGroupComm:
+    """The same exchange over an existing torch.distributed process group (any backend).
+
+    `DPComm` (RCCL through the C ABI) is the production path.  This one issues the SUM
+    all-reduce of the step's [grads | tau' | score sums | counts | losses] buffer with
+    torch.distributed on the current stream, so the data-parallel step can also run
+    where RCCL cannot, e.g. several ranks sharing one GPU over gloo (tests, rehearsals).
+    """
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        self._dist = dist
+        self.group = group
+        self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+
+    def allreduce_grad(self, state_struct, stream, grad=None):
+        if self.world == 1:
+            return
+        if grad is None:
+            raise ValueError("ProcessGroupComm needs the grad tensor")
+        self._dist.all_reduce(grad, op=self._dist.ReduceOp.SUM, group=self.group)
+
+    def close(self):
+        pass

@@ -39,6 +39,31 @@ def _dev_batch(batch, device, labels=True):
     return x, pad, y
 
 
+class _StepLossFn(torch.autograd.Function):
+    """total_loss whose backward hands the step's analytic gradient to the student params.
+
+    forward(loss, flat_grad, W1, b1, W2, b2) -> loss; d(loss)/d(param) = slices of flat_grad
+    (computed by the fused kernels against the parameters the forward saw)."""
+
+    @staticmethod
+    def forward(ctx, loss, flat_grad, *params):
+        ctx.save_for_backward(flat_grad)
+        ctx.shapes = [p.shape for p in params]
+        return loss.detach().clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        (flat,) = ctx.saved_tensors
+        out, off = [], 0
+        for shp in ctx.shapes:
+            n = 1
+            for d in shp:
+                n *= d
+            out.append((flat[off:off + n] * g).view(shp))
+            off += n
+        return (None, None, *out)
+
+
 class DADStep:
     """Owns the device state of the DAD step around an `SSRLModel`.
 
@@ -82,6 +107,7 @@ class DADStep:
         self._ws = None
         self._bufs = {}
         self.kernel_events = None     # list -> (start, end) events around each encoder launch
+        self._shadow_dirty = False
         self.refresh_shadow()
 
     # ----------------------------------------------------------------------------- state
@@ -106,6 +132,7 @@ class DADStep:
         """Re-derive the bf16 W1 shadows after the caller changed the model's parameters."""
         st = self._state_struct(0)
         _lib.check(_lib.lib().dad_refresh_shadow(st, self._stream()), "dad_refresh_shadow")
+        self._shadow_dirty = False
 
     def state_dict(self):
         return {"exp_avg": self.exp_avg.clone(), "exp_avg_sq": self.exp_avg_sq.clone(),
@@ -167,8 +194,8 @@ class DADStep:
                               counter=self.global_step,
                               dp_world=self.comm.world if self.comm is not None else 1, splits=self.splits)
 
-    def step(self, clean_batch, noisy_batch, epoch, lr=None, draws=None):
-        """One full training step; returns the reference's loss dict as 0-d device tensors."""
+    def _prepare(self, clean_batch, noisy_batch, epoch, lr, draws):
+        """Device batch + POD structs for one step (shared by step() and train_step())."""
         dev = self.device
         xc, mc, yc = _dev_batch(clean_batch, dev)
         warm = epoch < self.view.WARMUP_EPOCHS
@@ -203,8 +230,16 @@ class DADStep:
                 setattr(bt, k, v.data_ptr())
             keep.append(dd)
         st = self._state_struct(Bn, Bc)
-        self._loss_vec = torch.empty(4, device=dev)          # written by the optimizer kernel
+        self._loss_vec = torch.empty(4, device=dev)          # written by the optimizer/commit kernel
         st.losses = self._loss_vec.data_ptr()
+        self._keepalive = (xc, mc, yc, xn, mn, keep)
+        return cfg, bt, st
+
+    def step(self, clean_batch, noisy_batch, epoch, lr=None, draws=None):
+        """One full training step; returns the reference's loss dict as 0-d device tensors."""
+        if self._shadow_dirty:
+            self.refresh_shadow()
+        cfg, bt, st = self._prepare(clean_batch, noisy_batch, epoch, lr, draws)
         ws = self._workspace(cfg)
         stream = self._stream()
         L = _lib.lib()
@@ -218,12 +253,37 @@ class DADStep:
             ev.append((e0, e1))
         _lib.check(L.dad_step_backward(cfg, bt, st, _lib.ptr(ws), stream), "dad_step_backward")
         if self.comm is not None and self.comm.world > 1:
-            self.comm.allreduce_grad(st, stream)
+            self.comm.allreduce_grad(st, stream, grad=self.grad)
         _lib.check(L.dad_step_apply(cfg, st, _lib.ptr(ws), stream), "dad_step_apply")
         self.adam_step += 1
         self.global_step += 1
-        self._keepalive = (xc, mc, yc, xn, mn, keep)
         return self.losses()
+
+    def train_step(self, clean_batch, noisy_batch, epoch, draws=None):
+        """Trainer.train_step (I/train.py:397-471) with an autograd-compatible total_loss.
+
+        For callers that keep the reference loop body (I/train.py:484-492):
+        `losses['total_loss'].backward()` deposits the kernels' analytic gradient into the
+        student parameters' .grad, then the caller's clip_grad_norm_, optimizer.step() and
+        model.update_teacher_ema() run as in the reference.  The DACP state update happens
+        here, as in calculate_mask.  The other loss terms are returned detached.
+        """
+        if self.comm is not None and self.comm.world > 1:
+            raise RuntimeError("train_step is the single-process shim; use step() with a DPComm")
+        self.refresh_shadow()        # the caller's optimizer/EMA changed the fp32 params
+        cfg, bt, st = self._prepare(clean_batch, noisy_batch, epoch, None, draws)
+        ws = self._workspace(cfg)
+        stream = self._stream()
+        L = _lib.lib()
+        _lib.check(L.dad_step_compute(cfg, bt, st, _lib.ptr(ws), stream), "dad_step_compute")
+        _lib.check(L.dad_step_commit(cfg, st, _lib.ptr(ws), stream), "dad_step_commit")
+        self.global_step += 1
+        self._shadow_dirty = True
+        out = self.losses()
+        m = self.model
+        params = m._plist(m.student_encoder, m.student_classifier)
+        out["total_loss"] = _StepLossFn.apply(out["total_loss"], self.grad[:_lib.DAD_NPARAM].clone(), *params)
+        return out
 
     def losses(self):
         """Loss dict of the last step (keys of I/train.py:468-470 + scl_loss for CASIA/EMODB)."""

@@ -1,0 +1,96 @@
+"""Data-parallel HIP step, world_size 2 on the one-GPU box: two ranks share cuda:0 and
+exchange the step's [grads | tau' | sums | counts | losses] buffer with ProcessGroupComm over
+gloo.  That runs the kernels' DP path (dad_norm rank-mean, replicated clip/Adam/EMA, DACP
+commit of the mean tau'); the RCCL transport itself (DPComm) is exercised by the driver's
+multi-GPU bench.  Each rank checks itself against the oracle's DP step on its own shard.
+"""
+import multiprocessing as mp
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+B, T, SEED = 12, 40, 21
+SCHEDULE = [35, 60]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _rank_main(rank, world, port, q):
+    try:
+        import torch
+        import torch.distributed as dist
+        import dadpkg
+        import gpu_harness as gh
+        from oracle import dad_oracle, synth
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        p = dadpkg.pkg()
+        cfg = dad_oracle.make_cfg("iemocap")
+        model = p.SSRLModel().cuda()
+        step = p.DADStep(model, p.ConfigView(cfg, flavor="iemocap"), precision="fp32", rng="explicit",
+                         comm=p.ProcessGroupComm())
+        st = synth.make_state(SEED, 1)
+        gh.load_state(step, st)
+        orc = dad_oracle.DADOracle(*synth.init_weights(SEED)[:4], cfg)
+        orc.load_state(st)
+
+        def allreduce(v):
+            t = torch.from_numpy(np.ascontiguousarray(v, np.float64))
+            dist.all_reduce(t)
+            return t.numpy()
+
+        msgs = []
+        for k, epoch in enumerate(SCHEDULE):
+            inp = synth.make_step_inputs(SEED + 100 * rank, k, B, T)
+            o = gh.run_step(step, inp, epoch)
+            r = orc.step(inp, epoch, allreduce=allreduce, world=world)
+            gh.close(o["total_loss"], r["losses_mean"][0], 1e-4, "rank mean total loss")
+            np.testing.assert_array_equal(o["mask"], r["mask"])
+            for i in range(4):
+                gh.close_grad(o["grads"][i], r["grads_mean"][i], "rank %d step %d mean grad %d" % (rank, k, i))
+                gh.close_grad(o["student"][i], r["student"][i], "rank %d step %d student %d" % (rank, k, i))
+                gh.close_grad(o["teacher"][i], r["teacher"][i], "rank %d step %d teacher %d" % (rank, k, i))
+            np.testing.assert_allclose(o["dacp"][0:4], orc.dacp.tau, rtol=0, atol=1e-6)
+            np.testing.assert_allclose(o["dacp"][12:16], orc.dacp.score_cnt, rtol=0, atol=0)
+            msgs.append(o["student"][0].copy())
+        # replicas agree bit-for-bit
+        mine = torch.from_numpy(np.concatenate([m.reshape(-1) for m in msgs]).astype(np.float64))
+        other = mine.clone()
+        dist.broadcast(other, src=0)
+        assert torch.equal(mine, other), "ranks diverged"
+        dist.destroy_process_group()
+        q.put((rank, "ok"))
+    except BaseException as e:  # report to the parent instead of hanging it
+        import traceback
+        q.put((rank, "FAIL: %r\n%s" % (e, traceback.format_exc())))
+
+
+def test_dp_step_two_ranks_match_oracle():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in procs:
+            rank, msg = q.get(timeout=400)
+            res[rank] = msg
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.exitcode is None:
+                p.kill()
+    assert res == {0: "ok", 1: "ok"}, res

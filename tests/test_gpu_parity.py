@@ -193,3 +193,45 @@ def test_modular_encoder_matches_torch_fp32():
     m.update_teacher_ema()
     exp = t0 * np.float32(0.99) + m.student_flat * np.float32(1.0 - 0.99)
     assert gh.rel(m.teacher_flat.cpu(), exp.cpu()) < 1e-6
+
+
+def test_train_step_shim_with_reference_loop_body():
+    """Autograd-compatible train_step + the reference's own loop body (I/train.py:484-492):
+    total_loss.backward(), torch clip_grad_norm_, torch Adam (seeded with the same moments),
+    update_teacher_ema -- against the oracle's full step."""
+    cfg = dad_oracle.make_cfg("iemocap")
+    inp = _problem(B=16, T=40, seed=4)
+    st = synth.make_state(4, 1)
+    step = gh.make_step(cfg)
+    gh.load_state(step, st)
+    orc = dad_oracle.DADOracle(*synth.init_weights(4)[:4], cfg)
+    orc.load_state(st)
+    m = step.model
+    m.ema_momentum = cfg["EMA_MOMENTUM"]
+    params = m._plist(m.student_encoder, m.student_classifier)
+    lr = dad_oracle.cosine_lr(cfg, 60)
+    opt = torch.optim.Adam(params, lr=lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=cfg["WEIGHT_DECAY"])
+    for p, ea, eas in zip(params, st["exp_avg"], st["exp_avg_sq"]):
+        opt.state[p] = {"step": torch.tensor(float(st["nstep"])),
+                        "exp_avg": torch.from_numpy(np.asarray(ea, np.float32)).cuda(),
+                        "exp_avg_sq": torch.from_numpy(np.asarray(eas, np.float32)).cuda()}
+    clean, noisy, draws = gh.batches(inp)
+    opt.zero_grad()
+    losses = step.train_step(clean, noisy, 60, draws=draws)
+    assert losses["total_loss"].requires_grad
+    losses["total_loss"].backward()
+    torch.nn.utils.clip_grad_norm_(params, cfg["MAX_GRAD_NORM"])
+    opt.step()
+    m.update_teacher_ema()
+    torch.cuda.synchronize()
+    r = orc.step(inp, 60)
+    for k in ("total_loss", "supervised_ce_loss", "consistency_loss", "ecda_loss"):
+        _cmp_loss(float(losses[k].detach()), r[k], k)
+    student = gh.unflat(m.student_flat.detach().cpu().numpy())
+    teacher = gh.unflat(m.teacher_flat.detach().cpu().numpy())
+    for k in range(4):
+        gh.close_grad(student[k], r["student"][k], "shim student %d" % k)
+        gh.close_grad(teacher[k], r["teacher"][k], "shim teacher %d" % k)
+    np.testing.assert_allclose(step.dacp[0:4].cpu().numpy(), r["tau_after"], atol=1e-6)
+    # a fused step afterwards sees the caller-updated parameters (bf16 shadows refreshed)
+    assert step._shadow_dirty
