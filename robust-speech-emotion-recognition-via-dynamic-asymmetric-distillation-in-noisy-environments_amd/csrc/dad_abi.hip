@@ -132,8 +132,8 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   // bf16: 8-wave workgroups, 4 noisy slabs (teacher + student waves) or 8 clean slabs each
   const dim3 egrid_bf16((Bn * G.ncn + 3) / 4 + (G.Bc * G.ncc + 7) / 8);
   if (do_encode) {
-    if (bf16) hipLaunchKernelGGL(dad_encode_bf16, egrid_bf16, dim3(512), 0, stream, ea);
-    else hipLaunchKernelGGL(dad_encode_f32, egrid, dim3(256), 0, stream, ea);
+    if (bf16) hipLaunchKernelGGL(dad_encode_bf16, egrid_bf16, dim3(DAD_ENC_BF16_THREADS), 0, stream, ea);
+    else hipLaunchKernelGGL(dad_encode_f32, egrid, dim3(DAD_ENC_F32_THREADS), 0, stream, ea);
     DAD_TRY(hipGetLastError());
   }
   if (!do_backward) return DAD_OK;
@@ -149,7 +149,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   pa.p_drop = cfg->p_drop; pa.drop_scale = cfg->drop_scale;
   pa.emb = st->emb; pa.vlen = vlen; pa.logits = st->logits;
   pa.part_cnt = part_cnt; pa.cnt_tot = cnt_tot;
-  hipLaunchKernelGGL(dad_pool, dim3(G.Bc + Bn), dim3(256), 0, stream, pa);
+  hipLaunchKernelGGL(dad_pool, dim3(G.Bc + Bn), dim3(DAD_POOL_THREADS), 0, stream, pa);
   DAD_TRY(hipGetLastError());
 
   // 3. losses, DACP mask, analytic backward to dL/de and the classifier grads
@@ -159,7 +159,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   if (explicit_rng) { ta.keep1 = bt->keep1; ta.keep2 = bt->keep2; }
   ta.key_drop1 = k.drop1; ta.key_drop2 = k.drop2;
   ta.dacp = st->dacp; ta.tailf = st->tail; ta.ge = ge; ta.grad = st->grad;
-  hipLaunchKernelGGL(dad_tail, dim3(1), dim3(1024), 0, stream, ta);
+  hipLaunchKernelGGL(dad_tail, dim3(1), dim3(DAD_TAIL_THREADS), 0, stream, ta);
   DAD_TRY(hipGetLastError());
 
   // 4. ECDA (class-aware MMD + compactness + repulsion) and its embedding grads
@@ -168,7 +168,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
     memset(&ca, 0, sizeof(ca));
     ca.cfg = *cfg; ca.yc = bt->yc; ca.emb = st->emb; ca.tailf = st->tail;
     ca.tail_terms = st->tail + DAD_T_ECDA_TERM; ca.ge = ge; ca.scratch = ecda_scratch;
-    hipLaunchKernelGGL(dad_ecda, dim3(DAD_C), dim3(256), 0, stream, ca);
+    hipLaunchKernelGGL(dad_ecda, dim3(DAD_C), dim3(DAD_ECDA_THREADS), 0, stream, ca);
     DAD_TRY(hipGetLastError());
   }
 
@@ -182,8 +182,8 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   wa.key_strong = k.strong; wa.key_feat = k.feat; wa.key_tstart = k.tstart;
   wa.strong_std = cfg->strong_std; wa.feat_p = cfg->feat_p;
   wa.bits = bits; wa.ge = ge; wa.vlen = vlen; wa.xs_bf16 = xs_bf16; wa.wpart = wpart;
-  if (bf16) hipLaunchKernelGGL(dad_wgrad_bf16, dim3(6 * splits), dim3(256), 0, stream, wa);
-  else hipLaunchKernelGGL(dad_wgrad_f32, dim3(6 * splits), dim3(256), 0, stream, wa);
+  if (bf16) hipLaunchKernelGGL(dad_wgrad_bf16, dim3(6 * splits), dim3(DAD_WGRAD_THREADS), 0, stream, wa);
+  else hipLaunchKernelGGL(dad_wgrad_f32, dim3(6 * splits), dim3(DAD_WGRAD_THREADS), 0, stream, wa);
   DAD_TRY(hipGetLastError());
 
   // 6. reduce partials -> dW1, db1; loss totals; squared-norm partials (single GPU)
@@ -194,7 +194,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   ra.w_kl = cfg->w_kl; ra.w_ecda = cfg->w_ecda;
   ra.wpart = wpart; ra.ge = ge; ra.vlen = vlen; ra.cnt_tot = cnt_tot; ra.tailf = st->tail;
   ra.grad = st->grad; ra.normpart = normpart;
-  hipLaunchKernelGGL(dad_reduce, dim3(193), dim3(256), 0, stream, ra);
+  hipLaunchKernelGGL(dad_reduce, dim3(DAD_REDUCE_BLOCKS), dim3(DAD_REDUCE_THREADS), 0, stream, ra);
   DAD_TRY(hipGetLastError());
   return DAD_OK;
 }
@@ -224,7 +224,7 @@ int dad_step_apply(const dad_config* cfg, const dad_state* st, void* workspace, 
   const DadWs L = dad_ws_layout(geom_of(cfg), max_splits_of(cfg), cfg->precision);
   float* normpart = ws_ptr<float>(workspace, L.normpart);
   const int nblk = (DAD_NPARAM + 1023) / 1024;
-  int nnorm = 193;
+  int nnorm = DAD_REDUCE_BLOCKS;
   if (cfg->dp_world > 1) {
     hipLaunchKernelGGL(dad_norm, dim3(nblk), dim3(256), 0, stream, st->grad, normpart, 1.0f / (float)cfg->dp_world);
     DAD_TRY(hipGetLastError());
@@ -239,7 +239,7 @@ int dad_step_apply(const dad_config* cfg, const dad_state* st, void* workspace, 
   oa.w1bf_teacher = reinterpret_cast<__bf16*>(st->w1bf_teacher);
   oa.dacp = st->dacp; oa.tailf = st->tail; oa.normpart = normpart; oa.nnorm = nnorm;
   oa.losses_out = st->losses;
-  hipLaunchKernelGGL(dad_optim, dim3(nblk), dim3(256), 0, stream, oa);
+  hipLaunchKernelGGL(dad_optim, dim3(nblk), dim3(DAD_OPTIM_THREADS), 0, stream, oa);
   DAD_TRY(hipGetLastError());
   return DAD_OK;
 }
@@ -335,8 +335,8 @@ int encoder_forward_impl(const float* x, const uint8_t* pad, int B, int T, const
   ea.bits = ws_ptr<uint32_t>(workspace, L.bits);
   const dim3 egrid((B * G.ncc + 3) / 4);
   if (precision == DAD_PREC_BF16)
-    hipLaunchKernelGGL(dad_encode_bf16, dim3((B * G.ncc + 7) / 8), dim3(512), 0, stream, ea);
-  else hipLaunchKernelGGL(dad_encode_f32, egrid, dim3(256), 0, stream, ea);
+    hipLaunchKernelGGL(dad_encode_bf16, dim3((B * G.ncc + 7) / 8), dim3(DAD_ENC_BF16_THREADS), 0, stream, ea);
+  else hipLaunchKernelGGL(dad_encode_f32, egrid, dim3(DAD_ENC_F32_THREADS), 0, stream, ea);
   DAD_TRY(hipGetLastError());
   if (e_out) {
     hipLaunchKernelGGL(dad_embed_kernel, dim3(B), dim3(256), 0, stream, ea.part_sum, pad, B, T, G.ncc, vlen_out,
@@ -397,7 +397,7 @@ int dad_encoder_backward(const float* x, const uint8_t* pad, int B, int T, const
   wa.g = G; wa.warmup = 1; wa.splits = splits;
   wa.xc = x; wa.bits = ws_ptr<uint32_t>(workspace, L.bits); wa.ge = de; wa.vlen = vlen;
   wa.wpart = ws_ptr<float>(workspace, L.wpart);
-  hipLaunchKernelGGL(dad_wgrad_f32, dim3(6 * splits), dim3(256), 0, stream, wa);
+  hipLaunchKernelGGL(dad_wgrad_f32, dim3(6 * splits), dim3(DAD_WGRAD_THREADS), 0, stream, wa);
   DAD_TRY(hipGetLastError());
   float* gflat = ws_ptr<float>(workspace, L.gflat);
   DadReduceArgs ra;
@@ -405,7 +405,7 @@ int dad_encoder_backward(const float* x, const uint8_t* pad, int B, int T, const
   ra.g = G; ra.splits = splits; ra.warmup = 1; ra.want_norm = 0;
   ra.wpart = wa.wpart; ra.ge = de; ra.vlen = vlen; ra.cnt_tot = cnt_tot;
   ra.tailf = nullptr; ra.grad = gflat; ra.normpart = ws_ptr<float>(workspace, L.normpart);
-  hipLaunchKernelGGL(dad_reduce, dim3(193), dim3(256), 0, stream, ra);
+  hipLaunchKernelGGL(dad_reduce, dim3(DAD_REDUCE_BLOCKS), dim3(DAD_REDUCE_THREADS), 0, stream, ra);
   DAD_TRY(hipGetLastError());
   DAD_TRY(hipMemcpyAsync(dw1, gflat + DAD_OFF_W1, sizeof(float) * DAD_H * DAD_D, hipMemcpyDeviceToDevice, stream));
   DAD_TRY(hipMemcpyAsync(db1, gflat + DAD_OFF_B1, sizeof(float) * DAD_H, hipMemcpyDeviceToDevice, stream));

@@ -2,6 +2,20 @@
 #pragma once
 #include "dad_common.h"
 
+// Block sizes: kernels index with these, launches use them; every kernel whose indexing
+// depends on its block size exits uniformly if launched with another one.
+#define DAD_ENC_BF16_THREADS 512
+#define DAD_ENC_F32_THREADS 256
+#define DAD_POOL_THREADS 256
+#define DAD_TAIL_THREADS 1024
+#define DAD_ECDA_THREADS 512
+#define DAD_WGRAD_THREADS 256
+#define DAD_REDUCE_THREADS 256
+#define DAD_REDUCE_BLOCKS 193
+#define DAD_OPTIM_THREADS 256
+#define DAD_GUARD_BLOCK(n) \
+  if (blockDim.x != (n) || blockDim.y != 1 || blockDim.z != 1) return
+
 struct DadEncodeArgs {
   DadGeom g;
   int warmup, mask_len, start_hi;

@@ -147,7 +147,8 @@ __device__ __forceinline__ void encode_finish(const DadEncodeArgs& a, const Enco
 }  // namespace
 
 // ------------------------------------------------------------------- FP32 (parity mode)
-__global__ __launch_bounds__(256) void dad_encode_f32(DadEncodeArgs a) {
+__global__ __launch_bounds__(DAD_ENC_F32_THREADS) void dad_encode_f32(DadEncodeArgs a) {
+  DAD_GUARD_BLOCK(DAD_ENC_F32_THREADS);
   __shared__ __attribute__((aligned(16))) uint32_t lds_bits_all[4][DAD_SLAB * DAD_HT];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
@@ -455,7 +456,8 @@ __device__ __forceinline__ void encode_bf16_body(const DadEncodeArgs& a, char (*
   encode_epilogue(a, acc, bias, e.sum_slab, e.cnt_slab, e.bits_row, vbits, lds_bits_all[wv]);
 }
 
-__global__ __launch_bounds__(512, 1) void dad_encode_bf16(DadEncodeArgs a) {
+__global__ __launch_bounds__(DAD_ENC_BF16_THREADS, 1) void dad_encode_bf16(DadEncodeArgs a) {
+  DAD_GUARD_BLOCK(DAD_ENC_BF16_THREADS);
   __shared__ __attribute__((aligned(16))) char wbuf[2][2 * ENC_WCHUNK_BYTES];
   __shared__ __attribute__((aligned(16))) uint32_t lds_bits_all[ENC_WAVES][DAD_SLAB * DAD_HT];
   __shared__ __attribute__((aligned(16))) float featkeep[DAD_D];

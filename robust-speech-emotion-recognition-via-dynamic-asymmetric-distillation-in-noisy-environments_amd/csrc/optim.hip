@@ -34,7 +34,8 @@ __global__ void dad_commit_kernel(dad_config cfg, const float* grad, float* dacp
   dacp_commit(cfg, grad, dacp, tid);
 }
 
-__global__ __launch_bounds__(256) void dad_optim(DadOptimArgs a) {
+__global__ __launch_bounds__(DAD_OPTIM_THREADS) void dad_optim(DadOptimArgs a) {
+  DAD_GUARD_BLOCK(DAD_OPTIM_THREADS);
   __shared__ float coef_s;
   const dad_config& cfg = a.cfg;
   const int tid = threadIdx.x;

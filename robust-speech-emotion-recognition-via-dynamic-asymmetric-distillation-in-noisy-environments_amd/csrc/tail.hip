@@ -13,10 +13,12 @@
 // (softmax -> certainty -> quantile -> EMA threshold -> mask); double accumulators for
 // the batch sums.  The per-class set sizes are data dependent; everything is decided on
 // device (no host sync), so the step is graph-capturable.
+#include <type_traits>
+
 #include "dad_common.h"
 #include "dad_kernels.h"
 
-#define TAIL_THREADS 1024
+#define TAIL_THREADS DAD_TAIL_THREADS
 
 __device__ __forceinline__ float block_sum_f(float v, float* red) {
   v = dad_wave_sum(v);
@@ -52,7 +54,8 @@ __device__ __forceinline__ float keep_value(const uint8_t* keep, uint32_t key, i
 
 // ------------------------------------------------------------------------------ pool
 // blocks [0, Bc): clean utterances; blocks [Bc, Bc+Bn): noisy utterances (teacher + strong)
-__global__ __launch_bounds__(256) void dad_pool(DadPoolArgs a) {
+__global__ __launch_bounds__(DAD_POOL_THREADS) void dad_pool(DadPoolArgs a) {
+  DAD_GUARD_BLOCK(DAD_POOL_THREADS);
   __shared__ float red[8];
   __shared__ float zred[8][4];
   const DadGeom& g = a.g;
@@ -117,6 +120,7 @@ __global__ __launch_bounds__(256) void dad_pool(DadPoolArgs a) {
 
 // ------------------------------------------------------------------------------ tail
 __global__ __launch_bounds__(TAIL_THREADS) void dad_tail(DadTailArgs a) {
+  DAD_GUARD_BLOCK(TAIL_THREADS);
   const dad_config& cfg = a.cfg;
   const int B = cfg.B;                       // clean utterances
   const int Bn = cfg.warmup ? 0 : cfg.Bn;    // noisy utterances
@@ -349,7 +353,10 @@ __global__ __launch_bounds__(TAIL_THREADS) void dad_tail(DadTailArgs a) {
 // (I/utils.py:633-650) runs in workgroup 0.  Each workgroup only writes the embedding
 // grads of ITS class members (clean: label == c, noisy: masked & pseudo-label == c), so
 // no atomics are needed and the result is deterministic.
-#define ECDA_THREADS 256
+#define ECDA_THREADS DAD_ECDA_THREADS
+static_assert(ECDA_THREADS % DAD_H == 0 && ECDA_THREADS >= DAD_H, "ECDA column groups");
+#define ECDA_GROUPS (ECDA_THREADS / DAD_H)   // column groups of 256 threads
+#define ECDA_BATCH 4                         // member rows per read-modify-write batch
 #define ECDA_NZ 80           // members staged in LDS (n <= 80); larger sets read global
 
 struct EcdaSmem {
@@ -358,8 +365,8 @@ struct EcdaSmem {
   int idx[2 * DAD_MAX_BATCH];     // member list: [0,ns) clean rows, [ns,n) noisy rows
   float wt[2 * DAD_MAX_BATCH];    // member weights
   float cent[DAD_C][DAD_H];
-  double dred[8];
-  float fred[8];
+  double dred[ECDA_THREADS / 64];
+  float fred[ECDA_THREADS / 64];
   int cnt_clean[DAD_C], cnt_noisy[DAD_C];
   int lab[DAD_MAX_BATCH];         // clean labels
   int prd[DAD_MAX_BATCH];         // noisy pseudo-labels, -1 where not masked in
@@ -414,20 +421,24 @@ __device__ int ecda_compact(EcdaSmem& S, int n, int base, Flag flag, Wgt weight)
   return base;
 }
 
-// Member embeddings: staged in LDS when n <= ECDA_NZ, read from global otherwise.
+// Member embeddings: staged in LDS when n <= ECDA_NZ, read from global otherwise.  The two
+// cases are separate instantiations so that every access has a known address space (a
+// run-time LDS-or-global select compiles to flat loads with full waits).
+template <bool STAGED>
 struct EcdaRows {
   const float* emb_c;
   const float* emb_s;
-  const EcdaSmem* S;
+  EcdaSmem& S;
   int ns;
-  bool staged;
   __device__ __forceinline__ const float* row(int a) const {
-    return staged ? &S->z[a * DAD_H] : ((a < ns ? emb_c : emb_s) + (size_t)S->idx[a] * DAD_H);
+    if constexpr (STAGED) return &S.z[a * DAD_H];
+    else return (a < ns ? emb_c : emb_s) + (size_t)S.idx[a] * DAD_H;
   }
 };
 
-__device__ __forceinline__ void ecda_stage(EcdaSmem& S, const EcdaRows& R, int n) {
-  if (R.staged) {
+template <bool STAGED>
+__device__ __forceinline__ void ecda_stage(EcdaSmem& S, const EcdaRows<STAGED>& R, int n) {
+  if constexpr (STAGED) {
 #pragma unroll 4
     for (int k = threadIdx.x; k < n * (DAD_H / 4); k += ECDA_THREADS) {
       const int a = k / (DAD_H / 4), q = k - a * (DAD_H / 4);
@@ -442,7 +453,8 @@ __device__ __forceinline__ void ecda_stage(EcdaSmem& S, const EcdaRows& R, int n
 // [0, ns) (clean embeddings) and [ns, n) (strong embeddings).  Leaves the symmetric
 // coefficient matrix Csym = dmmd/dD + (dmmd/dD)^T in D, so that
 // dmmd/dz_i = 2 sum_j Csym_ij (z_i - z_j).  Returns mmd (valid in all threads).
-__device__ float ecda_mmd_coef(EcdaSmem& S, const EcdaRows& R, int n, float* D) {
+template <bool STAGED>
+__device__ __forceinline__ float ecda_mmd_coef(EcdaSmem& S, const EcdaRows<STAGED>& R, int n, float* D) {
   const int tid = threadIdx.x;
   const int ns = R.ns;
   // pairwise squared distances (I/utils.py:533-537).  Lane reads float4 (q + i + j) mod 64
@@ -456,15 +468,14 @@ __device__ float ecda_mmd_coef(EcdaSmem& S, const EcdaRows& R, int n, float* D) 
       const f32x4* zi = reinterpret_cast<const f32x4*>(R.row(i));
       const f32x4* zj = reinterpret_cast<const f32x4*>(R.row(j));
       const int rot = (i + j) & 63;
-#pragma unroll 8
+      f32x4 acc = f32x4{};            // four independent chains instead of one 256-long one
+#pragma unroll 4
       for (int q = 0; q < DAD_H / 4; ++q) {
         const int qq = (q + rot) & 63;
         const f32x4 df = zj[qq] - zi[qq];
-        d += df[0] * df[0];
-        d += df[1] * df[1];
-        d += df[2] * df[2];
-        d += df[3] * df[3];
+        acc += df * df;
       }
+      d = (acc[0] + acc[1]) + (acc[2] + acc[3]);
     }
     D[p] = d;
     part += d;
@@ -516,40 +527,44 @@ __device__ float ecda_mmd_coef(EcdaSmem& S, const EcdaRows& R, int n, float* D) 
   return mmd;
 }
 
-// Embedding grads of the members, one column (hh = tid) per thread, eight member rows per
-// batch: the eight read-modify-write loads of ge are issued together (the rows are
+// Embedding grads of the members, one column (hh = tid % 256) per thread, members split
+// over the ECDA_GROUPS column groups, ECDA_BATCH member rows per batch: the batch's
+// read-modify-write loads of ge are issued together (the rows are
 // distinct, but the compiler cannot prove it, so a plain loop would serialise them):
 //   g = mmd_scale * 2 sum_j Csym_ij (z_i - z_j)            (all members, if D)
 //     + comp_scale * (z_i - mu_c) + rep_g                    (noisy members)
 // comp_part accumulates sum ||z_i - mu_c||^2 over noisy members (when cent).
-__device__ void ecda_member_grads(const EcdaSmem& S, const EcdaRows& R, int n, const float* D, float mmd_scale,
-                                  const float* cent, float comp_scale, float rep_g, float* ge_c, float* ge_s,
-                                  float& comp_part) {
-  const int hh = threadIdx.x;
+template <bool STAGED>
+__device__ __forceinline__ void ecda_member_grads(EcdaSmem& S, const EcdaRows<STAGED>& R, int n, const float* D,
+                                                  float mmd_scale, const float* cent, float comp_scale, float rep_g,
+                                                  float* ge_c, float* ge_s, float& comp_part) {
+  const int hh = threadIdx.x & (DAD_H - 1);
+  const int grp = threadIdx.x / DAD_H;
   const int ns = R.ns;
-  for (int m0 = 0; m0 < n; m0 += 8) {
-    float old[8];
-    float* dst[8];
+  // group grp owns members grp, grp + G, grp + 2G, ...; ECDA_BATCH of them per batch
+  for (int m0 = grp; m0 < n; m0 += ECDA_BATCH * ECDA_GROUPS) {
+    float old[ECDA_BATCH];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int m = m0 + u;
-      dst[u] = nullptr;
-      if (m < n) {
-        dst[u] = (m < ns ? ge_c : ge_s) + (size_t)S.idx[m] * DAD_H + hh;
-        old[u] = *dst[u];
-      }
+    for (int u = 0; u < ECDA_BATCH; ++u) {
+      const int m = m0 + u * ECDA_GROUPS;
+      if (m < n) old[u] = (m < ns ? ge_c : ge_s)[(size_t)S.idx[m] * DAD_H + hh];
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int m = m0 + u;
+    for (int u = 0; u < ECDA_BATCH; ++u) {
+      const int m = m0 + u * ECDA_GROUPS;
       if (m >= n) break;
       float g = 0.0f;
       float zi = 0.0f;
       if (D || cent) zi = R.row(m)[hh];
       if (D) {
-        float acc = 0.0f;
-        for (int j = 0; j < n; ++j) acc += D[m * n + j] * (zi - R.row(j)[hh]);
-        g = mmd_scale * (2.0f * acc);
+        float acc0 = 0.0f, acc1 = 0.0f;
+        int j = 0;
+        for (; j + 1 < n; j += 2) {
+          acc0 += D[m * n + j] * (zi - R.row(j)[hh]);
+          acc1 += D[m * n + j + 1] * (zi - R.row(j + 1)[hh]);
+        }
+        if (j < n) acc0 += D[m * n + j] * (zi - R.row(j)[hh]);
+        g = mmd_scale * (2.0f * (acc0 + acc1));
       }
       if (m >= ns) {
         if (cent) {
@@ -559,12 +574,13 @@ __device__ void ecda_member_grads(const EcdaSmem& S, const EcdaRows& R, int n, c
         }
         g += rep_g;
       }
-      *dst[u] = old[u] + g;
+      (m < ns ? ge_c : ge_s)[(size_t)S.idx[m] * DAD_H + hh] = old[u] + g;
     }
   }
 }
 
 __global__ __launch_bounds__(ECDA_THREADS) void dad_ecda(DadEcdaArgs a) {
+  DAD_GUARD_BLOCK(ECDA_THREADS);
   __shared__ EcdaSmem S;
   __shared__ float pdist[DAD_C][DAD_C];
   const dad_config& cfg = a.cfg;
@@ -589,6 +605,9 @@ __global__ __launch_bounds__(ECDA_THREADS) void dad_ecda(DadEcdaArgs a) {
   }
   if (tid < DAD_C) { S.cnt_clean[tid] = 0; S.cnt_noisy[tid] = 0; }
   __syncthreads();
+#ifdef DAD_PROBE_ECDA_EXIT0
+  return;
+#endif
 
   if (!cfg.class_aware) {
     // global MMD ablation: all clean vs all masked noisy, unit weights (I/utils.py:633-650)
@@ -598,13 +617,18 @@ __global__ __launch_bounds__(ECDA_THREADS) void dad_ecda(DadEcdaArgs a) {
     n = ecda_compact(S, Bn, n, [&](int i) { return S.prd[i] >= 0; }, [](int) { return 1.0f; });
     const int nt = n - ns;
     if (ns >= 2 && nt >= 2) {
-      const EcdaRows R{emb_c, emb_s, &S, ns, n <= ECDA_NZ};
-      float* D = R.staged ? S.dm : scratch;
-      ecda_stage(S, R, n);
-      const float mmd = ecda_mmd_coef(S, R, n, D);
-      float unused = 0.0f;
-      ecda_member_grads(S, R, n, D, wscale, nullptr, 0.0f, 0.0f, ge_c, ge_s, unused);
-      if (tid == 0) { a.tail_terms[0] = mmd; a.tail_terms[DAD_T_ECDA_GATE - DAD_T_ECDA_TERM] = 1.0f; }
+      auto run = [&](auto staged_tag) {
+        constexpr bool ST = decltype(staged_tag)::value;
+        const EcdaRows<ST> R{emb_c, emb_s, S, ns};
+        float* D = ST ? S.dm : scratch;
+        ecda_stage(S, R, n);
+        const float mmd = ecda_mmd_coef(S, R, n, D);
+        float unused = 0.0f;
+        ecda_member_grads(S, R, n, D, wscale, nullptr, 0.0f, 0.0f, ge_c, ge_s, unused);
+        if (tid == 0) { a.tail_terms[0] = mmd; a.tail_terms[DAD_T_ECDA_GATE - DAD_T_ECDA_TERM] = 1.0f; }
+      };
+      if (n <= ECDA_NZ) run(std::true_type{});
+      else run(std::false_type{});
     }
     return;
   }
@@ -620,13 +644,15 @@ __global__ __launch_bounds__(ECDA_THREADS) void dad_ecda(DadEcdaArgs a) {
   // noisy centroids of every class (needed for the repulsion term): four utterance groups
   // x 64 float4 columns, all loads of a group in flight, partials combined in fixed order
   {
-    float* part = S.z;   // [4 groups][C][H], before the members are staged
+    float* part = S.z;   // [NG groups][C][H], before the members are staged
+    constexpr int NG = ECDA_THREADS / 64;
+    static_assert(NG * DAD_C * DAD_H <= ECDA_NZ * DAD_H, "centroid partials must fit in S.z");
     const int g = tid >> 6, q = tid & 63;
     f32x4 cs[DAD_C];
 #pragma unroll
     for (int k = 0; k < DAD_C; ++k) cs[k] = f32x4{};
-#pragma unroll 16
-    for (int b = g; b < Bn; b += 4) {
+#pragma unroll 4
+    for (int b = g; b < Bn; b += NG) {
       const int pk = S.prd[b];
       const f32x4 e = reinterpret_cast<const f32x4*>(emb_s + (size_t)b * DAD_H)[q];
 #pragma unroll
@@ -635,11 +661,11 @@ __global__ __launch_bounds__(ECDA_THREADS) void dad_ecda(DadEcdaArgs a) {
 #pragma unroll
     for (int k = 0; k < DAD_C; ++k) reinterpret_cast<f32x4*>(part + (g * DAD_C + k) * DAD_H)[q] = cs[k];
     __syncthreads();
-    const int hh = tid;
+    for (int e = tid; e < DAD_C * DAD_H; e += ECDA_THREADS) {
+      const int k = e / DAD_H, hh = e & (DAD_H - 1);
+      float sk = 0.0f;
 #pragma unroll
-    for (int k = 0; k < DAD_C; ++k) {
-      const float sk = ((part[(0 * DAD_C + k) * DAD_H + hh] + part[(1 * DAD_C + k) * DAD_H + hh]) +
-                        part[(2 * DAD_C + k) * DAD_H + hh]) + part[(3 * DAD_C + k) * DAD_H + hh];
+      for (int gg = 0; gg < NG; ++gg) sk += part[(gg * DAD_C + k) * DAD_H + hh];
       S.cent[k][hh] = S.cnt_noisy[k] > 0 ? sk / (float)S.cnt_noisy[k] : 0.0f;
     }
   }
@@ -689,7 +715,7 @@ __global__ __launch_bounds__(ECDA_THREADS) void dad_ecda(DadEcdaArgs a) {
   const bool rep_on = nvalid > 1 && S.cnt_noisy[c] > 0 && rep_coef != 0.0f;
   float rep_g = 0.0f;
   if (rep_on) {
-    const int hh = tid;
+    const int hh = tid & (DAD_H - 1);
     float gsum = 0.0f;
     for (int q = 0; q < ncls; ++q) {
       if (q == c || S.cnt_noisy[q] == 0) continue;
@@ -705,18 +731,30 @@ __global__ __launch_bounds__(ECDA_THREADS) void dad_ecda(DadEcdaArgs a) {
   const int ns = n;
   n = ecda_compact(S, Bn, n, [&](int i) { return S.prd[i] == c; }, [&](int i) { return S.scr[i]; });
   const int nt = n - ns;
-  const EcdaRows R{emb_c, emb_s, &S, ns, n <= ECDA_NZ};
-  float* D = nullptr;
   float mmd = 0.0f;
-  if (gated[c]) {
-    D = R.staged ? S.dm : scratch;
-    ecda_stage(S, R, n);
-    mmd = ecda_mmd_coef(S, R, n, D);
-  }
-  // compactness (I/utils.py:614-616): mean_j ||z_j - mu||^2, grad (2/nt)(z_j - mu)
   float cpart = 0.0f;
-  ecda_member_grads(S, R, n, D, wscale * att_c, gated[c] ? S.cent[c] : nullptr,
-                    wscale * att_c * cfg.ecda_gamma * (2.0f / (float)nt), rep_g, ge_c, ge_s, cpart);
+  auto run = [&](auto staged_tag) {
+    constexpr bool ST = decltype(staged_tag)::value;
+    const EcdaRows<ST> R{emb_c, emb_s, S, ns};
+    float* D = nullptr;
+    if (gated[c]) {
+      D = ST ? S.dm : scratch;
+      ecda_stage(S, R, n);
+#ifdef DAD_PROBE_ECDA_NOMMD
+      D = nullptr;
+#else
+      mmd = ecda_mmd_coef(S, R, n, D);
+#endif
+    }
+    // compactness (I/utils.py:614-616): mean_j ||z_j - mu||^2, grad (2/nt)(z_j - mu)
+#ifdef DAD_PROBE_ECDA_NOGRAD
+    if (false)
+#endif
+    ecda_member_grads(S, R, n, D, wscale * att_c, gated[c] ? S.cent[c] : nullptr,
+                      wscale * att_c * cfg.ecda_gamma * (2.0f / (float)nt), rep_g, ge_c, ge_s, cpart);
+  };
+  if (n <= ECDA_NZ) run(std::true_type{});
+  else run(std::false_type{});
   if (!gated[c]) return;
   const float comp = ecda_block_sum_f(S, cpart) / (float)nt;
   if (tid == 0) {

@@ -65,7 +65,8 @@ __device__ __forceinline__ int wg_total(const DadWgradArgs& a) {
 // ------------------------------------------------------------------- FP32 (parity mode)
 // grid = 6 column blocks x splits; wave = 32 columns x 256 rows of dW1.
 // v_mfma_f32_32x32x2_f32: A[i=h][k] = G[row k][h], B[k][j=d] = x[row k][d] (k = 2 rows).
-__global__ __launch_bounds__(256) void dad_wgrad_f32(DadWgradArgs a) {
+__global__ __launch_bounds__(DAD_WGRAD_THREADS) void dad_wgrad_f32(DadWgradArgs a) {
+  DAD_GUARD_BLOCK(DAD_WGRAD_THREADS);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int dblk = blockIdx.x % 6, split = blockIdx.x / 6;
   const int d0 = (dblk * 4 + wv) * 32;
@@ -269,7 +270,8 @@ __device__ __forceinline__ void wg_phase(const DadWgradArgs& a, int lo, int hi, 
   }
 }
 
-__global__ __launch_bounds__(256, 1) void dad_wgrad_bf16(DadWgradArgs a) {
+__global__ __launch_bounds__(DAD_WGRAD_THREADS, 1) void dad_wgrad_bf16(DadWgradArgs a) {
+  DAD_GUARD_BLOCK(DAD_WGRAD_THREADS);
   __shared__ __attribute__((aligned(16))) __bf16 Xt[DAD_SLAB * WG_XP];
   __shared__ __attribute__((aligned(16))) __bf16 Gt[DAD_SLAB * WG_GP];
   __shared__ __attribute__((aligned(16))) float sc[DAD_H];
@@ -307,7 +309,9 @@ __global__ __launch_bounds__(256, 1) void dad_wgrad_bf16(DadWgradArgs a) {
 // blocks [0,192): dW1 = sum_s wpart[s] (fixed order) + squared-norm partial;
 // block 192: db1 = sum_b (dL/de_b / len_b) * active_count_b, the W2/b2 norm partial and
 // the loss totals (I/train.py:462-466).
-__global__ __launch_bounds__(256) void dad_reduce(DadReduceArgs a) {
+static_assert(DAD_REDUCE_BLOCKS == DAD_H * DAD_D / 1024 + 1, "dad_reduce: 1024 dW1 floats per block + the db1 block");
+__global__ __launch_bounds__(DAD_REDUCE_THREADS) void dad_reduce(DadReduceArgs a) {
+  DAD_GUARD_BLOCK(DAD_REDUCE_THREADS);
   __shared__ double red[4];
   const int tid = threadIdx.x;
   double sq = 0.0;

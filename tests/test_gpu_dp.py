@@ -34,7 +34,8 @@ def _rank_main(rank, world, port, q):
         from oracle import dad_oracle, synth
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import datetime
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=120))
         p = dadpkg.pkg()
         cfg = dad_oracle.make_cfg("iemocap")
         model = p.SSRLModel().cuda()
@@ -86,7 +87,7 @@ def test_dp_step_two_ranks_match_oracle():
     res = {}
     try:
         for _ in procs:
-            rank, msg = q.get(timeout=400)
+            rank, msg = q.get(timeout=300)
             res[rank] = msg
     finally:
         for p in procs:
