@@ -50,7 +50,7 @@ extern "C" {
  * [4,8) Q (class_quality_scores), [8,12) epoch score sums, [12,16) epoch counts,
  * [16,20) calibrated anchors */
 #define DAD_DACP_FLOATS 20
-#define DAD_NORM_BLOCKS 256
+#define DAD_NORM_BLOCKS 1024
 
 /* per-step outputs ("tail" buffer): header then per-sample arrays */
 #define DAD_TAIL_HDR 64

@@ -11,7 +11,8 @@
 #define DAD_ECDA_THREADS 512
 #define DAD_WGRAD_THREADS 256
 #define DAD_REDUCE_THREADS 256
-#define DAD_REDUCE_BLOCKS 193
+#define DAD_REDUCE_COLS 256                                  // dW1 floats per reduce block
+#define DAD_REDUCE_BLOCKS (DAD_H * DAD_D / DAD_REDUCE_COLS + 1)   // + the db1 block
 #define DAD_OPTIM_THREADS 256
 #define DAD_GUARD_BLOCK(n) \
   if (blockDim.x != (n) || blockDim.y != 1 || blockDim.z != 1) return

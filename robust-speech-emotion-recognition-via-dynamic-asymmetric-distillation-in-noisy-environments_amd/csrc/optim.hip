@@ -34,15 +34,57 @@ __global__ void dad_commit_kernel(dad_config cfg, const float* grad, float* dacp
   dacp_commit(cfg, grad, dacp, tid);
 }
 
+// Elementwise clip + Adam + EMA over this block's 1024 parameters.  __restrict__ (no-alias
+// scopes once inlined) lets all four elements' loads issue before the first store.
+__device__ __forceinline__ void adam_ema_update(const dad_config& cfg, float coef, size_t n0,
+                                                const float* __restrict__ grad, float* __restrict__ student,
+                                                float* __restrict__ teacher, float* __restrict__ exp_avg,
+                                                float* __restrict__ exp_avg_sq, __bf16* __restrict__ w1bf_s,
+                                                __bf16* __restrict__ w1bf_t) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const size_t i = n0 + (size_t)k * 256 + tid;
+    if (i >= DAD_NPARAM) break;
+    float g = grad[i] * coef;
+    float p = student[i];
+    g = g + cfg.weight_decay * p;                               // grad.add(param, alpha=wd)
+    float m = exp_avg[i];
+    m = m + cfg.one_m_beta1 * (g - m);                          // exp_avg.lerp_(grad, 1-beta1)
+    float v = exp_avg_sq[i];
+    v = v * cfg.beta2 + cfg.one_m_beta2 * g * g;                // mul_(beta2).addcmul_(g, g, 1-beta2)
+    const float denom = sqrtf(v) / cfg.bc2_sqrt + cfg.adam_eps;
+    p = p + (-cfg.lr_step_size) * (m / denom);                  // addcdiv_(m, denom, -step_size)
+    exp_avg[i] = m;
+    exp_avg_sq[i] = v;
+    student[i] = p;
+    float t = teacher[i];
+    if (!cfg.warmup) {
+      t = t * cfg.ema_m + p * cfg.ema_one_m;
+      teacher[i] = t;
+    }
+    if (i < (size_t)DAD_H * DAD_D) {
+      w1bf_s[i] = (__bf16)p;
+      w1bf_t[i] = (__bf16)t;
+    }
+  }
+}
+
 __global__ __launch_bounds__(DAD_OPTIM_THREADS) void dad_optim(DadOptimArgs a) {
   DAD_GUARD_BLOCK(DAD_OPTIM_THREADS);
   __shared__ float coef_s;
+  __shared__ double nred[DAD_OPTIM_THREADS / 64];
   const dad_config& cfg = a.cfg;
   const int tid = threadIdx.x;
+  // global norm from the squared-norm partials: all threads load, fixed-order combine
+  double s = 0.0;
+  for (int k = tid; k < a.nnorm; k += DAD_OPTIM_THREADS) s += (double)a.normpart[k];
+  s = dad_wave_sum_d(s);
+  if ((tid & 63) == 0) nred[tid >> 6] = s;
+  __syncthreads();
   if (tid < 64) {
-    double s = 0.0;
-    for (int k = tid; k < a.nnorm; k += 64) s += (double)a.normpart[k];
-    s = dad_wave_sum_d(s);
+    s = 0.0;
+    for (int k = 0; k < DAD_OPTIM_THREADS / 64; ++k) s += nred[k];
     if (tid == 0) {
       const float norm = (float)sqrt(s);
       float coef = 1.0f;
@@ -60,33 +102,8 @@ __global__ __launch_bounds__(DAD_OPTIM_THREADS) void dad_optim(DadOptimArgs a) {
   }
   if (blockIdx.x == 0) dacp_commit(cfg, a.grad, a.dacp, tid);
   __syncthreads();
-  const float coef = coef_s;
-  const size_t n0 = (size_t)blockIdx.x * 1024;
-  for (int k = 0; k < 4; ++k) {
-    const size_t i = n0 + (size_t)k * 256 + tid;
-    if (i >= DAD_NPARAM) break;
-    float g = a.grad[i] * coef;
-    float p = a.student[i];
-    g = g + cfg.weight_decay * p;                               // grad.add(param, alpha=wd)
-    float m = a.exp_avg[i];
-    m = m + cfg.one_m_beta1 * (g - m);                          // exp_avg.lerp_(grad, 1-beta1)
-    float v = a.exp_avg_sq[i];
-    v = v * cfg.beta2 + cfg.one_m_beta2 * g * g;                // mul_(beta2).addcmul_(g, g, 1-beta2)
-    const float denom = sqrtf(v) / cfg.bc2_sqrt + cfg.adam_eps;
-    p = p + (-cfg.lr_step_size) * (m / denom);                  // addcdiv_(m, denom, -step_size)
-    a.exp_avg[i] = m;
-    a.exp_avg_sq[i] = v;
-    a.student[i] = p;
-    float t = a.teacher[i];
-    if (!cfg.warmup) {
-      t = t * cfg.ema_m + p * cfg.ema_one_m;
-      a.teacher[i] = t;
-    }
-    if (i < (size_t)DAD_H * DAD_D) {
-      a.w1bf_student[i] = (__bf16)p;
-      a.w1bf_teacher[i] = (__bf16)t;
-    }
-  }
+  adam_ema_update(cfg, coef_s, (size_t)blockIdx.x * 1024, a.grad, a.student, a.teacher, a.exp_avg, a.exp_avg_sq,
+                  a.w1bf_student, a.w1bf_teacher);
 }
 
 // DACPManager.update_class_quality_scores_epoch (I/utils.py:430-447)

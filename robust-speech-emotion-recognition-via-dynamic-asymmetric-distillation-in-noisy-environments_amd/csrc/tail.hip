@@ -69,41 +69,51 @@ __global__ __launch_bounds__(DAD_POOL_THREADS) void dad_pool(DadPoolArgs a) {
   float len = 0.0f;
   for (int t = h; t < T; t += 256) len += pad[(size_t)b * T + t] == 0 ? 1.0f : 0.0f;
   len = block_sum_f(len, red);
-  if (h == 0) a.vlen[blk] = len;
   const float* W2s = a.student + DAD_OFF_W2;
   const float* b2s = a.student + DAD_OFF_B2;
   const float* W2t = a.teacher + DAD_OFF_W2;
   const float* b2t = a.teacher + DAD_OFF_B2;
   const size_t nsc = (size_t)g.Bc * g.ncc, nsn = (size_t)g.Bn * g.ncn;
   const int nbr = noisy ? 2 : 1;
+  const int nc = noisy ? g.ncn : g.ncc;
+  // every load first (slab partials of both branches, active counts, W2 columns, keep
+  // flag), then the stores: a store between loads would serialise them on possible aliasing
+  size_t slab0[2];
+  int erow[2];
+  if (!noisy) { slab0[0] = (size_t)b * g.ncc; erow[0] = b; slab0[1] = slab0[0]; erow[1] = b; }
+  else {
+    slab0[0] = nsc + (size_t)b * g.ncn;        erow[0] = g.Bc + b;          // teacher (weak)
+    slab0[1] = nsc + nsn + (size_t)b * g.ncn;  erow[1] = g.Bc + g.Bn + b;   // student (strong)
+  }
+  const size_t cslab0 = noisy ? nsc + (size_t)b * g.ncn : (size_t)b * g.ncc;
+  float ssum[2] = {0.0f, 0.0f};
+  float cnt = 0.0f;
+  for (int c = 0; c < nc; ++c) {
+    ssum[0] += a.part_sum[(slab0[0] + c) * DAD_H + h];
+    if (noisy) ssum[1] += a.part_sum[(slab0[1] + c) * DAD_H + h];
+    cnt += a.part_cnt[(cslab0 + c) * DAD_H + h];
+  }
+  float w2s[4], w2t[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    w2s[c] = W2s[c * DAD_H + h];
+    w2t[c] = noisy ? W2t[c * DAD_H + h] : 0.0f;
+  }
+  const float kv = !noisy ? keep_value(a.keep1, a.key_drop1, b, h, a.p_drop, a.drop_scale)
+                          : keep_value(a.keep2, a.key_drop2, b, h, a.p_drop, a.drop_scale);
   float zp[2][4];
   for (int k = 0; k < nbr; ++k) {
-    // part_sum slab base and embedding row of this (branch, utterance)
-    size_t slab0;
-    int nc, erow;
-    if (!noisy) { slab0 = (size_t)b * g.ncc; nc = g.ncc; erow = b; }
-    else if (k == 0) { slab0 = nsc + (size_t)b * g.ncn; nc = g.ncn; erow = g.Bc + b; }              // teacher
-    else { slab0 = nsc + nsn + (size_t)b * g.ncn; nc = g.ncn; erow = g.Bc + g.Bn + b; }           // strong
-    float s = 0.0f;
-    for (int c = 0; c < nc; ++c) s += a.part_sum[(slab0 + c) * DAD_H + h];
-    const float e = s / fmaxf(len, 1.0f);
-    a.emb[(size_t)erow * DAD_H + h] = e;
-    if (k == nbr - 1) {
-      // active-row count per (utterance, h) of the branch that gets a gradient (clean / strong)
-      const size_t cslab0 = noisy ? nsc + (size_t)b * g.ncn : (size_t)b * g.ncc;
-      float cnt = 0.0f;
-      for (int c = 0; c < nc; ++c) cnt += a.part_cnt[(cslab0 + c) * DAD_H + h];
-      a.cnt_tot[(size_t)(noisy ? g.Bc + b : b) * DAD_H + h] = cnt;
-    }
-    float d;
+    const float e = ssum[k] / fmaxf(len, 1.0f);
+    a.emb[(size_t)erow[k] * DAD_H + h] = e;
     const bool teacher = noisy && k == 0;
-    if (!noisy) d = e * keep_value(a.keep1, a.key_drop1, b, h, a.p_drop, a.drop_scale);
-    else if (!teacher) d = e * keep_value(a.keep2, a.key_drop2, b, h, a.p_drop, a.drop_scale);
-    else d = e;   // teacher classifier: dropout p = 0 (I/model.py:121)
-    const float* W2 = teacher ? W2t : W2s;
+    // teacher classifier: dropout p = 0 (I/model.py:121); students: dropout masks #1 / #2
+    const float d = teacher ? e : e * kv;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) zp[k][c] = dad_wave_sum(W2[c * DAD_H + h] * d);
+    for (int c = 0; c < 4; ++c) zp[k][c] = dad_wave_sum((teacher ? w2t[c] : w2s[c]) * d);
   }
+  // active-row count per (utterance, h) of the branch that gets a gradient (clean / strong)
+  a.cnt_tot[(size_t)(noisy ? g.Bc + b : b) * DAD_H + h] = cnt;
+  if (h == 0) a.vlen[blk] = len;
   if (l == 0)
     for (int k = 0; k < nbr; ++k)
       for (int c = 0; c < 4; ++c) zred[k * 4 + c][w] = zp[k][c];
@@ -119,6 +129,43 @@ __global__ __launch_bounds__(DAD_POOL_THREADS) void dad_pool(DadPoolArgs a) {
 }
 
 // ------------------------------------------------------------------------------ tail
+// classifier backward of one pass for utterances b = qg, qg+4, ...: dL/de (through the
+// dropout) and this thread's dW2 partial.  __restrict__ (turned into no-alias scopes when
+// inlined) lets the loads of a batch of utterances issue before the ge stores of the
+// previous one; eight utterances per batch keep their loads in flight together.
+__device__ __forceinline__ void cls_backward(const float* __restrict__ emb, const uint8_t* __restrict__ keep,
+                                             float* __restrict__ ge, const float (*gz)[DAD_C], int n, int qg,
+                                             int h, uint32_t key, float p, float scale, const float (&w2h)[4],
+                                             float (&gw)[4]) {
+  for (int b0 = qg; b0 < n; b0 += 4 * 8) {
+    float ev[8], kv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int b = b0 + 4 * u;
+      ev[u] = 0.0f;
+      kv[u] = 0.0f;
+      if (b < n) {
+        ev[u] = emb[(size_t)b * DAD_H + h];
+        kv[u] = keep_value(keep, key, b, h, p, scale);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int b = b0 + 4 * u;
+      if (b < n) {
+        const float d = ev[u] * kv[u];
+        float g = 0.0f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          gw[c] += gz[b][c] * d;
+          g += w2h[c] * gz[b][c];
+        }
+        ge[(size_t)b * DAD_H + h] = g * kv[u];
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(TAIL_THREADS) void dad_tail(DadTailArgs a) {
   DAD_GUARD_BLOCK(TAIL_THREADS);
   const dad_config& cfg = a.cfg;
@@ -309,31 +356,10 @@ __global__ __launch_bounds__(TAIL_THREADS) void dad_tail(DadTailArgs a) {
   const int h = tid & (DAD_H - 1), qg = tid >> 8;
   const float* W2 = a.student + DAD_OFF_W2;
   const float w2h[4] = {W2[h], W2[DAD_H + h], W2[2 * DAD_H + h], W2[3 * DAD_H + h]};
-  const float* e0 = a.emb;
-  const float* e2 = a.emb + (size_t)(B + Bn) * DAD_H;
   float gw[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  for (int b = qg; b < B; b += 4) {
-    const float k1 = keep_value(a.keep1, a.key_drop1, b, h, cfg.p_drop, cfg.drop_scale);
-    const float d0 = e0[(size_t)b * DAD_H + h] * k1;
-    float g0 = 0.0f;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      gw[c] += gz[0][b][c] * d0;
-      g0 += w2h[c] * gz[0][b][c];
-    }
-    a.ge[(size_t)b * DAD_H + h] = g0 * k1;
-  }
-  for (int b = qg; b < Bn; b += 4) {
-    const float k2 = keep_value(a.keep2, a.key_drop2, b, h, cfg.p_drop, cfg.drop_scale);
-    const float d2 = e2[(size_t)b * DAD_H + h] * k2;
-    float g2 = 0.0f;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      gw[c] += gz[1][b][c] * d2;
-      g2 += w2h[c] * gz[1][b][c];
-    }
-    a.ge[(size_t)(B + b) * DAD_H + h] = g2 * k2;
-  }
+  cls_backward(a.emb, a.keep1, a.ge, gz[0], B, qg, h, a.key_drop1, cfg.p_drop, cfg.drop_scale, w2h, gw);
+  cls_backward(a.emb + (size_t)(B + Bn) * DAD_H, a.keep2, a.ge + (size_t)B * DAD_H, gz[1], Bn, qg, h, a.key_drop2,
+               cfg.p_drop, cfg.drop_scale, w2h, gw);
 #pragma unroll
   for (int c = 0; c < 4; ++c) gwp[qg][c][h] = gw[c];
   __syncthreads();

@@ -306,38 +306,61 @@ __global__ __launch_bounds__(DAD_WGRAD_THREADS, 1) void dad_wgrad_bf16(DadWgradA
 }
 
 // ---------------------------------------------------------------- reduce + squared norms
-// blocks [0,192): dW1 = sum_s wpart[s] (fixed order) + squared-norm partial;
-// block 192: db1 = sum_b (dL/de_b / len_b) * active_count_b, the W2/b2 norm partial and
+// blocks [0, NB): DAD_REDUCE_COLS floats of dW1 each = sum_s wpart[s] + squared-norm partial.
+//   thread = (float4 column, split group kg): group kg sums splits kg, kg+4, ... with its
+//   loads in flight together, then the four groups are combined in fixed order (deterministic).
+// block NB: db1 = sum_b (dL/de_b / len_b) * active_count_b, the W2/b2 norm partial and
 // the loss totals (I/train.py:462-466).
-static_assert(DAD_REDUCE_BLOCKS == DAD_H * DAD_D / 1024 + 1, "dad_reduce: 1024 dW1 floats per block + the db1 block");
+static_assert(DAD_REDUCE_THREADS == 4 * (DAD_REDUCE_COLS / 4), "dad_reduce: 4 split groups x float4 columns");
+static_assert(DAD_REDUCE_BLOCKS <= DAD_NORM_BLOCKS, "norm partials must fit the workspace");
+static_assert((DAD_NPARAM + 1023) / 1024 <= DAD_NORM_BLOCKS, "dad_norm partials must fit the workspace");
 __global__ __launch_bounds__(DAD_REDUCE_THREADS) void dad_reduce(DadReduceArgs a) {
   DAD_GUARD_BLOCK(DAD_REDUCE_THREADS);
-  __shared__ double red[4];
+  __shared__ double red[DAD_REDUCE_THREADS / 64];
+  __shared__ f32x4 part[4][DAD_REDUCE_COLS / 4 > DAD_H / 4 ? DAD_REDUCE_COLS / 4 : DAD_H / 4];
   const int tid = threadIdx.x;
+  constexpr int NB = DAD_REDUCE_BLOCKS - 1;
   double sq = 0.0;
-  if (blockIdx.x < 192) {
-    const size_t e0 = (size_t)blockIdx.x * 1024 + (size_t)tid * 4;
+  if (blockIdx.x < NB) {
+    const int col = tid & (DAD_REDUCE_COLS / 4 - 1), kg = tid / (DAD_REDUCE_COLS / 4);
+    const size_t e0 = (size_t)blockIdx.x * DAD_REDUCE_COLS + (size_t)col * 4;
     f32x4 s = f32x4{};
-    for (int k = 0; k < a.splits; ++k) s += *reinterpret_cast<const f32x4*>(a.wpart + (size_t)k * DAD_H * DAD_D + e0);
-    *reinterpret_cast<f32x4*>(a.grad + DAD_OFF_W1 + e0) = s;
-    for (int e = 0; e < 4; ++e) sq += (double)s[e] * s[e];
+#pragma unroll 4
+    for (int k = kg; k < a.splits; k += 4) s += *reinterpret_cast<const f32x4*>(a.wpart + (size_t)k * DAD_H * DAD_D + e0);
+    part[kg][col] = s;
+    __syncthreads();
+    if (kg == 0) {
+      const f32x4 t = ((part[0][col] + part[1][col]) + part[2][col]) + part[3][col];
+      *reinterpret_cast<f32x4*>(a.grad + DAD_OFF_W1 + e0) = t;
+      for (int e = 0; e < 4; ++e) sq += (double)t[e] * t[e];
+    }
   } else {
-    // db1[h] = sum_r dL/de[r][h] / max(1, len_r) * active_count[r][h]  (independent loads, 4 chains)
-    const int h = tid;
+    // db1[h] = sum_r dL/de[r][h] / max(1, len_r) * active_count[r][h]: thread = (4 hidden
+    // units as a float4, row group rg); rows rg, rg+4, ... in batches of 8 with all their
+    // loads in flight, then the four row groups combined in fixed order.
     const DadGeom& g = a.g;
     const int nb = g.Bc + (a.warmup ? 0 : g.Bn);
-    float acc4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-    int r = 0;
-    for (; r + 4 <= nb; r += 4) {
+    const int hq = tid & (DAD_H / 4 - 1), rg = tid / (DAD_H / 4);
+    f32x4 acc = f32x4{};
+    for (int r0 = rg; r0 < nb; r0 += 4 * 8) {
+      f32x4 gv[8], cv[8];
+      float lv[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int rr = r + u;
-        acc4[u] += a.ge[(size_t)rr * DAD_H + h] / fmaxf(a.vlen[rr], 1.0f) * a.cnt_tot[(size_t)rr * DAD_H + h];
+      for (int u = 0; u < 8; ++u) {
+        const int r = min(r0 + 4 * u, nb - 1);
+        gv[u] = reinterpret_cast<const f32x4*>(a.ge + (size_t)r * DAD_H)[hq];
+        cv[u] = reinterpret_cast<const f32x4*>(a.cnt_tot + (size_t)r * DAD_H)[hq];
+        lv[u] = a.vlen[r];
       }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (r0 + 4 * u < nb) acc += gv[u] / fmaxf(lv[u], 1.0f) * cv[u];
     }
-    for (; r < nb; ++r) acc4[0] += a.ge[(size_t)r * DAD_H + h] / fmaxf(a.vlen[r], 1.0f) * a.cnt_tot[(size_t)r * DAD_H + h];
-    const double gb = ((double)acc4[0] + acc4[1]) + ((double)acc4[2] + acc4[3]);
-    const float db1 = (float)gb;
+    part[rg][hq] = acc;
+    __syncthreads();
+    const int h = tid;
+    const float db1 = ((part[0][h >> 2][h & 3] + part[1][h >> 2][h & 3]) + part[2][h >> 2][h & 3]) +
+                      part[3][h >> 2][h & 3];
     a.grad[DAD_OFF_B1 + h] = db1;
     sq = (double)db1 * db1;
     if (!a.tailf) return;   // modular encoder backward: W1/b1 only
@@ -365,7 +388,11 @@ __global__ __launch_bounds__(DAD_REDUCE_THREADS) void dad_reduce(DadReduceArgs a
   double v = dad_wave_sum_d(sq);
   if ((tid & 63) == 0) red[tid >> 6] = v;
   __syncthreads();
-  if (tid == 0) a.normpart[blockIdx.x] = (float)(((red[0] + red[1]) + red[2]) + red[3]);
+  if (tid == 0) {
+    double t = 0.0;
+    for (int k = 0; k < DAD_REDUCE_THREADS / 64; ++k) t += red[k];
+    a.normpart[blockIdx.x] = (float)t;
+  }
 }
 
 // Data-parallel path: after the SUM all-reduce, average (grads, thresholds, losses) and
