@@ -18,6 +18,19 @@
 #include "dad_common.h"
 #include "dad_kernels.h"
 
+#ifdef DAD_PROBE_STAMPS
+// diagnostic build only: per-workgroup [start, after-loop, end] wall clocks (100 MHz)
+__device__ unsigned long long g_enc_stamps[4096 * 3];
+extern "C" int dad_probe_read_stamps(void* host, int n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_enc_stamps), sizeof(unsigned long long) * 3 * n, 0,
+                                  hipMemcpyDeviceToHost);
+}
+#define ENC_STAMP(k) \
+  if (threadIdx.x == 0 && blockIdx.x < 4096) g_enc_stamps[blockIdx.x * 3 + (k)] = wall_clock64()
+#else
+#define ENC_STAMP(k)
+#endif
+
 namespace {
 
 struct EncodeGeom {
@@ -88,10 +101,14 @@ __device__ __forceinline__ void encode_epilogue(const DadEncodeArgs& a, const f3
   const int lane = threadIdx.x & 63;
   const int j = lane & 31, kh = lane >> 5;
   const bool want_bits = bits_row >= 0;
+  // all bias loads up front: a load between the part_sum stores would wait on each of them
+  float bhs[DAD_HT];
+#pragma unroll
+  for (int ht = 0; ht < DAD_HT; ++ht) bhs[ht] = bias[ht * 32 + j];
 #pragma unroll
   for (int ht = 0; ht < DAD_HT; ++ht) {
     const int h = ht * 32 + j;
-    const float bh = bias[h];
+    const float bh = bhs[ht];
     float s = 0.0f, n = 0.0f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -102,12 +119,12 @@ __device__ __forceinline__ void encode_epilogue(const DadEncodeArgs& a, const f3
       s += act ? pre : 0.0f;
       n += act ? 1.0f : 0.0f;
       if (want_bits) {
+        // the ballot is wave-uniform: every lane writes the same word to the same address
+        // (no lane-0 branch per row)
         const uint64_t m = __ballot(act);
-        if (lane == 0) {
-          const int row0 = dad_acc_row(r, 0);
-          lds_bits[row0 * DAD_HT + ht] = (uint32_t)m;
-          lds_bits[(row0 + 4) * DAD_HT + ht] = (uint32_t)(m >> 32);
-        }
+        const int row0 = dad_acc_row(r, 0);
+        lds_bits[row0 * DAD_HT + ht] = (uint32_t)m;
+        lds_bits[(row0 + 4) * DAD_HT + ht] = (uint32_t)(m >> 32);
       }
     }
     s += __shfl_xor(s, 32, 64);
@@ -442,22 +459,32 @@ __device__ __forceinline__ void encode_bf16_body(const DadEncodeArgs& a, char (*
   for (int ch = 0; ch < ENC_NCH; ch += 2) {
     compute(ch, xa);
     x_load(xa, xrow, min(ch + 2, last), kh);
+#ifndef DAD_PROBE_NOW
     w_store<TWO>(wb_, wbuf[1]);
     w_load<TWO>(wb_, W0, W1, min(ch + 3, last));
+#endif
     __syncthreads();
     compute(ch + 1, xb);
     x_load(xb, xrow, min(ch + 3, last), kh);
+#ifndef DAD_PROBE_NOW
     w_store<TWO>(wa, wbuf[0]);            // past the end: overwrites a buffer nobody reads again
     w_load<TWO>(wa, W0, W1, min(ch + 4, last));
+#endif
     __syncthreads();
   }
+  if (wv == 0) ENC_STAMP(1);
   if (!active) return;
   const float* bias = e.kind == 1 ? a.b1_teacher : a.b1_student;
+#ifdef DAD_PROBE_NOEPI
+  if (acc[0][0] == 12345.0f && acc[7][15] == 54321.0f)   // keeps the accumulators live
+#endif
   encode_epilogue(a, acc, bias, e.sum_slab, e.cnt_slab, e.bits_row, vbits, lds_bits_all[wv]);
+  if (wv == 0) ENC_STAMP(2);
 }
 
 __global__ __launch_bounds__(DAD_ENC_BF16_THREADS, 1) void dad_encode_bf16(DadEncodeArgs a) {
   DAD_GUARD_BLOCK(DAD_ENC_BF16_THREADS);
+  ENC_STAMP(0);
   __shared__ __attribute__((aligned(16))) char wbuf[2][2 * ENC_WCHUNK_BYTES];
   __shared__ __attribute__((aligned(16))) uint32_t lds_bits_all[ENC_WAVES][DAD_SLAB * DAD_HT];
   __shared__ __attribute__((aligned(16))) float featkeep[DAD_D];
