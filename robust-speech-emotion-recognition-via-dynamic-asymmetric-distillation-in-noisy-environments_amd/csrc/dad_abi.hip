@@ -2,6 +2,8 @@
 // kernel sequence of one DAD step.  Enqueue-only: no allocation, no synchronisation.
 #include <string.h>
 
+#include <mutex>
+
 #include "dad_common.h"
 #include "dad_kernels.h"
 
@@ -53,6 +55,33 @@ inline Keys keys_of(const dad_config* c) {
   k.drop1 = dad_stream_key(c->seed, c->counter, DAD_RNG_DROP1);
   k.drop2 = dad_stream_key(c->seed, c->counter, DAD_RNG_DROP2);
   return k;
+}
+
+// Second stream per device for work that only depends on the forward: the
+// loss-independent factor S_u of the weight gradient runs there while pool/tail/ECDA
+// (a handful of workgroups) run on the caller's stream.  Fork/join by events, so the
+// step stays enqueue-only and graph-capturable.
+struct SideStream {
+  hipStream_t s = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+constexpr int kMaxDevices = 64;
+SideStream g_side[kMaxDevices];
+std::mutex g_side_mu;
+
+int side_stream(SideStream** out) {
+  int dev = 0;
+  DAD_TRY(hipGetDevice(&dev));
+  if (dev < 0 || dev >= kMaxDevices) return DAD_E_ARG;
+  std::lock_guard<std::mutex> lk(g_side_mu);
+  SideStream& ss = g_side[dev];
+  if (!ss.s) {
+    DAD_TRY(hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking));
+    DAD_TRY(hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming));
+    DAD_TRY(hipEventCreateWithFlags(&ss.join, hipEventDisableTiming));
+  }
+  *out = &ss;
+  return DAD_OK;
 }
 
 }  // namespace
@@ -107,7 +136,6 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   float* vlen = ws_ptr<float>(workspace, L.vlen);
   float* cnt_tot = ws_ptr<float>(workspace, L.cnt_tot);
   float* ge = ws_ptr<float>(workspace, L.ge);
-  float* wpart = ws_ptr<float>(workspace, L.wpart);
   float* normpart = ws_ptr<float>(workspace, L.normpart);
   float* ecda_scratch = ws_ptr<float>(workspace, L.ecda);
   __bf16* xs_bf16 = ws_ptr<__bf16>(workspace, L.xs_bf16);
@@ -138,7 +166,32 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   }
   if (!do_backward) return DAD_OK;
 
-  // 2. pooled embeddings + classifier logits
+  // 2. loss-independent factor of dW1 on the side stream: S_u = bits_u^T X_u per utterance
+  //    (clean rows, then the strong-augmented noisy rows), concurrent with 3-5
+  SideStream* side = nullptr;
+  {
+    const int rc = side_stream(&side);
+    if (rc) return rc;
+  }
+  const int nutt = G.Bc + Bn;
+  float* sbuf = ws_ptr<float>(workspace, L.sbuf);
+  DadWgradArgs wa;
+  memset(&wa, 0, sizeof(wa));
+  wa.g = G; wa.warmup = cfg->warmup; wa.splits = nutt; wa.per_utt = 1;
+  wa.mask_len = cfg->mask_len; wa.start_hi = cfg->start_hi;
+  wa.xc = bt->xc; wa.xn = bt->xn;
+  if (explicit_rng) { wa.ns = bt->ns; wa.u = bt->u; wa.start = bt->start; }
+  wa.key_strong = k.strong; wa.key_feat = k.feat; wa.key_tstart = k.tstart;
+  wa.strong_std = cfg->strong_std; wa.feat_p = cfg->feat_p;
+  wa.bits = bits; wa.ge = ge; wa.vlen = vlen; wa.xs_bf16 = xs_bf16; wa.wpart = sbuf;
+  DAD_TRY(hipEventRecord(side->fork, stream));
+  DAD_TRY(hipStreamWaitEvent(side->s, side->fork, 0));
+  if (bf16) hipLaunchKernelGGL(dad_wgrad_bf16, dim3(6 * nutt), dim3(DAD_WGRAD_THREADS), 0, side->s, wa);
+  else hipLaunchKernelGGL(dad_wgrad_f32, dim3(6 * nutt), dim3(DAD_WGRAD_THREADS), 0, side->s, wa);
+  DAD_TRY(hipGetLastError());
+  DAD_TRY(hipEventRecord(side->join, side->s));
+
+  // 3. pooled embeddings + classifier logits
   DadPoolArgs pa;
   memset(&pa, 0, sizeof(pa));
   pa.g = G; pa.warmup = cfg->warmup;
@@ -152,7 +205,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   hipLaunchKernelGGL(dad_pool, dim3(G.Bc + Bn), dim3(DAD_POOL_THREADS), 0, stream, pa);
   DAD_TRY(hipGetLastError());
 
-  // 3. losses, DACP mask, analytic backward to dL/de and the classifier grads
+  // 4. losses, DACP mask, analytic backward to dL/de and the classifier grads
   DadTailArgs ta;
   memset(&ta, 0, sizeof(ta));
   ta.cfg = *cfg; ta.yc = bt->yc; ta.logits = st->logits; ta.emb = st->emb; ta.student = st->student;
@@ -162,7 +215,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   hipLaunchKernelGGL(dad_tail, dim3(1), dim3(DAD_TAIL_THREADS), 0, stream, ta);
   DAD_TRY(hipGetLastError());
 
-  // 4. ECDA (class-aware MMD + compactness + repulsion) and its embedding grads
+  // 5. ECDA (class-aware MMD + compactness + repulsion) and its embedding grads
   if (!cfg->warmup) {
     DadEcdaArgs ca;
     memset(&ca, 0, sizeof(ca));
@@ -172,29 +225,16 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
     DAD_TRY(hipGetLastError());
   }
 
-  // 5. encoder weight gradient (split-K partial slabs)
-  DadWgradArgs wa;
-  memset(&wa, 0, sizeof(wa));
-  wa.g = G; wa.warmup = cfg->warmup; wa.splits = splits;
-  wa.mask_len = cfg->mask_len; wa.start_hi = cfg->start_hi;
-  wa.xc = bt->xc; wa.xn = bt->xn;
-  if (explicit_rng) { wa.ns = bt->ns; wa.u = bt->u; wa.start = bt->start; }
-  wa.key_strong = k.strong; wa.key_feat = k.feat; wa.key_tstart = k.tstart;
-  wa.strong_std = cfg->strong_std; wa.feat_p = cfg->feat_p;
-  wa.bits = bits; wa.ge = ge; wa.vlen = vlen; wa.xs_bf16 = xs_bf16; wa.wpart = wpart;
-  if (bf16) hipLaunchKernelGGL(dad_wgrad_bf16, dim3(6 * splits), dim3(DAD_WGRAD_THREADS), 0, stream, wa);
-  else hipLaunchKernelGGL(dad_wgrad_f32, dim3(6 * splits), dim3(DAD_WGRAD_THREADS), 0, stream, wa);
-  DAD_TRY(hipGetLastError());
-
-  // 6. reduce partials -> dW1, db1; loss totals; squared-norm partials (single GPU)
+  // 6. join; dW1 = sum_u (dL/de_u / len_u) * S_u, db1, loss totals, squared-norm partials
+  DAD_TRY(hipStreamWaitEvent(stream, side->join, 0));
   DadReduceArgs ra;
   memset(&ra, 0, sizeof(ra));
-  ra.g = G; ra.splits = splits; ra.warmup = cfg->warmup;
+  ra.g = G; ra.splits = nutt; ra.warmup = cfg->warmup;
   ra.want_norm = cfg->dp_world == 1;
   ra.w_kl = cfg->w_kl; ra.w_ecda = cfg->w_ecda;
-  ra.wpart = wpart; ra.ge = ge; ra.vlen = vlen; ra.cnt_tot = cnt_tot; ra.tailf = st->tail;
+  ra.wpart = sbuf; ra.ge = ge; ra.vlen = vlen; ra.cnt_tot = cnt_tot; ra.tailf = st->tail;
   ra.grad = st->grad; ra.normpart = normpart;
-  hipLaunchKernelGGL(dad_reduce, dim3(DAD_REDUCE_BLOCKS), dim3(DAD_REDUCE_THREADS), 0, stream, ra);
+  hipLaunchKernelGGL(dad_wsum, dim3(DAD_REDUCE_BLOCKS), dim3(DAD_REDUCE_THREADS), 0, stream, ra);
   DAD_TRY(hipGetLastError());
   return DAD_OK;
 }
@@ -288,7 +328,7 @@ int dad_refresh_shadow(const dad_state* st, void* stream_) {
 size_t dad_encoder_workspace_bytes(int B, int T) {
   if (B < 1 || T < 1) return 0;
   const DadGeom g = dad_geom(B, T, 0, 0);
-  return dad_ws_layout(g, dad_auto_splits(g, DAD_PREC_FP32, 1), DAD_PREC_FP32).bytes;
+  return dad_ws_layout(g, dad_auto_splits(g, DAD_PREC_FP32, 1), DAD_PREC_FP32, false).bytes;
 }
 
 }  // extern "C"
@@ -371,7 +411,7 @@ int dad_encoder_forward(const float* x, const uint8_t* pad, int B, int T, const 
   if (B < 1 || B > DAD_MAX_BATCH || T < 1) return DAD_E_SHAPE;
   if (precision != DAD_PREC_FP32 && precision != DAD_PREC_BF16) return DAD_E_ARG;
   const DadGeom G = dad_geom(B, T, 0, 0);
-  const DadWs L = dad_ws_layout(G, dad_auto_splits(G, DAD_PREC_FP32, 1), DAD_PREC_FP32);
+  const DadWs L = dad_ws_layout(G, dad_auto_splits(G, DAD_PREC_FP32, 1), DAD_PREC_FP32, false);
   return encoder_forward_impl(x, pad, B, T, w1, b1, precision, workspace, (hipStream_t)stream, L,
                               ws_ptr<float>(workspace, L.vlen), e_out);
 }
@@ -383,7 +423,7 @@ int dad_encoder_backward(const float* x, const uint8_t* pad, int B, int T, const
   hipStream_t stream = (hipStream_t)stream_;
   const DadGeom G = dad_geom(B, T, 0, 0);
   const int splits = dad_auto_splits(G, DAD_PREC_FP32, 1);
-  const DadWs L = dad_ws_layout(G, splits, DAD_PREC_FP32);
+  const DadWs L = dad_ws_layout(G, splits, DAD_PREC_FP32, false);
   float* vlen = ws_ptr<float>(workspace, L.vlen);
   // recompute the ReLU'/valid bits and per-slab active counts (FP32 forward)
   int rc = encoder_forward_impl(x, pad, B, T, w1, b1, DAD_PREC_FP32, workspace, stream, L, nullptr, nullptr);

@@ -147,6 +147,7 @@ struct DadWs {
   size_t xs_bf16;    // bf16 [Bn][Tn][768]          BF16 mode: strong-augmented input (wgrad operand)
   size_t w1bf;       // bf16 [H][D]                 modular encoder ops: bf16 copy of W1
   size_t gflat;      // f32 [DAD_GRAD_FLOATS]       modular encoder backward: scratch grad vector
+  size_t sbuf;       // f32 [Bc + Bn][H][D]         S_u = bits_u^T X_u, the loss-independent factor of dW1
   size_t bytes;
   int splits;
 };
@@ -161,7 +162,8 @@ static inline int dad_auto_splits(const DadGeom& g, int precision, int warmup) {
   return total < target ? total : target;
 }
 
-static inline DadWs dad_ws_layout(const DadGeom& g, int splits, int precision) {
+// fused = the train step's layout (with the S_u buffer); the modular encoder ops pass false.
+static inline DadWs dad_ws_layout(const DadGeom& g, int splits, int precision, bool fused = true) {
   DadWs w;
   const size_t nsc = (size_t)g.Bc * g.ncc, nsn = (size_t)g.Bn * g.ncn;
   const size_t nb = (size_t)g.Bc + g.Bn;
@@ -179,6 +181,7 @@ static inline DadWs dad_ws_layout(const DadGeom& g, int splits, int precision) {
   w.xs_bf16 = off;  off = dad_align(off + (precision == DAD_PREC_BF16 ? 2 * (size_t)g.Bn * g.Tn * DAD_D : 0));
   w.w1bf = off;     off = dad_align(off + 2 * (size_t)DAD_H * DAD_D);
   w.gflat = off;    off = dad_align(off + sizeof(float) * DAD_GRAD_FLOATS);
+  w.sbuf = off;     off = dad_align(off + (fused ? sizeof(float) * nb * DAD_H * DAD_D : 0));
   w.bytes = off;
   return w;
 }

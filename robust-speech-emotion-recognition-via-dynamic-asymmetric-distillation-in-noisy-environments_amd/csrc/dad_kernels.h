@@ -79,6 +79,7 @@ struct DadWgradArgs {
   const uint32_t* bits; const float* ge; const float* vlen;
   const __bf16* xs_bf16;
   float* wpart;
+  int per_utt;   // 1: one split per utterance with G = ReLU' bits (S_u = bits_u^T X_u into wpart[u])
 };
 
 struct DadReduceArgs {
@@ -105,6 +106,7 @@ __global__ void dad_tail(DadTailArgs a);
 __global__ void dad_ecda(DadEcdaArgs a);
 __global__ void dad_wgrad_f32(DadWgradArgs a);
 __global__ void dad_wgrad_bf16(DadWgradArgs a);
+__global__ void dad_wsum(DadReduceArgs a);
 __global__ void dad_reduce(DadReduceArgs a);
 __global__ void dad_norm(float* grad, float* normpart, float inv_world);
 __global__ void dad_optim(DadOptimArgs a);

@@ -9,6 +9,12 @@
 // per-(utterance, h) scale dL/de / len.  The strong branch's augmented input is
 //   FP32: regenerated exactly (same counter-RNG function, or re-read explicit noise);
 //   BF16: re-read from the bf16 copy the forward stored (the exact MFMA operand it used).
+//
+// Fused step (per_utt = 1): the loss-dependent scale factors out of the row sum,
+//   dW1[h][:] = sum_u (dL/de_u[h] / len_u) * S_u[h][:],   S_u = bits_u^T X_u,
+// so the GEMM (S_u per utterance, G = 0/1 exact in bf16) runs as soon as the forward has
+// produced the bits -- concurrently with pool/tail/ECDA on a second stream -- and only the
+// streaming weighted sum dad_wsum remains on the critical path.
 #include "dad_common.h"
 #include "dad_kernels.h"
 
@@ -60,6 +66,21 @@ __device__ __forceinline__ int wg_total(const DadWgradArgs& a) {
   return a.g.Bc * a.g.ncc + (a.warmup ? 0 : a.g.Bn * a.g.ncn);
 }
 
+// slab range [s0, s1) of a split: contiguous share of all slabs, or (per_utt) the slabs
+// of utterance `split` (clean utterances first, then noisy)
+__device__ __forceinline__ void wg_range(const DadWgradArgs& a, int split, int& s0, int& s1) {
+  if (a.per_utt) {
+    const DadGeom& g = a.g;
+    if (split < g.Bc) { s0 = split * g.ncc; s1 = s0 + g.ncc; }
+    else { s0 = g.Bc * g.ncc + (split - g.Bc) * g.ncn; s1 = s0 + g.ncn; }
+  } else {
+    const int total = wg_total(a);
+    const int per = (total + a.splits - 1) / a.splits;
+    s0 = split * per;
+    s1 = min(total, s0 + per);
+  }
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------- FP32 (parity mode)
@@ -71,10 +92,8 @@ __global__ __launch_bounds__(DAD_WGRAD_THREADS) void dad_wgrad_f32(DadWgradArgs 
   const int dblk = blockIdx.x % 6, split = blockIdx.x / 6;
   const int d0 = (dblk * 4 + wv) * 32;
   const int i = lane & 31, kh = lane >> 5;
-  const int total = wg_total(a);
-  const int per = (total + a.splits - 1) / a.splits;
-  const int s0 = split * per;
-  const int s1 = min(total, s0 + per);
+  int s0, s1;
+  wg_range(a, split, s0, s1);
   f32x16 acc[DAD_HT];
 #pragma unroll
   for (int ht = 0; ht < DAD_HT; ++ht) acc[ht] = f32x16{};
@@ -82,10 +101,15 @@ __global__ __launch_bounds__(DAD_WGRAD_THREADS) void dad_wgrad_f32(DadWgradArgs 
   for (int s = s0; s < s1; ++s) {
     const SlabIdx q = wg_slab(a, s);
     const float* X = q.br ? a.xn : a.xc;
-    const float len = fmaxf(a.vlen[q.erow], 1.0f);
     float scale[DAD_HT];
+    if (a.per_utt) {
 #pragma unroll
-    for (int ht = 0; ht < DAD_HT; ++ht) scale[ht] = a.ge[(size_t)q.erow * DAD_H + ht * 32 + i] / len;
+      for (int ht = 0; ht < DAD_HT; ++ht) scale[ht] = 1.0f;
+    } else {
+      const float len = fmaxf(a.vlen[q.erow], 1.0f);
+#pragma unroll
+      for (int ht = 0; ht < DAD_HT; ++ht) scale[ht] = a.ge[(size_t)q.erow * DAD_H + ht * 32 + i] / len;
+    }
     int st = 0;
     float fkeep = 1.0f;
     if (q.br) {
@@ -184,8 +208,13 @@ __device__ __forceinline__ void wg_load(const DadWgradArgs& a, int s, int dbase,
   }
 #pragma unroll
   for (int m = 0; m < 4; ++m) r.word[m] = a.bits[(bits_row + (tid >> 5) + 8 * m) * DAD_HT + ((tid & 31) >> 2)];
-  r.ge = a.ge[(size_t)erow * DAD_H + tid];
-  r.len = a.vlen[erow];
+  if (a.per_utt) {
+    r.ge = 1.0f;
+    r.len = 1.0f;
+  } else {
+    r.ge = a.ge[(size_t)erow * DAD_H + tid];
+    r.len = a.vlen[erow];
+  }
 }
 
 template <int BR>
@@ -280,10 +309,8 @@ __global__ __launch_bounds__(DAD_WGRAD_THREADS, 1) void dad_wgrad_bf16(DadWgradA
   const int kh = lane >> 5;
   const int dblk = blockIdx.x % 6, split = blockIdx.x / 6;
   const int dbase = dblk * 128;
-  const int total = wg_total(a);
-  const int per = (total + a.splits - 1) / a.splits;
-  const int s0 = split * per;
-  const int s1 = min(total, s0 + per);
+  int s0, s1;
+  wg_range(a, split, s0, s1);
   const int nsc = a.g.Bc * a.g.ncc;
   f32x16 acc[2][4];
 #pragma unroll
@@ -311,6 +338,63 @@ __global__ __launch_bounds__(DAD_WGRAD_THREADS, 1) void dad_wgrad_bf16(DadWgradA
 //   loads in flight together, then the four groups are combined in fixed order (deterministic).
 // block NB: db1 = sum_b (dL/de_b / len_b) * active_count_b, the W2/b2 norm partial and
 // the loss totals (I/train.py:462-466).
+// db1[h] = sum_r dL/de[r][h] / max(1, len_r) * active_count[r][h], the W2/b2 squared-norm
+// partial and the loss totals (I/train.py:462-466).  Returns this thread's norm share.
+static_assert(DAD_REDUCE_THREADS == DAD_H, "db1 block: one thread per hidden unit");
+__device__ double db1_and_totals(const DadReduceArgs& a, f32x4 (*part)[DAD_H / 4]) {
+  const int tid = threadIdx.x;
+  double sq = 0.0;
+  // thread = (4 hidden
+  // units as a float4, row group rg); rows rg, rg+4, ... in batches of 8 with all their
+  // loads in flight, then the four row groups combined in fixed order.
+  const DadGeom& g = a.g;
+  const int nb = g.Bc + (a.warmup ? 0 : g.Bn);
+  const int hq = tid & (DAD_H / 4 - 1), rg = tid / (DAD_H / 4);
+  f32x4 acc = f32x4{};
+  for (int r0 = rg; r0 < nb; r0 += 4 * 8) {
+    f32x4 gv[8], cv[8];
+    float lv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int r = min(r0 + 4 * u, nb - 1);
+      gv[u] = reinterpret_cast<const f32x4*>(a.ge + (size_t)r * DAD_H)[hq];
+      cv[u] = reinterpret_cast<const f32x4*>(a.cnt_tot + (size_t)r * DAD_H)[hq];
+      lv[u] = a.vlen[r];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (r0 + 4 * u < nb) acc += gv[u] / fmaxf(lv[u], 1.0f) * cv[u];
+  }
+  part[rg][hq] = acc;
+  __syncthreads();
+  const int h = tid;
+  const float db1 = ((part[0][h >> 2][h & 3] + part[1][h >> 2][h & 3]) + part[2][h >> 2][h & 3]) +
+                    part[3][h >> 2][h & 3];
+  a.grad[DAD_OFF_B1 + h] = db1;
+  sq = (double)db1 * db1;
+  if (!a.tailf) return sq;   // modular encoder backward: W1/b1 only
+  for (int c = 0; c < 4; ++c) {
+    const float g = a.grad[DAD_OFF_W2 + c * DAD_H + h];
+    sq += (double)g * g;
+  }
+  if (h < 4) {
+    const float g = a.grad[DAD_OFF_B2 + h];
+    sq += (double)g * g;
+  }
+  if (h == 0) {
+    const float* tf = a.tailf;
+    const float ecda = ((tf[DAD_T_ECDA_TERM] + tf[DAD_T_ECDA_TERM + 1]) + tf[DAD_T_ECDA_TERM + 2]) +
+                       tf[DAD_T_ECDA_TERM + 3];
+    const float ce = tf[DAD_T_CE], kl = tf[DAD_T_KL];
+    float* ex = a.grad + DAD_NPARAM;
+    ex[12] = ce + a.w_kl * kl + a.w_ecda * ecda;
+    ex[13] = ce;
+    ex[14] = kl;
+    ex[15] = ecda;
+  }
+  return sq;
+}
+
 static_assert(DAD_REDUCE_THREADS == 4 * (DAD_REDUCE_COLS / 4), "dad_reduce: 4 split groups x float4 columns");
 static_assert(DAD_REDUCE_BLOCKS <= DAD_NORM_BLOCKS, "norm partials must fit the workspace");
 static_assert((DAD_NPARAM + 1023) / 1024 <= DAD_NORM_BLOCKS, "dad_norm partials must fit the workspace");
@@ -335,54 +419,63 @@ __global__ __launch_bounds__(DAD_REDUCE_THREADS) void dad_reduce(DadReduceArgs a
       for (int e = 0; e < 4; ++e) sq += (double)t[e] * t[e];
     }
   } else {
-    // db1[h] = sum_r dL/de[r][h] / max(1, len_r) * active_count[r][h]: thread = (4 hidden
-    // units as a float4, row group rg); rows rg, rg+4, ... in batches of 8 with all their
-    // loads in flight, then the four row groups combined in fixed order.
+    sq = db1_and_totals(a, part);
+  }
+  if (!a.want_norm) return;
+  double v = dad_wave_sum_d(sq);
+  if ((tid & 63) == 0) red[tid >> 6] = v;
+  __syncthreads();
+  if (tid == 0) {
+    double t = 0.0;
+    for (int k = 0; k < DAD_REDUCE_THREADS / 64; ++k) t += red[k];
+    a.normpart[blockIdx.x] = (float)t;
+  }
+}
+
+// Fused-step weight-gradient finish: dW1[h][d] = sum_u g_u[h] * S_u[h][d],
+// g_u[h] = dL/de_u[h] / max(1, len_u).  Blocks [0, NB): DAD_REDUCE_COLS columns of one
+// row h; thread = (float4 column, utterance group ug), utterances ug, ug+4, ... with eight
+// loads in flight, the four groups combined in fixed order (deterministic).  Block NB:
+// db1, W2/b2 norm share, loss totals.  Every block: its squared-norm partial.
+static_assert(DAD_D % DAD_REDUCE_COLS == 0, "dad_wsum: whole blocks per dW1 row");
+__global__ __launch_bounds__(DAD_REDUCE_THREADS) void dad_wsum(DadReduceArgs a) {
+  DAD_GUARD_BLOCK(DAD_REDUCE_THREADS);
+  __shared__ double red[DAD_REDUCE_THREADS / 64];
+  __shared__ f32x4 part[4][DAD_H / 4];
+  __shared__ float gsh[2 * DAD_MAX_BATCH];
+  const int tid = threadIdx.x;
+  constexpr int NB = DAD_REDUCE_BLOCKS - 1;
+  double sq = 0.0;
+  if (blockIdx.x < NB) {
     const DadGeom& g = a.g;
-    const int nb = g.Bc + (a.warmup ? 0 : g.Bn);
-    const int hq = tid & (DAD_H / 4 - 1), rg = tid / (DAD_H / 4);
-    f32x4 acc = f32x4{};
-    for (int r0 = rg; r0 < nb; r0 += 4 * 8) {
-      f32x4 gv[8], cv[8];
-      float lv[8];
+    const int nutt = g.Bc + (a.warmup ? 0 : g.Bn);
+    const int h = blockIdx.x / (DAD_D / DAD_REDUCE_COLS);
+    const int dcol0 = (blockIdx.x % (DAD_D / DAD_REDUCE_COLS)) * DAD_REDUCE_COLS;
+    for (int u = tid; u < nutt; u += DAD_REDUCE_THREADS) gsh[u] = a.ge[(size_t)u * DAD_H + h] / fmaxf(a.vlen[u], 1.0f);
+    __syncthreads();
+    const int col = tid & (DAD_REDUCE_COLS / 4 - 1), ug = tid / (DAD_REDUCE_COLS / 4);
+    const size_t off = (size_t)h * DAD_D + dcol0 + (size_t)col * 4;
+    f32x4 s = f32x4{};
+    for (int u0 = ug; u0 < nutt; u0 += 4 * 8) {
+      f32x4 v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int r = min(r0 + 4 * u, nb - 1);
-        gv[u] = reinterpret_cast<const f32x4*>(a.ge + (size_t)r * DAD_H)[hq];
-        cv[u] = reinterpret_cast<const f32x4*>(a.cnt_tot + (size_t)r * DAD_H)[hq];
-        lv[u] = a.vlen[r];
+      for (int k = 0; k < 8; ++k) {
+        const int u = min(u0 + 4 * k, nutt - 1);
+        v[k] = *reinterpret_cast<const f32x4*>(a.wpart + (size_t)u * DAD_H * DAD_D + off);
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (r0 + 4 * u < nb) acc += gv[u] / fmaxf(lv[u], 1.0f) * cv[u];
+      for (int k = 0; k < 8; ++k)
+        if (u0 + 4 * k < nutt) s += gsh[u0 + 4 * k] * v[k];
     }
-    part[rg][hq] = acc;
+    part[ug][col] = s;
     __syncthreads();
-    const int h = tid;
-    const float db1 = ((part[0][h >> 2][h & 3] + part[1][h >> 2][h & 3]) + part[2][h >> 2][h & 3]) +
-                      part[3][h >> 2][h & 3];
-    a.grad[DAD_OFF_B1 + h] = db1;
-    sq = (double)db1 * db1;
-    if (!a.tailf) return;   // modular encoder backward: W1/b1 only
-    for (int c = 0; c < 4; ++c) {
-      const float g = a.grad[DAD_OFF_W2 + c * DAD_H + h];
-      sq += (double)g * g;
+    if (ug == 0) {
+      const f32x4 t = ((part[0][col] + part[1][col]) + part[2][col]) + part[3][col];
+      *reinterpret_cast<f32x4*>(a.grad + DAD_OFF_W1 + off) = t;
+      for (int e = 0; e < 4; ++e) sq += (double)t[e] * t[e];
     }
-    if (h < 4) {
-      const float g = a.grad[DAD_OFF_B2 + h];
-      sq += (double)g * g;
-    }
-    if (h == 0) {
-      const float* tf = a.tailf;
-      const float ecda = ((tf[DAD_T_ECDA_TERM] + tf[DAD_T_ECDA_TERM + 1]) + tf[DAD_T_ECDA_TERM + 2]) +
-                         tf[DAD_T_ECDA_TERM + 3];
-      const float ce = tf[DAD_T_CE], kl = tf[DAD_T_KL];
-      float* ex = a.grad + DAD_NPARAM;
-      ex[12] = ce + a.w_kl * kl + a.w_ecda * ecda;
-      ex[13] = ce;
-      ex[14] = kl;
-      ex[15] = ecda;
-    }
+  } else {
+    sq = db1_and_totals(a, part);
   }
   if (!a.want_norm) return;
   double v = dad_wave_sum_d(sq);
