@@ -2,6 +2,7 @@
 // kernel sequence of one DAD step.  Enqueue-only: no allocation, no synchronisation.
 #include <string.h>
 
+#include <algorithm>
 #include <mutex>
 
 #include "dad_common.h"
@@ -64,7 +65,12 @@ inline Keys keys_of(const dad_config* c) {
 struct SideStream {
   hipStream_t s = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
+  int cus = 0;   // compute units of the device
 };
+// CUs the side-stream GEMM leaves free, so the caller-stream kernels that run meanwhile
+// (pool, the one-workgroup tail, ECDA's per-class workgroups) are dispatched at once
+// instead of waiting for a register file to drain
+constexpr int kReservedCUs = 32;   // 4 per XCD (workgroups are spread round-robin over the 8 XCDs)
 constexpr int kMaxDevices = 64;
 SideStream g_side[kMaxDevices];
 std::mutex g_side_mu;
@@ -79,6 +85,7 @@ int side_stream(SideStream** out) {
     DAD_TRY(hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking));
     DAD_TRY(hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming));
     DAD_TRY(hipEventCreateWithFlags(&ss.join, hipEventDisableTiming));
+    DAD_TRY(hipDeviceGetAttribute(&ss.cus, hipDeviceAttributeMultiprocessorCount, dev));
   }
   *out = &ss;
   return DAD_OK;
@@ -136,6 +143,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   float* vlen = ws_ptr<float>(workspace, L.vlen);
   float* cnt_tot = ws_ptr<float>(workspace, L.cnt_tot);
   float* ge = ws_ptr<float>(workspace, L.ge);
+  float* ge_ecda = ws_ptr<float>(workspace, L.ge_ecda);
   float* normpart = ws_ptr<float>(workspace, L.normpart);
   float* ecda_scratch = ws_ptr<float>(workspace, L.ecda);
   __bf16* xs_bf16 = ws_ptr<__bf16>(workspace, L.xs_bf16);
@@ -184,10 +192,13 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   wa.key_strong = k.strong; wa.key_feat = k.feat; wa.key_tstart = k.tstart;
   wa.strong_std = cfg->strong_std; wa.feat_p = cfg->feat_p;
   wa.bits = bits; wa.ge = ge; wa.vlen = vlen; wa.xs_bf16 = xs_bf16; wa.wpart = sbuf;
+  wa.ntiles = 6 * nutt;
+  if (bf16) wa.wpart_bf16 = reinterpret_cast<__bf16*>(sbuf);   // S_u in bf16 (G is 0/1: exact operands)
+  const int sgrid = std::max(1, std::min(wa.ntiles, side->cus - kReservedCUs));
   DAD_TRY(hipEventRecord(side->fork, stream));
   DAD_TRY(hipStreamWaitEvent(side->s, side->fork, 0));
-  if (bf16) hipLaunchKernelGGL(dad_wgrad_bf16, dim3(6 * nutt), dim3(DAD_WGRAD_THREADS), 0, side->s, wa);
-  else hipLaunchKernelGGL(dad_wgrad_f32, dim3(6 * nutt), dim3(DAD_WGRAD_THREADS), 0, side->s, wa);
+  if (bf16) hipLaunchKernelGGL(dad_wgrad_bf16, dim3(sgrid), dim3(DAD_WGRAD_THREADS), 0, side->s, wa);
+  else hipLaunchKernelGGL(dad_wgrad_f32, dim3(sgrid), dim3(DAD_WGRAD_THREADS), 0, side->s, wa);
   DAD_TRY(hipGetLastError());
   DAD_TRY(hipEventRecord(side->join, side->s));
 
@@ -211,7 +222,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   ta.cfg = *cfg; ta.yc = bt->yc; ta.logits = st->logits; ta.emb = st->emb; ta.student = st->student;
   if (explicit_rng) { ta.keep1 = bt->keep1; ta.keep2 = bt->keep2; }
   ta.key_drop1 = k.drop1; ta.key_drop2 = k.drop2;
-  ta.dacp = st->dacp; ta.tailf = st->tail; ta.ge = ge; ta.grad = st->grad;
+  ta.dacp = st->dacp; ta.tailf = st->tail; ta.ge = ge; ta.ge_ecda = ge_ecda; ta.grad = st->grad;
   hipLaunchKernelGGL(dad_tail, dim3(1), dim3(DAD_TAIL_THREADS), 0, stream, ta);
   DAD_TRY(hipGetLastError());
 
@@ -220,7 +231,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
     DadEcdaArgs ca;
     memset(&ca, 0, sizeof(ca));
     ca.cfg = *cfg; ca.yc = bt->yc; ca.emb = st->emb; ca.tailf = st->tail;
-    ca.tail_terms = st->tail + DAD_T_ECDA_TERM; ca.ge = ge; ca.scratch = ecda_scratch;
+    ca.tail_terms = st->tail + DAD_T_ECDA_TERM; ca.ge = ge_ecda; ca.scratch = ecda_scratch;
     hipLaunchKernelGGL(dad_ecda, dim3(DAD_C), dim3(DAD_ECDA_THREADS), 0, stream, ca);
     DAD_TRY(hipGetLastError());
   }
@@ -232,7 +243,8 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   ra.g = G; ra.splits = nutt; ra.warmup = cfg->warmup;
   ra.want_norm = cfg->dp_world == 1;
   ra.w_kl = cfg->w_kl; ra.w_ecda = cfg->w_ecda;
-  ra.wpart = sbuf; ra.ge = ge; ra.vlen = vlen; ra.cnt_tot = cnt_tot; ra.tailf = st->tail;
+  ra.wpart = sbuf; ra.wpart_bf16 = wa.wpart_bf16; ra.ge_ecda = ge_ecda;
+  ra.ge = ge; ra.vlen = vlen; ra.cnt_tot = cnt_tot; ra.tailf = st->tail;
   ra.grad = st->grad; ra.normpart = normpart;
   hipLaunchKernelGGL(dad_wsum, dim3(DAD_REDUCE_BLOCKS), dim3(DAD_REDUCE_THREADS), 0, stream, ra);
   DAD_TRY(hipGetLastError());
@@ -434,7 +446,7 @@ int dad_encoder_backward(const float* x, const uint8_t* pad, int B, int T, const
   DAD_TRY(hipGetLastError());
   DadWgradArgs wa;
   memset(&wa, 0, sizeof(wa));
-  wa.g = G; wa.warmup = 1; wa.splits = splits;
+  wa.g = G; wa.warmup = 1; wa.splits = splits; wa.ntiles = 6 * splits;
   wa.xc = x; wa.bits = ws_ptr<uint32_t>(workspace, L.bits); wa.ge = de; wa.vlen = vlen;
   wa.wpart = ws_ptr<float>(workspace, L.wpart);
   hipLaunchKernelGGL(dad_wgrad_f32, dim3(6 * splits), dim3(DAD_WGRAD_THREADS), 0, stream, wa);

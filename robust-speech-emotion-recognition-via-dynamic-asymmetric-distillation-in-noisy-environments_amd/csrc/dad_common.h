@@ -140,7 +140,8 @@ struct DadWs {
   size_t bits;       // u32 [Bc*tpc + Bn*tpn][8]    ReLU' & valid bits per row and 32-wide h tile
   size_t vlen;       // f32 [Bc + Bn]               valid lengths (clean | noisy)
   size_t cnt_tot;    // f32 [Bc + Bn][H]            active-row counts per utterance (clean | strong)
-  size_t ge;         // f32 [Bc + Bn][H]            dL/de_clean | dL/de_strong
+  size_t ge;         // f32 [Bc + Bn][H]            dL/de_clean | dL/de_strong (CE/KL part)
+  size_t ge_ecda;    // f32 [Bc + Bn][H]            ECDA part of dL/de (valid when the ECDA term is on)
   size_t wpart;      // f32 [S][H][D]               split-K weight-gradient partial slabs
   size_t normpart;   // f32 [DAD_NORM_BLOCKS]       squared-norm partials
   size_t ecda;       // f32 [C][Bc+Bn][Bc+Bn]       ECDA pairwise scratch for large member sets
@@ -175,6 +176,7 @@ static inline DadWs dad_ws_layout(const DadGeom& g, int splits, int precision, b
   w.vlen = off;     off = dad_align(off + sizeof(float) * nb);
   w.cnt_tot = off;  off = dad_align(off + sizeof(float) * nb * DAD_H);
   w.ge = off;       off = dad_align(off + sizeof(float) * nb * DAD_H);
+  w.ge_ecda = off;  off = dad_align(off + sizeof(float) * nb * DAD_H);
   w.wpart = off;    off = dad_align(off + sizeof(float) * (size_t)splits * DAD_H * DAD_D);
   w.normpart = off; off = dad_align(off + sizeof(float) * DAD_NORM_BLOCKS);
   w.ecda = off;     off = dad_align(off + sizeof(float) * DAD_C * nb * nb);

@@ -55,7 +55,8 @@ struct DadTailArgs {
   uint32_t key_drop1, key_drop2;
   float* dacp;            // persistent DACP state (read; committed by the optimizer kernel)
   float* tailf;           // per-step outputs (see DAD_TAIL_* in dad.h)
-  float* ge;              // [Bc+Bn][H] dL/de
+  float* ge;              // [Bc+Bn][H] dL/de (CE/KL part)
+  float* ge_ecda;         // [Bc+Bn][H] zeroed here; ECDA writes its member rows after
   float* grad;            // flat grads (W2, b2 written here) + extras
 };
 
@@ -65,7 +66,7 @@ struct DadEcdaArgs {
   const float* emb;
   const float* tailf;
   float* tail_terms;      // per-class loss terms
-  float* ge;
+  float* ge;              // ECDA part of dL/de: every row written (members: grads, others: 0)
   float* scratch;         // global fallback for large member sets
 };
 
@@ -79,7 +80,9 @@ struct DadWgradArgs {
   const uint32_t* bits; const float* ge; const float* vlen;
   const __bf16* xs_bf16;
   float* wpart;
-  int per_utt;   // 1: one split per utterance with G = ReLU' bits (S_u = bits_u^T X_u into wpart[u])
+  int per_utt;         // 1: one split per utterance with G = ReLU' bits (S_u = bits_u^T X_u into wpart[u])
+  int ntiles;          // 6 column blocks x splits; workgroups stride over them (grid may be smaller)
+  __bf16* wpart_bf16;  // non-null: partials stored in bf16 here instead of wpart
 };
 
 struct DadReduceArgs {
@@ -87,6 +90,8 @@ struct DadReduceArgs {
   int splits, warmup, want_norm;
   float w_kl, w_ecda;
   const float* wpart; const float* ge; const float* vlen; const float* cnt_tot;
+  const __bf16* wpart_bf16;   // dad_wsum: bf16 S_u instead of wpart
+  const float* ge_ecda;       // ECDA part of dL/de, added to ge (zeros where ECDA wrote nothing)
   const float* tailf;
   float* grad; float* normpart;
 };

@@ -18,6 +18,26 @@
 #include "dad_common.h"
 #include "dad_kernels.h"
 
+#ifdef DAD_PROBE_STAMPS
+// diagnostic build only: ECDA per-class phase wall clocks (100 MHz), 12 slots per class
+__device__ unsigned long long g_ecda_stamps[DAD_C * 12 + 4];   // + tail start/end
+extern "C" int dad_probe_read_ecda_stamps(void* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ecda_stamps), sizeof(g_ecda_stamps), 0, hipMemcpyDeviceToHost);
+}
+#define ECDA_STAMP(k) \
+  if (threadIdx.x == 0) g_ecda_stamps[blockIdx.x * 12 + (k)] = wall_clock64()
+__device__ __forceinline__ void g_ecda_stamps_n(int c, int n, int ns) {
+  g_ecda_stamps[c * 12 + 10] = (unsigned long long)n;
+  g_ecda_stamps[c * 12 + 11] = (unsigned long long)ns;
+}
+#define TAIL_STAMP(k) \
+  if (threadIdx.x == 0) g_ecda_stamps[DAD_C * 12 + (k)] = wall_clock64()
+#else
+#define ECDA_STAMP(k)
+#define TAIL_STAMP(k)
+#define g_ecda_stamps_n(c, n, ns)
+#endif
+
 #define TAIL_THREADS DAD_TAIL_THREADS
 
 __device__ __forceinline__ float block_sum_f(float v, float* red) {
@@ -134,7 +154,8 @@ __global__ __launch_bounds__(DAD_POOL_THREADS) void dad_pool(DadPoolArgs a) {
 // inlined) lets the loads of a batch of utterances issue before the ge stores of the
 // previous one; eight utterances per batch keep their loads in flight together.
 __device__ __forceinline__ void cls_backward(const float* __restrict__ emb, const uint8_t* __restrict__ keep,
-                                             float* __restrict__ ge, const float (*gz)[DAD_C], int n, int qg,
+                                             float* __restrict__ ge, float* __restrict__ ge_ecda,
+                                             const float (*gz)[DAD_C], int n, int qg,
                                              int h, uint32_t key, float p, float scale, const float (&w2h)[4],
                                              float (&gw)[4]) {
   for (int b0 = qg; b0 < n; b0 += 4 * 8) {
@@ -161,6 +182,7 @@ __device__ __forceinline__ void cls_backward(const float* __restrict__ emb, cons
           g += w2h[c] * gz[b][c];
         }
         ge[(size_t)b * DAD_H + h] = g * kv[u];
+        ge_ecda[(size_t)b * DAD_H + h] = 0.0f;   // ECDA overwrites its member rows afterwards
       }
     }
   }
@@ -168,6 +190,7 @@ __device__ __forceinline__ void cls_backward(const float* __restrict__ emb, cons
 
 __global__ __launch_bounds__(TAIL_THREADS) void dad_tail(DadTailArgs a) {
   DAD_GUARD_BLOCK(TAIL_THREADS);
+  TAIL_STAMP(0);
   const dad_config& cfg = a.cfg;
   const int B = cfg.B;                       // clean utterances
   const int Bn = cfg.warmup ? 0 : cfg.Bn;    // noisy utterances
@@ -357,9 +380,9 @@ __global__ __launch_bounds__(TAIL_THREADS) void dad_tail(DadTailArgs a) {
   const float* W2 = a.student + DAD_OFF_W2;
   const float w2h[4] = {W2[h], W2[DAD_H + h], W2[2 * DAD_H + h], W2[3 * DAD_H + h]};
   float gw[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  cls_backward(a.emb, a.keep1, a.ge, gz[0], B, qg, h, a.key_drop1, cfg.p_drop, cfg.drop_scale, w2h, gw);
-  cls_backward(a.emb + (size_t)(B + Bn) * DAD_H, a.keep2, a.ge + (size_t)B * DAD_H, gz[1], Bn, qg, h, a.key_drop2,
-               cfg.p_drop, cfg.drop_scale, w2h, gw);
+  cls_backward(a.emb, a.keep1, a.ge, a.ge_ecda, gz[0], B, qg, h, a.key_drop1, cfg.p_drop, cfg.drop_scale, w2h, gw);
+  cls_backward(a.emb + (size_t)(B + Bn) * DAD_H, a.keep2, a.ge + (size_t)B * DAD_H, a.ge_ecda + (size_t)B * DAD_H,
+               gz[1], Bn, qg, h, a.key_drop2, cfg.p_drop, cfg.drop_scale, w2h, gw);
 #pragma unroll
   for (int c = 0; c < 4; ++c) gwp[qg][c][h] = gw[c];
   __syncthreads();
@@ -372,6 +395,7 @@ __global__ __launch_bounds__(TAIL_THREADS) void dad_tail(DadTailArgs a) {
     for (int b = 0; b < Bn; ++b) s += (double)gz[1][b][tid];
     a.grad[DAD_OFF_B2 + tid] = (float)s;
   }
+  TAIL_STAMP(1);
 }
 
 // ------------------------------------------------------------------------------ ECDA
@@ -379,6 +403,7 @@ __global__ __launch_bounds__(TAIL_THREADS) void dad_tail(DadTailArgs a) {
 // (I/utils.py:633-650) runs in workgroup 0.  Each workgroup only writes the embedding
 // grads of ITS class members (clean: label == c, noisy: masked & pseudo-label == c), so
 // no atomics are needed and the result is deterministic.
+
 #define ECDA_THREADS DAD_ECDA_THREADS
 static_assert(ECDA_THREADS % DAD_H == 0 && ECDA_THREADS >= DAD_H, "ECDA column groups");
 #define ECDA_GROUPS (ECDA_THREADS / DAD_H)   // column groups of 256 threads
@@ -553,10 +578,9 @@ __device__ __forceinline__ float ecda_mmd_coef(EcdaSmem& S, const EcdaRows<STAGE
   return mmd;
 }
 
-// Embedding grads of the members, one column (hh = tid % 256) per thread, members split
-// over the ECDA_GROUPS column groups, ECDA_BATCH member rows per batch: the batch's
-// read-modify-write loads of ge are issued together (the rows are
-// distinct, but the compiler cannot prove it, so a plain loop would serialise them):
+// Embedding grads of the members into the ECDA part of dL/de (plain stores over the zeros
+// the tail wrote; a row belongs to at most one class), one column (hh = tid % 256) per
+// thread, members split over the ECDA_GROUPS column groups:
 //   g = mmd_scale * 2 sum_j Csym_ij (z_i - z_j)            (all members, if D)
 //     + comp_scale * (z_i - mu_c) + rep_g                    (noisy members)
 // comp_part accumulates sum ||z_i - mu_c||^2 over noisy members (when cent).
@@ -569,12 +593,6 @@ __device__ __forceinline__ void ecda_member_grads(EcdaSmem& S, const EcdaRows<ST
   const int ns = R.ns;
   // group grp owns members grp, grp + G, grp + 2G, ...; ECDA_BATCH of them per batch
   for (int m0 = grp; m0 < n; m0 += ECDA_BATCH * ECDA_GROUPS) {
-    float old[ECDA_BATCH];
-#pragma unroll
-    for (int u = 0; u < ECDA_BATCH; ++u) {
-      const int m = m0 + u * ECDA_GROUPS;
-      if (m < n) old[u] = (m < ns ? ge_c : ge_s)[(size_t)S.idx[m] * DAD_H + hh];
-    }
 #pragma unroll
     for (int u = 0; u < ECDA_BATCH; ++u) {
       const int m = m0 + u * ECDA_GROUPS;
@@ -600,7 +618,7 @@ __device__ __forceinline__ void ecda_member_grads(EcdaSmem& S, const EcdaRows<ST
         }
         g += rep_g;
       }
-      (m < ns ? ge_c : ge_s)[(size_t)S.idx[m] * DAD_H + hh] = old[u] + g;
+      (m < ns ? ge_c : ge_s)[(size_t)S.idx[m] * DAD_H + hh] = g;
     }
   }
 }
@@ -613,7 +631,8 @@ __global__ __launch_bounds__(ECDA_THREADS) void dad_ecda(DadEcdaArgs a) {
   const int B = cfg.B, Bn = cfg.Bn;
   const int c = blockIdx.x, tid = threadIdx.x;
   const float* tf = a.tailf;
-  if (tf[DAD_T_ECDA_ON] == 0.0f) return;
+  ECDA_STAMP(0);
+  const float ecda_on = tf[DAD_T_ECDA_ON];   // branched on after the metadata loads are issued
   const float* score = tf + DAD_TAIL_HDR;
   const float* predf = tf + DAD_TAIL_HDR + Bn;
   const float* mask = tf + DAD_TAIL_HDR + 2 * Bn;
@@ -631,6 +650,8 @@ __global__ __launch_bounds__(ECDA_THREADS) void dad_ecda(DadEcdaArgs a) {
   }
   if (tid < DAD_C) { S.cnt_clean[tid] = 0; S.cnt_noisy[tid] = 0; }
   __syncthreads();
+  ECDA_STAMP(1);
+  if (ecda_on == 0.0f) return;   // the tail left the ECDA gradient rows at zero
 #ifdef DAD_PROBE_ECDA_EXIT0
   return;
 #endif
@@ -642,7 +663,8 @@ __global__ __launch_bounds__(ECDA_THREADS) void dad_ecda(DadEcdaArgs a) {
     const int ns = n;
     n = ecda_compact(S, Bn, n, [&](int i) { return S.prd[i] >= 0; }, [](int) { return 1.0f; });
     const int nt = n - ns;
-    if (ns >= 2 && nt >= 2) {
+    const bool gate = ns >= 2 && nt >= 2;
+    if (gate) {
       auto run = [&](auto staged_tag) {
         constexpr bool ST = decltype(staged_tag)::value;
         const EcdaRows<ST> R{emb_c, emb_s, S, ns};
@@ -696,6 +718,7 @@ __global__ __launch_bounds__(ECDA_THREADS) void dad_ecda(DadEcdaArgs a) {
     }
   }
   __syncthreads();
+  ECDA_STAMP(2);
   // class attention (I/utils.py:597-599)
   const float* w = tf + DAD_T_W;
   float att[DAD_C];
@@ -710,17 +733,25 @@ __global__ __launch_bounds__(ECDA_THREADS) void dad_ecda(DadEcdaArgs a) {
   int nvalid = 0;
   for (int k = 0; k < ncls; ++k) nvalid += S.cnt_noisy[k] > 0;
   const int npairs = nvalid * (nvalid - 1) / 2;
-  if (tid < DAD_C * DAD_C) {
-    const int p = tid / DAD_C, q = tid % DAD_C;
+  {
+    // 16 (p, q) pairs x 256 dims over all threads: 32 threads per pair, 8 dims each,
+    // combined by a 32-lane reduction (pair-symmetric order, so pdist stays symmetric)
+    const int pair = tid / 32, l32 = tid & 31;
     float d = 0.0f;
-    if (p < ncls && q < ncls && S.cnt_noisy[p] > 0 && S.cnt_noisy[q] > 0 && p != q) {
-      for (int hh = 0; hh < DAD_H; ++hh) {
-        const float df = S.cent[p][hh] - S.cent[q][hh];
-        d += df * df;
+    if (pair < DAD_C * DAD_C) {
+      const int p = pair / DAD_C, q = pair % DAD_C;
+      const int lo = p < q ? p : q, hi = p < q ? q : p;
+      if (p < ncls && q < ncls && S.cnt_noisy[p] > 0 && S.cnt_noisy[q] > 0 && p != q) {
+#pragma unroll
+        for (int k = 0; k < DAD_H / 32; ++k) {
+          const float df = S.cent[lo][l32 * (DAD_H / 32) + k] - S.cent[hi][l32 * (DAD_H / 32) + k];
+          d += df * df;
+        }
       }
-      d = sqrtf(d);
     }
-    pdist[p][q] = d;
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) d += __shfl_xor(d, o, 32);
+    if (pair < DAD_C * DAD_C && l32 == 0) pdist[pair / DAD_C][pair % DAD_C] = sqrtf(d);
   }
   __syncthreads();
   float rep = 0.0f;
@@ -751,9 +782,11 @@ __global__ __launch_bounds__(ECDA_THREADS) void dad_ecda(DadEcdaArgs a) {
     rep_g = wscale * rep_coef * (-gsum / (float)npairs / (float)S.cnt_noisy[c]);
   }
   if (!gated[c] && !rep_on) return;
+  ECDA_STAMP(3);
   // members of class c: clean (label c, weight 1) then masked noisy (pseudo-label c, weight = score);
   // a class below the gate only needs its noisy members (repulsion)
   int n = gated[c] ? ecda_compact(S, B, 0, [&](int i) { return S.lab[i] == c; }, [](int) { return 1.0f; }) : 0;
+  ECDA_STAMP(5);
   const int ns = n;
   n = ecda_compact(S, Bn, n, [&](int i) { return S.prd[i] == c; }, [&](int i) { return S.scr[i]; });
   const int nt = n - ns;
@@ -766,11 +799,13 @@ __global__ __launch_bounds__(ECDA_THREADS) void dad_ecda(DadEcdaArgs a) {
     if (gated[c]) {
       D = ST ? S.dm : scratch;
       ecda_stage(S, R, n);
+      ECDA_STAMP(6);
 #ifdef DAD_PROBE_ECDA_NOMMD
       D = nullptr;
 #else
       mmd = ecda_mmd_coef(S, R, n, D);
 #endif
+      ECDA_STAMP(7);
     }
     // compactness (I/utils.py:614-616): mean_j ||z_j - mu||^2, grad (2/nt)(z_j - mu)
 #ifdef DAD_PROBE_ECDA_NOGRAD
@@ -782,9 +817,11 @@ __global__ __launch_bounds__(ECDA_THREADS) void dad_ecda(DadEcdaArgs a) {
   if (n <= ECDA_NZ) run(std::true_type{});
   else run(std::false_type{});
   if (!gated[c]) return;
+  ECDA_STAMP(8);
   const float comp = ecda_block_sum_f(S, cpart) / (float)nt;
   if (tid == 0) {
     a.tail_terms[c] = att_c * (mmd + cfg.ecda_gamma * comp + cfg.ecda_delta * rep);
+    g_ecda_stamps_n(c, n, ns);
     a.tail_terms[DAD_T_ECDA_GATE - DAD_T_ECDA_TERM + c] = 1.0f;
   }
 }

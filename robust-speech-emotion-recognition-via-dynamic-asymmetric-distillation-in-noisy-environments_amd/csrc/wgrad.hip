@@ -89,9 +89,10 @@ __device__ __forceinline__ void wg_range(const DadWgradArgs& a, int split, int& 
 __global__ __launch_bounds__(DAD_WGRAD_THREADS) void dad_wgrad_f32(DadWgradArgs a) {
   DAD_GUARD_BLOCK(DAD_WGRAD_THREADS);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int dblk = blockIdx.x % 6, split = blockIdx.x / 6;
-  const int d0 = (dblk * 4 + wv) * 32;
   const int i = lane & 31, kh = lane >> 5;
+  for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+  const int dblk = tile % 6, split = tile / 6;
+  const int d0 = (dblk * 4 + wv) * 32;
   int s0, s1;
   wg_range(a, split, s0, s1);
   f32x16 acc[DAD_HT];
@@ -144,6 +145,7 @@ __global__ __launch_bounds__(DAD_WGRAD_THREADS) void dad_wgrad_f32(DadWgradArgs 
   for (int ht = 0; ht < DAD_HT; ++ht)
 #pragma unroll
     for (int r = 0; r < 16; ++r) out[(size_t)(ht * 32 + dad_acc_row(r, kh)) * DAD_D + d] = acc[ht][r];
+  }
 }
 
 // ------------------------------------------------------------ BF16 (throughput mode)
@@ -307,11 +309,14 @@ __global__ __launch_bounds__(DAD_WGRAD_THREADS, 1) void dad_wgrad_bf16(DadWgradA
   const int tid = threadIdx.x;
   const int lane = tid & 63, wv = tid >> 6;
   const int kh = lane >> 5;
-  const int dblk = blockIdx.x % 6, split = blockIdx.x / 6;
+  const int nsc = a.g.Bc * a.g.ncc;
+  // workgroups stride over (utterance or split) x column-block tiles; a grid smaller than
+  // the tile count leaves CUs free for concurrent work on the caller's stream
+  for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+  const int dblk = tile % 6, split = tile / 6;
   const int dbase = dblk * 128;
   int s0, s1;
   wg_range(a, split, s0, s1);
-  const int nsc = a.g.Bc * a.g.ncc;
   f32x16 acc[2][4];
 #pragma unroll
   for (int m = 0; m < 2; ++m)
@@ -319,7 +324,7 @@ __global__ __launch_bounds__(DAD_WGRAD_THREADS, 1) void dad_wgrad_bf16(DadWgradA
     for (int n = 0; n < 4; ++n) acc[m][n] = f32x16{};
   wg_phase<0>(a, s0, min(s1, nsc), dbase, Xt, Gt, sc, acc);
   wg_phase<1>(a, max(s0, nsc) - nsc, s1 - nsc, dbase, Xt, Gt, sc, acc);
-  float* out = a.wpart + (size_t)split * DAD_H * DAD_D;
+  const size_t obase = (size_t)split * DAD_H * DAD_D;
 #pragma unroll
   for (int m = 0; m < 2; ++m)
 #pragma unroll
@@ -328,16 +333,18 @@ __global__ __launch_bounds__(DAD_WGRAD_THREADS, 1) void dad_wgrad_bf16(DadWgradA
       for (int r = 0; r < 16; ++r) {
         const int h = (2 * wv + m) * 32 + dad_acc_row(r, kh);
         const int d = dbase + 32 * n + (lane & 31);
-        out[(size_t)h * DAD_D + d] = acc[m][n][r];
+        if (a.wpart_bf16) a.wpart_bf16[obase + (size_t)h * DAD_D + d] = (__bf16)acc[m][n][r];
+        else a.wpart[obase + (size_t)h * DAD_D + d] = acc[m][n][r];
       }
+  }
 }
 
 // ---------------------------------------------------------------- reduce + squared norms
 // blocks [0, NB): DAD_REDUCE_COLS floats of dW1 each = sum_s wpart[s] + squared-norm partial.
 //   thread = (float4 column, split group kg): group kg sums splits kg, kg+4, ... with its
 //   loads in flight together, then the four groups are combined in fixed order (deterministic).
-// block NB: db1 = sum_b (dL/de_b / len_b) * active_count_b, the W2/b2 norm partial and
-// the loss totals (I/train.py:462-466).
+// block NB: db1, the W2/b2 norm partial and the loss totals (db1_and_totals below).
+//
 // db1[h] = sum_r dL/de[r][h] / max(1, len_r) * active_count[r][h], the W2/b2 squared-norm
 // partial and the loss totals (I/train.py:462-466).  Returns this thread's norm share.
 static_assert(DAD_REDUCE_THREADS == DAD_H, "db1 block: one thread per hidden unit");
@@ -350,6 +357,7 @@ __device__ double db1_and_totals(const DadReduceArgs& a, f32x4 (*part)[DAD_H / 4
   const DadGeom& g = a.g;
   const int nb = g.Bc + (a.warmup ? 0 : g.Bn);
   const int hq = tid & (DAD_H / 4 - 1), rg = tid / (DAD_H / 4);
+  const bool ecda = a.ge_ecda != nullptr;
   f32x4 acc = f32x4{};
   for (int r0 = rg; r0 < nb; r0 += 4 * 8) {
     f32x4 gv[8], cv[8];
@@ -358,6 +366,7 @@ __device__ double db1_and_totals(const DadReduceArgs& a, f32x4 (*part)[DAD_H / 4
     for (int u = 0; u < 8; ++u) {
       const int r = min(r0 + 4 * u, nb - 1);
       gv[u] = reinterpret_cast<const f32x4*>(a.ge + (size_t)r * DAD_H)[hq];
+      if (ecda) gv[u] += reinterpret_cast<const f32x4*>(a.ge_ecda + (size_t)r * DAD_H)[hq];
       cv[u] = reinterpret_cast<const f32x4*>(a.cnt_tot + (size_t)r * DAD_H)[hq];
       lv[u] = a.vlen[r];
     }
@@ -451,17 +460,36 @@ __global__ __launch_bounds__(DAD_REDUCE_THREADS) void dad_wsum(DadReduceArgs a) 
     const int nutt = g.Bc + (a.warmup ? 0 : g.Bn);
     const int h = blockIdx.x / (DAD_D / DAD_REDUCE_COLS);
     const int dcol0 = (blockIdx.x % (DAD_D / DAD_REDUCE_COLS)) * DAD_REDUCE_COLS;
-    for (int u = tid; u < nutt; u += DAD_REDUCE_THREADS) gsh[u] = a.ge[(size_t)u * DAD_H + h] / fmaxf(a.vlen[u], 1.0f);
+    // dL/de = CE/KL part + ECDA part (zeros unless ECDA wrote the row this step)
+    const bool ecda = a.ge_ecda != nullptr;
+    for (int u = tid; u < nutt; u += DAD_REDUCE_THREADS) {
+      float gu = a.ge[(size_t)u * DAD_H + h];
+      if (ecda) gu += a.ge_ecda[(size_t)u * DAD_H + h];
+      gsh[u] = gu / fmaxf(a.vlen[u], 1.0f);
+    }
     __syncthreads();
     const int col = tid & (DAD_REDUCE_COLS / 4 - 1), ug = tid / (DAD_REDUCE_COLS / 4);
     const size_t off = (size_t)h * DAD_D + dcol0 + (size_t)col * 4;
     f32x4 s = f32x4{};
     for (int u0 = ug; u0 < nutt; u0 += 4 * 8) {
       f32x4 v[8];
+      if (a.wpart_bf16) {
+        bf16x4 vb[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int u = min(u0 + 4 * k, nutt - 1);
-        v[k] = *reinterpret_cast<const f32x4*>(a.wpart + (size_t)u * DAD_H * DAD_D + off);
+        for (int k = 0; k < 8; ++k) {
+          const int u = min(u0 + 4 * k, nutt - 1);
+          vb[k] = *reinterpret_cast<const bf16x4*>(a.wpart_bf16 + (size_t)u * DAD_H * DAD_D + off);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[k][e] = (float)vb[k][e];
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int u = min(u0 + 4 * k, nutt - 1);
+          v[k] = *reinterpret_cast<const f32x4*>(a.wpart + (size_t)u * DAD_H * DAD_D + off);
+        }
       }
 #pragma unroll
       for (int k = 0; k < 8; ++k)

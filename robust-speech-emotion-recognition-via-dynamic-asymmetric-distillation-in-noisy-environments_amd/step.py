@@ -311,6 +311,7 @@ class DADStep:
             "tau_after": t[_lib.T_TAU_AFTER:_lib.T_TAU_AFTER + 4],
             "ecda_terms": t[_lib.T_ECDA_TERM:_lib.T_ECDA_TERM + 4],
             "clip_norm": t[_lib.T_CLIPNORM], "clip_coef": t[_lib.T_CLIPCOEF], "msum": t[_lib.T_MSUM],
+            "ecda_on": t[_lib.T_ECDA_ON],
             "grad": self.grad[:_lib.DAD_NPARAM], "nb": nb,
         }
 

@@ -109,7 +109,8 @@ def close(a, b, tol, what):
 
 
 def ws_ge(step, Bc, Tc, Bn, Tn):
-    """dL/de rows [Bc+Bn][256] from the step's workspace (mirror of dad_ws_layout)."""
+    """dL/de rows [Bc+Bn][256] from the step's workspace (mirror of dad_ws_layout): CE/KL
+    part + ECDA part."""
     al = lambda x: (x + 255) & ~255
     ncc, ncn = (Tc + 31) // 32, (Tn + 31) // 32
     tpc, tpn = ncc * 32, ncn * 32
@@ -120,4 +121,7 @@ def ws_ge(step, Bc, Tc, Bn, Tn):
     off = al(off + 4 * (Bc + Bn))                            # vlen
     off = al(off + 4 * (Bc + Bn) * 256)                      # cnt_tot
     ws = step._ws
-    return ws[off:off + 4 * (Bc + Bn) * 256].view(torch.float32).view(Bc + Bn, 256).cpu().numpy()
+    n = 4 * (Bc + Bn) * 256
+    ge = ws[off:off + n].view(torch.float32).view(Bc + Bn, 256).cpu().numpy()
+    off_e = al(off + n)                                      # ge_ecda (zeros where ECDA wrote nothing)
+    return ge + ws[off_e:off_e + n].view(torch.float32).view(Bc + Bn, 256).cpu().numpy()

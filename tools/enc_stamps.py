@@ -35,6 +35,16 @@ def main():
     st = np.frombuffer(buf, dtype=np.uint64).reshape(nwg, 3).astype(np.int64)
     t0 = st[:, 0].min()
     us = (st - t0) / 100.0            # 100 MHz -> us
+    ebuf = (ctypes.c_ulonglong * (4 * 12 + 4))()
+    if hasattr(L, "dad_probe_read_ecda_stamps") and L.dad_probe_read_ecda_stamps(ebuf) == 0:
+        e = np.frombuffer(ebuf, dtype=np.uint64).astype(np.int64)
+        rel = lambda v: (v - t0) / 100.0
+        print("encoder end %.1f us; tail %.1f -> %.1f us" % (us[:, 2].max(), rel(e[48]), rel(e[49])))
+        names = ["start", "meta", "centroid", "gates", "zero", "compact", "stage", "mmd", "grads"]
+        for c in range(4):
+            row = e[c * 12:c * 12 + 9]
+            parts = ["%s %.1f" % (names[k], rel(row[k])) for k in range(9) if row[k] > 0]
+            print("ecda class %d (n=%d ns=%d): %s" % (c, e[c * 12 + 10], e[c * 12 + 11], "  ".join(parts)))
     for name, sl in (("noisy", slice(0, n_noisy)), ("clean", slice(n_noisy, nwg))):
         s = us[sl]
         print("%-5s n=%3d start p0/p50/p100 %.1f/%.1f/%.1f  loop p50/p100 %.1f/%.1f  epi p50/p100 %.1f/%.1f  "
