@@ -91,6 +91,39 @@ int side_stream(SideStream** out) {
   return DAD_OK;
 }
 
+int device_cus(int* out) {
+  static int cache[kMaxDevices];
+  int dev = 0;
+  DAD_TRY(hipGetDevice(&dev));
+  if (dev < 0 || dev >= kMaxDevices) return DAD_E_ARG;
+  if (!cache[dev]) DAD_TRY(hipDeviceGetAttribute(&cache[dev], hipDeviceAttributeMultiprocessorCount, dev));
+  *out = cache[dev];
+  return DAD_OK;
+}
+
+// Workgroup split of the W-stationary encoder (encode_ws.hip): one persistent workgroup per
+// CU, teacher : student in proportion to their work (32-row slab costs: clean 1, weak
+// kWsWeak, strong kWsStrong -- the augmentation RNG dominates a noisy slab), more
+// workgroups than CUs only when a range would exceed DAD_ENC_WS_MAXJ jobs.
+constexpr float kWsWeak = 1.03f, kWsStrong = 1.47f;   // measured (tools/ws_stamps.py fit)
+void ws_split(const DadGeom& G, int Bn, int cus, int& nt, int& ns) {
+  const int Jt = Bn * G.ncn, Jc = G.Bc * G.ncc, Js = Jt;
+  if (Jt == 0) {
+    nt = 0;
+    ns = std::min(cus, Jc);
+  } else {
+    const double tot = Jt * (double)kWsWeak + Jc + Js * (double)kWsStrong;
+    nt = (int)(cus * (Jt * (double)kWsWeak) / tot + 0.5);
+    nt = std::max(1, std::min(cus - 1, nt));
+    ns = cus - nt;
+    nt = std::min(nt, Jt);
+    ns = std::min(ns, Jc + Js);
+  }
+  nt = std::max(nt, (Jt + DAD_ENC_WS_MAXJ - 1) / DAD_ENC_WS_MAXJ);
+  const double wtot = Jc + Js * (double)kWsStrong;
+  ns = std::max(ns, (int)(wtot / (DAD_ENC_WS_MAXJ - 2)) + 1);
+}
+
 }  // namespace
 
 extern "C" {
@@ -165,11 +198,21 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   ea.part_sum = part_sum; ea.part_cnt = part_cnt; ea.bits = bits; ea.xs_bf16 = xs_bf16;
   const int nwaves = G.Bc * G.ncc + Bn * G.ncn;
   const dim3 egrid((nwaves + 3) / 4);
-  // bf16: 8-wave workgroups, 4 noisy slabs (teacher + student waves) or 8 clean slabs each
-  const dim3 egrid_bf16((Bn * G.ncn + 3) / 4 + (G.Bc * G.ncc + 7) / 8);
   if (do_encode) {
-    if (bf16) hipLaunchKernelGGL(dad_encode_bf16, egrid_bf16, dim3(DAD_ENC_BF16_THREADS), 0, stream, ea);
-    else hipLaunchKernelGGL(dad_encode_f32, egrid, dim3(DAD_ENC_F32_THREADS), 0, stream, ea);
+    if (bf16) {
+      int cus = 0;
+      const int rc = device_cus(&cus);
+      if (rc) return rc;
+      ws_split(G, Bn, cus, ea.ws_nt, ea.ws_ns);
+      ea.ws_wstrong = kWsStrong;
+      if (ea.ws_nt + ea.ws_ns > 0) {
+        if (explicit_rng) hipLaunchKernelGGL(dad_encode_ws_explicit, dim3(ea.ws_nt + ea.ws_ns), dim3(DAD_ENC_WS_THREADS), 0,
+                                             stream, ea);
+        else hipLaunchKernelGGL(dad_encode_ws, dim3(ea.ws_nt + ea.ws_ns), dim3(DAD_ENC_WS_THREADS), 0, stream, ea);
+      }
+    } else {
+      hipLaunchKernelGGL(dad_encode_f32, egrid, dim3(DAD_ENC_F32_THREADS), 0, stream, ea);
+    }
     DAD_TRY(hipGetLastError());
   }
   if (!do_backward) return DAD_OK;
@@ -364,9 +407,10 @@ __global__ __launch_bounds__(256) void dad_embed_kernel(const float* part_sum, c
   if (h == 0 && vlen) vlen[b] = len;
 }
 
+// bf16 copy of W1 in the W-stationary encoder's fragment order (dad_w1frag_index)
 __global__ __launch_bounds__(256) void dad_w1bf_kernel(const float* w, __bf16* out) {
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (i < (size_t)DAD_H * DAD_D) out[i] = (__bf16)w[i];
+  if (i < (size_t)DAD_H * DAD_D) out[dad_w1frag_index((uint32_t)(i / DAD_D), (uint32_t)(i % DAD_D))] = (__bf16)w[i];
 }
 
 int encoder_forward_impl(const float* x, const uint8_t* pad, int B, int T, const float* w1, const float* b1,
@@ -386,9 +430,16 @@ int encoder_forward_impl(const float* x, const uint8_t* pad, int B, int T, const
   ea.part_cnt = ws_ptr<float>(workspace, L.part_cnt);
   ea.bits = ws_ptr<uint32_t>(workspace, L.bits);
   const dim3 egrid((B * G.ncc + 3) / 4);
-  if (precision == DAD_PREC_BF16)
-    hipLaunchKernelGGL(dad_encode_bf16, dim3((B * G.ncc + 7) / 8), dim3(DAD_ENC_BF16_THREADS), 0, stream, ea);
-  else hipLaunchKernelGGL(dad_encode_f32, egrid, dim3(DAD_ENC_F32_THREADS), 0, stream, ea);
+  if (precision == DAD_PREC_BF16) {
+    int cus = 0;
+    const int rc = device_cus(&cus);
+    if (rc) return rc;
+    ws_split(G, 0, cus, ea.ws_nt, ea.ws_ns);
+    ea.ws_wstrong = kWsStrong;
+    hipLaunchKernelGGL(dad_encode_ws, dim3(ea.ws_nt + ea.ws_ns), dim3(DAD_ENC_WS_THREADS), 0, stream, ea);
+  } else {
+    hipLaunchKernelGGL(dad_encode_f32, egrid, dim3(DAD_ENC_F32_THREADS), 0, stream, ea);
+  }
   DAD_TRY(hipGetLastError());
   if (e_out) {
     hipLaunchKernelGGL(dad_embed_kernel, dim3(B), dim3(256), 0, stream, ea.part_sum, pad, B, T, G.ncc, vlen_out,

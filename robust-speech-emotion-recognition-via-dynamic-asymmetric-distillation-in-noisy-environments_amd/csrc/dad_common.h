@@ -64,31 +64,55 @@ static inline uint32_t dad_stream_key(uint64_t seed, uint64_t counter, uint32_t 
   return (uint32_t)(z ^ (z >> 32));
 }
 
-// uniform in (0, 1]  (24-bit resolution)
-__device__ __forceinline__ float dad_u01_open0(uint32_t h) {
-  return (float)((h >> 8) + 1u) * (1.0f / 16777216.0f);
-}
-// uniform in [0, 1)
+// uniform in [0, 1)  (24-bit resolution)
 __device__ __forceinline__ float dad_u01(uint32_t h) { return (float)(h >> 8) * (1.0f / 16777216.0f); }
 
-// Two standard normals from two hashes (Box-Muller; v_log/v_sqrt/v_sin/v_cos).
-__device__ __forceinline__ void dad_box_muller(uint32_t h0, uint32_t h1, float& z0, float& z1) {
-  float u1 = dad_u01_open0(h0);
-  float u2 = dad_u01(h1);
-  float r = __builtin_amdgcn_sqrtf(-1.38629436112f * __builtin_amdgcn_logf(u1));  // -2 ln u1
-  z0 = r * __builtin_amdgcn_cosf(u2);   // v_cos_f32 takes revolutions: cos(2*pi*u2)
-  z1 = r * __builtin_amdgcn_sinf(u2);
+// Two normals of standard deviation s from ONE hash: Box-Muller on its two 16-bit halves,
+// each turned into a float in [1, 2) by bit placement (no int->float convert):
+//   f1 = 1 + hi/2^16, u1 = 2 - f1 = 1 - hi/2^16 in [2^-16, 1]  (never 0)
+//   f2 = 1 + lo/2^16: v_sin/v_cos take revolutions, so sin(2 pi f2) = sin(2 pi lo/2^16)
+//   r = s sqrt(-2 ln u1) = sqrt(c log2 u1) with c = -2 ln2 s^2 folded into one constant
+//   z0 = r cos(2 pi u2),  z1 = r sin(2 pi u2);   |z| <= 4.71 s.
+// Element i of a stream takes normal (i & 1) of pair i >> 1, so every kernel that needs
+// the value of element i regenerates it bit for bit.
+#define DAD_NEG2LN2 (-1.38629436112f)
+__device__ __forceinline__ void dad_normal_pair_c(uint32_t key, uint32_t pair, float c, float& z0, float& z1) {
+  const uint32_t h = dad_rng32(pair, key);
+  const float f1 = __uint_as_float(((h >> 9) & 0x007fff80u) | 0x3f800000u);
+  const float f2 = __uint_as_float(((h << 7) & 0x007fff80u) | 0x3f800000u);
+  const float r = __builtin_amdgcn_sqrtf(c * __builtin_amdgcn_logf(2.0f - f1));
+  z0 = r * __builtin_amdgcn_cosf(f2);
+  z1 = r * __builtin_amdgcn_sinf(f2);
+}
+__device__ __forceinline__ void dad_normal_pair(uint32_t key, uint32_t pair, float& z0, float& z1) {
+  dad_normal_pair_c(key, pair, DAD_NEG2LN2, z0, z1);
 }
 
-// 4 normals for elements (row, d..d+3) of a [rows][768] tensor in stream `key`.
+// normal of element idx of stream `key`
+__device__ __forceinline__ float dad_normal1(uint32_t key, uint32_t idx) {
+  float z0, z1;
+  dad_normal_pair(key, idx >> 1, z0, z1);
+  return (idx & 1u) ? z1 : z0;
+}
+
+// 4 normals for elements (row, d..d+3) of a [rows][768] tensor in stream `key` (d % 4 == 0).
 __device__ __forceinline__ f32x4 dad_normal4(uint32_t key, uint32_t row, uint32_t d) {
-  uint32_t i = row * (uint32_t)DAD_D + d;
+  const uint32_t p = (row * (uint32_t)DAD_D + d) >> 1;
   f32x4 z;
   float a, b, c, e;
-  dad_box_muller(dad_rng32(i, key), dad_rng32(i + 1u, key), a, b);
-  dad_box_muller(dad_rng32(i + 2u, key), dad_rng32(i + 3u, key), c, e);
+  dad_normal_pair(key, p, a, b);
+  dad_normal_pair(key, p + 1u, c, e);
   z[0] = a; z[1] = b; z[2] = c; z[3] = e;
   return z;
+}
+
+// W1 bf16 shadow layout = the B-fragment order of the W-stationary encoder (encode_ws.hip):
+// fragment ((w*4 + t)*24 + ks) is 64 lanes x 8 bf16, lane l holding
+// W1[h = 64w + 16t + (l & 15)][k = 32ks + 8(l >> 4) + j], so each wave loads its resident
+// W1 with fully coalesced 1 KB reads.
+__host__ __device__ __forceinline__ uint32_t dad_w1frag_index(uint32_t h, uint32_t k) {
+  const uint32_t w = h >> 6, t = (h >> 4) & 3u, n = h & 15u, ks = k >> 5, q = (k >> 3) & 3u, j = k & 7u;
+  return ((((w * 4u + t) * 24u + ks) * 64u) + n + 16u * q) * 8u + j;
 }
 
 __device__ __forceinline__ float dad_uniform_at(uint32_t key, uint32_t idx) {

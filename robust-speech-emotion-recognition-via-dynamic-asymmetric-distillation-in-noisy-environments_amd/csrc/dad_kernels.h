@@ -4,8 +4,9 @@
 
 // Block sizes: kernels index with these, launches use them; every kernel whose indexing
 // depends on its block size exits uniformly if launched with another one.
-#define DAD_ENC_BF16_THREADS 512
 #define DAD_ENC_F32_THREADS 256
+#define DAD_ENC_WS_THREADS 512                               // W-stationary bf16 encoder (8 waves, two per SIMD)
+#define DAD_ENC_WS_MAXJ 256                                  // max 32-row jobs per encoder workgroup
 #define DAD_POOL_THREADS 256
 #define DAD_TAIL_THREADS 1024
 #define DAD_ECDA_THREADS 512
@@ -31,6 +32,8 @@ struct DadEncodeArgs {
   float weak_std, strong_std, feat_p;
   float* part_sum; float* part_cnt; uint32_t* bits;
   __bf16* xs_bf16;          // BF16 mode: strong-augmented input as fed to the MFMA (for wgrad)
+  int ws_nt, ws_ns;         // dad_encode_ws: teacher / student workgroups
+  float ws_wstrong;         // dad_encode_ws: cost of a strong slab relative to a clean one
 };
 
 struct DadPoolArgs {
@@ -105,7 +108,8 @@ struct DadOptimArgs {
 };
 
 __global__ void dad_encode_f32(DadEncodeArgs a);
-__global__ void dad_encode_bf16(DadEncodeArgs a);
+__global__ void dad_encode_ws(DadEncodeArgs a);            // counter RNG
+__global__ void dad_encode_ws_explicit(DadEncodeArgs a);   // explicit noise tensors (parity)
 __global__ void dad_pool(DadPoolArgs a);
 __global__ void dad_tail(DadTailArgs a);
 __global__ void dad_ecda(DadEcdaArgs a);

@@ -1,0 +1,624 @@
+// W-stationary BF16 encoder: the throughput-mode forward of all three encoder passes.
+//
+// Replaces, per step (I/train.py:399,406-410,439):
+//   student_encoder(clean)                         Emotion2VecEncoder.forward, I/model.py:18-41
+//   teacher_encoder(weak_augment(noisy))           + DataAugmentation.weak_augment, I/utils.py:328-331
+//   student_encoder(strong_augment(noisy))         + strong_augment/_apply_temporal_masking, I/utils.py:333-375
+// and emits what the rest of the step consumes: per-32-row-slab pooled ReLU sums and active
+// counts, the ReLU'-and-valid bit mask, and the bf16 strong-augmented input (wgrad operand).
+//
+// Shape of the work: out[rows][256] = x[rows][768] . W1^T with tens of thousands of rows and
+// W1 only 384 KB in bf16.  So W1 is STATIONARY: a persistent workgroup holds all 256 hidden
+// units of ONE network's W1 in its register file (each wave 256/WAVES hidden units x 768 k,
+// read in place as MFMA B operands) and streams 16-row sub-slabs of x through LDS:
+//
+//   HBM fp32 rows --LDS-DMA (global_load_lds_dwordx4, 2 stages x 48 KB in flight)--> raw ring
+//   raw ring --augment (counter-RNG Box-Muller, feature mask, temporal zero) + cvt bf16-->
+//      bf16 tile ring (2 x 24 KB; 16-B chunks XOR-swizzled by row: conflict-free A reads)
+//   bf16 tile --ds_read_b128 A fragments--> v_mfma_f32_16x16x32_bf16 against the resident W1
+//   accumulators --bias, ReLU, valid mask, row sums, ballots--> slab partials + ReLU' bits
+//
+// Each x element is fetched once per network that consumes it and augmented once.  Roles are
+// per workgroup: TEACHER workgroups (teacher W1) run the weak-augmented noisy slabs, STUDENT
+// workgroups (student W1) the clean slabs and the strong-augmented noisy slabs.  Jobs (32-row
+// slabs) are split into contiguous, cost-weighted ranges (host: ws_split in dad_abi.hip).
+//
+// Pipeline per wave (iteration q = sub-slab q of the workgroup's range):
+//   wait for the wave's own DMA of sub-slab q+1 (counted vmcnt: the stores and the youngest
+//   DMA batch stay in flight) -> MFMA(q) with convert(q+1) -> epilogue(q) -> DMA of sub-slab
+//   q+3 into the raw stage convert(q+1) just freed -> barrier.
+#include <type_traits>
+
+#include "dad_common.h"
+#include "dad_kernels.h"
+
+#ifdef DAD_PROBE_STAMPS
+// diagnostic build only (never the product library): per-workgroup wave-0 timeline
+// [start, after prologue, end (100 MHz wall clock), role<<16 | sub-slabs]
+__device__ unsigned long long g_ws_stamps[4096 * 10];
+// [4..9]: wave-0 cycles summed over the loop in: DMA wait, MFMA, convert, epilogue, DMA issue, barrier
+#define WS_CLK() __builtin_amdgcn_s_memtime()
+extern "C" int dad_probe_read_ws_stamps(void* host, int n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ws_stamps), sizeof(unsigned long long) * 10 * n, 0,
+                                  hipMemcpyDeviceToHost);
+}
+#define WS_STAMP(k, v) \
+  if (threadIdx.x == 0 && blockIdx.x < 4096) g_ws_stamps[blockIdx.x * 10 + (k)] = (v)
+#else
+#define WS_STAMP(k, v)
+#define WS_CLK() 0ull
+#endif
+
+namespace {
+
+constexpr int kSub = 16;                       // rows per sub-slab (one MFMA M tile)
+constexpr int kKS = DAD_D / 32;                // 24 k-steps of v_mfma_f32_16x16x32_bf16
+constexpr int kRawRow = DAD_D * 4;             // 3072 B
+constexpr int kRawStage = kSub * kRawRow;      // 48 KB
+constexpr int kTileRow = DAD_D * 2;            // 1536 B
+constexpr int kTile = kSub * kTileRow;         // 24 KB
+// tiles first: every A-fragment / tile address then fits ds_read/ds_write's 16-bit immediate
+constexpr int kOffTile = 0;
+constexpr int kOffRaw = 2 * kTile;             // 48 KB
+constexpr int kOffFK = kOffRaw + 2 * kRawStage;  // 144 KB: feature keep flags f32[768]
+constexpr int kOffVB = kOffFK + DAD_D * 4;     // valid bits u32[DAD_ENC_WS_MAXJ]
+constexpr int kLds = kOffVB + 4 * DAD_ENC_WS_MAXJ;
+static_assert(kLds <= 160 * 1024, "LDS budget");
+
+enum { KIND_CLEAN = 0, KIND_WEAK = 1, KIND_STRONG = 2 };
+
+// Every scalar the kernel needs, copied out of the kernel arguments once: a select between
+// two argument fields must not become a select between their addresses (which drags the
+// argument block into scratch and makes every job field a VGPR).
+struct Ctx {
+  int Bc, Tc, ncc, tpc, Bn, Tn, ncn, tpn;
+  uint32_t mcc, mcn;     // division magics for ncc / ncn (fast_div)
+  int nsc, nsn, Jc, Js;
+  int mask_len, start_hi;
+  const float* xc; const float* xn;
+  const uint8_t* mc; const uint8_t* mn;
+  const float* nw; const float* ns; const float* u; const int64_t* start;
+  uint32_t key_weak, key_strong, key_feat, key_tstart;
+  float wstd, sstd, feat_p;
+  float* part_sum; float* part_cnt; uint32_t* bits; __bf16* xs;
+};
+
+__device__ __forceinline__ Ctx ctx_of(const DadEncodeArgs& a) {
+  Ctx c;
+  c.Bc = a.g.Bc; c.Tc = a.g.Tc; c.ncc = a.g.ncc; c.tpc = a.g.tpc;
+  c.Bn = a.g.Bn; c.Tn = a.g.Tn; c.ncn = a.g.ncn; c.tpn = a.g.tpn;
+  c.nsc = c.Bc * c.ncc; c.nsn = c.Bn * c.ncn;
+  c.mcc = c.ncc > 1 ? 0xffffffffu / (uint32_t)c.ncc + 1u : 0u;
+  c.mcn = c.ncn > 1 ? 0xffffffffu / (uint32_t)c.ncn + 1u : 0u;
+  c.Jc = c.nsc; c.Js = a.warmup ? 0 : c.nsn;
+  c.mask_len = a.mask_len; c.start_hi = a.start_hi;
+  c.xc = a.xc; c.xn = a.xn; c.mc = a.mc; c.mn = a.mn;
+  c.nw = a.nw; c.ns = a.ns; c.u = a.u; c.start = a.start;
+  c.key_weak = a.key_weak; c.key_strong = a.key_strong; c.key_feat = a.key_feat; c.key_tstart = a.key_tstart;
+  c.wstd = a.weak_std; c.sstd = a.strong_std; c.feat_p = a.feat_p;
+  c.part_sum = a.part_sum; c.part_cnt = a.part_cnt; c.bits = a.bits; c.xs = a.xs_bf16;
+  return c;
+}
+
+// n / d for the slab counts per utterance: m = floor(2^32 / d) + 1 (0 for d = 1) is exact for
+// n * d < 2^32; one scalar multiply-high instead of a ~40-instruction scalar division on a
+// path every sub-slab takes several times
+__device__ __forceinline__ int fast_div(int n, uint32_t m) {
+  return m ? (int)__umulhi((uint32_t)n, m) : n;
+}
+
+struct Job {
+  int kind, b, c, T;
+  long row0;        // [b][T] row of frame 0
+  long sum_slab;    // part_sum slab
+  long cnt_slab;    // part_cnt slab (student only)
+  long bits_row;    // first bits row of the slab (student only)
+};
+
+// job j of the workgroup's role list: teacher -> weak slab j; student -> clean slab j, then
+// strong slab j - Jc.  Slab numbering matches dad_pool / the weight gradient.
+__device__ __forceinline__ Job job_of(const Ctx& C, bool teacher, int j) {
+  Job J;
+  const bool noisy = teacher || j >= C.Jc;
+  const int s = (teacher || j < C.Jc) ? j : j - C.Jc;
+  const int nc = noisy ? C.ncn : C.ncc;
+  J.kind = teacher ? KIND_WEAK : (noisy ? KIND_STRONG : KIND_CLEAN);
+  J.b = fast_div(s, noisy ? C.mcn : C.mcc);
+  J.c = s - J.b * nc;
+  J.T = noisy ? C.Tn : C.Tc;
+  J.row0 = (long)J.b * J.T;
+  J.sum_slab = teacher ? (long)C.nsc + s : (noisy ? (long)C.nsc + C.nsn + s : (long)s);
+  J.cnt_slab = noisy ? (long)C.nsc + s : (long)s;
+  J.bits_row = noisy ? (long)C.Bc * C.tpc + (long)J.b * C.tpn + (long)J.c * DAD_SLAB
+                     : (long)J.b * C.tpc + (long)J.c * DAD_SLAB;
+  return J;
+}
+
+// Contiguous job range of workgroup wg.  Teacher workgroups split the weak slabs evenly;
+// student workgroups split clean (cost 1) + strong (cost wstrong) slabs by cost.
+__device__ __forceinline__ void job_range(const Ctx& C, int wg, int nt, int ns, float wstrong, bool& teacher,
+                                          int& j0, int& j1) {
+  const int Jt = C.Js;
+  teacher = wg < nt;
+  if (teacher) {
+    j0 = (int)((long)wg * Jt / nt);
+    j1 = (int)((long)(wg + 1) * Jt / nt);
+    return;
+  }
+  const int k = wg - nt;
+  const float wtot = (float)C.Jc + (float)C.Js * wstrong;
+  auto at = [&](int kk) -> int {
+    if (kk >= ns) return C.Jc + C.Js;
+    const float B = wtot * (float)kk / (float)ns;
+    const int j = B <= (float)C.Jc ? (int)(B + 0.5f) : C.Jc + (int)((B - (float)C.Jc) / wstrong + 0.5f);
+    return j < 0 ? 0 : (j > C.Jc + C.Js ? C.Jc + C.Js : j);
+  };
+  j0 = at(k);
+  j1 = at(k + 1);
+}
+
+template <int NOISE>
+__device__ __forceinline__ int tstart_of(const Ctx& C, int b) {
+  if (NOISE && C.start) return (int)C.start[b];
+  const uint32_t h = dad_rng32((uint32_t)b, C.key_tstart);
+  return (int)(((uint64_t)h * (uint64_t)C.start_hi) >> 32);
+}
+
+// LDS-DMA: 16 B per lane of `src` into LDS at lds_dst + 16 * lane (M0 = wave-uniform base).
+// Inline asm: hipcc neither counts it nor drains it at barriers; the kernel counts it.
+__device__ __forceinline__ void glds16(const void* src, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(src), "s"(lds_dst) : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+// a per-lane value the compiler must treat as new: addresses derived from it are computed
+// where they are used instead of being hoisted out of the loop as ~30 long-lived VGPRs (the
+// resident W1 leaves a wave only 64 registers for everything else)
+__device__ __forceinline__ int opaque(int x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Per-workgroup-shape constants: WAVES waves, each holding NT 16-wide hidden-unit tiles of W1
+// (NT * 96 registers) and converting RPW of the 16 rows of each sub-slab.
+template <int WAVES>
+struct Shape {
+  static constexpr int kThreads = 64 * WAVES;
+  static constexpr int NT = 16 / WAVES;        // 16-h tiles per wave
+  static constexpr int HW = 16 * NT;           // hidden units per wave
+  static constexpr int RPW = kSub / WAVES;     // rows converted per wave
+  static constexpr int kDma = 3 * RPW;         // LDS-DMA instructions per wave per sub-slab
+  static constexpr int kXsRow = 3;             // bf16 strong-x stores per converted row
+  // 4 waves (one per SIMD, 512 registers): 256 of the 384 W1 registers in AGPRs.
+  // 8 waves (two per SIMD, 256 registers): all 192 in VGPRs, no AGPRs at all.
+  static constexpr bool AGPR_W = WAVES == 4;
+  static constexpr bool STAGGER = WAVES == 8;  // two waves per SIMD: opposite MFMA / convert order
+};
+
+// DMA the wave's RPW rows of sub-slab (J, half) into a raw stage.  Frames past the
+// utterance are clamped to its last frame (masked out by the valid bits).
+template <class S>
+__device__ __forceinline__ void dma_rows(const float* x, const Job& J, int half, int w, uint32_t stage_base,
+                                         int lane) {
+#pragma unroll
+  for (int i = 0; i < S::RPW; ++i) {
+    const int r = S::RPW * w + i;
+    const int t = min(J.c * DAD_SLAB + half * kSub + r, J.T - 1);
+    const float* src = x + (size_t)(J.row0 + t) * DAD_D + 4 * lane;
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(stage_base + (uint32_t)(r * kRawRow));
+#pragma unroll
+    for (int k = 0; k < 3; ++k) glds16(src + 256 * k, dst + 1024u * (uint32_t)k);
+  }
+}
+
+// rows of sub-slab (J, half) this wave converts that exist in the utterance (the others are
+// clamped duplicates: their tile rows are left stale and masked out)
+template <class S>
+__device__ __forceinline__ int live_rows(const Job& J, int half, int w) {
+  const int t0 = J.c * DAD_SLAB + half * kSub + S::RPW * w;
+  const int n = J.T - t0;
+  return n < 0 ? 0 : (n > S::RPW ? S::RPW : n);
+}
+
+// Convert the wave's rows of sub-slab (J, HALF): raw stage -> bf16 tile; STRONG also stores
+// the bf16 row to HBM for the weight gradient.  Straight-line code per KIND (one basic block,
+// so the 3*RPW independent RNG chains interleave): rows past the utterance are converted as
+// copies of its last row (identical bytes to the same xs address), temporally masked rows
+// are selected to zero after the RNG.  Noise comes pre-scaled (dad_normal_pair_c).
+template <class S, int NOISE, int KIND, int HALF>
+__device__ __forceinline__ void ws_convert(const Ctx& C, const Job& J, int w, int lane_, const float* raw, char* tile,
+                                           const float* fk) {
+  constexpr bool strong = KIND == KIND_STRONG;
+  const int lane = opaque(lane_);
+  const int st = (strong && C.mask_len > 0) ? tstart_of<NOISE>(C, J.b) : -(1 << 30);
+  const uint32_t key = strong ? C.key_strong : C.key_weak;
+  const float sd = strong ? C.sstd : C.wstd;
+  const float cscale = DAD_NEG2LN2 * sd * sd;
+  const float* nsrc = strong ? C.ns : C.nw;
+#pragma unroll
+  for (int i = 0; i < S::RPW; ++i) {
+    const int r = S::RPW * w + i;                               // row within the sub-slab (w uniform)
+    const int t = min(J.c * DAD_SLAB + HALF * kSub + r, J.T - 1);
+    const long grow = J.row0 + t;
+    const bool tzero = t >= st && t < st + C.mask_len;          // I/utils.py:365-372 (padded Tmax)
+    const float* rrow = raw + r * DAD_D + 4 * lane;
+    char* trow = tile + r * kTileRow + 16 * ((lane >> 1) ^ (r & 15)) + 8 * (lane & 1);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int d = 256 * k + 4 * lane;
+      f32x4 v = *reinterpret_cast<const f32x4*>(rrow + 256 * k);
+      if constexpr (KIND != KIND_CLEAN) {
+        f32x4 n;
+        if constexpr (NOISE) {
+          n = *reinterpret_cast<const f32x4*>(nsrc + (size_t)grow * DAD_D + d);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) n[e] *= sd;
+        } else {
+          const uint32_t p = ((uint32_t)grow * (uint32_t)DAD_D + (uint32_t)d) >> 1;
+          float z0, z1, z2, z3;
+          dad_normal_pair_c(key, p, cscale, z0, z1);
+          dad_normal_pair_c(key, p + 1u, cscale, z2, z3);
+          n = f32x4{z0, z1, z2, z3};
+        }
+        // reference op order: x + std*N, then * feature mask, then temporal zero
+        // (I/utils.py:330,338-344,365-372)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = v[e] + n[e];
+        if constexpr (strong) {
+          const f32x4 kp = *reinterpret_cast<const f32x4*>(fk + d);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = tzero ? 0.0f : v[e] * kp[e];
+        }
+      }
+      bf16x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (__bf16)v[e];
+      *reinterpret_cast<bf16x4*>(trow + 512 * k) = o;         // chunk 32k + (lane>>1), swizzled by row
+      if constexpr (strong) *reinterpret_cast<bf16x4*>(C.xs + (size_t)grow * DAD_D + d) = o;
+      // one unit (4 elements, 2 Box-Muller pairs) per scheduling region: the wave's partner on
+      // the SIMD covers its dependent latency, and nothing is hoisted across units
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
+// One MFMA against a resident W1 fragment, as inline asm so the fragment is read in place as
+// the B operand (the compiler otherwise parks W1 in the accumulator file and copies 4
+// registers back per MFMA).  AGPR-resident fragments: "a"; VGPR-resident: "v".  The first
+// k-step takes C = 0; a chain on one accumulator needs no wait states.
+template <bool AGPR, bool FIRST>
+__device__ __forceinline__ void mfma1(f32x4& acc, const bf16x8& xa, const bf16x8& wfr) {
+  if constexpr (AGPR) {
+    if constexpr (FIRST) asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(acc) : "v"(xa), "a"(wfr));
+    else asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(xa), "a"(wfr));
+  } else {
+    if constexpr (FIRST) asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(acc) : "v"(xa), "v"(wfr));
+    else asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(xa), "v"(wfr));
+  }
+}
+
+// A fragment of k-step KS: rows lane&15, k = 32KS + 8(lane>>4) .. +7.  The XOR swizzle only
+// touches the low 4 bits of the chunk index, so chunk (4KS + g) ^ row = 16(KS>>2) +
+// ((4(KS&3) + g) ^ row): four per-lane offsets aoff[KS&3] plus an immediate 256(KS>>2).
+template <int KS>
+__device__ __forceinline__ bf16x8 afrag(const char* tile, const int (&aoff)[4]) {
+  return *reinterpret_cast<const bf16x8*>(tile + aoff[KS & 3] + 256 * (KS >> 2));
+}
+
+// acc[t] = x_tile(16 rows) . W1[hw + 16t .. +15]^T over K = 768, the next k-step's A fragment
+// read while the current one's MFMAs issue.
+template <class S, int KS>
+__device__ __forceinline__ void ws_mfma_from(const char* tile, const int (&aoff)[4], const bf16x8 (&wf)[S::NT][kKS],
+                                             f32x4 (&acc)[S::NT], bf16x8 xa) {
+  if constexpr (KS < kKS) {
+    bf16x8 xn;
+    if constexpr (KS + 1 < kKS) xn = afrag<KS + 1>(tile, aoff);
+#pragma unroll
+    for (int t = 0; t < S::NT; ++t) {
+      const bool agpr = S::AGPR_W && (t < 2 || (t == 2 && KS < 16));
+      if (agpr) mfma1<true, KS == 0>(acc[t], xa, wf[t][KS]);
+      else mfma1<false, KS == 0>(acc[t], xa, wf[t][KS]);
+    }
+    if constexpr (KS + 1 < kKS) ws_mfma_from<S, KS + 1>(tile, aoff, wf, acc, xn);
+  }
+}
+template <class S>
+__device__ __forceinline__ void ws_mfma(const char* tile, const int (&aoff)[4], const bf16x8 (&wf)[S::NT][kKS],
+                                        f32x4 (&acc)[S::NT]) {
+  ws_mfma_from<S, 0>(tile, aoff, wf, acc, afrag<0>(tile, aoff));
+  // MFMA D -> VALU readers of the epilogue (hipcc pads nothing after an asm MFMA)
+  if constexpr (S::NT == 4) asm volatile("s_nop 7\n\ts_nop 7" ::"v"(acc[0]), "v"(acc[1]), "v"(acc[2]), "v"(acc[3]));
+  else asm volatile("s_nop 7\n\ts_nop 7" ::"v"(acc[0]), "v"(acc[1]));
+}
+
+// lane L of x := uniform v (v_writelane_b32; hipcc has no builtin for it)
+template <int L>
+__device__ __forceinline__ void writelane(uint32_t& x, uint32_t v) {
+  asm("v_writelane_b32 %0, %1, %2" : "+v"(x) : "s"(v), "i"(L));
+}
+
+// sum over the 4 row groups (lane >> 4) of a 16x16 C tile column: v_permlane32_swap and
+// v_permlane16_swap (gfx950) with both operands = x give [x_lo, x_lo] + [x_hi, x_hi]
+__device__ __forceinline__ float rowgroup_sum(float x) {
+  const uint32_t xi = __float_as_uint(x);
+  const auto a = __builtin_amdgcn_permlane32_swap(xi, xi, false, false);
+  const float s1 = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const uint32_t si = __float_as_uint(s1);
+  const auto b = __builtin_amdgcn_permlane16_swap(si, si, false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
+// rows r, 4+r, 8+r, 12+r of the sub-slab from the ballots of register r: row 4g + r takes
+// 16-bit field g of ballot (t, r) for tile t.  Pairs of fields pack with s_pack_{ll,hh}_b32_b16
+// on the scalar unit; each row's word lands in lane rho by v_writelane.
+template <class S, int R>
+__device__ __forceinline__ void bits_words(const uint64_t (&bal)[S::NT][4], uint32_t& my0, uint32_t& my1) {
+  if constexpr (R < 4) {
+    const uint32_t a_lo = (uint32_t)bal[0][R], a_hi = (uint32_t)(bal[0][R] >> 32);
+    const uint32_t b_lo = (uint32_t)bal[1][R], b_hi = (uint32_t)(bal[1][R] >> 32);
+    writelane<R>(my0, (a_lo & 0xffffu) | (b_lo << 16));
+    writelane<4 + R>(my0, (a_lo >> 16) | (b_lo & 0xffff0000u));
+    writelane<8 + R>(my0, (a_hi & 0xffffu) | (b_hi << 16));
+    writelane<12 + R>(my0, (a_hi >> 16) | (b_hi & 0xffff0000u));
+    if constexpr (S::NT == 4) {
+      const uint32_t c_lo = (uint32_t)bal[2][R], c_hi = (uint32_t)(bal[2][R] >> 32);
+      const uint32_t d_lo = (uint32_t)bal[3][R], d_hi = (uint32_t)(bal[3][R] >> 32);
+      writelane<R>(my1, (c_lo & 0xffffu) | (d_lo << 16));
+      writelane<4 + R>(my1, (c_lo >> 16) | (d_lo & 0xffff0000u));
+      writelane<8 + R>(my1, (c_hi & 0xffffu) | (d_hi << 16));
+      writelane<12 + R>(my1, (c_hi >> 16) | (d_hi & 0xffff0000u));
+    }
+    bits_words<S, R + 1>(bal, my0, my1);
+  }
+}
+
+// bias + ReLU + valid mask of one sub-slab.  Per-lane partial sums/counts (4 rows of the C
+// tile) accumulate over the job's two sub-slabs and are reduced across the 4 row groups only
+// at the job's end (HALF 1).  Student: the ReLU'-and-valid bits of the 16 rows.
+// Stores: student 1 (bits) + 2 at HALF 1 (sums, counts); teacher 1 at HALF 1 (sums).
+template <class S, bool TEACHER, int HALF>
+__device__ __forceinline__ void ws_epilogue(const Ctx& C, const Job& J, int w, int lane, uint32_t vmask,
+                                            const float (&bh)[S::NT], const f32x4 (&acc)[S::NT], float (&ssum)[S::NT],
+                                            float (&scnt)[S::NT]) {
+  const int g = lane >> 4;
+  uint64_t bal[S::NT][4];
+#pragma unroll
+  for (int t = 0; t < S::NT; ++t) {
+    float s = 0.0f, n = 0.0f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const bool v = (vmask >> (4 * g + r)) & 1u;     // C/D layout: row = 4(lane>>4) + r, col = lane&15
+      const float pre = acc[t][r] + bh[t];
+      const bool act = v && pre > 0.0f;
+      s += act ? pre : 0.0f;
+      if constexpr (!TEACHER) {
+        n += act ? 1.0f : 0.0f;
+        bal[t][r] = __ballot(act);
+      }
+    }
+    ssum[t] = HALF ? ssum[t] + s : s;
+    if constexpr (!TEACHER) scnt[t] = HALF ? scnt[t] + n : n;
+  }
+  const int hw = S::HW * w;
+  if constexpr (!TEACHER) {
+    // row rho = 4g + r of the sub-slab: its bits of h = hw + 16t + col are field g of ballot
+    // (t, r).  Words are assembled from the (uniform) ballots on the scalar unit and dropped
+    // into lane rho with v_writelane -- no per-lane select of a ballot (which hipcc lowers to
+    // a scratch array).
+    uint32_t my0 = 0, my1 = 0;
+    bits_words<S, 0>(bal, my0, my1);
+    uint32_t* dst = C.bits + (size_t)(J.bits_row + HALF * kSub + (lane & 15)) * DAD_HT;
+    if constexpr (S::NT == 4) {
+      if (lane < 16) *reinterpret_cast<uint2*>(dst + 2 * w) = uint2{my0, my1};
+    } else {
+      if (lane < 16) dst[w] = my0;
+    }
+  }
+  if constexpr (HALF == 1) {
+    const int t = lane >> 4;                           // h = hw + lane (lanes < HW)
+    float sv = 0.0f, cv = 0.0f;
+#pragma unroll
+    for (int k = 0; k < S::NT; ++k) {
+      const float a = rowgroup_sum(ssum[k]);
+      sv = t == k ? a : sv;
+      if constexpr (!TEACHER) {
+        const float c = rowgroup_sum(scnt[k]);
+        cv = t == k ? c : cv;
+      }
+    }
+    if (lane < S::HW) {
+      C.part_sum[(size_t)J.sum_slab * DAD_H + hw + lane] = sv;
+      if constexpr (!TEACHER) C.part_cnt[(size_t)J.cnt_slab * DAD_H + hw + lane] = cv;
+    }
+  }
+}
+
+
+// VMEM instructions one wave issues per sub-slab (the counted vmcnt waits depend on them)
+template <class S>
+__device__ __forceinline__ constexpr int n_xs(int kind) { return kind == KIND_STRONG ? S::kXsRow * S::RPW : 0; }
+template <bool TEACHER, int HALF>
+__device__ __forceinline__ constexpr int n_epi() { return TEACHER ? HALF : 1 + 2 * HALF; }
+
+template <int N>
+__device__ __forceinline__ void wait_vm_sw(int n) {
+  // n in {0, 1, 3} + {0, 12 (xs)} + {0, kDma}: the handful of counts the pipeline produces
+  switch (n) {
+    case 0: wait_vm<0>(); break;     case 1: wait_vm<1>(); break;     case 3: wait_vm<3>(); break;
+    case N: wait_vm<N>(); break;     case N + 1: wait_vm<N + 1>(); break; case N + 3: wait_vm<N + 3>(); break;
+    case 2 * N: wait_vm<2 * N>(); break; case 2 * N + 1: wait_vm<2 * N + 1>(); break;
+    case 2 * N + 3: wait_vm<2 * N + 3>(); break;
+    default: wait_vm<0>(); break;
+  }
+}
+
+}  // namespace
+
+template <int WAVES, int NOISE, bool TEACHER>
+__device__ __forceinline__ void ws_loop(const Ctx& C, const int j0, const int Q, const int w, const int lane,
+                                        char* smem, const uint32_t sbase, const bf16x8 (&wf)[16 / WAVES][kKS],
+                                        const float (&bh)[16 / WAVES], const float* fk, const uint32_t* vb) {
+  using S = Shape<WAVES>;
+  float ssum[S::NT], scnt[S::NT];
+  const float* raw0 = reinterpret_cast<const float*>(smem + kOffRaw);
+  const float* raw1 = reinterpret_cast<const float*>(smem + kOffRaw + kRawStage);
+  char* tile0 = smem + kOffTile;
+  char* tile1 = smem + kOffTile + kTile;
+  auto jobq = [&](int q) { return job_of(C, TEACHER, j0 + (q >> 1)); };
+  auto dma = [&](int q) {
+    if (q < Q) {
+      const Job J = jobq(q);
+      dma_rows<S>(J.kind == KIND_CLEAN ? C.xc : C.xn, J, q & 1, w, sbase + kOffRaw + (q & 1) * kRawStage, lane);
+    }
+  };
+  // convert sub-slab q (its half HN is a template parameter: raw stage and tile HN)
+  auto convert = [&](auto hn_tag, const Job& J) {
+    constexpr int HN = decltype(hn_tag)::value;
+    const float* rawp = HN ? raw1 : raw0;
+    char* tl = HN ? tile1 : tile0;
+    if constexpr (TEACHER) ws_convert<S, NOISE, KIND_WEAK, HN>(C, J, w, lane, rawp, tl, fk);
+    else if (J.kind == KIND_CLEAN) ws_convert<S, NOISE, KIND_CLEAN, HN>(C, J, w, lane, rawp, tl, fk);
+    else ws_convert<S, NOISE, KIND_STRONG, HN>(C, J, w, lane, rawp, tl, fk);
+  };
+  // sub-slab q (half H): MFMA on tile H, convert sub-slab q+1 (half 1-H), epilogue, DMA q+3
+  auto iter = [&](auto h_tag, int q) {
+    constexpr int H = decltype(h_tag)::value;
+    f32x4 acc[S::NT];
+    int aoff[4];
+    {
+      const int ln = opaque(lane);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) aoff[m] = (ln & 15) * kTileRow + 16 * ((4 * m + (ln >> 4)) ^ (ln & 15));
+    }
+    unsigned long long c0 = WS_CLK(), c1 = c0, c2 = c0;
+    if (q + 1 < Q) {
+      const Job Jn = jobq(q + 1);
+      // this wave's DMA of sub-slab q+1 (issued at the end of iteration q-2) has landed once at
+      // most these younger VMEM ops remain: xs stores of convert(q), epilogue(q-1), DMA(q+2)
+      wait_vm_sw<S::kDma>(n_xs<S>(jobq(q).kind) + (q > 0 ? n_epi<TEACHER, 1 - H>() : 0) +
+                          (q + 2 < Q ? S::kDma : 0));
+      c1 = WS_CLK();
+      // The two waves sharing a SIMD (w and w + WAVES/2) run the two halves in opposite
+      // order, so one's MFMA chain overlaps the other's RNG/convert VALU work between barriers.
+      if (S::STAGGER && w >= WAVES / 2) {
+        convert(std::integral_constant<int, 1 - H>{}, Jn);
+        c2 = WS_CLK();
+        ws_mfma<S>(H ? tile1 : tile0, aoff, wf, acc);
+      } else {
+        ws_mfma<S>(H ? tile1 : tile0, aoff, wf, acc);
+#ifdef DAD_PROBE_STAMPS
+        asm volatile("s_nop 0" ::"v"(acc[0]), "v"(acc[S::NT - 1]));
+#endif
+        c2 = WS_CLK();
+        convert(std::integral_constant<int, 1 - H>{}, Jn);
+      }
+    } else {
+      ws_mfma<S>(H ? tile1 : tile0, aoff, wf, acc);
+    }
+    const unsigned long long c3 = WS_CLK();
+    const uint32_t vmask = (vb[q >> 1] >> (16 * H)) & 0xffffu;
+    ws_epilogue<S, TEACHER, H>(C, jobq(q), w, lane, vmask, bh, acc, ssum, scnt);
+    const unsigned long long c4 = WS_CLK();
+    dma(q + 3);
+    const unsigned long long c5 = WS_CLK();
+    lds_barrier();
+#ifdef DAD_PROBE_STAMPS
+    const unsigned long long c6 = WS_CLK();
+    if (threadIdx.x == 0 && blockIdx.x < 4096) {
+      unsigned long long* g = g_ws_stamps + blockIdx.x * 10;
+      g[4] += c1 - c0; g[5] += c2 - c1; g[6] += c3 - c2; g[7] += c4 - c3; g[8] += c5 - c4; g[9] += c6 - c5;
+    }
+#else
+    (void)c0; (void)c1; (void)c2; (void)c3; (void)c4; (void)c5;
+#endif
+  };
+  dma(0);
+  dma(1);
+  wait_vm_sw<S::kDma>(Q > 1 ? S::kDma : 0);   // sub-slab 0 landed
+  convert(std::integral_constant<int, 0>{}, jobq(0));
+  dma(2);
+  lds_barrier();
+  for (int q = 0; q < Q; q += 2) {   // Q is even: a job is two sub-slabs
+    iter(std::integral_constant<int, 0>{}, q);
+    iter(std::integral_constant<int, 1>{}, q + 1);
+  }
+  wait_vm<0>();
+}
+
+// NOISE: 0 = counter RNG, 1 = explicit noise tensors (parity mode)
+template <int WAVES, int NOISE>
+__device__ __forceinline__ void encode_ws_body(const DadEncodeArgs& a, char* smem) {
+  using S = Shape<WAVES>;
+  WS_STAMP(0, wall_clock64());
+#ifdef DAD_PROBE_STAMPS
+  if (threadIdx.x == 0 && blockIdx.x < 4096)
+    for (int k = 4; k < 10; ++k) g_ws_stamps[blockIdx.x * 10 + k] = 0;
+#endif
+  const Ctx C = ctx_of(a);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  bool teacher;
+  int j0, j1;
+  job_range(C, blockIdx.x, a.ws_nt, a.ws_ns, a.ws_wstrong, teacher, j0, j1);
+  const int nj = j1 - j0;
+  if (nj <= 0) return;
+  const uint32_t sbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;   // LDS byte address
+
+  // ---- prologue: feature keep flags, valid bits of every job, resident W1, bias
+  float* fk = reinterpret_cast<float*>(smem + kOffFK);
+  uint32_t* vb = reinterpret_cast<uint32_t*>(smem + kOffVB);
+  if (!teacher)
+    for (int d = tid; d < DAD_D; d += S::kThreads) {
+      const float u = C.u ? C.u[d] : dad_uniform_at(C.key_feat, (uint32_t)d);
+      fk[d] = u > C.feat_p ? 1.0f : 0.0f;     // I/utils.py:343 (rand(D) > p)
+    }
+  for (int p = tid; p < nj * DAD_SLAB; p += S::kThreads) {
+    const Job J = job_of(C, teacher, j0 + p / DAD_SLAB);
+    const int t = J.c * DAD_SLAB + (p & (DAD_SLAB - 1));
+    const uint8_t* pad = J.kind == KIND_CLEAN ? C.mc : C.mn;
+    const bool v = t < J.T && pad[J.row0 + t] == 0;
+    const uint64_t bal = __ballot(v);
+    if ((lane & 31) == 0) vb[p / DAD_SLAB] = (uint32_t)(bal >> (lane & 32));
+  }
+  asm volatile("" ::: "memory");   // the pad/u loads above retire before W1 is requested
+  const bf16x8* W = reinterpret_cast<const bf16x8*>(teacher ? a.w1bf_teacher : a.w1bf_student);
+  const float* bias = teacher ? a.b1_teacher : a.b1_student;
+  const int hw = S::HW * w;
+  bf16x8 wf[S::NT][kKS];           // fragment-major shadow (dad_w1frag_index): 1 KB coalesced loads
+#pragma unroll
+  for (int t = 0; t < S::NT; ++t)
+#pragma unroll
+    for (int ks = 0; ks < kKS; ++ks) wf[t][ks] = W[(size_t)(((hw >> 4) + t) * kKS + ks) * 64 + lane];
+  float bh[S::NT];
+#pragma unroll
+  for (int t = 0; t < S::NT; ++t) bh[t] = bias[hw + 16 * t + (lane & 15)];
+  __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): W1 and bias resident (a wait the compiler sees)
+  lds_barrier();                        // fk / vb visible (no DMA in flight yet)
+  WS_STAMP(1, wall_clock64());
+  if (teacher) ws_loop<WAVES, NOISE, true>(C, j0, 2 * nj, w, lane, smem, sbase, wf, bh, fk, vb);
+  else ws_loop<WAVES, NOISE, false>(C, j0, 2 * nj, w, lane, smem, sbase, wf, bh, fk, vb);
+  WS_STAMP(2, wall_clock64());
+  WS_STAMP(3, ((unsigned long long)teacher << 16) | (unsigned long long)(2 * nj));
+}
+
+
+// Counter-RNG (throughput) and explicit-noise (parity) kernels are separate so the noise
+// loads do not share the register allocation of the throughput kernel.
+__global__ __launch_bounds__(DAD_ENC_WS_THREADS, 1) void dad_encode_ws(DadEncodeArgs a) {
+  DAD_GUARD_BLOCK(DAD_ENC_WS_THREADS);
+  __shared__ __attribute__((aligned(16))) char smem[kLds];
+  encode_ws_body<DAD_ENC_WS_THREADS / 64, 0>(a, smem);
+}
+
+__global__ __launch_bounds__(DAD_ENC_WS_THREADS, 1) void dad_encode_ws_explicit(DadEncodeArgs a) {
+  DAD_GUARD_BLOCK(DAD_ENC_WS_THREADS);
+  __shared__ __attribute__((aligned(16))) char smem[kLds];
+  encode_ws_body<DAD_ENC_WS_THREADS / 64, 1>(a, smem);
+}

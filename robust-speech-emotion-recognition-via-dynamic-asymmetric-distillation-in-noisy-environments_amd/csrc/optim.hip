@@ -64,8 +64,9 @@ __device__ __forceinline__ void adam_ema_update(const dad_config& cfg, float coe
       teacher[i] = t;
     }
     if (i < (size_t)DAD_H * DAD_D) {
-      w1bf_s[i] = (__bf16)p;
-      w1bf_t[i] = (__bf16)t;
+      const uint32_t f = dad_w1frag_index((uint32_t)(i / DAD_D), (uint32_t)(i % DAD_D));
+      w1bf_s[f] = (__bf16)p;
+      w1bf_t[f] = (__bf16)t;
     }
   }
 }
@@ -121,8 +122,9 @@ __global__ __launch_bounds__(256) void dad_shadow_kernel(const float* student, c
                                                          __bf16* wt) {
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (i < (size_t)DAD_H * DAD_D) {
-    ws[i] = (__bf16)student[i];
-    wt[i] = (__bf16)teacher[i];
+    const uint32_t f = dad_w1frag_index((uint32_t)(i / DAD_D), (uint32_t)(i % DAD_D));
+    ws[f] = (__bf16)student[i];
+    wt[f] = (__bf16)teacher[i];
   }
 }
 

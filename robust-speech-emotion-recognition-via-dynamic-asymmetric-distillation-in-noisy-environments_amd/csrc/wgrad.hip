@@ -20,13 +20,6 @@
 
 namespace {
 
-__device__ __forceinline__ float wg_normal1(uint32_t key, uint32_t idx) {
-  float z0, z1;
-  const uint32_t base = idx & ~1u;
-  dad_box_muller(dad_rng32(base, key), dad_rng32(base | 1u, key), z0, z1);
-  return (idx & 1u) ? z1 : z0;
-}
-
 __device__ __forceinline__ int wg_tstart(const DadWgradArgs& a, int b) {
   if (a.start) return (int)a.start[b];
   const uint32_t h = dad_rng32((uint32_t)b, a.key_tstart);
@@ -125,7 +118,7 @@ __global__ __launch_bounds__(DAD_WGRAD_THREADS) void dad_wgrad_f32(DadWgradArgs 
       const size_t grow = q.row0 + (tin ? t : 0);
       float x = tin ? X[grow * DAD_D + d] : 0.0f;
       if (q.br && tin) {
-        const float n = a.ns ? a.ns[grow * DAD_D + d] : wg_normal1(a.key_strong, (uint32_t)(grow * DAD_D + d));
+        const float n = a.ns ? a.ns[grow * DAD_D + d] : dad_normal1(a.key_strong, (uint32_t)(grow * DAD_D + d));
         const float sn = n * a.strong_std;
         x = (x + sn) * fkeep;
         if (a.mask_len > 0 && t >= st && t < st + a.mask_len) x = 0.0f;

@@ -1,0 +1,83 @@
+"""BF16 throughput mode (the W-stationary encoder, csrc/encode_ws.hip) against FP32.
+
+Two references:
+  * the NumPy oracle with the reference's injected draws (rng='explicit'), on the edge
+    geometries of test_gpu_parity (ragged lengths, slab-boundary crossings, Bc != Bn,
+    Tc != Tn, warm-up and post-warm-up) -- checks the augmentation, the encoder, the
+    pooling and the slab bookkeeping of the bf16 path;
+  * the FP32 parity-mode kernels driven by the SAME counter RNG (rng='counter') -- the
+    benchmark's configuration, including the in-kernel noise, feature mask and temporal
+    mask, at the bench geometry B=64, T=300.
+Tolerance: bf16 operands with fp32 accumulation -> embeddings/logits within 2e-2 of the
+tensor max; gradient direction cosine > 0.99 whenever the discrete DACP mask agrees.
+"""
+import numpy as np
+import pytest
+
+import gpu_harness as gh
+from oracle import dad_oracle, synth
+from test_gpu_parity import EDGE, _problem
+
+pytestmark = pytest.mark.gpu
+BF16_TOL = 2e-2
+
+
+def _grad_cos(g1, g2):
+    a = np.concatenate([x.reshape(-1) for x in g1]).astype(np.float64)
+    b = np.concatenate([x.reshape(-1) for x in g2]).astype(np.float64)
+    return float(a @ b / max(1e-30, np.linalg.norm(a) * np.linalg.norm(b)))
+
+
+@pytest.mark.parametrize("geom", EDGE, ids=lambda g: "B%dT%d_Bn%dTn%d" % (g["B"], g["T"], g["Bn"], g["Tn"]))
+def test_bf16_step_edge_geometries_vs_oracle(geom):
+    cfg = dad_oracle.make_cfg("iemocap")
+    g = dict(geom)
+    ragged = g.pop("ragged", True)
+    inp = _problem(ragged=ragged, **g)
+    st = synth.make_state(3, 1)
+    step = gh.make_step(cfg, precision="bf16")
+    orc = dad_oracle.DADOracle(*synth.init_weights(3)[:4], cfg)
+    for epoch in (0, 60):
+        gh.load_state(step, st)
+        orc.load_state(st)
+        o = gh.run_step(step, inp, epoch)
+        r = orc.step(inp, epoch)
+        gh.close(o["e_clean"], r["e_clean"], BF16_TOL, "%s e%d e_clean" % (geom, epoch))
+        gh.close(o["z_clean"], r["z_clean"], BF16_TOL, "%s e%d z_clean" % (geom, epoch))
+        if epoch >= 30:
+            gh.close(o["e_teacher"], r["e_teacher"], BF16_TOL, "%s e_teacher" % (geom,))
+            gh.close(o["e_strong"], r["e_strong"], BF16_TOL, "%s e_strong" % (geom,))
+            gh.close(o["z_strong"], r["z_strong"], BF16_TOL, "%s z_strong" % (geom,))
+        if epoch < 30 or np.array_equal(o["mask"], r["mask"]):
+            assert _grad_cos(o["grads"], r["grads"]) > 0.99, (geom, epoch)
+
+
+@pytest.mark.parametrize("B,T", [(16, 100), (64, 300)])
+def test_bf16_counter_rng_matches_fp32_counter_rng(B, T):
+    """Same seed -> same in-kernel noise, feature mask, temporal mask and dropout in both modes."""
+    cfg = dad_oracle.make_cfg("iemocap")
+    inp = _problem(B=B, T=T, seed=4, ragged=True)
+    st = synth.make_state(4, 1)
+    outs = []
+    for prec in ("fp32", "bf16"):
+        step = gh.make_step(cfg, precision=prec, rng="counter", seed=77)
+        gh.load_state(step, st)
+        outs.append(gh.run_step(step, inp, 60, with_draws=False))
+    f, b = outs
+    for k in ("e_clean", "e_teacher", "e_strong", "z_clean", "z_teacher", "z_strong"):
+        gh.close(b[k], f[k], BF16_TOL, "counter %s B%d T%d" % (k, B, T))
+    if np.array_equal(b["mask"], f["mask"]):
+        assert _grad_cos(b["grads"], f["grads"]) > 0.99
+    for k in ("total_loss", "supervised_ce_loss", "consistency_loss", "ecda_loss"):
+        assert np.isfinite(b[k])
+
+
+def test_bf16_counter_steps_stay_finite():
+    cfg = dad_oracle.make_cfg("iemocap")
+    step = gh.make_step(cfg, precision="bf16", rng="counter", seed=3)
+    gh.load_state(step, synth.make_state(6, 1))
+    for k in range(4):
+        inp = _problem(B=24, T=70, seed=10 + k, Bn=20, Tn=90)
+        o = gh.run_step(step, inp, 40 + k, with_draws=False)
+        assert all(np.isfinite(o[n]) for n in ("total_loss", "supervised_ce_loss", "consistency_loss", "ecda_loss"))
+        assert all(np.all(np.isfinite(p)) for p in o["student"])

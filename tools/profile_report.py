@@ -71,9 +71,10 @@ def main():
     title, dst = sys.argv[1], sys.argv[2]
     prof = sys.argv[3] if len(sys.argv) > 3 else "gpurun_out/prof"
     pmc_dir = sys.argv[4] if len(sys.argv) > 4 else "gpurun_out/pmc"
-    out = ["# " + title, "", "## Kernel durations (rocprofv3 --kernel-trace --stats)", ""]
-    out += kernel_stats(prof)
-    tl = timeline(prof)
+    out = ["# " + title, ""]
+    if os.path.isdir(prof):
+        out += ["## Kernel durations (rocprofv3 --kernel-trace --stats)", ""] + kernel_stats(prof)
+    tl = timeline(prof) if os.path.isdir(prof) else []
     if tl:
         out += ["", "## Last profiled step: kernel timeline", ""] + tl
     if os.path.isdir(pmc_dir):
