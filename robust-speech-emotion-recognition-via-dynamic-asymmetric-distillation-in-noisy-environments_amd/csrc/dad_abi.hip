@@ -179,6 +179,8 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   float* ge_ecda = ws_ptr<float>(workspace, L.ge_ecda);
   float* normpart = ws_ptr<float>(workspace, L.normpart);
   float* ecda_scratch = ws_ptr<float>(workspace, L.ecda);
+  float* gzb = ws_ptr<float>(workspace, L.gzb);
+  uint32_t* eflag = ws_ptr<uint32_t>(workspace, L.eflag);
   __bf16* xs_bf16 = ws_ptr<__bf16>(workspace, L.xs_bf16);
   const bool bf16 = cfg->precision == DAD_PREC_BF16;
 
@@ -266,6 +268,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   if (explicit_rng) { ta.keep1 = bt->keep1; ta.keep2 = bt->keep2; }
   ta.key_drop1 = k.drop1; ta.key_drop2 = k.drop2;
   ta.dacp = st->dacp; ta.tailf = st->tail; ta.ge = ge; ta.ge_ecda = ge_ecda; ta.grad = st->grad;
+  ta.gzb = gzb; ta.eflag = eflag;
   hipLaunchKernelGGL(dad_tail, dim3(1), dim3(DAD_TAIL_THREADS), 0, stream, ta);
   DAD_TRY(hipGetLastError());
 
@@ -274,7 +277,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
     DadEcdaArgs ca;
     memset(&ca, 0, sizeof(ca));
     ca.cfg = *cfg; ca.yc = bt->yc; ca.emb = st->emb; ca.tailf = st->tail;
-    ca.tail_terms = st->tail + DAD_T_ECDA_TERM; ca.ge = ge_ecda; ca.scratch = ecda_scratch;
+    ca.tail_terms = st->tail + DAD_T_ECDA_TERM; ca.ge = ge_ecda; ca.scratch = ecda_scratch; ca.eflag = eflag;
     hipLaunchKernelGGL(dad_ecda, dim3(DAD_C), dim3(DAD_ECDA_THREADS), 0, stream, ca);
     DAD_TRY(hipGetLastError());
   }
@@ -287,6 +290,9 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   ra.want_norm = cfg->dp_world == 1;
   ra.w_kl = cfg->w_kl; ra.w_ecda = cfg->w_ecda;
   ra.wpart = sbuf; ra.wpart_bf16 = wa.wpart_bf16; ra.ge_ecda = ge_ecda;
+  ra.gzb = gzb; ra.eflag = eflag; ra.student = st->student; ra.emb = st->emb;
+  if (explicit_rng) { ra.keep1 = bt->keep1; ra.keep2 = bt->keep2; }
+  ra.key_drop1 = k.drop1; ra.key_drop2 = k.drop2; ra.p_drop = cfg->p_drop; ra.drop_scale = cfg->drop_scale;
   ra.ge = ge; ra.vlen = vlen; ra.cnt_tot = cnt_tot; ra.tailf = st->tail;
   ra.grad = st->grad; ra.normpart = normpart;
   hipLaunchKernelGGL(dad_wsum, dim3(DAD_REDUCE_BLOCKS), dim3(DAD_REDUCE_THREADS), 0, stream, ra);

@@ -119,17 +119,55 @@ __device__ __forceinline__ float dad_uniform_at(uint32_t key, uint32_t idx) {
   return dad_u01(dad_rng32(idx, key));
 }
 
+// classifier dropout keep factor of (utterance b, hidden unit h): nn.Dropout(p) in training
+// mode, inverted scaling (I/model.py:54-64); explicit mask (parity) or counter RNG
+__device__ __forceinline__ float keep_value(const uint8_t* keep, uint32_t key, int b, int h, float p, float scale) {
+  if (p <= 0.0f) return 1.0f;
+  bool k;
+  if (keep) k = keep[(size_t)b * DAD_H + h] != 0;
+  else k = dad_uniform_at(key, (uint32_t)(b * DAD_H + h)) >= p;
+  return k ? scale : 0.0f;
+}
+
+
 // ---------------------------------------------------------------------------------
-// wave helpers (wave64)
+// wave helpers (wave64).  Sums use DPP (row_shr 1/2/4/8 inside each 16-lane row, then
+// row_bcast:15 / row_bcast:31 across rows; lane 63 ends with the total, broadcast by
+// v_readlane): six VALU ops per level-free reduction instead of six LDS-routed shuffles.
+template <int CTRL, int RM = 0xf>
+__device__ __forceinline__ int dad_dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, RM, 0xf, true);
+}
+template <int CTRL, int RM = 0xf>
+__device__ __forceinline__ float dad_dpp_f(float v) {
+  return __int_as_float(dad_dpp_i<CTRL, RM>(__float_as_int(v)));
+}
+template <int CTRL, int RM = 0xf>
+__device__ __forceinline__ double dad_dpp_d(double v) {
+  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  const int lo = dad_dpp_i<CTRL, RM>((int)(uint32_t)u), hi = dad_dpp_i<CTRL, RM>((int)(uint32_t)(u >> 32));
+  return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
+}
 __device__ __forceinline__ float dad_wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += dad_dpp_f<0x111>(v);
+  v += dad_dpp_f<0x112>(v);
+  v += dad_dpp_f<0x114>(v);
+  v += dad_dpp_f<0x118>(v);
+  v += dad_dpp_f<0x142, 0xa>(v);
+  v += dad_dpp_f<0x143, 0xc>(v);
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 __device__ __forceinline__ double dad_wave_sum_d(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += dad_dpp_d<0x111>(v);
+  v += dad_dpp_d<0x112>(v);
+  v += dad_dpp_d<0x114>(v);
+  v += dad_dpp_d<0x118>(v);
+  v += dad_dpp_d<0x142, 0xa>(v);
+  v += dad_dpp_d<0x143, 0xc>(v);
+  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, 63);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), 63);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 __device__ __forceinline__ float dad_wave_max(float v) {
 #pragma unroll
@@ -165,7 +203,9 @@ struct DadWs {
   size_t vlen;       // f32 [Bc + Bn]               valid lengths (clean | noisy)
   size_t cnt_tot;    // f32 [Bc + Bn][H]            active-row counts per utterance (clean | strong)
   size_t ge;         // f32 [Bc + Bn][H]            dL/de_clean | dL/de_strong (CE/KL part)
-  size_t ge_ecda;    // f32 [Bc + Bn][H]            ECDA part of dL/de (valid when the ECDA term is on)
+  size_t ge_ecda;    // f32 [Bc + Bn][H]            ECDA part of dL/de (rows flagged in eflag)
+  size_t gzb;        // f32 [Bc + Bn][C]            dL/dz per utterance (clean | strong), from dad_tail
+  size_t eflag;      // u32 [Bc + Bn]               1: ECDA wrote this row of ge_ecda this step
   size_t wpart;      // f32 [S][H][D]               split-K weight-gradient partial slabs
   size_t normpart;   // f32 [DAD_NORM_BLOCKS]       squared-norm partials
   size_t ecda;       // f32 [C][Bc+Bn][Bc+Bn]       ECDA pairwise scratch for large member sets
@@ -201,6 +241,8 @@ static inline DadWs dad_ws_layout(const DadGeom& g, int splits, int precision, b
   w.cnt_tot = off;  off = dad_align(off + sizeof(float) * nb * DAD_H);
   w.ge = off;       off = dad_align(off + sizeof(float) * nb * DAD_H);
   w.ge_ecda = off;  off = dad_align(off + sizeof(float) * nb * DAD_H);
+  w.gzb = off;      off = dad_align(off + sizeof(float) * nb * DAD_C);
+  w.eflag = off;    off = dad_align(off + sizeof(uint32_t) * nb);
   w.wpart = off;    off = dad_align(off + sizeof(float) * (size_t)splits * DAD_H * DAD_D);
   w.normpart = off; off = dad_align(off + sizeof(float) * DAD_NORM_BLOCKS);
   w.ecda = off;     off = dad_align(off + sizeof(float) * DAD_C * nb * nb);

@@ -8,12 +8,13 @@
 #define DAD_ENC_WS_THREADS 512                               // W-stationary bf16 encoder (8 waves, two per SIMD)
 #define DAD_ENC_WS_MAXJ 256                                  // max 32-row jobs per encoder workgroup
 #define DAD_POOL_THREADS 256
-#define DAD_TAIL_THREADS 1024
+#define DAD_TAIL_THREADS 512
 #define DAD_ECDA_THREADS 512
 #define DAD_WGRAD_THREADS 256
 #define DAD_REDUCE_THREADS 256
 #define DAD_REDUCE_COLS 256                                  // dW1 floats per reduce block
-#define DAD_REDUCE_BLOCKS (DAD_H * DAD_D / DAD_REDUCE_COLS + 1)   // + the db1 block
+#define DAD_REDUCE_XBLK 16                                   // db1 / dW2 / totals blocks (16 hidden units each)
+#define DAD_REDUCE_BLOCKS (DAD_H * DAD_D / DAD_REDUCE_COLS + DAD_REDUCE_XBLK)
 #define DAD_OPTIM_THREADS 256
 #define DAD_GUARD_BLOCK(n) \
   if (blockDim.x != (n) || blockDim.y != 1 || blockDim.z != 1) return
@@ -59,7 +60,9 @@ struct DadTailArgs {
   float* dacp;            // persistent DACP state (read; committed by the optimizer kernel)
   float* tailf;           // per-step outputs (see DAD_TAIL_* in dad.h)
   float* ge;              // [Bc+Bn][H] dL/de (CE/KL part)
-  float* ge_ecda;         // [Bc+Bn][H] zeroed here; ECDA writes its member rows after
+  float* ge_ecda;         // [Bc+Bn][H] modular path only (fused step: ge_ecda rows are flagged)
+  float* gzb;             // [Bc+Bn][C] dL/dz per utterance (clean | strong)
+  uint32_t* eflag;        // [Bc+Bn]    zeroed here; ECDA flags the rows it writes
   float* grad;            // flat grads (W2, b2 written here) + extras
 };
 
@@ -69,7 +72,8 @@ struct DadEcdaArgs {
   const float* emb;
   const float* tailf;
   float* tail_terms;      // per-class loss terms
-  float* ge;              // ECDA part of dL/de: every row written (members: grads, others: 0)
+  float* ge;              // ECDA part of dL/de: member rows written (and flagged in eflag)
+  uint32_t* eflag;
   float* scratch;         // global fallback for large member sets
 };
 
@@ -94,7 +98,14 @@ struct DadReduceArgs {
   float w_kl, w_ecda;
   const float* wpart; const float* ge; const float* vlen; const float* cnt_tot;
   const __bf16* wpart_bf16;   // dad_wsum: bf16 S_u instead of wpart
-  const float* ge_ecda;       // ECDA part of dL/de, added to ge (zeros where ECDA wrote nothing)
+  const float* ge_ecda;       // ECDA part of dL/de, added where eflag is set
+  // fused step: dL/de is not materialised; the classifier part is rebuilt per (utterance, h)
+  // as keep(u,h) * sum_c W2[c][h] gzb[u][c] (nn.Linear + dropout backward, I/model.py:62-63)
+  const float* gzb; const uint32_t* eflag;
+  const float* student; const float* emb;
+  const uint8_t* keep1; const uint8_t* keep2;
+  uint32_t key_drop1, key_drop2;
+  float p_drop, drop_scale;
   const float* tailf;
   float* grad; float* normpart;
 };

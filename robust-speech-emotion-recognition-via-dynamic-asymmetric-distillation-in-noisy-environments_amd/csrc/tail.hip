@@ -20,7 +20,7 @@
 
 #ifdef DAD_PROBE_STAMPS
 // diagnostic build only: ECDA per-class phase wall clocks (100 MHz), 12 slots per class
-__device__ unsigned long long g_ecda_stamps[DAD_C * 12 + 4];   // + tail start/end
+__device__ unsigned long long g_ecda_stamps[DAD_C * 12 + 12];   // + tail phases
 extern "C" int dad_probe_read_ecda_stamps(void* host) {
   return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ecda_stamps), sizeof(g_ecda_stamps), 0, hipMemcpyDeviceToHost);
 }
@@ -64,13 +64,6 @@ __device__ __forceinline__ double block_sum_d(double v, double* red) {
   return s;
 }
 
-__device__ __forceinline__ float keep_value(const uint8_t* keep, uint32_t key, int b, int h, float p, float scale) {
-  if (p <= 0.0f) return 1.0f;
-  bool k;
-  if (keep) k = keep[(size_t)b * DAD_H + h] != 0;
-  else k = dad_uniform_at(key, (uint32_t)(b * DAD_H + h)) >= p;
-  return k ? scale : 0.0f;
-}
 
 // ------------------------------------------------------------------------------ pool
 // blocks [0, Bc): clean utterances; blocks [Bc, Bc+Bn): noisy utterances (teacher + strong)
@@ -149,42 +142,27 @@ __global__ __launch_bounds__(DAD_POOL_THREADS) void dad_pool(DadPoolArgs a) {
 }
 
 // ------------------------------------------------------------------------------ tail
-// classifier backward of one pass for utterances b = qg, qg+4, ...: dL/de (through the
-// dropout) and this thread's dW2 partial.  __restrict__ (turned into no-alias scopes when
-// inlined) lets the loads of a batch of utterances issue before the ge stores of the
-// previous one; eight utterances per batch keep their loads in flight together.
-__device__ __forceinline__ void cls_backward(const float* __restrict__ emb, const uint8_t* __restrict__ keep,
-                                             float* __restrict__ ge, float* __restrict__ ge_ecda,
-                                             const float (*gz)[DAD_C], int n, int qg,
-                                             int h, uint32_t key, float p, float scale, const float (&w2h)[4],
-                                             float (&gw)[4]) {
-  for (int b0 = qg; b0 < n; b0 += 4 * 8) {
-    float ev[8], kv[8];
+// Latency design (one workgroup, ~30 dependent phases): every global input is requested at
+// kernel entry -- logits, labels, the DACP state, W2 and the embedding values of the
+// classifier backward -- so a single memory round trip is paid; the O(B^2) DACP ranks, the
+// per-class epoch statistics and the b2 reduction are spread over the whole block with
+// fixed-order (deterministic) combines instead of serial loops.
+
+// fixed-order block reduction of 4 doubles (one per class), result valid in all threads
+__device__ __forceinline__ void block_sum4_d(double (&v)[4], double (*red)[4]) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int b = b0 + 4 * u;
-      ev[u] = 0.0f;
-      kv[u] = 0.0f;
-      if (b < n) {
-        ev[u] = emb[(size_t)b * DAD_H + h];
-        kv[u] = keep_value(keep, key, b, h, p, scale);
-      }
-    }
+  for (int c = 0; c < 4; ++c) v[c] = dad_wave_sum_d(v[c]);
+  __syncthreads();
+  if (l == 0)
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int b = b0 + 4 * u;
-      if (b < n) {
-        const float d = ev[u] * kv[u];
-        float g = 0.0f;
+    for (int c = 0; c < 4; ++c) red[w][c] = v[c];
+  __syncthreads();
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          gw[c] += gz[b][c] * d;
-          g += w2h[c] * gz[b][c];
-        }
-        ge[(size_t)b * DAD_H + h] = g * kv[u];
-        ge_ecda[(size_t)b * DAD_H + h] = 0.0f;   // ECDA overwrites its member rows afterwards
-      }
-    }
+  for (int c = 0; c < 4; ++c) {
+    double s = 0.0;
+    for (int k = 0; k < TAIL_THREADS / 64; ++k) s += red[k][c];
+    v[c] = s;
   }
 }
 
@@ -196,8 +174,8 @@ __global__ __launch_bounds__(TAIL_THREADS) void dad_tail(DadTailArgs a) {
   const int Bn = cfg.warmup ? 0 : cfg.Bn;    // noisy utterances
   const int tid = threadIdx.x;
   __shared__ double dred[16];
+  __shared__ double dred4[TAIL_THREADS / 64][4];
   __shared__ float fred[16];
-  __shared__ float gwp[4][DAD_C][DAD_H];              // classifier weight-grad partials
   __shared__ float gz[2][DAD_MAX_BATCH][DAD_C];       // dL/dz clean, strong
   __shared__ float sq[DAD_MAX_BATCH][DAD_C];          // teacher probs
   __shared__ float ss[DAD_MAX_BATCH];                 // certainty scores
@@ -206,7 +184,7 @@ __global__ __launch_bounds__(TAIL_THREADS) void dad_tail(DadTailArgs a) {
   __shared__ float srt[DAD_C][DAD_MAX_BATCH];         // per-class sorted scores
   __shared__ int ncls[DAD_C];
   __shared__ float tau_new[DAD_C];
-  __shared__ float sflag[4];
+  __shared__ float dstate[20];                        // DACP state: tau | Q | (sums) | (counts) | anchors
 
   float* tf = a.tailf;
   float* extras = a.grad + DAD_NPARAM;
@@ -215,15 +193,24 @@ __global__ __launch_bounds__(TAIL_THREADS) void dad_tail(DadTailArgs a) {
   const float* z2 = a.logits + (size_t)(B + Bn) * DAD_C;
   const float eps = cfg.ls_eps;
 
+  // ---- every global input up front (one round trip; consumed in this order)
+  f32x4 zc = f32x4{}, zt = f32x4{}, zs = f32x4{};
+  int yb = 0;
+  if (tid < B) { zc = reinterpret_cast<const f32x4*>(z0)[tid]; yb = (int)a.yc[tid]; }
+  if (tid < Bn) { zt = reinterpret_cast<const f32x4*>(z1)[tid]; zs = reinterpret_cast<const f32x4*>(z2)[tid]; }
+  if (tid >= TAIL_THREADS - 20) dstate[tid - (TAIL_THREADS - 20)] = a.dacp[tid - (TAIL_THREADS - 20)];
+
   // ---- supervised CE with label smoothing on the clean logits (I/train.py:364,400)
   double ce_part = 0.0;
   for (int b = tid; b < B; b += TAIL_THREADS) {
     float z[4], m = -INFINITY;
-    for (int c = 0; c < 4; ++c) { z[c] = z0[b * 4 + c]; m = fmaxf(m, z[c]); }
+    if (b == tid) { z[0] = zc[0]; z[1] = zc[1]; z[2] = zc[2]; z[3] = zc[3]; }
+    else for (int c = 0; c < 4; ++c) z[c] = z0[b * 4 + c];
+    for (int c = 0; c < 4; ++c) m = fmaxf(m, z[c]);
     float se = 0.0f;
     for (int c = 0; c < 4; ++c) se += expf(z[c] - m);
     const float lse = m + logf(se);
-    const int y = (int)a.yc[b];
+    const int y = b == tid ? yb : (int)a.yc[b];
     float lsum = 0.0f;
     for (int c = 0; c < 4; ++c) {
       const float ls = z[c] - lse;
@@ -234,6 +221,7 @@ __global__ __launch_bounds__(TAIL_THREADS) void dad_tail(DadTailArgs a) {
     ce_part += -(1.0 - (double)eps) * (double)(z[y] - lse) - (double)eps * 0.25 * (double)lsum;
   }
   const double ce = block_sum_d(ce_part, dred) / (double)B;
+  TAIL_STAMP(2);
 
   float kl = 0.0f, msum = 0.0f;
   int kl_on = 0;
@@ -241,7 +229,9 @@ __global__ __launch_bounds__(TAIL_THREADS) void dad_tail(DadTailArgs a) {
     // ---- teacher probs (I/train.py:409-410) and certainty (I/utils.py:400-428)
     for (int b = tid; b < Bn; b += TAIL_THREADS) {
       float z[4], m = -INFINITY;
-      for (int c = 0; c < 4; ++c) { z[c] = z1[b * 4 + c]; m = fmaxf(m, z[c]); }
+      if (b == tid) { z[0] = zt[0]; z[1] = zt[1]; z[2] = zt[2]; z[3] = zt[3]; }
+      else for (int c = 0; c < 4; ++c) z[c] = z1[b * 4 + c];
+      for (int c = 0; c < 4; ++c) m = fmaxf(m, z[c]);
       float e[4], se = 0.0f;
       for (int c = 0; c < 4; ++c) { e[c] = expf(z[c] - m); se += e[c]; }
       float q[4], mx = -1.0f;
@@ -263,29 +253,39 @@ __global__ __launch_bounds__(TAIL_THREADS) void dad_tail(DadTailArgs a) {
     }
     if (tid < DAD_C) ncls[tid] = 0;
     __syncthreads();
+    TAIL_STAMP(3);
     if (cfg.use_dacp) {
       // ---- DACPManager.calculate_mask (I/utils.py:449-507)
-      const float* Q = a.dacp + 4;
-      const float* tau = a.dacp;
-      const float* anchors = a.dacp + 16;
-      // per-class order statistics: rank of each score inside its pseudo-label class
-      for (int b = tid; b < Bn; b += TAIL_THREADS) {
-        const int c = sp[b];
-        const float s = ss[b];
-        int rank = 0;
-        for (int k = 0; k < Bn; ++k) {
-          if (sp[k] != c) continue;
-          const float o = ss[k];
-          rank += (o < s || (o == s && k < b)) ? 1 : 0;
+      // rank of each score inside its pseudo-label class (ties by index): 16 threads per
+      // utterance, each counting a strided share of the others, combined by a 16-lane sum
+      {
+        const int bb = tid >> 4, part = tid & 15;
+        for (int b0 = 0; b0 < Bn; b0 += TAIL_THREADS / 16) {
+          const int b = b0 + bb;
+          int cnt = 0, c = 0;
+          float sv = 0.0f;
+          if (b < Bn) {
+            c = sp[b];
+            sv = ss[b];
+            for (int k = part; k < Bn; k += 16) {
+              const float o = ss[k];
+              cnt += (sp[k] == c && (o < sv || (o == sv && k < b))) ? 1 : 0;
+            }
+          }
+#pragma unroll
+          for (int o = 8; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 16);
+          if (b < Bn && part == 0) {
+            srt[c][cnt] = sv;
+            atomicAdd(&ncls[c], 1);
+          }
         }
-        srt[c][rank] = s;
-        atomicAdd(&ncls[c], 1);
       }
       __syncthreads();
       if (tid < DAD_C) {
         const int c = tid;
-        const float qmean = (((Q[0] + Q[1]) + Q[2]) + Q[3]) / 4.0f;
-        const float wc = 1.0f / (1.0f + expf(-(cfg.dacp_k * (Q[c] - qmean))));
+        const float* Qs = dstate + 4;
+        const float qmean = (((Qs[0] + Qs[1]) + Qs[2]) + Qs[3]) / 4.0f;
+        const float wc = 1.0f / (1.0f + expf(-(cfg.dacp_k * (Qs[c] - qmean))));
         const int n = ncls[c];
         float that;
         if (n > 0) {
@@ -297,29 +297,35 @@ __global__ __launch_bounds__(TAIL_THREADS) void dad_tail(DadTailArgs a) {
           const float vlo = srt[c][lo], vhi = srt[c][hi];
           that = wgt < 0.5f ? vlo + wgt * (vhi - vlo) : vhi - (vhi - vlo) * (1.0f - wgt);
         } else {
-          that = tau[c];
+          that = dstate[c];
         }
         const float adj = cfg.dacp_lambda * (wc - 0.5f);
-        const float fl = fmaxf(that + adj, anchors[c]);
-        const float tn = cfg.dacp_alpha * tau[c] + cfg.dacp_one_m_alpha * fl;
+        const float fl = fmaxf(that + adj, dstate[16 + c]);
+        const float tn = cfg.dacp_alpha * dstate[c] + cfg.dacp_one_m_alpha * fl;
         tau_new[c] = tn;
         tf[DAD_T_W + c] = wc;
-        tf[DAD_T_TAU_BEFORE + c] = tau[c];
+        tf[DAD_T_TAU_BEFORE + c] = dstate[c];
         tf[DAD_T_TAU_AFTER + c] = tn;
         tf[DAD_T_FLOORED + c] = fl;
         tf[DAD_T_TAU_HAT + c] = that;
         extras[0 + c] = fl;
       }
       __syncthreads();
+      // mask, and the epoch statistics for update_class_quality_scores_epoch
+      // (I/utils.py:503-505): per-class score sums and counts, fixed-order block reduction
       for (int b = tid; b < Bn; b += TAIL_THREADS) sm[b] = ss[b] >= tau_new[sp[b]] ? 1.0f : 0.0f;
-      // epoch statistics for update_class_quality_scores_epoch (I/utils.py:503-505)
+      double st4[4] = {0.0, 0.0, 0.0, 0.0}, ct4[4] = {0.0, 0.0, 0.0, 0.0};
+      for (int b = tid; b < Bn; b += TAIL_THREADS)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          st4[c] += sp[b] == c ? (double)ss[b] : 0.0;
+          ct4[c] += sp[b] == c ? 1.0 : 0.0;
+        }
+      block_sum4_d(st4, dred4);
+      block_sum4_d(ct4, dred4);
       if (tid < DAD_C) {
-        double s = 0.0;
-        int n = 0;
-        for (int b = 0; b < Bn; ++b)
-          if (sp[b] == tid) { s += ss[b]; ++n; }
-        extras[4 + tid] = (float)s;
-        extras[8 + tid] = (float)n;
+        extras[4 + tid] = (float)st4[tid];
+        extras[8 + tid] = (float)ct4[tid];
       }
     } else {
       // fixed threshold (I/train.py:417-420): mask = float(max prob >= thr), weights = ones
@@ -332,6 +338,9 @@ __global__ __launch_bounds__(TAIL_THREADS) void dad_tail(DadTailArgs a) {
       }
     }
     __syncthreads();
+    TAIL_STAMP(4);
+  }
+  if (!cfg.warmup) {
     float mpart = 0.0f;
     for (int b = tid; b < Bn; b += TAIL_THREADS) mpart += sm[b];
     msum = block_sum_f(mpart, fred);
@@ -341,7 +350,9 @@ __global__ __launch_bounds__(TAIL_THREADS) void dad_tail(DadTailArgs a) {
     const float denom = msum + 1e-8f;
     for (int b = tid; b < Bn; b += TAIL_THREADS) {
       float z[4], m = -INFINITY;
-      for (int c = 0; c < 4; ++c) { z[c] = z2[b * 4 + c]; m = fmaxf(m, z[c]); }
+      if (b == tid) { z[0] = zs[0]; z[1] = zs[1]; z[2] = zs[2]; z[3] = zs[3]; }
+      else for (int c = 0; c < 4; ++c) z[c] = z2[b * 4 + c];
+      for (int c = 0; c < 4; ++c) m = fmaxf(m, z[c]);
       float se = 0.0f;
       for (int c = 0; c < 4; ++c) se += expf(z[c] - m);
       const float lse = m + logf(se);
@@ -356,6 +367,7 @@ __global__ __launch_bounds__(TAIL_THREADS) void dad_tail(DadTailArgs a) {
     }
     const double kls = block_sum_d(kl_part, dred);
     kl = kl_on ? (float)(kls / (double)denom) : 0.0f;
+    TAIL_STAMP(5);
   }
   // ---- per-sample outputs (noisy batch) for inspection / ECDA
   for (int b = tid; b < Bn; b += TAIL_THREADS) {
@@ -374,27 +386,25 @@ __global__ __launch_bounds__(TAIL_THREADS) void dad_tail(DadTailArgs a) {
     for (int c = 0; c < 4; ++c) { tf[DAD_T_ECDA_TERM + c] = 0.0f; tf[DAD_T_ECDA_GATE + c] = 0.0f; }
   }
   __syncthreads();
-  // ---- classifier backward (nn.Linear + nn.Dropout, I/model.py:62-63), both passes.
-  // thread (h, q): hidden unit h, utterances b = q mod 4 (independent loads, 4-way split)
-  const int h = tid & (DAD_H - 1), qg = tid >> 8;
-  const float* W2 = a.student + DAD_OFF_W2;
-  const float w2h[4] = {W2[h], W2[DAD_H + h], W2[2 * DAD_H + h], W2[3 * DAD_H + h]};
-  float gw[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  cls_backward(a.emb, a.keep1, a.ge, a.ge_ecda, gz[0], B, qg, h, a.key_drop1, cfg.p_drop, cfg.drop_scale, w2h, gw);
-  cls_backward(a.emb + (size_t)(B + Bn) * DAD_H, a.keep2, a.ge + (size_t)B * DAD_H, a.ge_ecda + (size_t)B * DAD_H,
-               gz[1], Bn, qg, h, a.key_drop2, cfg.p_drop, cfg.drop_scale, w2h, gw);
+  TAIL_STAMP(6);
+  // ---- dL/dz of every utterance for the weight-gradient kernels (which rebuild the
+  // classifier part of dL/de on the fly, I/model.py:62-63), the b2 grad, ECDA row flags
+  for (int b = tid; b < B; b += TAIL_THREADS)
+    *reinterpret_cast<f32x4*>(a.gzb + (size_t)b * DAD_C) = f32x4{gz[0][b][0], gz[0][b][1], gz[0][b][2], gz[0][b][3]};
+  for (int b = tid; b < Bn; b += TAIL_THREADS)
+    *reinterpret_cast<f32x4*>(a.gzb + (size_t)(B + b) * DAD_C) =
+        f32x4{gz[1][b][0], gz[1][b][1], gz[1][b][2], gz[1][b][3]};
+  for (int b = tid; b < B + Bn; b += TAIL_THREADS) a.eflag[b] = 0u;
+  double b2s[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int b = tid; b < B; b += TAIL_THREADS)
 #pragma unroll
-  for (int c = 0; c < 4; ++c) gwp[qg][c][h] = gw[c];
-  __syncthreads();
-  if (qg == 0)
-    for (int c = 0; c < 4; ++c)
-      a.grad[DAD_OFF_W2 + c * DAD_H + h] = ((gwp[0][c][h] + gwp[1][c][h]) + gwp[2][c][h]) + gwp[3][c][h];
-  if (tid < 4) {
-    double s = 0.0;
-    for (int b = 0; b < B; ++b) s += (double)gz[0][b][tid];
-    for (int b = 0; b < Bn; ++b) s += (double)gz[1][b][tid];
-    a.grad[DAD_OFF_B2 + tid] = (float)s;
-  }
+    for (int c = 0; c < 4; ++c) b2s[c] += (double)gz[0][b][c];
+  for (int b = tid; b < Bn; b += TAIL_THREADS)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) b2s[c] += (double)gz[1][b][c];
+  block_sum4_d(b2s, dred4);
+  TAIL_STAMP(7);
+  if (tid < 4) a.grad[DAD_OFF_B2 + tid] = (float)b2s[tid];
   TAIL_STAMP(1);
 }
 
@@ -587,7 +597,8 @@ __device__ __forceinline__ float ecda_mmd_coef(EcdaSmem& S, const EcdaRows<STAGE
 template <bool STAGED>
 __device__ __forceinline__ void ecda_member_grads(EcdaSmem& S, const EcdaRows<STAGED>& R, int n, const float* D,
                                                   float mmd_scale, const float* cent, float comp_scale, float rep_g,
-                                                  float* ge_c, float* ge_s, float& comp_part) {
+                                                  float* ge_c, float* ge_s, uint32_t* eflag, int B_,
+                                                  float& comp_part) {
   const int hh = threadIdx.x & (DAD_H - 1);
   const int grp = threadIdx.x / DAD_H;
   const int ns = R.ns;
@@ -619,6 +630,7 @@ __device__ __forceinline__ void ecda_member_grads(EcdaSmem& S, const EcdaRows<ST
         g += rep_g;
       }
       (m < ns ? ge_c : ge_s)[(size_t)S.idx[m] * DAD_H + hh] = g;
+      if (hh == 0) eflag[m < ns ? S.idx[m] : B_ + S.idx[m]] = 1u;
     }
   }
 }
@@ -651,7 +663,7 @@ __global__ __launch_bounds__(ECDA_THREADS) void dad_ecda(DadEcdaArgs a) {
   if (tid < DAD_C) { S.cnt_clean[tid] = 0; S.cnt_noisy[tid] = 0; }
   __syncthreads();
   ECDA_STAMP(1);
-  if (ecda_on == 0.0f) return;   // the tail left the ECDA gradient rows at zero
+  if (ecda_on == 0.0f) return;   // no row flagged: the ECDA part of dL/de is zero
 #ifdef DAD_PROBE_ECDA_EXIT0
   return;
 #endif
@@ -672,7 +684,7 @@ __global__ __launch_bounds__(ECDA_THREADS) void dad_ecda(DadEcdaArgs a) {
         ecda_stage(S, R, n);
         const float mmd = ecda_mmd_coef(S, R, n, D);
         float unused = 0.0f;
-        ecda_member_grads(S, R, n, D, wscale, nullptr, 0.0f, 0.0f, ge_c, ge_s, unused);
+        ecda_member_grads(S, R, n, D, wscale, nullptr, 0.0f, 0.0f, ge_c, ge_s, a.eflag, B, unused);
         if (tid == 0) { a.tail_terms[0] = mmd; a.tail_terms[DAD_T_ECDA_GATE - DAD_T_ECDA_TERM] = 1.0f; }
       };
       if (n <= ECDA_NZ) run(std::true_type{});
@@ -812,7 +824,7 @@ __global__ __launch_bounds__(ECDA_THREADS) void dad_ecda(DadEcdaArgs a) {
     if (false)
 #endif
     ecda_member_grads(S, R, n, D, wscale * att_c, gated[c] ? S.cent[c] : nullptr,
-                      wscale * att_c * cfg.ecda_gamma * (2.0f / (float)nt), rep_g, ge_c, ge_s, cpart);
+                      wscale * att_c * cfg.ecda_gamma * (2.0f / (float)nt), rep_g, ge_c, ge_s, a.eflag, B, cpart);
   };
   if (n <= ECDA_NZ) run(std::true_type{});
   else run(std::false_type{});

@@ -333,66 +333,97 @@ __global__ __launch_bounds__(DAD_WGRAD_THREADS, 1) void dad_wgrad_bf16(DadWgradA
 }
 
 // ---------------------------------------------------------------- reduce + squared norms
-// blocks [0, NB): DAD_REDUCE_COLS floats of dW1 each = sum_s wpart[s] + squared-norm partial.
-//   thread = (float4 column, split group kg): group kg sums splits kg, kg+4, ... with its
-//   loads in flight together, then the four groups are combined in fixed order (deterministic).
-// block NB: db1, the W2/b2 norm partial and the loss totals (db1_and_totals below).
-//
-// db1[h] = sum_r dL/de[r][h] / max(1, len_r) * active_count[r][h], the W2/b2 squared-norm
-// partial and the loss totals (I/train.py:462-466).  Returns this thread's norm share.
-static_assert(DAD_REDUCE_THREADS == DAD_H, "db1 block: one thread per hidden unit");
-__device__ double db1_and_totals(const DadReduceArgs& a, f32x4 (*part)[DAD_H / 4]) {
+// blocks [0, NB): DAD_REDUCE_COLS floats of dW1 each (+ squared-norm partial).
+// blocks NB + e, e < DAD_REDUCE_XBLK: hidden units 16e .. 16e+15 of
+//   db1[h]    = sum_r dL/de[r][h] / max(1, len_r) * active_count[r][h]      (autograd of b1)
+//   dW2[c][h] = sum_r dL/dz[r][c] * dropout(e_r)[h]   (fused step; the tail no longer does it)
+// their squared-norm share, and (e = 0) the b2 norm share and the loss totals
+// (I/train.py:462-466).  Thread = (hidden unit hl, row group rg): rows rg, rg+16, ...;
+// the 16 row groups are combined in fixed order (deterministic).
+static_assert(DAD_REDUCE_THREADS == 256 && DAD_H == 16 * DAD_REDUCE_XBLK, "extra blocks: 16 h x 16 row groups");
+
+// Fused step: dL/de of utterance row u (clean u < Bc, strong Bc + b), hidden unit h: the
+// classifier part keep(u,h) * sum_c W2[c][h] dL/dz[u][c] (nn.Linear + nn.Dropout backward,
+// I/model.py:62-63) plus the ECDA part where ECDA wrote the row.
+__device__ __forceinline__ float fused_ge1(const DadReduceArgs& a, int Bc, int u, int h, const float (&w2)[4],
+                                           float* kv_out = nullptr) {
+  const f32x4 gz = *reinterpret_cast<const f32x4*>(a.gzb + (size_t)u * DAD_C);
+  const bool strong = u >= Bc;
+  const int b = strong ? u - Bc : u;
+  const float kv = strong ? keep_value(a.keep2, a.key_drop2, b, h, a.p_drop, a.drop_scale)
+                          : keep_value(a.keep1, a.key_drop1, b, h, a.p_drop, a.drop_scale);
+  if (kv_out) *kv_out = kv;
+  const float z = ((w2[0] * gz[0] + w2[1] * gz[1]) + w2[2] * gz[2]) + w2[3] * gz[3];
+  float g = z * kv;
+  if (a.eflag[u]) g += a.ge_ecda[(size_t)u * DAD_H + h];
+  return g;
+}
+
+__device__ double extra_block(const DadReduceArgs& a, int e) {
+  __shared__ float xs[16][16][6];
   const int tid = threadIdx.x;
-  double sq = 0.0;
-  // thread = (4 hidden
-  // units as a float4, row group rg); rows rg, rg+4, ... in batches of 8 with all their
-  // loads in flight, then the four row groups combined in fixed order.
+  const int hl = tid & 15, rg = tid >> 4;
+  const int h = 16 * e + hl;
   const DadGeom& g = a.g;
   const int nb = g.Bc + (a.warmup ? 0 : g.Bn);
-  const int hq = tid & (DAD_H / 4 - 1), rg = tid / (DAD_H / 4);
+  const bool fused = a.gzb != nullptr;
   const bool ecda = a.ge_ecda != nullptr;
-  f32x4 acc = f32x4{};
-  for (int r0 = rg; r0 < nb; r0 += 4 * 8) {
-    f32x4 gv[8], cv[8];
-    float lv[8];
+  float w2[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  if (fused)
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int r = min(r0 + 4 * u, nb - 1);
-      gv[u] = reinterpret_cast<const f32x4*>(a.ge + (size_t)r * DAD_H)[hq];
-      if (ecda) gv[u] += reinterpret_cast<const f32x4*>(a.ge_ecda + (size_t)r * DAD_H)[hq];
-      cv[u] = reinterpret_cast<const f32x4*>(a.cnt_tot + (size_t)r * DAD_H)[hq];
-      lv[u] = a.vlen[r];
+    for (int c = 0; c < 4; ++c) w2[c] = a.student[DAD_OFF_W2 + c * DAD_H + h];
+  float db = 0.0f, gw[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  for (int r = rg; r < nb; r += 16) {
+    float gv, kv = 1.0f;
+    if (fused) {
+      gv = fused_ge1(a, g.Bc, r, h, w2, &kv);
+    } else {
+      gv = a.ge[(size_t)r * DAD_H + h];
+      if (ecda) gv += a.ge_ecda[(size_t)r * DAD_H + h];
     }
+    db += gv / fmaxf(a.vlen[r], 1.0f) * a.cnt_tot[(size_t)r * DAD_H + h];
+    if (fused) {
+      // dW2[c][h] = sum_u dL/dz[u][c] * dropout(e_u)[h]  (student clean / strong embeddings)
+      const bool strong = r >= g.Bc;
+      const int erow = strong ? g.Bn + r : r;   // strong row b lives at Bc + Bn + b
+      const float d = a.emb[(size_t)erow * DAD_H + h] * kv;
+      const f32x4 gz = *reinterpret_cast<const f32x4*>(a.gzb + (size_t)r * DAD_C);
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
-      if (r0 + 4 * u < nb) acc += gv[u] / fmaxf(lv[u], 1.0f) * cv[u];
+      for (int c = 0; c < 4; ++c) gw[c] += gz[c] * d;
+    }
   }
-  part[rg][hq] = acc;
+  xs[rg][hl][0] = db;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) xs[rg][hl][1 + c] = gw[c];
   __syncthreads();
-  const int h = tid;
-  const float db1 = ((part[0][h >> 2][h & 3] + part[1][h >> 2][h & 3]) + part[2][h >> 2][h & 3]) +
-                    part[3][h >> 2][h & 3];
-  a.grad[DAD_OFF_B1 + h] = db1;
-  sq = (double)db1 * db1;
-  if (!a.tailf) return sq;   // modular encoder backward: W1/b1 only
-  for (int c = 0; c < 4; ++c) {
-    const float g = a.grad[DAD_OFF_W2 + c * DAD_H + h];
-    sq += (double)g * g;
+  double sq = 0.0;
+  if (tid < 16 * 5) {
+    const int k = tid >> 4, hh = tid & 15;   // k: 0 = db1, 1..4 = dW2 row c = k-1
+    float v = xs[0][hh][k];
+    for (int q = 1; q < 16; ++q) v += xs[q][hh][k];
+    if (k == 0) {
+      a.grad[DAD_OFF_B1 + 16 * e + hh] = v;
+      sq = (double)v * v;
+    } else if (a.tailf) {
+      if (fused) a.grad[DAD_OFF_W2 + (k - 1) * DAD_H + 16 * e + hh] = v;
+      else v = a.grad[DAD_OFF_W2 + (k - 1) * DAD_H + 16 * e + hh];
+      sq = (double)v * v;
+    }
   }
-  if (h < 4) {
-    const float g = a.grad[DAD_OFF_B2 + h];
-    sq += (double)g * g;
+  if (e == 0 && a.tailf && tid >= 96 && tid < 100) {
+    const float gb = a.grad[DAD_OFF_B2 + tid - 96];
+    sq += (double)gb * gb;
   }
-  if (h == 0) {
+  if (e == 0 && a.tailf && tid == 128) {
     const float* tf = a.tailf;
-    const float ecda = ((tf[DAD_T_ECDA_TERM] + tf[DAD_T_ECDA_TERM + 1]) + tf[DAD_T_ECDA_TERM + 2]) +
-                       tf[DAD_T_ECDA_TERM + 3];
+    const float ecda_l = ((tf[DAD_T_ECDA_TERM] + tf[DAD_T_ECDA_TERM + 1]) + tf[DAD_T_ECDA_TERM + 2]) +
+                         tf[DAD_T_ECDA_TERM + 3];
     const float ce = tf[DAD_T_CE], kl = tf[DAD_T_KL];
     float* ex = a.grad + DAD_NPARAM;
-    ex[12] = ce + a.w_kl * kl + a.w_ecda * ecda;
+    ex[12] = ce + a.w_kl * kl + a.w_ecda * ecda_l;
     ex[13] = ce;
     ex[14] = kl;
-    ex[15] = ecda;
+    ex[15] = ecda_l;
   }
   return sq;
 }
@@ -405,7 +436,7 @@ __global__ __launch_bounds__(DAD_REDUCE_THREADS) void dad_reduce(DadReduceArgs a
   __shared__ double red[DAD_REDUCE_THREADS / 64];
   __shared__ f32x4 part[4][DAD_REDUCE_COLS / 4 > DAD_H / 4 ? DAD_REDUCE_COLS / 4 : DAD_H / 4];
   const int tid = threadIdx.x;
-  constexpr int NB = DAD_REDUCE_BLOCKS - 1;
+  constexpr int NB = DAD_REDUCE_BLOCKS - DAD_REDUCE_XBLK;
   double sq = 0.0;
   if (blockIdx.x < NB) {
     const int col = tid & (DAD_REDUCE_COLS / 4 - 1), kg = tid / (DAD_REDUCE_COLS / 4);
@@ -421,7 +452,7 @@ __global__ __launch_bounds__(DAD_REDUCE_THREADS) void dad_reduce(DadReduceArgs a
       for (int e = 0; e < 4; ++e) sq += (double)t[e] * t[e];
     }
   } else {
-    sq = db1_and_totals(a, part);
+    sq = extra_block(a, blockIdx.x - NB);
   }
   if (!a.want_norm) return;
   double v = dad_wave_sum_d(sq);
@@ -446,20 +477,18 @@ __global__ __launch_bounds__(DAD_REDUCE_THREADS) void dad_wsum(DadReduceArgs a) 
   __shared__ f32x4 part[4][DAD_H / 4];
   __shared__ float gsh[2 * DAD_MAX_BATCH];
   const int tid = threadIdx.x;
-  constexpr int NB = DAD_REDUCE_BLOCKS - 1;
+  constexpr int NB = DAD_REDUCE_BLOCKS - DAD_REDUCE_XBLK;
   double sq = 0.0;
   if (blockIdx.x < NB) {
     const DadGeom& g = a.g;
     const int nutt = g.Bc + (a.warmup ? 0 : g.Bn);
     const int h = blockIdx.x / (DAD_D / DAD_REDUCE_COLS);
     const int dcol0 = (blockIdx.x % (DAD_D / DAD_REDUCE_COLS)) * DAD_REDUCE_COLS;
-    // dL/de = CE/KL part + ECDA part (zeros unless ECDA wrote the row this step)
-    const bool ecda = a.ge_ecda != nullptr;
-    for (int u = tid; u < nutt; u += DAD_REDUCE_THREADS) {
-      float gu = a.ge[(size_t)u * DAD_H + h];
-      if (ecda) gu += a.ge_ecda[(size_t)u * DAD_H + h];
-      gsh[u] = gu / fmaxf(a.vlen[u], 1.0f);
-    }
+    // dL/de = classifier part + ECDA part (where ECDA wrote the row this step)
+    const float w2h[4] = {a.student[DAD_OFF_W2 + h], a.student[DAD_OFF_W2 + DAD_H + h],
+                          a.student[DAD_OFF_W2 + 2 * DAD_H + h], a.student[DAD_OFF_W2 + 3 * DAD_H + h]};
+    for (int u = tid; u < nutt; u += DAD_REDUCE_THREADS)
+      gsh[u] = fused_ge1(a, g.Bc, u, h, w2h) / fmaxf(a.vlen[u], 1.0f);
     __syncthreads();
     const int col = tid & (DAD_REDUCE_COLS / 4 - 1), ug = tid / (DAD_REDUCE_COLS / 4);
     const size_t off = (size_t)h * DAD_D + dcol0 + (size_t)col * 4;
@@ -496,7 +525,7 @@ __global__ __launch_bounds__(DAD_REDUCE_THREADS) void dad_wsum(DadReduceArgs a) 
       for (int e = 0; e < 4; ++e) sq += (double)t[e] * t[e];
     }
   } else {
-    sq = db1_and_totals(a, part);
+    sq = extra_block(a, blockIdx.x - NB);
   }
   if (!a.want_norm) return;
   double v = dad_wave_sum_d(sq);
