@@ -30,12 +30,19 @@ inline int check_cfg(const dad_config* c) {
 inline DadGeom geom_of(const dad_config* c) { return dad_geom(c->B, c->T, c->Bn, c->Tn); }
 
 inline int splits_of(const dad_config* c) {
-  return c->splits > 0 ? c->splits : dad_auto_splits(geom_of(c), c->precision, c->warmup);
+  const DadGeom g = geom_of(c);
+  if (c->splits <= 0) return dad_auto_splits(g, c->precision, c->warmup);
+  if (c->precision != DAD_PREC_BF16) return c->splits;
+  // dad_wgrad_direct holds at most WGD_MAXU slabs' utterances per split
+  const int total = g.Bc * g.ncc + (c->warmup ? 0 : g.Bn * g.ncn);
+  return std::max(c->splits, dad_wgd_min_splits(total));
 }
 
 inline int max_splits_of(const dad_config* c) {
   // the workspace is sized for the largest split count any step with this geometry may use
-  return c->splits > 0 ? c->splits : dad_auto_splits(geom_of(c), c->precision, 0);
+  dad_config post = *c;
+  post.warmup = 0;
+  return std::max(splits_of(c), splits_of(&post));
 }
 
 template <typename T>
@@ -219,33 +226,33 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   }
   if (!do_backward) return DAD_OK;
 
-  // 2. loss-independent factor of dW1 on the side stream: S_u = bits_u^T X_u per utterance
-  //    (clean rows, then the strong-augmented noisy rows), concurrent with 3-5
-  SideStream* side = nullptr;
-  {
-    const int rc = side_stream(&side);
-    if (rc) return rc;
-  }
+  // 2. FP32: the loss-independent factor of dW1 on the side stream, S_u = bits_u^T X_u per
+  //    utterance (clean rows, then the strong-augmented noisy rows), concurrent with 3-5.
+  //    BF16: the direct GEMM runs after ECDA (6), with dL/de folded into its A operand.
   const int nutt = G.Bc + Bn;
   float* sbuf = ws_ptr<float>(workspace, L.sbuf);
   DadWgradArgs wa;
   memset(&wa, 0, sizeof(wa));
-  wa.g = G; wa.warmup = cfg->warmup; wa.splits = nutt; wa.per_utt = 1;
+  wa.g = G; wa.warmup = cfg->warmup;
   wa.mask_len = cfg->mask_len; wa.start_hi = cfg->start_hi;
   wa.xc = bt->xc; wa.xn = bt->xn;
   if (explicit_rng) { wa.ns = bt->ns; wa.u = bt->u; wa.start = bt->start; }
   wa.key_strong = k.strong; wa.key_feat = k.feat; wa.key_tstart = k.tstart;
   wa.strong_std = cfg->strong_std; wa.feat_p = cfg->feat_p;
-  wa.bits = bits; wa.ge = ge; wa.vlen = vlen; wa.xs_bf16 = xs_bf16; wa.wpart = sbuf;
-  wa.ntiles = 6 * nutt;
-  if (bf16) wa.wpart_bf16 = reinterpret_cast<__bf16*>(sbuf);   // S_u in bf16 (G is 0/1: exact operands)
-  const int sgrid = std::max(1, std::min(wa.ntiles, side->cus - kReservedCUs));
-  DAD_TRY(hipEventRecord(side->fork, stream));
-  DAD_TRY(hipStreamWaitEvent(side->s, side->fork, 0));
-  if (bf16) hipLaunchKernelGGL(dad_wgrad_bf16, dim3(sgrid), dim3(DAD_WGRAD_THREADS), 0, side->s, wa);
-  else hipLaunchKernelGGL(dad_wgrad_f32, dim3(sgrid), dim3(DAD_WGRAD_THREADS), 0, side->s, wa);
-  DAD_TRY(hipGetLastError());
-  DAD_TRY(hipEventRecord(side->join, side->s));
+  wa.bits = bits; wa.ge = ge; wa.vlen = vlen; wa.xs_bf16 = xs_bf16;
+  SideStream* side = nullptr;
+  if (!bf16) {
+    const int rc = side_stream(&side);
+    if (rc) return rc;
+    wa.splits = nutt; wa.per_utt = 1; wa.wpart = sbuf;
+    wa.ntiles = 6 * nutt;
+    const int sgrid = std::max(1, std::min(wa.ntiles, side->cus - kReservedCUs));
+    DAD_TRY(hipEventRecord(side->fork, stream));
+    DAD_TRY(hipStreamWaitEvent(side->s, side->fork, 0));
+    hipLaunchKernelGGL(dad_wgrad_f32, dim3(sgrid), dim3(DAD_WGRAD_THREADS), 0, side->s, wa);
+    DAD_TRY(hipGetLastError());
+    DAD_TRY(hipEventRecord(side->join, side->s));
+  }
 
   // 3. pooled embeddings + classifier logits
   DadPoolArgs pa;
@@ -282,20 +289,33 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
     DAD_TRY(hipGetLastError());
   }
 
-  // 6. join; dW1 = sum_u (dL/de_u / len_u) * S_u, db1, loss totals, squared-norm partials
-  DAD_TRY(hipStreamWaitEvent(stream, side->join, 0));
+  // 6. dW1 (BF16: direct split-K GEMM; FP32: join, then sum_u (dL/de_u / len_u) * S_u), db1,
+  //    dW2, loss totals, squared-norm partials
   DadReduceArgs ra;
   memset(&ra, 0, sizeof(ra));
-  ra.g = G; ra.splits = nutt; ra.warmup = cfg->warmup;
+  ra.g = G; ra.warmup = cfg->warmup;
   ra.want_norm = cfg->dp_world == 1;
   ra.w_kl = cfg->w_kl; ra.w_ecda = cfg->w_ecda;
-  ra.wpart = sbuf; ra.wpart_bf16 = wa.wpart_bf16; ra.ge_ecda = ge_ecda;
+  ra.ge_ecda = ge_ecda;
   ra.gzb = gzb; ra.eflag = eflag; ra.student = st->student; ra.emb = st->emb;
   if (explicit_rng) { ra.keep1 = bt->keep1; ra.keep2 = bt->keep2; }
   ra.key_drop1 = k.drop1; ra.key_drop2 = k.drop2; ra.p_drop = cfg->p_drop; ra.drop_scale = cfg->drop_scale;
   ra.ge = ge; ra.vlen = vlen; ra.cnt_tot = cnt_tot; ra.tailf = st->tail;
   ra.grad = st->grad; ra.normpart = normpart;
-  hipLaunchKernelGGL(dad_wsum, dim3(DAD_REDUCE_BLOCKS), dim3(DAD_REDUCE_THREADS), 0, stream, ra);
+  if (bf16) {
+    wa.splits = splits; wa.per_utt = 0;
+    wa.wpart = ws_ptr<float>(workspace, L.wpart);
+    wa.ntiles = WGD_NDB * splits;
+    const int grid = (wa.ntiles + 7) / 8 * 8;   // multiple of 8: XCD-aware tile order
+    hipLaunchKernelGGL(dad_wgrad_direct, dim3(grid), dim3(DAD_WGRAD_THREADS), 0, stream, wa, ra);
+    DAD_TRY(hipGetLastError());
+    ra.splits = splits; ra.wpart = wa.wpart;
+    hipLaunchKernelGGL(dad_reduce, dim3(DAD_REDUCE_BLOCKS), dim3(DAD_REDUCE_THREADS), 0, stream, ra);
+  } else {
+    DAD_TRY(hipStreamWaitEvent(stream, side->join, 0));
+    ra.splits = nutt; ra.wpart = sbuf;
+    hipLaunchKernelGGL(dad_wsum, dim3(DAD_REDUCE_BLOCKS), dim3(DAD_REDUCE_THREADS), 0, stream, ra);
+  }
   DAD_TRY(hipGetLastError());
   return DAD_OK;
 }

@@ -199,7 +199,7 @@ static inline __host__ __device__ DadGeom dad_geom(int Bc, int Tc, int Bn, int T
 struct DadWs {
   size_t part_sum;   // f32 [Bc*ncc + 2*Bn*ncn][H]  per-slab pooled ReLU sums (clean | teacher-weak | strong)
   size_t part_cnt;   // f32 [Bc*ncc + Bn*ncn][H]    per-slab active-row counts (clean | strong)
-  size_t bits;       // u32 [Bc*tpc + Bn*tpn][8]    ReLU' & valid bits per row and 32-wide h tile
+  size_t bits;       // u32 [Bc*ncc + Bn*ncn][H]    ReLU'-and-valid row mask per (slab, h): bit r = row r
   size_t vlen;       // f32 [Bc + Bn]               valid lengths (clean | noisy)
   size_t cnt_tot;    // f32 [Bc + Bn][H]            active-row counts per utterance (clean | strong)
   size_t ge;         // f32 [Bc + Bn][H]            dL/de_clean | dL/de_strong (CE/KL part)
@@ -212,19 +212,24 @@ struct DadWs {
   size_t xs_bf16;    // bf16 [Bn][Tn][768]          BF16 mode: strong-augmented input (wgrad operand)
   size_t w1bf;       // bf16 [H][D]                 modular encoder ops: bf16 copy of W1
   size_t gflat;      // f32 [DAD_GRAD_FLOATS]       modular encoder backward: scratch grad vector
-  size_t sbuf;       // f32 [Bc + Bn][H][D]         S_u = bits_u^T X_u, the loss-independent factor of dW1
+  size_t sbuf;       // f32 [Bc + Bn][H][D]         FP32 step: S_u = bits_u^T X_u, the loss-independent factor of dW1
   size_t bytes;
   int splits;
 };
 
 static inline size_t dad_align(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// weight-gradient split-K factor: enough workgroups to cover the chip (6 column blocks
-// per split), bounded by the number of 32-row slabs.
+// weight-gradient split-K factor.  FP32 (dad_wgrad_f32, 6 column blocks per split): 64
+// splits.  BF16 (dad_wgrad_direct, 12 column blocks per split): 21 splits -> 252 workgroups,
+// one per CU, and never more than WGD_MAXU = 64 slabs per split (its dL/de table in LDS).
+// Both are bounded by the number of 32-row slabs.
+static inline int dad_wgd_min_splits(int total) { return (total + 63) / 64; }
 static inline int dad_auto_splits(const DadGeom& g, int precision, int warmup) {
   const int total = g.Bc * g.ncc + (warmup ? 0 : g.Bn * g.ncn);
-  const int target = precision == DAD_PREC_BF16 ? 43 : 64;
-  return total < target ? total : target;
+  const int target = precision == DAD_PREC_BF16 ? 21 : 64;
+  int s = total < target ? total : target;
+  if (precision == DAD_PREC_BF16 && s < dad_wgd_min_splits(total)) s = dad_wgd_min_splits(total);
+  return s;
 }
 
 // fused = the train step's layout (with the S_u buffer); the modular encoder ops pass false.
@@ -249,7 +254,7 @@ static inline DadWs dad_ws_layout(const DadGeom& g, int splits, int precision, b
   w.xs_bf16 = off;  off = dad_align(off + (precision == DAD_PREC_BF16 ? 2 * (size_t)g.Bn * g.Tn * DAD_D : 0));
   w.w1bf = off;     off = dad_align(off + 2 * (size_t)DAD_H * DAD_D);
   w.gflat = off;    off = dad_align(off + sizeof(float) * DAD_GRAD_FLOATS);
-  w.sbuf = off;     off = dad_align(off + (fused ? sizeof(float) * nb * DAD_H * DAD_D : 0));
+  w.sbuf = off;     off = dad_align(off + (fused && precision != DAD_PREC_BF16 ? sizeof(float) * nb * DAD_H * DAD_D : 0));
   w.bytes = off;
   return w;
 }

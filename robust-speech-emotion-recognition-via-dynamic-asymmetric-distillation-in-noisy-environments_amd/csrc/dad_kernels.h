@@ -11,6 +11,13 @@
 #define DAD_TAIL_THREADS 512
 #define DAD_ECDA_THREADS 512
 #define DAD_WGRAD_THREADS 256
+// dad_wgrad_direct (BF16): 64-column blocks, slab-range splits of at most WGD_MAXU slabs,
+// WGD_DEPTH slabs in flight per workgroup, x tile row pitch WGD_XP bf16 (192 B)
+#define WGD_DB 64
+#define WGD_NDB (DAD_D / WGD_DB)
+#define WGD_MAXU 64
+#define WGD_DEPTH 4
+#define WGD_XP 96
 #define DAD_REDUCE_THREADS 256
 #define DAD_REDUCE_COLS 256                                  // dW1 floats per reduce block
 #define DAD_REDUCE_XBLK 16                                   // db1 / dW2 / totals blocks (16 hidden units each)
@@ -88,8 +95,7 @@ struct DadWgradArgs {
   const __bf16* xs_bf16;
   float* wpart;
   int per_utt;         // 1: one split per utterance with G = ReLU' bits (S_u = bits_u^T X_u into wpart[u])
-  int ntiles;          // 6 column blocks x splits; workgroups stride over them (grid may be smaller)
-  __bf16* wpart_bf16;  // non-null: partials stored in bf16 here instead of wpart
+  int ntiles;          // column blocks x splits; workgroups stride over them (grid may be smaller)
 };
 
 struct DadReduceArgs {
@@ -97,7 +103,6 @@ struct DadReduceArgs {
   int splits, warmup, want_norm;
   float w_kl, w_ecda;
   const float* wpart; const float* ge; const float* vlen; const float* cnt_tot;
-  const __bf16* wpart_bf16;   // dad_wsum: bf16 S_u instead of wpart
   const float* ge_ecda;       // ECDA part of dL/de, added where eflag is set
   // fused step: dL/de is not materialised; the classifier part is rebuilt per (utterance, h)
   // as keep(u,h) * sum_c W2[c][h] gzb[u][c] (nn.Linear + dropout backward, I/model.py:62-63)
@@ -125,7 +130,7 @@ __global__ void dad_pool(DadPoolArgs a);
 __global__ void dad_tail(DadTailArgs a);
 __global__ void dad_ecda(DadEcdaArgs a);
 __global__ void dad_wgrad_f32(DadWgradArgs a);
-__global__ void dad_wgrad_bf16(DadWgradArgs a);
+__global__ void dad_wgrad_direct(DadWgradArgs a, DadReduceArgs r);
 __global__ void dad_wsum(DadReduceArgs a);
 __global__ void dad_reduce(DadReduceArgs a);
 __global__ void dad_norm(float* grad, float* normpart, float inv_world);

@@ -81,14 +81,13 @@ __device__ __forceinline__ void augment4(const DadEncodeArgs& a, f32x4 x, int gr
 }
 
 // Pool one 32x256 accumulator set: bias + ReLU + padding mask + sum over the slab rows.
-// sum_slab / cnt_slab index part_sum / part_cnt; bits_row (< 0: no bits) is the first
-// row of this slab in the bits buffer.
+// sum_slab / cnt_slab index part_sum / part_cnt; bits_slab (< 0: no bits) is the slab's
+// index in the ReLU' buffer, which holds one 32-bit row mask per (slab, h).
 __device__ __forceinline__ void encode_epilogue(const DadEncodeArgs& a, const f32x16* acc, const float* bias,
-                                                size_t sum_slab, long cnt_slab, long bits_row, uint32_t vbits,
-                                                uint32_t* lds_bits) {
+                                                size_t sum_slab, long cnt_slab, long bits_slab, uint32_t vbits) {
   const int lane = threadIdx.x & 63;
   const int j = lane & 31, kh = lane >> 5;
-  const bool want_bits = bits_row >= 0;
+  const bool want_bits = bits_slab >= 0;
   // all bias loads up front: a load between the part_sum stores would wait on each of them
   float bhs[DAD_HT];
 #pragma unroll
@@ -98,6 +97,7 @@ __device__ __forceinline__ void encode_epilogue(const DadEncodeArgs& a, const f3
     const int h = ht * 32 + j;
     const float bh = bhs[ht];
     float s = 0.0f, n = 0.0f;
+    uint32_t m = 0;   // this lane's rows of h (C layout: rows dad_acc_row(r, kh))
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int row = dad_acc_row(r, kh);
@@ -106,46 +106,32 @@ __device__ __forceinline__ void encode_epilogue(const DadEncodeArgs& a, const f3
       const bool act = v && pre > 0.0f;
       s += act ? pre : 0.0f;
       n += act ? 1.0f : 0.0f;
-      if (want_bits) {
-        // the ballot is wave-uniform: every lane writes the same word to the same address
-        // (no lane-0 branch per row)
-        const uint64_t m = __ballot(act);
-        const int row0 = dad_acc_row(r, 0);
-        lds_bits[row0 * DAD_HT + ht] = (uint32_t)m;
-        lds_bits[(row0 + 4) * DAD_HT + ht] = (uint32_t)(m >> 32);
-      }
+      m |= act ? (1u << row) : 0u;
     }
     s += __shfl_xor(s, 32, 64);
     n += __shfl_xor(n, 32, 64);
+    m |= (uint32_t)__shfl_xor((int)m, 32, 64);
     if (kh == 0) {
       a.part_sum[sum_slab * DAD_H + h] = s;
       if (cnt_slab >= 0) a.part_cnt[(size_t)cnt_slab * DAD_H + h] = n;
+      if (want_bits) a.bits[(size_t)bits_slab * DAD_H + h] = m;
     }
-  }
-  if (want_bits) {
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): lane 0's LDS writes landed
-    __builtin_amdgcn_wave_barrier();
-    // 32 rows x 8 words = 1 KB per slab, stored contiguously: 16 B per lane
-    const uint4 w = reinterpret_cast<const uint4*>(lds_bits)[lane];
-    reinterpret_cast<uint4*>(a.bits + (size_t)bits_row * DAD_HT)[lane] = w;
   }
 }
 
 // epilogues of one wave: clean -> (clean sums, clean counts, clean bits);
 // noisy -> teacher sums (no grads), then strong sums/counts/bits
 __device__ __forceinline__ void encode_finish(const DadEncodeArgs& a, const EncodeGeom& e, const f32x16* acc0,
-                                              const f32x16* acc1, uint32_t vbits, uint32_t* lb) {
+                                              const f32x16* acc1, uint32_t vbits) {
   const DadGeom& g = a.g;
   if (!e.noisy) {
-    encode_epilogue(a, acc0, a.b1_student, e.sum_slab, (long)e.sum_slab,
-                    (long)e.b * g.tpc + (long)e.c * DAD_SLAB, vbits, lb);
+    encode_epilogue(a, acc0, a.b1_student, e.sum_slab, (long)e.sum_slab, (long)e.sum_slab, vbits);
   } else {
     const size_t nslab_n = (size_t)g.Bn * g.ncn;
     const size_t local = e.sum_slab - (size_t)g.Bc * g.ncc;
-    encode_epilogue(a, acc0, a.b1_teacher, e.sum_slab, -1, -1, vbits, lb);
-    encode_epilogue(a, acc1, a.b1_student, e.sum_slab + nslab_n, (long)((size_t)g.Bc * g.ncc + local),
-                    (long)g.Bc * g.tpc + (long)e.b * g.tpn + (long)e.c * DAD_SLAB, vbits, lb);
+    const long strong_slab = (long)((size_t)g.Bc * g.ncc + local);
+    encode_epilogue(a, acc0, a.b1_teacher, e.sum_slab, -1, -1, vbits);
+    encode_epilogue(a, acc1, a.b1_student, e.sum_slab + nslab_n, strong_slab, strong_slab, vbits);
   }
 }
 
@@ -154,7 +140,6 @@ __device__ __forceinline__ void encode_finish(const DadEncodeArgs& a, const Enco
 // ------------------------------------------------------------------- FP32 (parity mode)
 __global__ __launch_bounds__(DAD_ENC_F32_THREADS) void dad_encode_f32(DadEncodeArgs a) {
   DAD_GUARD_BLOCK(DAD_ENC_F32_THREADS);
-  __shared__ __attribute__((aligned(16))) uint32_t lds_bits_all[4][DAD_SLAB * DAD_HT];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const int wid = blockIdx.x * 4 + wv;
@@ -212,5 +197,5 @@ __global__ __launch_bounds__(DAD_ENC_F32_THREADS) void dad_encode_f32(DadEncodeA
       }
     }
   }
-  encode_finish(a, g, acc0, acc1, vbits, lds_bits_all[wv]);
+  encode_finish(a, g, acc0, acc1, vbits);
 }

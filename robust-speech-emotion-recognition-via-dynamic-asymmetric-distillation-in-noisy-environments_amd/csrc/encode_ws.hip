@@ -111,8 +111,7 @@ struct Job {
   int kind, b, c, T;
   long row0;        // [b][T] row of frame 0
   long sum_slab;    // part_sum slab
-  long cnt_slab;    // part_cnt slab (student only)
-  long bits_row;    // first bits row of the slab (student only)
+  long cnt_slab;    // part_cnt slab = ReLU' row-mask slab (student only)
 };
 
 // job j of the workgroup's role list: teacher -> weak slab j; student -> clean slab j, then
@@ -129,8 +128,6 @@ __device__ __forceinline__ Job job_of(const Ctx& C, bool teacher, int j) {
   J.row0 = (long)J.b * J.T;
   J.sum_slab = teacher ? (long)C.nsc + s : (noisy ? (long)C.nsc + C.nsn + s : (long)s);
   J.cnt_slab = noisy ? (long)C.nsc + s : (long)s;
-  J.bits_row = noisy ? (long)C.Bc * C.tpc + (long)J.b * C.tpn + (long)J.c * DAD_SLAB
-                     : (long)J.b * C.tpc + (long)J.c * DAD_SLAB;
   return J;
 }
 
@@ -338,12 +335,6 @@ __device__ __forceinline__ void ws_mfma(const char* tile, const int (&aoff)[4], 
   else asm volatile("s_nop 7\n\ts_nop 7" ::"v"(acc[0]), "v"(acc[1]));
 }
 
-// lane L of x := uniform v (v_writelane_b32; hipcc has no builtin for it)
-template <int L>
-__device__ __forceinline__ void writelane(uint32_t& x, uint32_t v) {
-  asm("v_writelane_b32 %0, %1, %2" : "+v"(x) : "s"(v), "i"(L));
-}
-
 // sum over the 4 row groups (lane >> 4) of a 16x16 C tile column: v_permlane32_swap and
 // v_permlane16_swap (gfx950) with both operands = x give [x_lo, x_lo] + [x_hi, x_hi]
 __device__ __forceinline__ float rowgroup_sum(float x) {
@@ -355,43 +346,29 @@ __device__ __forceinline__ float rowgroup_sum(float x) {
   return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
-// rows r, 4+r, 8+r, 12+r of the sub-slab from the ballots of register r: row 4g + r takes
-// 16-bit field g of ballot (t, r) for tile t.  Pairs of fields pack with s_pack_{ll,hh}_b32_b16
-// on the scalar unit; each row's word lands in lane rho by v_writelane.
-template <class S, int R>
-__device__ __forceinline__ void bits_words(const uint64_t (&bal)[S::NT][4], uint32_t& my0, uint32_t& my1) {
-  if constexpr (R < 4) {
-    const uint32_t a_lo = (uint32_t)bal[0][R], a_hi = (uint32_t)(bal[0][R] >> 32);
-    const uint32_t b_lo = (uint32_t)bal[1][R], b_hi = (uint32_t)(bal[1][R] >> 32);
-    writelane<R>(my0, (a_lo & 0xffffu) | (b_lo << 16));
-    writelane<4 + R>(my0, (a_lo >> 16) | (b_lo & 0xffff0000u));
-    writelane<8 + R>(my0, (a_hi & 0xffffu) | (b_hi << 16));
-    writelane<12 + R>(my0, (a_hi >> 16) | (b_hi & 0xffff0000u));
-    if constexpr (S::NT == 4) {
-      const uint32_t c_lo = (uint32_t)bal[2][R], c_hi = (uint32_t)(bal[2][R] >> 32);
-      const uint32_t d_lo = (uint32_t)bal[3][R], d_hi = (uint32_t)(bal[3][R] >> 32);
-      writelane<R>(my1, (c_lo & 0xffffu) | (d_lo << 16));
-      writelane<4 + R>(my1, (c_lo >> 16) | (d_lo & 0xffff0000u));
-      writelane<8 + R>(my1, (c_hi & 0xffffu) | (d_hi << 16));
-      writelane<12 + R>(my1, (c_hi >> 16) | (d_hi & 0xffff0000u));
-    }
-    bits_words<S, R + 1>(bal, my0, my1);
-  }
+// OR over the 4 row groups, same swaps as rowgroup_sum
+__device__ __forceinline__ uint32_t rowgroup_or(uint32_t x) {
+  const auto a = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+  const uint32_t s1 = a[0] | a[1];
+  const auto b = __builtin_amdgcn_permlane16_swap(s1, s1, false, false);
+  return b[0] | b[1];
 }
 
 // bias + ReLU + valid mask of one sub-slab.  Per-lane partial sums/counts (4 rows of the C
 // tile) accumulate over the job's two sub-slabs and are reduced across the 4 row groups only
-// at the job's end (HALF 1).  Student: the ReLU'-and-valid bits of the 16 rows.
-// Stores: student 1 (bits) + 2 at HALF 1 (sums, counts); teacher 1 at HALF 1 (sums).
+// at the job's end (HALF 1).  Student: the ReLU'-and-valid row mask of each hidden unit (bit
+// r = row r of the 32-row slab): a lane's 4 rows form a nibble, the 4 row groups are OR-ed
+// by lane swaps, the two halves meet in bw and one 32-lane store writes the job's words.
+// Stores: student 3 at HALF 1 (row masks, sums, counts); teacher 1 at HALF 1 (sums).
 template <class S, bool TEACHER, int HALF>
 __device__ __forceinline__ void ws_epilogue(const Ctx& C, const Job& J, int w, int lane, uint32_t vmask,
                                             const float (&bh)[S::NT], const f32x4 (&acc)[S::NT], float (&ssum)[S::NT],
-                                            float (&scnt)[S::NT]) {
+                                            float (&scnt)[S::NT], uint32_t (&bw)[S::NT]) {
   const int g = lane >> 4;
-  uint64_t bal[S::NT][4];
 #pragma unroll
   for (int t = 0; t < S::NT; ++t) {
     float s = 0.0f, n = 0.0f;
+    uint32_t nib = 0;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const bool v = (vmask >> (4 * g + r)) & 1u;     // C/D layout: row = 4(lane>>4) + r, col = lane&15
@@ -400,30 +377,21 @@ __device__ __forceinline__ void ws_epilogue(const Ctx& C, const Job& J, int w, i
       s += act ? pre : 0.0f;
       if constexpr (!TEACHER) {
         n += act ? 1.0f : 0.0f;
-        bal[t][r] = __ballot(act);
+        nib |= act ? (1u << r) : 0u;
       }
     }
     ssum[t] = HALF ? ssum[t] + s : s;
-    if constexpr (!TEACHER) scnt[t] = HALF ? scnt[t] + n : n;
-  }
-  const int hw = S::HW * w;
-  if constexpr (!TEACHER) {
-    // row rho = 4g + r of the sub-slab: its bits of h = hw + 16t + col are field g of ballot
-    // (t, r).  Words are assembled from the (uniform) ballots on the scalar unit and dropped
-    // into lane rho with v_writelane -- no per-lane select of a ballot (which hipcc lowers to
-    // a scratch array).
-    uint32_t my0 = 0, my1 = 0;
-    bits_words<S, 0>(bal, my0, my1);
-    uint32_t* dst = C.bits + (size_t)(J.bits_row + HALF * kSub + (lane & 15)) * DAD_HT;
-    if constexpr (S::NT == 4) {
-      if (lane < 16) *reinterpret_cast<uint2*>(dst + 2 * w) = uint2{my0, my1};
-    } else {
-      if (lane < 16) dst[w] = my0;
+    if constexpr (!TEACHER) {
+      scnt[t] = HALF ? scnt[t] + n : n;
+      const uint32_t m16 = rowgroup_or(nib << (4 * g));   // rows 0..15 of the sub-slab, h = hw + 16t + col
+      bw[t] = HALF ? bw[t] | (m16 << 16) : m16;
     }
   }
+  const int hw = S::HW * w;
   if constexpr (HALF == 1) {
     const int t = lane >> 4;                           // h = hw + lane (lanes < HW)
     float sv = 0.0f, cv = 0.0f;
+    uint32_t mv = 0;
 #pragma unroll
     for (int k = 0; k < S::NT; ++k) {
       const float a = rowgroup_sum(ssum[k]);
@@ -431,11 +399,15 @@ __device__ __forceinline__ void ws_epilogue(const Ctx& C, const Job& J, int w, i
       if constexpr (!TEACHER) {
         const float c = rowgroup_sum(scnt[k]);
         cv = t == k ? c : cv;
+        mv = t == k ? bw[k] : mv;
       }
     }
     if (lane < S::HW) {
       C.part_sum[(size_t)J.sum_slab * DAD_H + hw + lane] = sv;
-      if constexpr (!TEACHER) C.part_cnt[(size_t)J.cnt_slab * DAD_H + hw + lane] = cv;
+      if constexpr (!TEACHER) {
+        C.part_cnt[(size_t)J.cnt_slab * DAD_H + hw + lane] = cv;
+        C.bits[(size_t)J.cnt_slab * DAD_H + hw + lane] = mv;
+      }
     }
   }
 }
@@ -445,7 +417,7 @@ __device__ __forceinline__ void ws_epilogue(const Ctx& C, const Job& J, int w, i
 template <class S>
 __device__ __forceinline__ constexpr int n_xs(int kind) { return kind == KIND_STRONG ? S::kXsRow * S::RPW : 0; }
 template <bool TEACHER, int HALF>
-__device__ __forceinline__ constexpr int n_epi() { return TEACHER ? HALF : 1 + 2 * HALF; }
+__device__ __forceinline__ constexpr int n_epi() { return TEACHER ? HALF : 3 * HALF; }
 
 template <int N>
 __device__ __forceinline__ void wait_vm_sw(int n) {
@@ -467,6 +439,7 @@ __device__ __forceinline__ void ws_loop(const Ctx& C, const int j0, const int Q,
                                         const float (&bh)[16 / WAVES], const float* fk, const uint32_t* vb) {
   using S = Shape<WAVES>;
   float ssum[S::NT], scnt[S::NT];
+  uint32_t bw[S::NT];
   const float* raw0 = reinterpret_cast<const float*>(smem + kOffRaw);
   const float* raw1 = reinterpret_cast<const float*>(smem + kOffRaw + kRawStage);
   char* tile0 = smem + kOffTile;
@@ -524,7 +497,7 @@ __device__ __forceinline__ void ws_loop(const Ctx& C, const int j0, const int Q,
     }
     const unsigned long long c3 = WS_CLK();
     const uint32_t vmask = (vb[q >> 1] >> (16 * H)) & 0xffffu;
-    ws_epilogue<S, TEACHER, H>(C, jobq(q), w, lane, vmask, bh, acc, ssum, scnt);
+    ws_epilogue<S, TEACHER, H>(C, jobq(q), w, lane, vmask, bh, acc, ssum, scnt, bw);
     const unsigned long long c4 = WS_CLK();
     dma(q + 3);
     const unsigned long long c5 = WS_CLK();

@@ -10,11 +10,11 @@
 //   FP32: regenerated exactly (same counter-RNG function, or re-read explicit noise);
 //   BF16: re-read from the bf16 copy the forward stored (the exact MFMA operand it used).
 //
-// Fused step (per_utt = 1): the loss-dependent scale factors out of the row sum,
+// FP32 fused step (per_utt = 1): the loss-dependent scale factors out of the row sum,
 //   dW1[h][:] = sum_u (dL/de_u[h] / len_u) * S_u[h][:],   S_u = bits_u^T X_u,
-// so the GEMM (S_u per utterance, G = 0/1 exact in bf16) runs as soon as the forward has
-// produced the bits -- concurrently with pool/tail/ECDA on a second stream -- and only the
-// streaming weighted sum dad_wsum remains on the critical path.
+// so the GEMM runs as soon as the forward has produced the bits (on a second stream) and
+// dad_wsum applies the scale.  BF16 fused step: dad_wgrad_direct after the losses, with the
+// scale folded into the A operand (one GEMM, no S_u round trip through HBM).
 #include "dad_common.h"
 #include "dad_kernels.h"
 
@@ -36,7 +36,7 @@ struct SlabIdx {
   int br, b, c, T;
   int erow;          // row of ge / vlen (clean b, or Bc + b)
   size_t row0;       // [b][T] row of frame 0
-  size_t bits_row;   // first row of this slab in the bits buffer
+  size_t bits_slab;  // slab index in the ReLU' row-mask buffer (= s)
 };
 __device__ __forceinline__ SlabIdx wg_slab(const DadWgradArgs& a, int s) {
   const DadGeom& g = a.g;
@@ -50,8 +50,7 @@ __device__ __forceinline__ SlabIdx wg_slab(const DadWgradArgs& a, int s) {
   r.T = r.br ? g.Tn : g.Tc;
   r.erow = r.br ? g.Bc + r.b : r.b;
   r.row0 = (size_t)r.b * r.T;
-  r.bits_row = r.br ? (size_t)g.Bc * g.tpc + (size_t)r.b * g.tpn + (size_t)r.c * DAD_SLAB
-                    : (size_t)r.b * g.tpc + (size_t)r.c * DAD_SLAB;
+  r.bits_slab = (size_t)s;
   return r;
 }
 
@@ -72,6 +71,24 @@ __device__ __forceinline__ void wg_range(const DadWgradArgs& a, int split, int& 
     s0 = split * per;
     s1 = min(total, s0 + per);
   }
+}
+
+// Fused step: dL/de of utterance row u (clean u < Bc, strong Bc + b), hidden unit h: the
+// classifier part keep(u,h) * sum_c W2[c][h] dL/dz[u][c] (nn.Linear + nn.Dropout backward,
+// I/model.py:62-63) plus the ECDA part where ECDA wrote the row.
+__device__ __forceinline__ float fused_ge1(const DadReduceArgs& a, int Bc, int u, int h, const float (&w2)[4],
+                                           float* kv_out = nullptr) {
+  const f32x4 gz = *reinterpret_cast<const f32x4*>(a.gzb + (size_t)u * DAD_C);
+  const bool strong = u >= Bc;
+  const int b = strong ? u - Bc : u;
+  const float kv = strong ? keep_value(a.keep2, a.key_drop2, b, h, a.p_drop, a.drop_scale)
+                          : keep_value(a.keep1, a.key_drop1, b, h, a.p_drop, a.drop_scale);
+  if (kv_out) *kv_out = kv;
+  const float z = ((w2[0] * gz[0] + w2[1] * gz[1]) + w2[2] * gz[2]) + w2[3] * gz[3];
+  // branch-free: the row is read whatever the flag (unflagged rows hold stale values), so a
+  // caller's loop over utterances keeps all its loads in flight
+  const float ec = a.ge_ecda[(size_t)u * DAD_H + h];
+  return z * kv + (a.eflag[u] ? ec : 0.0f);
 }
 
 }  // namespace
@@ -110,7 +127,10 @@ __global__ __launch_bounds__(DAD_WGRAD_THREADS) void dad_wgrad_f32(DadWgradArgs 
       st = a.mask_len > 0 ? wg_tstart(a, q.b) : 0;
       fkeep = wg_featkeep(a, d);
     }
-    const uint32_t* bw = a.bits + q.bits_row * DAD_HT;
+    // row masks of this lane's hidden units h = 32 ht + i (bit r = row r of the slab)
+    uint32_t mw[DAD_HT];
+#pragma unroll
+    for (int ht = 0; ht < DAD_HT; ++ht) mw[ht] = a.bits[q.bits_slab * DAD_H + ht * 32 + i];
     for (int rr = 0; rr < DAD_SLAB; rr += 2) {
       if (q.c * DAD_SLAB + rr >= q.T) break;
       const int t = q.c * DAD_SLAB + rr + kh;
@@ -123,12 +143,9 @@ __global__ __launch_bounds__(DAD_WGRAD_THREADS) void dad_wgrad_f32(DadWgradArgs 
         x = (x + sn) * fkeep;
         if (a.mask_len > 0 && t >= st && t < st + a.mask_len) x = 0.0f;
       }
-      const uint4 w0 = *reinterpret_cast<const uint4*>(bw + (rr + kh) * DAD_HT);
-      const uint4 w1 = *reinterpret_cast<const uint4*>(bw + (rr + kh) * DAD_HT + 4);
-      const uint32_t wds[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
 #pragma unroll
       for (int ht = 0; ht < DAD_HT; ++ht) {
-        const float g = ((wds[ht] >> i) & 1u) ? scale[ht] : 0.0f;
+        const float g = ((mw[ht] >> (rr + kh)) & 1u) ? scale[ht] : 0.0f;
         acc[ht] = __builtin_amdgcn_mfma_f32_32x32x2f32(g, x, acc[ht], 0, 0, 0);
       }
     }
@@ -142,13 +159,25 @@ __global__ __launch_bounds__(DAD_WGRAD_THREADS) void dad_wgrad_f32(DadWgradArgs 
 }
 
 // ------------------------------------------------------------ BF16 (throughput mode)
-// grid = 6 column blocks (128 d) x splits; workgroup tile 256 h x 128 d; wave w owns
-// h tiles {2w, 2w+1} x d tiles 0..3 (8 accumulators).  Per 32-row slab the workgroup
-// stages x (bf16, [32][128]) and G (bf16, [32][256]) row-major in LDS and the waves read
-// k-major fragments with ds_read_b64_tr_b16 (k = rows).  Row pitches are padded by 64 B
-// so the four rows of a transposed read land on disjoint bank quarters.
-#define WG_XP 160   // Xt row pitch (bf16 elements) = 320 B
-#define WG_GP 288   // Gt row pitch (bf16 elements) = 576 B
+// Direct split-K GEMM after the losses: dW1 = sum_rows G[row]^T x[row] with
+//   G[row][h] = ReLU'(row, h) * valid(row) * dL/de_u[h] / max(1, len_u)      (u = row's utterance)
+// One workgroup per (column block of WGD_DB d, split of the slab list); 4 waves, wave w owns
+// h tiles {2w, 2w+1} x both 32-wide d tiles.  Per 32-row slab:
+//   x (fp32 clean rows, or the encoder's bf16 strong rows) -> bf16 [32][WGD_DB] in LDS, read
+//     as k-major B fragments with ds_read_b64_tr_b16 (192-B row pitch: the four rows of a
+//     transposed read land on disjoint bank quarters);
+//   G is never staged: the slab's ReLU' row masks (one u32 per h, 1 KB) go to LDS, and a
+//     lane's A fragment (8 rows of one h) is byte (16 ks + 8 (lane/32)) of its h's mask,
+//     expanded through a 256-entry LDS table into four 0xFFFF/0 dword masks and AND-ed with
+//     bf16(dL/de_u[h] / len_u) in both halves: one table read and four ANDs per fragment.
+// dL/de_u[h] / len_u for the workgroup's utterances is rebuilt once in the prologue from the
+// tail's per-utterance dL/dz and ECDA's flagged rows (fused_ge1).  Slab loads run WGD_DEPTH
+// slabs ahead in registers and LDS is double-buffered: one barrier per slab.
+// Output: one f32 partial slab per split, summed in fixed order by dad_reduce.
+static_assert(DAD_WGRAD_THREADS == 256 && DAD_H == 256, "dad_wgrad_direct: thread = (row, 8 columns) and thread = h");
+static_assert(WGD_DB == 64 && DAD_D % WGD_DB == 0, "dad_wgrad_direct: 8 threads x 8 columns per row");
+static_assert(WGD_DEPTH % 2 == 0, "dad_wgrad_direct: LDS buffer = slab parity");
+namespace {
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
@@ -170,166 +199,238 @@ __device__ __forceinline__ bf16x8 tr_frag(const __bf16* tile, int pitch, int row
   return r;
 }
 
-// Per-thread registers for one slab in flight: 4 rows x 4 columns of x (fp32 clean rows or
-// the encoder's bf16 strong rows), one ReLU' bits word and the dL/de row scale.  Loads are
-// unconditional (row index clamped into the utterance) so the compiler can keep several
-// slabs outstanding with partial vmcnt waits; out-of-range rows are zeroed when staged.
-template <int BR> struct XRaw { using T = f32x4; };
-template <> struct XRaw<1> { using T = bf16x4; };
-template <int BR> struct SlabRegs {
-  typename XRaw<BR>::T x[4];
-  uint32_t word[4];   // ReLU' bits of rows (tid>>5)+8m, hidden units 8*(tid&31) .. +7 in byte (tid&3)
-  float ge, len;
-  int nvalid;
+// one slab in flight: thread t holds 8 consecutive columns of row t/8 and the ReLU' row
+// mask of h = t; the slab's utterance slot and valid row count are wave-uniform
+template <int BR> struct WgdSlab {
+  f32x4 x[2];
+  uint32_t word;
+  int ul, nvalid;
+};
+template <> struct WgdSlab<1> {
+  bf16x8 x;
+  uint32_t word;
+  int ul, nvalid;
+};
+
+// slab cursor of one branch: (utterance b, slab c), advanced incrementally
+struct WgdCursor {
+  int s, b, c;
 };
 
 template <int BR>
-__device__ __forceinline__ void wg_load(const DadWgradArgs& a, int s, int dbase, SlabRegs<BR>& r) {
+__device__ __forceinline__ void wgd_load(const DadWgradArgs& a, const WgdCursor& q, int u0, int dbase,
+                                         WgdSlab<BR>& r) {
   const DadGeom& g = a.g;
   const int tid = threadIdx.x;
-  const int nc = BR ? g.ncn : g.ncc, T = BR ? g.Tn : g.Tc;
-  const int b = s / nc, c = s - b * nc;
-  const int erow = BR ? g.Bc + b : b;
-  const size_t bits_row = BR ? (size_t)g.Bc * g.tpc + (size_t)b * g.tpn + (size_t)c * DAD_SLAB
-                             : (size_t)b * g.tpc + (size_t)c * DAD_SLAB;
-  r.nvalid = T - c * DAD_SLAB;
-  const int col = (tid & 31) * 4;
-#pragma unroll
-  for (int m = 0; m < 4; ++m) {
-    const int t = min(c * DAD_SLAB + (tid >> 5) + 8 * m, T - 1);
-    const size_t off = ((size_t)b * T + t) * DAD_D + dbase + col;
-    if constexpr (BR == 0) r.x[m] = *reinterpret_cast<const f32x4*>(a.xc + off);
-    else r.x[m] = *reinterpret_cast<const bf16x4*>(a.xs_bf16 + off);
-  }
-#pragma unroll
-  for (int m = 0; m < 4; ++m) r.word[m] = a.bits[(bits_row + (tid >> 5) + 8 * m) * DAD_HT + ((tid & 31) >> 2)];
-  if (a.per_utt) {
-    r.ge = 1.0f;
-    r.len = 1.0f;
+  const int T = BR ? g.Tn : g.Tc;
+  const int row = tid >> 3;
+  const int t = min(q.c * DAD_SLAB + row, T - 1);
+  const size_t off = ((size_t)q.b * T + t) * DAD_D + dbase + (tid & 7) * 8;
+  const size_t bits_slab = BR ? (size_t)g.Bc * g.ncc + (size_t)q.b * g.ncn + q.c : (size_t)q.b * g.ncc + q.c;
+#ifdef DAD_PROBE_WGD_NOMEM
+  // diagnostic build only: no HBM traffic in the slab loop
+  const float fx = (float)(off & 1023);
+  if constexpr (BR == 0) { r.x[0] = f32x4{fx, fx, fx, fx}; r.x[1] = r.x[0]; }
+  else for (int e = 0; e < 8; ++e) r.x[e] = (__bf16)fx;
+  r.word = (uint32_t)(bits_slab * 2654435761u);
+#else
+  if constexpr (BR == 0) {
+    r.x[0] = *reinterpret_cast<const f32x4*>(a.xc + off);
+    r.x[1] = *reinterpret_cast<const f32x4*>(a.xc + off + 4);
   } else {
-    r.ge = a.ge[(size_t)erow * DAD_H + tid];
-    r.len = a.vlen[erow];
+    r.x = *reinterpret_cast<const bf16x8*>(a.xs_bf16 + off);
+  }
+  r.word = a.bits[bits_slab * DAD_H + tid];
+#endif
+  r.ul = (BR ? g.Bc + q.b : q.b) - u0;
+  r.nvalid = T - q.c * DAD_SLAB;
+}
+
+__device__ __forceinline__ void wgd_advance(WgdCursor& q, int nc, int last) {
+  if (q.s < last) {
+    ++q.s;
+    if (++q.c == nc) { q.c = 0; ++q.b; }
   }
 }
 
 template <int BR>
-__device__ __forceinline__ void wg_stage(const SlabRegs<BR>& r, __bf16* Xt, __bf16* Gt, float* sc) {
+__device__ __forceinline__ void wgd_stage(const WgdSlab<BR>& r, __bf16* Xt, uint32_t* bt) {
   const int tid = threadIdx.x;
-  const int col = (tid & 31) * 4;
-#pragma unroll
-  for (int m = 0; m < 4; ++m) {
-    const bool ok = (tid >> 5) + 8 * m < r.nvalid;
-    bf16x4 v;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = ok ? (__bf16)r.x[m][e] : (__bf16)0.0f;
-    *reinterpret_cast<bf16x4*>(&Xt[((tid >> 5) + 8 * m) * WG_XP + col]) = v;
-  }
-  sc[tid] = r.ge / fmaxf(r.len, 1.0f);
-  __syncthreads();
-  // G rows: 32 consecutive lanes write one 512-B row (conflict-free ds_write_b128)
-  const int c16 = tid & 31;
-  const f32x4 lo = reinterpret_cast<const f32x4*>(sc)[2 * c16];
-  const f32x4 hi = reinterpret_cast<const f32x4*>(sc)[2 * c16 + 1];
-#pragma unroll
-  for (int m = 0; m < 4; ++m) {
-    const uint32_t byte = r.word[m] >> ((c16 & 3) * 8);
-    bf16x8 gv;
+  const int row = tid >> 3;
+  const bool ok = row < r.nvalid;
+  bf16x8 v;
+  if constexpr (BR == 0) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      gv[e] = (__bf16)(((byte >> e) & 1u) ? lo[e] : 0.0f);
-      gv[e + 4] = (__bf16)(((byte >> (e + 4)) & 1u) ? hi[e] : 0.0f);
+      v[e] = (__bf16)(ok ? r.x[0][e] : 0.0f);
+      v[e + 4] = (__bf16)(ok ? r.x[1][e] : 0.0f);
     }
-    *reinterpret_cast<bf16x8*>(&Gt[((tid >> 5) + 8 * m) * WG_GP + c16 * 8]) = gv;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = ok ? r.x[e] : (__bf16)0.0f;
   }
+  *reinterpret_cast<bf16x8*>(&Xt[row * WGD_XP + (tid & 7) * 8]) = v;
+  bt[tid] = r.word;
 }
 
-__device__ __forceinline__ void wg_compute(const __bf16* Xt, const __bf16* Gt, int wv, f32x16 (&acc)[2][4]) {
+// A fragment of h tile ht, k rows 16 ks + 8 (lane/32) + 0..7: bit ? gb : 0 (bf16 bits).
+// lut[b] = the 0xFFFF/0 halfword masks of the 8 bits of b.
+__device__ __forceinline__ bf16x8 wgd_afrag(uint32_t mask, const uint4* lut, int ks, uint32_t gpair) {
+  const int lane = threadIdx.x & 63;
+#ifdef DAD_PROBE_WGD_NOAFRAG
+  const uint4 m = uint4{mask, mask >> 1, mask >> 2, mask >> 3};
+  (void)lut; (void)lane; (void)ks;
+#else
+  const uint4 m = lut[(mask >> (16 * ks + 8 * (lane >> 5))) & 0xffu];
+#endif
+  return __builtin_bit_cast(bf16x8, uint4{m.x & gpair, m.y & gpair, m.z & gpair, m.w & gpair});
+}
+
+__device__ __forceinline__ void wgd_compute(const __bf16* Xt, const uint32_t* bt, const uint4* lut,
+                                            const uint16_t* gs, int ul, int wv, f32x16 (&acc)[2][2]) {
+  const int i = threadIdx.x & 31;
+  uint32_t gp[2], mk[2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    const uint32_t gb = gs[ul * DAD_H + (2 * wv + m) * 32 + i];
+    gp[m] = gb | (gb << 16);
+    mk[m] = bt[(2 * wv + m) * 32 + i];
+  }
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
-    bf16x8 af[2], bfr[4];
+    bf16x8 af[2], bfr[2];
 #pragma unroll
-    for (int m = 0; m < 2; ++m) af[m] = tr_frag(Gt, WG_GP, 16 * ks, 32 * (2 * wv + m));
+    for (int n = 0; n < 2; ++n) bfr[n] = tr_frag(Xt, WGD_XP, 16 * ks, 32 * n);
 #pragma unroll
-    for (int n = 0; n < 4; ++n) bfr[n] = tr_frag(Xt, WG_XP, 16 * ks, 32 * n);
+    for (int m = 0; m < 2; ++m) af[m] = wgd_afrag(mk[m], lut, ks, gp[m]);
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
-      for (int n = 0; n < 4; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[m], bfr[n], acc[m][n], 0, 0, 0);
+      for (int n = 0; n < 2; ++n)
+        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[m], bfr[n], acc[m][n], 0, 0, 0);
   }
 }
 
-// slabs [lo, hi) of one branch; three slabs in flight in registers while the current one
-// is in LDS (the grid is ~one workgroup per CU, so memory-level parallelism has to come
-// from inside the workgroup)
+// slabs [lo, hi) of one branch (branch-local slab indices)
 template <int BR>
-__device__ __forceinline__ void wg_phase(const DadWgradArgs& a, int lo, int hi, int dbase, __bf16* Xt, __bf16* Gt,
-                                         float* sc, f32x16 (&acc)[2][4]) {
+__device__ __forceinline__ void wgd_phase(const DadWgradArgs& a, int lo, int hi, int u0, int dbase, __bf16* Xt,
+                                          uint32_t* bt, const uint4* lut, const uint16_t* gs, f32x16 (&acc)[2][2]) {
   if (lo >= hi) return;
   const int wv = threadIdx.x >> 6;
-  SlabRegs<BR> r0, r1, r2;
-  // prefetches are unconditional (slab index clamped to the last one): conditional loads
-  // make the compiler merge the paths' pending counts into a vmcnt(0) drain
+  const int nc = BR ? a.g.ncn : a.g.ncc;
   const int last = hi - 1;
-  wg_load<BR>(a, lo, dbase, r0);
-  wg_load<BR>(a, min(lo + 1, last), dbase, r1);
-  wg_load<BR>(a, min(lo + 2, last), dbase, r2);
-  for (int s = lo; s < hi; s += 3) {
-    __syncthreads();                 // previous compute finished reading Xt/Gt/sc
-    wg_stage<BR>(r0, Xt, Gt, sc);
-    wg_load<BR>(a, min(s + 3, last), dbase, r0);
-    __syncthreads();
-    wg_compute(Xt, Gt, wv, acc);
-    if (s + 1 >= hi) break;
-    __syncthreads();
-    wg_stage<BR>(r1, Xt, Gt, sc);
-    wg_load<BR>(a, min(s + 4, last), dbase, r1);
-    __syncthreads();
-    wg_compute(Xt, Gt, wv, acc);
-    if (s + 2 >= hi) break;
-    __syncthreads();
-    wg_stage<BR>(r2, Xt, Gt, sc);
-    wg_load<BR>(a, min(s + 5, last), dbase, r2);
-    __syncthreads();
-    wg_compute(Xt, Gt, wv, acc);
+  WgdCursor q;
+  q.s = lo; q.b = lo / nc; q.c = lo - q.b * nc;
+  WgdSlab<BR> r[WGD_DEPTH];
+  // loads are unconditional (cursor clamped at the last slab): conditional loads make the
+  // compiler merge the paths' pending counts into a vmcnt(0) drain
+#pragma unroll
+  for (int k = 0; k < WGD_DEPTH; ++k) {
+    wgd_load<BR>(a, q, u0, dbase, r[k]);
+    wgd_advance(q, nc, last);
   }
+  auto slot = [&](int k) {
+    __bf16* X = Xt + (k & 1) * (DAD_SLAB * WGD_XP);   // WGD_DEPTH even: buffer = slab parity
+    uint32_t* B = bt + (k & 1) * DAD_H;
+    wgd_stage<BR>(r[k], X, B);
+    const int ul = r[k].ul;
+    wgd_load<BR>(a, q, u0, dbase, r[k]);
+    wgd_advance(q, nc, last);
+    __syncthreads();
+#ifndef DAD_PROBE_WGD_NOCOMP
+    wgd_compute(X, B, lut, gs, ul, wv, acc);
+#else
+    (void)ul; (void)wv;
+#endif
+  };
+  // whole rounds of WGD_DEPTH slabs without early exits (an exit inside the round would
+  // reach the loop header with a different load order and force vmcnt(0) there), then the
+  // remainder
+  int s = lo;
+  for (; s + WGD_DEPTH <= hi; s += WGD_DEPTH) {
+#pragma unroll
+    for (int k = 0; k < WGD_DEPTH; ++k) slot(k);
+  }
+#pragma unroll
+  for (int k = 0; k < WGD_DEPTH - 1; ++k)
+    if (s + k < hi) slot(k);
 }
 
-__global__ __launch_bounds__(DAD_WGRAD_THREADS, 1) void dad_wgrad_bf16(DadWgradArgs a) {
+__device__ __forceinline__ int wgd_utt(const DadGeom& g, int s) {
+  const int nsc = g.Bc * g.ncc;
+  return s < nsc ? s / g.ncc : g.Bc + (s - nsc) / g.ncn;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(DAD_WGRAD_THREADS, 1) void dad_wgrad_direct(DadWgradArgs a, DadReduceArgs ra) {
   DAD_GUARD_BLOCK(DAD_WGRAD_THREADS);
-  __shared__ __attribute__((aligned(16))) __bf16 Xt[DAD_SLAB * WG_XP];
-  __shared__ __attribute__((aligned(16))) __bf16 Gt[DAD_SLAB * WG_GP];
-  __shared__ __attribute__((aligned(16))) float sc[DAD_H];
+  __shared__ __attribute__((aligned(16))) __bf16 Xt[2 * DAD_SLAB * WGD_XP];
+  __shared__ __attribute__((aligned(16))) uint32_t bt[2 * DAD_H];
+  __shared__ __attribute__((aligned(16))) uint4 lut[256];
+  __shared__ __attribute__((aligned(16))) uint16_t gs[WGD_MAXU * DAD_H];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wv = tid >> 6;
+  // XCD-aware tile order (grid is a multiple of 8; workgroups go round-robin over the 8
+  // XCDs): each XCD takes a consecutive run of tiles, so the column blocks of one split,
+  // which read the same ReLU' words, share an L2
+  const int per_xcd = gridDim.x >> 3;
+  const int tile = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+  if (tile >= a.ntiles) return;
+  const int split = tile / WGD_NDB, dblk = tile - split * WGD_NDB;
+  const int dbase = dblk * WGD_DB;
+  const DadGeom& g = a.g;
+  const int total = wg_total(a);
+  const int per = (total + a.splits - 1) / a.splits;
+  const int s0 = split * per, s1 = min(total, s0 + per);
+  const int nsc = g.Bc * g.ncc;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) acc[m][n] = f32x16{};
+  if (s0 < s1) {
+    // dL/de_u[h] / max(1, len_u) of this split's utterances (thread = h), as bf16; the
+    // host bounds a split to WGD_MAXU slabs, hence utterances
+    const int u0 = wgd_utt(g, s0), nu = wgd_utt(g, s1 - 1) - u0 + 1;
+    const float w2[4] = {ra.student[DAD_OFF_W2 + tid], ra.student[DAD_OFF_W2 + DAD_H + tid],
+                         ra.student[DAD_OFF_W2 + 2 * DAD_H + tid], ra.student[DAD_OFF_W2 + 3 * DAD_H + tid]};
+    for (int ul0 = 0; ul0 < nu; ul0 += 8) {
+      float v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {   // eight utterances' loads in flight (index clamped)
+        const int u = u0 + min(ul0 + k, nu - 1);
+        v[k] = fused_ge1(ra, g.Bc, u, tid, w2) / fmaxf(ra.vlen[u], 1.0f);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (ul0 + k < nu) gs[(ul0 + k) * DAD_H + tid] = __builtin_bit_cast(uint16_t, (__bf16)v[k]);
+    }
+    {
+      uint32_t e[4];
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+        e[p] = (((tid >> (2 * p)) & 1) ? 0x0000ffffu : 0u) | (((tid >> (2 * p + 1)) & 1) ? 0xffff0000u : 0u);
+      lut[tid] = uint4{e[0], e[1], e[2], e[3]};
+    }
+    // (the slab loop's first barrier orders these writes before the first read)
+    wgd_phase<0>(a, s0, min(s1, nsc), u0, dbase, Xt, bt, lut, gs, acc);
+    if (s1 > nsc) {
+      __syncthreads();   // the clean phase's last compute is done with its LDS buffer
+      wgd_phase<1>(a, max(s0, nsc) - nsc, s1 - nsc, u0, dbase, Xt, bt, lut, gs, acc);
+    }
+  }
+  float* out = a.wpart + (size_t)split * DAD_H * DAD_D;
   const int kh = lane >> 5;
-  const int nsc = a.g.Bc * a.g.ncc;
-  // workgroups stride over (utterance or split) x column-block tiles; a grid smaller than
-  // the tile count leaves CUs free for concurrent work on the caller's stream
-  for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
-  const int dblk = tile % 6, split = tile / 6;
-  const int dbase = dblk * 128;
-  int s0, s1;
-  wg_range(a, split, s0, s1);
-  f32x16 acc[2][4];
 #pragma unroll
   for (int m = 0; m < 2; ++m)
 #pragma unroll
-    for (int n = 0; n < 4; ++n) acc[m][n] = f32x16{};
-  wg_phase<0>(a, s0, min(s1, nsc), dbase, Xt, Gt, sc, acc);
-  wg_phase<1>(a, max(s0, nsc) - nsc, s1 - nsc, dbase, Xt, Gt, sc, acc);
-  const size_t obase = (size_t)split * DAD_H * DAD_D;
-#pragma unroll
-  for (int m = 0; m < 2; ++m)
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
+    for (int n = 0; n < 2; ++n)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int h = (2 * wv + m) * 32 + dad_acc_row(r, kh);
-        const int d = dbase + 32 * n + (lane & 31);
-        if (a.wpart_bf16) a.wpart_bf16[obase + (size_t)h * DAD_D + d] = (__bf16)acc[m][n][r];
-        else a.wpart[obase + (size_t)h * DAD_D + d] = acc[m][n][r];
+        out[(size_t)h * DAD_D + dbase + 32 * n + (lane & 31)] = acc[m][n][r];
       }
-  }
 }
 
 // ---------------------------------------------------------------- reduce + squared norms
@@ -341,23 +442,6 @@ __global__ __launch_bounds__(DAD_WGRAD_THREADS, 1) void dad_wgrad_bf16(DadWgradA
 // (I/train.py:462-466).  Thread = (hidden unit hl, row group rg): rows rg, rg+16, ...;
 // the 16 row groups are combined in fixed order (deterministic).
 static_assert(DAD_REDUCE_THREADS == 256 && DAD_H == 16 * DAD_REDUCE_XBLK, "extra blocks: 16 h x 16 row groups");
-
-// Fused step: dL/de of utterance row u (clean u < Bc, strong Bc + b), hidden unit h: the
-// classifier part keep(u,h) * sum_c W2[c][h] dL/dz[u][c] (nn.Linear + nn.Dropout backward,
-// I/model.py:62-63) plus the ECDA part where ECDA wrote the row.
-__device__ __forceinline__ float fused_ge1(const DadReduceArgs& a, int Bc, int u, int h, const float (&w2)[4],
-                                           float* kv_out = nullptr) {
-  const f32x4 gz = *reinterpret_cast<const f32x4*>(a.gzb + (size_t)u * DAD_C);
-  const bool strong = u >= Bc;
-  const int b = strong ? u - Bc : u;
-  const float kv = strong ? keep_value(a.keep2, a.key_drop2, b, h, a.p_drop, a.drop_scale)
-                          : keep_value(a.keep1, a.key_drop1, b, h, a.p_drop, a.drop_scale);
-  if (kv_out) *kv_out = kv;
-  const float z = ((w2[0] * gz[0] + w2[1] * gz[1]) + w2[2] * gz[2]) + w2[3] * gz[3];
-  float g = z * kv;
-  if (a.eflag[u]) g += a.ge_ecda[(size_t)u * DAD_H + h];
-  return g;
-}
 
 __device__ double extra_block(const DadReduceArgs& a, int e) {
   __shared__ float xs[16][16][6];
@@ -465,11 +549,11 @@ __global__ __launch_bounds__(DAD_REDUCE_THREADS) void dad_reduce(DadReduceArgs a
   }
 }
 
-// Fused-step weight-gradient finish: dW1[h][d] = sum_u g_u[h] * S_u[h][d],
+// FP32 fused-step weight-gradient finish: dW1[h][d] = sum_u g_u[h] * S_u[h][d],
 // g_u[h] = dL/de_u[h] / max(1, len_u).  Blocks [0, NB): DAD_REDUCE_COLS columns of one
 // row h; thread = (float4 column, utterance group ug), utterances ug, ug+4, ... with eight
-// loads in flight, the four groups combined in fixed order (deterministic).  Block NB:
-// db1, W2/b2 norm share, loss totals.  Every block: its squared-norm partial.
+// loads in flight, the four groups combined in fixed order (deterministic).  Blocks NB + e:
+// db1, dW2, norm shares, loss totals (extra_block).  Every block: its squared-norm partial.
 static_assert(DAD_D % DAD_REDUCE_COLS == 0, "dad_wsum: whole blocks per dW1 row");
 __global__ __launch_bounds__(DAD_REDUCE_THREADS) void dad_wsum(DadReduceArgs a) {
   DAD_GUARD_BLOCK(DAD_REDUCE_THREADS);
@@ -495,23 +579,10 @@ __global__ __launch_bounds__(DAD_REDUCE_THREADS) void dad_wsum(DadReduceArgs a) 
     f32x4 s = f32x4{};
     for (int u0 = ug; u0 < nutt; u0 += 4 * 8) {
       f32x4 v[8];
-      if (a.wpart_bf16) {
-        bf16x4 vb[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const int u = min(u0 + 4 * k, nutt - 1);
-          vb[k] = *reinterpret_cast<const bf16x4*>(a.wpart_bf16 + (size_t)u * DAD_H * DAD_D + off);
-        }
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[k][e] = (float)vb[k][e];
-      } else {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const int u = min(u0 + 4 * k, nutt - 1);
-          v[k] = *reinterpret_cast<const f32x4*>(a.wpart + (size_t)u * DAD_H * DAD_D + off);
-        }
+      for (int k = 0; k < 8; ++k) {
+        const int u = min(u0 + 4 * k, nutt - 1);
+        v[k] = *reinterpret_cast<const f32x4*>(a.wpart + (size_t)u * DAD_H * DAD_D + off);
       }
 #pragma unroll
       for (int k = 0; k < 8; ++k)

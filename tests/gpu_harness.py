@@ -106,22 +106,3 @@ def close(a, b, tol, what):
         raise AssertionError("%s: rel %.3e (tol %.1e) at %d: got %.9g want %.9g; max|want| %.6g; "
                              "n_bad(>tol) %d/%d" % (what, r, tol, i, a[i], b[i], np.abs(b).max(),
                                                     int((err > tol * np.abs(b).max()).sum()), a.size))
-
-
-def ws_ge(step, Bc, Tc, Bn, Tn):
-    """dL/de rows [Bc+Bn][256] from the step's workspace (mirror of dad_ws_layout): CE/KL
-    part + ECDA part."""
-    al = lambda x: (x + 255) & ~255
-    ncc, ncn = (Tc + 31) // 32, (Tn + 31) // 32
-    tpc, tpn = ncc * 32, ncn * 32
-    off = 0
-    off = al(off + 4 * (Bc * ncc + 2 * Bn * ncn) * 256)      # part_sum
-    off = al(off + 4 * (Bc * ncc + Bn * ncn) * 256)          # part_cnt
-    off = al(off + 4 * (Bc * tpc + Bn * tpn) * 8)            # bits
-    off = al(off + 4 * (Bc + Bn))                            # vlen
-    off = al(off + 4 * (Bc + Bn) * 256)                      # cnt_tot
-    ws = step._ws
-    n = 4 * (Bc + Bn) * 256
-    ge = ws[off:off + n].view(torch.float32).view(Bc + Bn, 256).cpu().numpy()
-    off_e = al(off + n)                                      # ge_ecda (zeros where ECDA wrote nothing)
-    return ge + ws[off_e:off_e + n].view(torch.float32).view(Bc + Bn, 256).cpu().numpy()
