@@ -34,6 +34,9 @@ METRIC = "utterances/sec (DAD train step) batch=64 at 1/2/4/8 MI355X; loss parit
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BF16_PEAK_TFLOPS = 2500.0      # dense bf16 MFMA
 FP32_PEAK_TFLOPS = 157.3       # f32 MFMA == f32 vector rate
+EVENT_EVERY = 4                # timed steps per encoder event pair
+CPU_BASELINE_SECONDS = 15.0    # bounded CPU sample (oracle steps until this much CPU time)
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_latest.json")   # tools/profile_report.py --json
 
 
 def init_model_weights(model, seed, margin=5.0):
@@ -74,8 +77,20 @@ def make_batches(P, n, B, T, seed, device, snr_db=5.0):
     return out
 
 
-def cpu_baseline(B, T, steps, epoch):
-    """The NumPy oracle (CPU restatement of the reference step) on this host's cores."""
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC summary (FETCH_SIZE x 2 + WRITE_SIZE,
+    MI355X_MICROARCH.md corrections), or None when no summary covers it."""
+    try:
+        d = json.load(open(PMC_SUMMARY))
+        k = d["kernels"][kernel]
+        return float(k["hbm_bytes_per_launch"]), d.get("source", PMC_SUMMARY)
+    except Exception:
+        return None, None
+
+
+def cpu_baseline(B, T, steps, epoch, seconds=CPU_BASELINE_SECONDS):
+    """The NumPy oracle (CPU restatement of the reference step) on this host's cores: at least
+    `steps` steps after one warm-up, continuing until `seconds` of steps have run."""
     from oracle import dad_oracle, synth
     try:
         import threadpoolctl
@@ -88,16 +103,18 @@ def cpu_baseline(B, T, steps, epoch):
     orc = dad_oracle.DADOracle(W1, b1, W2, b2, cfg)
     rng = np.random.default_rng(0)
     times = []
-    for k in range(steps + 1):
+    k = 0
+    while k < steps + 1 or (sum(times[1:]) < seconds and k < 200):
         inp = synth.make_step_inputs(0, k, B, T, ragged=False)
         inp = {n: inp[n] for n in ("xc", "mc", "yc", "xn", "mn", "yn")}    # draws sampled inside (like randn)
         t0 = time.perf_counter()
         orc.step(inp, epoch, rng=rng)
         times.append(time.perf_counter() - t0)
+        k += 1
     med = statistics.median(times[1:])
     return {"value": B / med, "unit": "utterances/s", "cores": int(cores), "kind": "port",
-            "sample": "%d steps (after 1 warm-up) of the NumPy oracle DAD step, B=%d T=%d epoch %d incl. "
-                      "noise sampling; median %.3f s/step" % (steps, B, T, epoch, med)}
+            "sample": "%d steps (after 1 warm-up, %.1f s) of the NumPy oracle DAD step, B=%d T=%d epoch %d incl. "
+                      "noise sampling; median %.3f s/step" % (len(times) - 1, sum(times[1:]), B, T, epoch, med)}
 
 
 def main():
@@ -134,8 +151,11 @@ def main():
     torch.cuda.synchronize()
 
     def run(n, events=None):
-        step.kernel_events = events
+        # encoder-launch events on every EVENT_EVERY-th step of the timed region only: a
+        # timing event pair costs a few microseconds of stream time, which would otherwise
+        # be charged to every step
         for i in range(n):
+            step.kernel_events = events if (events is not None and i % EVENT_EVERY == 0) else None
             c, nb = data[i % len(data)]
             step.step(c, nb, args.epoch)
         step.kernel_events = None
@@ -184,6 +204,8 @@ def main():
     flops = 2 * 768 * 256 * (2 * rows + 3 * rows)       # 5 encoder-sized contractions / step
     peak_tf = BF16_PEAK_TFLOPS if args.precision == "bf16" else FP32_PEAK_TFLOPS
     t_roof = max(flops / (peak_tf * 1e12), enc_bytes / (HBM_PEAK_GBS * 1e9))
+    enc_kernel = "dad_encode_ws" if args.precision == "bf16" else "dad_encode_f32"
+    traffic, traffic_src = pmc_traffic(enc_kernel)
     line = {
         "metric": METRIC, "value": value, "unit": "utterances/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
@@ -193,9 +215,9 @@ def main():
                                "counter-RNG augmentation in-kernel" % args.epoch,
                    "global_batch": B * world, "per_gpu_batch": B, "seq_len": T, "feature_dim": 768,
                    "parallelism": "dp%d" % world},
-        "roofline": {"bound": "hbm", "kernel": "dad_encode_%s" % args.precision, "achieved": enc_gbs,
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": enc_gbs / HBM_PEAK_GBS, "traffic": None,
-                     "avg_launch_ms": enc_ms, "algorithmic_bytes_per_launch": enc_bytes},
+        "roofline": {"bound": "hbm", "kernel": enc_kernel, "achieved": enc_gbs,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": enc_gbs / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_source": traffic_src, "avg_launch_ms": enc_ms, "algorithmic_bytes_per_launch": enc_bytes},
         "step_roofline": {"t_roof_us": t_roof * 1e6, "t_step_us": ms * 1e3, "frac": t_roof / (ms * 1e-3),
                           "flops_per_step": flops, "bytes_per_step": enc_bytes, "mfma_peak_tflops": peak_tf},
         "losses_last_step": losses, "mask_sum_last_step": msum,

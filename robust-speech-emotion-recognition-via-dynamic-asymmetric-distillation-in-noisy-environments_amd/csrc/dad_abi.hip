@@ -307,7 +307,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
     wa.wpart = ws_ptr<float>(workspace, L.wpart);
     wa.ntiles = WGD_NDB * splits;
     const int grid = (wa.ntiles + 7) / 8 * 8;   // multiple of 8: XCD-aware tile order
-    hipLaunchKernelGGL(dad_wgrad_direct, dim3(grid), dim3(DAD_WGRAD_THREADS), 0, stream, wa, ra);
+    hipLaunchKernelGGL(dad_wgrad_direct, dim3(grid), dim3(WGD_THREADS), 0, stream, wa, ra);
     DAD_TRY(hipGetLastError());
     ra.splits = splits; ra.wpart = wa.wpart;
     hipLaunchKernelGGL(dad_reduce, dim3(DAD_REDUCE_BLOCKS), dim3(DAD_REDUCE_THREADS), 0, stream, ra);

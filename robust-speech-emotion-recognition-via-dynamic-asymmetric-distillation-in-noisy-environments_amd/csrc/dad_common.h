@@ -209,7 +209,7 @@ struct DadWs {
   size_t wpart;      // f32 [S][H][D]               split-K weight-gradient partial slabs
   size_t normpart;   // f32 [DAD_NORM_BLOCKS]       squared-norm partials
   size_t ecda;       // f32 [C][Bc+Bn][Bc+Bn]       ECDA pairwise scratch for large member sets
-  size_t xs_bf16;    // bf16 [Bn][Tn][768]          BF16 mode: strong-augmented input (wgrad operand)
+  size_t xs_bf16;    // bf16 [Bc*Tc + Bn*Tn][768]   BF16 mode: the student's MFMA input, clean rows then strong rows (wgrad operand)
   size_t w1bf;       // bf16 [H][D]                 modular encoder ops: bf16 copy of W1
   size_t gflat;      // f32 [DAD_GRAD_FLOATS]       modular encoder backward: scratch grad vector
   size_t sbuf;       // f32 [Bc + Bn][H][D]         FP32 step: S_u = bits_u^T X_u, the loss-independent factor of dW1
@@ -251,7 +251,7 @@ static inline DadWs dad_ws_layout(const DadGeom& g, int splits, int precision, b
   w.wpart = off;    off = dad_align(off + sizeof(float) * (size_t)splits * DAD_H * DAD_D);
   w.normpart = off; off = dad_align(off + sizeof(float) * DAD_NORM_BLOCKS);
   w.ecda = off;     off = dad_align(off + sizeof(float) * DAD_C * nb * nb);
-  w.xs_bf16 = off;  off = dad_align(off + (precision == DAD_PREC_BF16 ? 2 * (size_t)g.Bn * g.Tn * DAD_D : 0));
+  w.xs_bf16 = off;  off = dad_align(off + (precision == DAD_PREC_BF16 ? 2 * ((size_t)g.Bc * g.Tc + (size_t)g.Bn * g.Tn) * DAD_D : 0));
   w.w1bf = off;     off = dad_align(off + 2 * (size_t)DAD_H * DAD_D);
   w.gflat = off;    off = dad_align(off + sizeof(float) * DAD_GRAD_FLOATS);
   w.sbuf = off;     off = dad_align(off + (fused && precision != DAD_PREC_BF16 ? sizeof(float) * nb * DAD_H * DAD_D : 0));

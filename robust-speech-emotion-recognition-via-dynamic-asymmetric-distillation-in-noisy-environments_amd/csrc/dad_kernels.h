@@ -12,12 +12,13 @@
 #define DAD_ECDA_THREADS 512
 #define DAD_WGRAD_THREADS 256
 // dad_wgrad_direct (BF16): 64-column blocks, slab-range splits of at most WGD_MAXU slabs,
-// WGD_DEPTH slabs in flight per workgroup, x tile row pitch WGD_XP bf16 (192 B)
+// WGD_DEPTH slabs in flight per group, x tile row pitch WGD_XP bf16 (192 B)
 #define WGD_DB 64
 #define WGD_NDB (DAD_D / WGD_DB)
 #define WGD_MAXU 64
 #define WGD_DEPTH 4
 #define WGD_XP 96
+#define WGD_THREADS 512   // two groups of 4 waves, one slab each per round (two waves per SIMD)
 #define DAD_REDUCE_THREADS 256
 #define DAD_REDUCE_COLS 256                                  // dW1 floats per reduce block
 #define DAD_REDUCE_XBLK 16                                   // db1 / dW2 / totals blocks (16 hidden units each)
@@ -39,7 +40,7 @@ struct DadEncodeArgs {
   uint32_t key_weak, key_strong, key_feat, key_tstart;
   float weak_std, strong_std, feat_p;
   float* part_sum; float* part_cnt; uint32_t* bits;
-  __bf16* xs_bf16;          // BF16 mode: strong-augmented input as fed to the MFMA (for wgrad)
+  __bf16* xs_bf16;          // BF16 mode: the student's MFMA input, clean rows then strong rows (for wgrad)
   int ws_nt, ws_ns;         // dad_encode_ws: teacher / student workgroups
   float ws_wstrong;         // dad_encode_ws: cost of a strong slab relative to a clean one
 };

@@ -5,7 +5,8 @@
 //   teacher_encoder(weak_augment(noisy))           + DataAugmentation.weak_augment, I/utils.py:328-331
 //   student_encoder(strong_augment(noisy))         + strong_augment/_apply_temporal_masking, I/utils.py:333-375
 // and emits what the rest of the step consumes: per-32-row-slab pooled ReLU sums and active
-// counts, the ReLU'-and-valid bit mask, and the bf16 strong-augmented input (wgrad operand).
+// counts, the ReLU'-and-valid row masks, and the bf16 student inputs (clean and strong-augmented
+// rows, the weight gradient's operand).
 //
 // Shape of the work: out[rows][256] = x[rows][768] . W1^T with tens of thousands of rows and
 // W1 only 384 KB in bf16.  So W1 is STATIONARY: a persistent workgroup holds all 256 hidden
@@ -80,7 +81,8 @@ struct Ctx {
   const float* nw; const float* ns; const float* u; const int64_t* start;
   uint32_t key_weak, key_strong, key_feat, key_tstart;
   float wstd, sstd, feat_p;
-  float* part_sum; float* part_cnt; uint32_t* bits; __bf16* xs;
+  float* part_sum; float* part_cnt; uint32_t* bits;
+  __bf16* xs; __bf16* xsn;   // bf16 copies of the student's MFMA input: clean rows, strong rows
 };
 
 __device__ __forceinline__ Ctx ctx_of(const DadEncodeArgs& a) {
@@ -96,7 +98,8 @@ __device__ __forceinline__ Ctx ctx_of(const DadEncodeArgs& a) {
   c.nw = a.nw; c.ns = a.ns; c.u = a.u; c.start = a.start;
   c.key_weak = a.key_weak; c.key_strong = a.key_strong; c.key_feat = a.key_feat; c.key_tstart = a.key_tstart;
   c.wstd = a.weak_std; c.sstd = a.strong_std; c.feat_p = a.feat_p;
-  c.part_sum = a.part_sum; c.part_cnt = a.part_cnt; c.bits = a.bits; c.xs = a.xs_bf16;
+  c.part_sum = a.part_sum; c.part_cnt = a.part_cnt; c.bits = a.bits;
+  c.xs = a.xs_bf16; c.xsn = a.xs_bf16 + (size_t)c.Bc * c.Tc * DAD_D;
   return c;
 }
 
@@ -192,7 +195,7 @@ struct Shape {
   static constexpr int HW = 16 * NT;           // hidden units per wave
   static constexpr int RPW = kSub / WAVES;     // rows converted per wave
   static constexpr int kDma = 3 * RPW;         // LDS-DMA instructions per wave per sub-slab
-  static constexpr int kXsRow = 3;             // bf16 strong-x stores per converted row
+  static constexpr int kXsRow = 3;             // bf16 x-copy stores per converted row (student)
   // 4 waves (one per SIMD, 512 registers): 256 of the 384 W1 registers in AGPRs.
   // 8 waves (two per SIMD, 256 registers): all 192 in VGPRs, no AGPRs at all.
   static constexpr bool AGPR_W = WAVES == 4;
@@ -224,7 +227,7 @@ __device__ __forceinline__ int live_rows(const Job& J, int half, int w) {
   return n < 0 ? 0 : (n > S::RPW ? S::RPW : n);
 }
 
-// Convert the wave's rows of sub-slab (J, HALF): raw stage -> bf16 tile; STRONG also stores
+// Convert the wave's rows of sub-slab (J, HALF): raw stage -> bf16 tile; CLEAN / STRONG also store
 // the bf16 row to HBM for the weight gradient.  Straight-line code per KIND (one basic block,
 // so the 3*RPW independent RNG chains interleave): rows past the utterance are converted as
 // copies of its last row (identical bytes to the same xs address), temporally masked rows
@@ -278,7 +281,7 @@ __device__ __forceinline__ void ws_convert(const Ctx& C, const Job& J, int w, in
 #pragma unroll
       for (int e = 0; e < 4; ++e) o[e] = (__bf16)v[e];
       *reinterpret_cast<bf16x4*>(trow + 512 * k) = o;         // chunk 32k + (lane>>1), swizzled by row
-      if constexpr (strong) *reinterpret_cast<bf16x4*>(C.xs + (size_t)grow * DAD_D + d) = o;
+      if constexpr (KIND != KIND_WEAK) *reinterpret_cast<bf16x4*>((strong ? C.xsn : C.xs) + (size_t)grow * DAD_D + d) = o;
       // one unit (4 elements, 2 Box-Muller pairs) per scheduling region: the wave's partner on
       // the SIMD covers its dependent latency, and nothing is hoisted across units
       __builtin_amdgcn_sched_barrier(0);
@@ -415,7 +418,7 @@ __device__ __forceinline__ void ws_epilogue(const Ctx& C, const Job& J, int w, i
 
 // VMEM instructions one wave issues per sub-slab (the counted vmcnt waits depend on them)
 template <class S>
-__device__ __forceinline__ constexpr int n_xs(int kind) { return kind == KIND_STRONG ? S::kXsRow * S::RPW : 0; }
+__device__ __forceinline__ constexpr int n_xs(int kind) { return kind != KIND_WEAK ? S::kXsRow * S::RPW : 0; }
 template <bool TEACHER, int HALF>
 __device__ __forceinline__ constexpr int n_epi() { return TEACHER ? HALF : 3 * HALF; }
 

@@ -78,10 +78,10 @@ __global__ __launch_bounds__(DAD_POOL_THREADS) void dad_pool(DadPoolArgs a) {
   const int b = noisy ? blk - g.Bc : blk;
   const int T = noisy ? g.Tn : g.Tc;
   const uint8_t* pad = noisy ? a.mn : a.mc;
-  // valid length (I/model.py:35: (1-mask).sum(dim=1))
+  // valid length (I/model.py:35: (1-mask).sum(dim=1)); reduced below, after every other
+  // load of the block has been issued
   float len = 0.0f;
   for (int t = h; t < T; t += 256) len += pad[(size_t)b * T + t] == 0 ? 1.0f : 0.0f;
-  len = block_sum_f(len, red);
   const float* W2s = a.student + DAD_OFF_W2;
   const float* b2s = a.student + DAD_OFF_B2;
   const float* W2t = a.teacher + DAD_OFF_W2;
@@ -101,10 +101,24 @@ __global__ __launch_bounds__(DAD_POOL_THREADS) void dad_pool(DadPoolArgs a) {
   const size_t cslab0 = noisy ? nsc + (size_t)b * g.ncn : (size_t)b * g.ncc;
   float ssum[2] = {0.0f, 0.0f};
   float cnt = 0.0f;
-  for (int c = 0; c < nc; ++c) {
-    ssum[0] += a.part_sum[(slab0[0] + c) * DAD_H + h];
-    if (noisy) ssum[1] += a.part_sum[(slab0[1] + c) * DAD_H + h];
-    cnt += a.part_cnt[(cslab0 + c) * DAD_H + h];
+  // slab partials in batches of 8 slabs, every load of a batch issued before the sums
+  // (index clamped, contribution masked; summed in slab order as before)
+  for (int c0 = 0; c0 < nc; c0 += 8) {
+    float p0[8], p1[8], pc[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = min(c0 + k, nc - 1);
+      p0[k] = a.part_sum[(slab0[0] + c) * DAD_H + h];
+      p1[k] = noisy ? a.part_sum[(slab0[1] + c) * DAD_H + h] : 0.0f;
+      pc[k] = a.part_cnt[(cslab0 + c) * DAD_H + h];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (c0 + k >= nc) break;
+      ssum[0] += p0[k];
+      ssum[1] += p1[k];
+      cnt += pc[k];
+    }
   }
   float w2s[4], w2t[4];
 #pragma unroll
@@ -114,6 +128,7 @@ __global__ __launch_bounds__(DAD_POOL_THREADS) void dad_pool(DadPoolArgs a) {
   }
   const float kv = !noisy ? keep_value(a.keep1, a.key_drop1, b, h, a.p_drop, a.drop_scale)
                           : keep_value(a.keep2, a.key_drop2, b, h, a.p_drop, a.drop_scale);
+  len = block_sum_f(len, red);
   float zp[2][4];
   for (int k = 0; k < nbr; ++k) {
     const float e = ssum[k] / fmaxf(len, 1.0f);

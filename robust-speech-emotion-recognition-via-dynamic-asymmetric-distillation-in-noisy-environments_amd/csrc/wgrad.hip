@@ -76,8 +76,10 @@ __device__ __forceinline__ void wg_range(const DadWgradArgs& a, int split, int& 
 // Fused step: dL/de of utterance row u (clean u < Bc, strong Bc + b), hidden unit h: the
 // classifier part keep(u,h) * sum_c W2[c][h] dL/dz[u][c] (nn.Linear + nn.Dropout backward,
 // I/model.py:62-63) plus the ECDA part where ECDA wrote the row.
-__device__ __forceinline__ float fused_ge1(const DadReduceArgs& a, int Bc, int u, int h, const float (&w2)[4],
-                                           float* kv_out = nullptr) {
+// ec = ge_ecda[u][h] as loaded by the caller (read whatever the flag: unflagged rows hold
+// stale values and are selected away, so a caller can keep all its loads in flight)
+__device__ __forceinline__ float fused_ge1_ec(const DadReduceArgs& a, int Bc, int u, int h, const float (&w2)[4],
+                                              float ec, float* kv_out = nullptr) {
   const f32x4 gz = *reinterpret_cast<const f32x4*>(a.gzb + (size_t)u * DAD_C);
   const bool strong = u >= Bc;
   const int b = strong ? u - Bc : u;
@@ -85,10 +87,11 @@ __device__ __forceinline__ float fused_ge1(const DadReduceArgs& a, int Bc, int u
                           : keep_value(a.keep1, a.key_drop1, b, h, a.p_drop, a.drop_scale);
   if (kv_out) *kv_out = kv;
   const float z = ((w2[0] * gz[0] + w2[1] * gz[1]) + w2[2] * gz[2]) + w2[3] * gz[3];
-  // branch-free: the row is read whatever the flag (unflagged rows hold stale values), so a
-  // caller's loop over utterances keeps all its loads in flight
-  const float ec = a.ge_ecda[(size_t)u * DAD_H + h];
   return z * kv + (a.eflag[u] ? ec : 0.0f);
+}
+__device__ __forceinline__ float fused_ge1(const DadReduceArgs& a, int Bc, int u, int h, const float (&w2)[4],
+                                           float* kv_out = nullptr) {
+  return fused_ge1_ec(a, Bc, u, h, w2, a.ge_ecda[(size_t)u * DAD_H + h], kv_out);
 }
 
 }  // namespace
@@ -161,22 +164,41 @@ __global__ __launch_bounds__(DAD_WGRAD_THREADS) void dad_wgrad_f32(DadWgradArgs 
 // ------------------------------------------------------------ BF16 (throughput mode)
 // Direct split-K GEMM after the losses: dW1 = sum_rows G[row]^T x[row] with
 //   G[row][h] = ReLU'(row, h) * valid(row) * dL/de_u[h] / max(1, len_u)      (u = row's utterance)
-// One workgroup per (column block of WGD_DB d, split of the slab list); 4 waves, wave w owns
-// h tiles {2w, 2w+1} x both 32-wide d tiles.  Per 32-row slab:
-//   x (fp32 clean rows, or the encoder's bf16 strong rows) -> bf16 [32][WGD_DB] in LDS, read
-//     as k-major B fragments with ds_read_b64_tr_b16 (192-B row pitch: the four rows of a
-//     transposed read land on disjoint bank quarters);
-//   G is never staged: the slab's ReLU' row masks (one u32 per h, 1 KB) go to LDS, and a
-//     lane's A fragment (8 rows of one h) is byte (16 ks + 8 (lane/32)) of its h's mask,
+// x is the encoder's bf16 copy of the student's MFMA input (clean rows, then the
+// strong-augmented rows), so one loop with one load type covers both branches.
+// One workgroup per (column block of WGD_DB d, split of the slab list), two groups of 4 waves
+// (two waves per SIMD): the groups take alternate slabs of the split and their accumulators
+// are summed through LDS at the end.  Wave w of a group owns h tiles {2w, 2w+1} x both
+// 32-wide d tiles.  Per 32-row slab:
+//   x -> LDS [32][WGD_DB] (192-B row pitch: the four rows of a transposed read land on
+//     disjoint bank quarters), read as k-major B fragments with ds_read_b64_tr_b16;
+//   G is never staged: each lane loads the ReLU' row masks (one u32 per h) of its own two
+//     hidden units straight into registers, and its A fragment (8 rows of one h) is byte
+//     (16 ks + 8 (lane/32)) of that mask,
 //     expanded through a 256-entry LDS table into four 0xFFFF/0 dword masks and AND-ed with
 //     bf16(dL/de_u[h] / len_u) in both halves: one table read and four ANDs per fragment.
-// dL/de_u[h] / len_u for the workgroup's utterances is rebuilt once in the prologue from the
-// tail's per-utterance dL/dz and ECDA's flagged rows (fused_ge1).  Slab loads run WGD_DEPTH
-// slabs ahead in registers and LDS is double-buffered: one barrier per slab.
-// Output: one f32 partial slab per split, summed in fixed order by dad_reduce.
-static_assert(DAD_WGRAD_THREADS == 256 && DAD_H == 256, "dad_wgrad_direct: thread = (row, 8 columns) and thread = h");
+// Software pipeline, one barrier per round: round j computes slab j from one LDS buffer while
+// it stages slab j+1 into the other and issues the loads of slab j+1+WGD_DEPTH, all in one
+// basic block so the staging VALU fills the MFMA gaps.  dL/de_u[h] / len_u of the
+// workgroup's utterances is rebuilt in the prologue (fused_ge1) while the first loads are in
+// flight.  Output: one f32 partial slab per split, summed in fixed order by dad_reduce.
+static_assert(WGD_THREADS == 512 && DAD_H == 256, "dad_wgrad_direct: two groups of 256 threads, thread = h");
 static_assert(WGD_DB == 64 && DAD_D % WGD_DB == 0, "dad_wgrad_direct: 8 threads x 8 columns per row");
-static_assert(WGD_DEPTH % 2 == 0, "dad_wgrad_direct: LDS buffer = slab parity");
+#ifdef DAD_PROBE_STAMPS
+// diagnostic build only: per-workgroup cycles of wave 0: [prologue, loop, epilogue, -,
+// sum over rounds of: compute+stage+load, barrier, -, -, rounds]
+__device__ unsigned long long g_wgd_stamps[512 * 10];
+extern "C" int dad_probe_read_wgd_stamps(void* host, int n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wgd_stamps), sizeof(unsigned long long) * 10 * n, 0,
+                                  hipMemcpyDeviceToHost);
+}
+#define WGD_CLK() __builtin_amdgcn_s_memtime()
+#define WGD_ACC(k, v) \
+  if (threadIdx.x == 0 && blockIdx.x < 512) g_wgd_stamps[blockIdx.x * 10 + (k)] += (v)
+#else
+#define WGD_CLK() 0ull
+#define WGD_ACC(k, v)
+#endif
 namespace {
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -199,78 +221,69 @@ __device__ __forceinline__ bf16x8 tr_frag(const __bf16* tile, int pitch, int row
   return r;
 }
 
-// one slab in flight: thread t holds 8 consecutive columns of row t/8 and the ReLU' row
-// mask of h = t; the slab's utterance slot and valid row count are wave-uniform
-template <int BR> struct WgdSlab {
-  f32x4 x[2];
-  uint32_t word;
-  int ul, nvalid;
-};
-template <> struct WgdSlab<1> {
+// one slab in flight: group thread t holds 8 consecutive columns of row t/8 (staged to LDS
+// for everyone) and the ReLU' row masks of its own A-fragment hidden units (kept in
+// registers); the slab's utterance slot and valid row count are wave-uniform
+struct WgdSlab {
   bf16x8 x;
-  uint32_t word;
+  uint32_t mw[2];
   int ul, nvalid;
 };
 
-// slab cursor of one branch: (utterance b, slab c), advanced incrementally
-struct WgdCursor {
-  int s, b, c;
+// Slab table of one group, one slab per lane: lane l (< 32) describes the group's slab j = l,
+// global slab s0 + grp + 2l (clean slabs first, then strong): its first x row (rows of the
+// bf16 copy: clean [b][Tc], then strong [b][Tn]) and (utterance slot << 8 | valid rows).
+// A load reads its slab's entry with v_readlane, so no cursor arithmetic runs per slab.
+struct WgdTable {
+  int row0, info;
 };
 
-template <int BR>
-__device__ __forceinline__ void wgd_load(const DadWgradArgs& a, const WgdCursor& q, int u0, int dbase,
-                                         WgdSlab<BR>& r) {
-  const DadGeom& g = a.g;
-  const int tid = threadIdx.x;
-  const int T = BR ? g.Tn : g.Tc;
-  const int row = tid >> 3;
-  const int t = min(q.c * DAD_SLAB + row, T - 1);
-  const size_t off = ((size_t)q.b * T + t) * DAD_D + dbase + (tid & 7) * 8;
-  const size_t bits_slab = BR ? (size_t)g.Bc * g.ncc + (size_t)q.b * g.ncn + q.c : (size_t)q.b * g.ncc + q.c;
+__device__ __forceinline__ WgdTable wgd_table(const DadGeom& g, int s, int u0) {
+  const int nsc = g.Bc * g.ncc;
+  const bool br = s >= nsc;
+  const int rem = br ? s - nsc : s;
+  const int nc = br ? g.ncn : g.ncc;
+  const int b = rem / nc, c = rem - b * nc;
+  const int T = br ? g.Tn : g.Tc;
+  WgdTable t;
+  t.row0 = (br ? g.Bc * g.Tc + b * T : b * T) + c * DAD_SLAB;
+  t.info = (((br ? g.Bc + b : b) - u0) << 8) | min(T - c * DAD_SLAB, DAD_SLAB);
+  return t;
+}
+
+// group slab j (wave-uniform, clamped by the caller): x rows (clamped into the slab's valid
+// rows) and this lane's two row masks; uniform base pointers + loop-invariant lane offsets
+__device__ __forceinline__ void wgd_load(const DadWgradArgs& a, const WgdTable& tab, int j, int sfirst, int dbase,
+                                         int wv, WgdSlab& r) {
+  const int tid = threadIdx.x & 255;
+  const int row0 = __builtin_amdgcn_readlane(tab.row0, j);
+  const int info = __builtin_amdgcn_readlane(tab.info, j);
+  r.nvalid = info & 255;
+  r.ul = info >> 8;
+  const int row = min(tid >> 3, r.nvalid - 1);
+  const __bf16* xb = a.xs_bf16 + (size_t)row0 * DAD_D + dbase;
+  const uint32_t* mb = a.bits + (size_t)(sfirst + 2 * j) * DAD_H;
 #ifdef DAD_PROBE_WGD_NOMEM
   // diagnostic build only: no HBM traffic in the slab loop
-  const float fx = (float)(off & 1023);
-  if constexpr (BR == 0) { r.x[0] = f32x4{fx, fx, fx, fx}; r.x[1] = r.x[0]; }
-  else for (int e = 0; e < 8; ++e) r.x[e] = (__bf16)fx;
-  r.word = (uint32_t)(bits_slab * 2654435761u);
+  for (int e = 0; e < 8; ++e) r.x[e] = (__bf16)(float)(row0 & 1023);
+  r.mw[0] = (uint32_t)row0 * 2654435761u;
+  r.mw[1] = r.mw[0] >> 3;
+  (void)xb; (void)mb; (void)row;
 #else
-  if constexpr (BR == 0) {
-    r.x[0] = *reinterpret_cast<const f32x4*>(a.xc + off);
-    r.x[1] = *reinterpret_cast<const f32x4*>(a.xc + off + 4);
-  } else {
-    r.x = *reinterpret_cast<const bf16x8*>(a.xs_bf16 + off);
-  }
-  r.word = a.bits[bits_slab * DAD_H + tid];
+  r.x = *reinterpret_cast<const bf16x8*>(xb + row * DAD_D + (tid & 7) * 8);
+  // masks of h = 32 (2 wv + m) + lane % 32 (both 32-lane halves load the same words)
+#pragma unroll
+  for (int m = 0; m < 2; ++m) r.mw[m] = mb[(2 * wv + m) * 32 + (tid & 31)];
 #endif
-  r.ul = (BR ? g.Bc + q.b : q.b) - u0;
-  r.nvalid = T - q.c * DAD_SLAB;
 }
 
-__device__ __forceinline__ void wgd_advance(WgdCursor& q, int nc, int last) {
-  if (q.s < last) {
-    ++q.s;
-    if (++q.c == nc) { q.c = 0; ++q.b; }
-  }
-}
-
-template <int BR>
-__device__ __forceinline__ void wgd_stage(const WgdSlab<BR>& r, __bf16* Xt, uint32_t* bt) {
-  const int tid = threadIdx.x;
+__device__ __forceinline__ void wgd_stage(const WgdSlab& r, __bf16* Xt) {
+  const int tid = threadIdx.x & 255;
   const int row = tid >> 3;
   const bool ok = row < r.nvalid;
-  bf16x8 v;
-  if constexpr (BR == 0) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      v[e] = (__bf16)(ok ? r.x[0][e] : 0.0f);
-      v[e + 4] = (__bf16)(ok ? r.x[1][e] : 0.0f);
-    }
-  } else {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = ok ? r.x[e] : (__bf16)0.0f;
-  }
-  *reinterpret_cast<bf16x8*>(&Xt[row * WGD_XP + (tid & 7) * 8]) = v;
-  bt[tid] = r.word;
+  const uint4 raw = __builtin_bit_cast(uint4, r.x);
+  const uint4 v = ok ? raw : uint4{0u, 0u, 0u, 0u};   // rows past the utterance: zero
+  *reinterpret_cast<uint4*>(&Xt[row * WGD_XP + (tid & 7) * 8]) = v;
 }
 
 // A fragment of h tile ht, k rows 16 ks + 8 (lane/32) + 0..7: bit ? gb : 0 (bf16 bits).
@@ -286,74 +299,55 @@ __device__ __forceinline__ bf16x8 wgd_afrag(uint32_t mask, const uint4* lut, int
   return __builtin_bit_cast(bf16x8, uint4{m.x & gpair, m.y & gpair, m.z & gpair, m.w & gpair});
 }
 
-__device__ __forceinline__ void wgd_compute(const __bf16* Xt, const uint32_t* bt, const uint4* lut,
-                                            const uint16_t* gs, int ul, int wv, f32x16 (&acc)[2][2]) {
+// one slab's operands for one wave: A (G) fragments a[ks][m], B (x) fragments b[ks][n]
+struct WgdFrag {
+  bf16x8 a[2][2], b[2][2];
+};
+
+__device__ __forceinline__ WgdFrag wgd_fetch(const __bf16* Xt, const uint32_t (&mk)[2], const uint4* lut,
+                                             const uint16_t* gs, int ul, int wv) {
+  WgdFrag f;
   const int i = threadIdx.x & 31;
-  uint32_t gp[2], mk[2];
+  uint32_t gp[2];
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
     const uint32_t gb = gs[ul * DAD_H + (2 * wv + m) * 32 + i];
     gp[m] = gb | (gb << 16);
-    mk[m] = bt[(2 * wv + m) * 32 + i];
   }
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
-    bf16x8 af[2], bfr[2];
 #pragma unroll
-    for (int n = 0; n < 2; ++n) bfr[n] = tr_frag(Xt, WGD_XP, 16 * ks, 32 * n);
+    for (int n = 0; n < 2; ++n) {
+#ifdef DAD_PROBE_WGD_NOTR
+      // diagnostic build only: B fragments without LDS reads
+      for (int e = 0; e < 8; ++e) f.b[ks][n][e] = __builtin_bit_cast(__bf16, (uint16_t)(mk[n] >> e));
+#else
+      f.b[ks][n] = tr_frag(Xt, WGD_XP, 16 * ks, 32 * n);
+#endif
+    }
 #pragma unroll
-    for (int m = 0; m < 2; ++m) af[m] = wgd_afrag(mk[m], lut, ks, gp[m]);
+    for (int m = 0; m < 2; ++m) f.a[ks][m] = wgd_afrag(mk[m], lut, ks, gp[m]);
+  }
+  return f;
+}
+
+__device__ __forceinline__ void wgd_mma(const WgdFrag& f, f32x16 (&acc)[2][2]) {
+#ifdef DAD_PROBE_WGD_NOMFMA
+  // diagnostic build only: operands fetched, no MFMAs
+  asm volatile("" ::"v"(f.a[0][0]), "v"(f.a[0][1]), "v"(f.a[1][0]), "v"(f.a[1][1]), "v"(f.b[0][0]), "v"(f.b[0][1]),
+               "v"(f.b[1][0]), "v"(f.b[1][1]));
+  (void)acc;
+#elif !defined(DAD_PROBE_WGD_NOCOMP)
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
       for (int n = 0; n < 2; ++n)
-        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[m], bfr[n], acc[m][n], 0, 0, 0);
-  }
-}
-
-// slabs [lo, hi) of one branch (branch-local slab indices)
-template <int BR>
-__device__ __forceinline__ void wgd_phase(const DadWgradArgs& a, int lo, int hi, int u0, int dbase, __bf16* Xt,
-                                          uint32_t* bt, const uint4* lut, const uint16_t* gs, f32x16 (&acc)[2][2]) {
-  if (lo >= hi) return;
-  const int wv = threadIdx.x >> 6;
-  const int nc = BR ? a.g.ncn : a.g.ncc;
-  const int last = hi - 1;
-  WgdCursor q;
-  q.s = lo; q.b = lo / nc; q.c = lo - q.b * nc;
-  WgdSlab<BR> r[WGD_DEPTH];
-  // loads are unconditional (cursor clamped at the last slab): conditional loads make the
-  // compiler merge the paths' pending counts into a vmcnt(0) drain
-#pragma unroll
-  for (int k = 0; k < WGD_DEPTH; ++k) {
-    wgd_load<BR>(a, q, u0, dbase, r[k]);
-    wgd_advance(q, nc, last);
-  }
-  auto slot = [&](int k) {
-    __bf16* X = Xt + (k & 1) * (DAD_SLAB * WGD_XP);   // WGD_DEPTH even: buffer = slab parity
-    uint32_t* B = bt + (k & 1) * DAD_H;
-    wgd_stage<BR>(r[k], X, B);
-    const int ul = r[k].ul;
-    wgd_load<BR>(a, q, u0, dbase, r[k]);
-    wgd_advance(q, nc, last);
-    __syncthreads();
-#ifndef DAD_PROBE_WGD_NOCOMP
-    wgd_compute(X, B, lut, gs, ul, wv, acc);
+        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[ks][m], f.b[ks][n], acc[m][n], 0, 0, 0);
 #else
-    (void)ul; (void)wv;
+  (void)f; (void)acc;
 #endif
-  };
-  // whole rounds of WGD_DEPTH slabs without early exits (an exit inside the round would
-  // reach the loop header with a different load order and force vmcnt(0) there), then the
-  // remainder
-  int s = lo;
-  for (; s + WGD_DEPTH <= hi; s += WGD_DEPTH) {
-#pragma unroll
-    for (int k = 0; k < WGD_DEPTH; ++k) slot(k);
-  }
-#pragma unroll
-  for (int k = 0; k < WGD_DEPTH - 1; ++k)
-    if (s + k < hi) slot(k);
 }
 
 __device__ __forceinline__ int wgd_utt(const DadGeom& g, int s) {
@@ -363,17 +357,20 @@ __device__ __forceinline__ int wgd_utt(const DadGeom& g, int s) {
 
 }  // namespace
 
-__global__ __launch_bounds__(DAD_WGRAD_THREADS, 1) void dad_wgrad_direct(DadWgradArgs a, DadReduceArgs ra) {
-  DAD_GUARD_BLOCK(DAD_WGRAD_THREADS);
-  __shared__ __attribute__((aligned(16))) __bf16 Xt[2 * DAD_SLAB * WGD_XP];
-  __shared__ __attribute__((aligned(16))) uint32_t bt[2 * DAD_H];
+__global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct(DadWgradArgs a, DadReduceArgs ra) {
+  DAD_GUARD_BLOCK(WGD_THREADS);
+  __shared__ __attribute__((aligned(16))) __bf16 Xt[2 * 2 * DAD_SLAB * WGD_XP];
   __shared__ __attribute__((aligned(16))) uint4 lut[256];
   __shared__ __attribute__((aligned(16))) uint16_t gs[WGD_MAXU * DAD_H];
+  __shared__ __attribute__((aligned(16))) float red[DAD_H * WGD_DB];
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wv = tid >> 6;
+  // wave-uniform by construction; readfirstlane lets the compiler keep the group's cursor
+  // and flags in scalar registers
+  const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane((tid >> 6) & 3);
+  const int grp = __builtin_amdgcn_readfirstlane(tid >> 8);
   // XCD-aware tile order (grid is a multiple of 8; workgroups go round-robin over the 8
   // XCDs): each XCD takes a consecutive run of tiles, so the column blocks of one split,
-  // which read the same ReLU' words, share an L2
+  // which read the same ReLU' row masks, share an L2
   const int per_xcd = gridDim.x >> 3;
   const int tile = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
   if (tile >= a.ntiles) return;
@@ -383,54 +380,134 @@ __global__ __launch_bounds__(DAD_WGRAD_THREADS, 1) void dad_wgrad_direct(DadWgra
   const int total = wg_total(a);
   const int per = (total + a.splits - 1) / a.splits;
   const int s0 = split * per, s1 = min(total, s0 + per);
-  const int nsc = g.Bc * g.ncc;
   f32x16 acc[2][2];
 #pragma unroll
   for (int m = 0; m < 2; ++m)
 #pragma unroll
     for (int n = 0; n < 2; ++n) acc[m][n] = f32x16{};
+#ifdef DAD_PROBE_STAMPS
+  if (tid == 0 && blockIdx.x < 512)
+    for (int k = 0; k < 10; ++k) g_wgd_stamps[blockIdx.x * 10 + k] = 0;
+#endif
+  const unsigned long long t0 = WGD_CLK();
+  unsigned long long t1 = t0, t2 = t0;
   if (s0 < s1) {
-    // dL/de_u[h] / max(1, len_u) of this split's utterances (thread = h), as bf16; the
-    // host bounds a split to WGD_MAXU slabs, hence utterances
+    // group g takes slabs s0 + g, s0 + g + 2, ...; both groups run nround rounds (barriers)
+    const int n = s1 - s0;
+    const int nround = (n + 1) >> 1;
+    const int mine = (n - grp + 1) >> 1;               // group 1 may have one slab fewer
+    const int cnt1 = n >> 1;
     const int u0 = wgd_utt(g, s0), nu = wgd_utt(g, s1 - 1) - u0 + 1;
-    const float w2[4] = {ra.student[DAD_OFF_W2 + tid], ra.student[DAD_OFF_W2 + DAD_H + tid],
-                         ra.student[DAD_OFF_W2 + 2 * DAD_H + tid], ra.student[DAD_OFF_W2 + 3 * DAD_H + tid]};
-    for (int ul0 = 0; ul0 < nu; ul0 += 8) {
-      float v[8];
+    __bf16* Xg = Xt + grp * (2 * DAD_SLAB * WGD_XP);
+    // dL/de_u[h] / max(1, len_u) of this split's utterances (group 0, thread = h) as bf16; the
+    // host bounds a split to WGD_MAXU slabs, hence utterances.  The first eight utterances'
+    // vector loads go out before the slab prefetch, so their math never waits on it.
+    float w2[4] = {0.0f, 0.0f, 0.0f, 0.0f}, ec0[8];
+    if (grp == 0) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {   // eight utterances' loads in flight (index clamped)
-        const int u = u0 + min(ul0 + k, nu - 1);
-        v[k] = fused_ge1(ra, g.Bc, u, tid, w2) / fmaxf(ra.vlen[u], 1.0f);
-      }
+      for (int c = 0; c < 4; ++c) w2[c] = ra.student[DAD_OFF_W2 + c * DAD_H + tid];
 #pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if (ul0 + k < nu) gs[(ul0 + k) * DAD_H + tid] = __builtin_bit_cast(uint16_t, (__bf16)v[k]);
+      for (int k = 0; k < 8; ++k) ec0[k] = ra.ge_ecda[(size_t)(u0 + min(k, nu - 1)) * DAD_H + tid];
     }
-    {
+    const int sfirst = s0 + grp;
+    const WgdTable tab = wgd_table(g, min(sfirst + 2 * (lane & 31), s1 - 1), u0);
+    const int jlast = max(mine - 1, 0);
+    WgdSlab r[WGD_DEPTH];
+    // loads are unconditional (slab index clamped at the group's last slab): conditional
+    // loads make the compiler merge the paths' pending counts into a vmcnt(0) drain
+#pragma unroll
+    for (int k = 0; k < WGD_DEPTH; ++k) wgd_load(a, tab, min(k, jlast), sfirst, dbase, wv, r[k]);
+    if (grp == 0) {
+      for (int ul0 = 0; ul0 < nu; ul0 += 8) {
+        float v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {   // eight utterances' loads in flight (index clamped)
+          const int u = u0 + min(ul0 + k, nu - 1);
+          v[k] = (ul0 == 0 ? fused_ge1_ec(ra, g.Bc, u, tid, w2, ec0[k]) : fused_ge1(ra, g.Bc, u, tid, w2)) /
+                 fmaxf(ra.vlen[u], 1.0f);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (ul0 + k < nu) gs[(ul0 + k) * DAD_H + tid] = __builtin_bit_cast(uint16_t, (__bf16)v[k]);
+      }
+    } else {
+      const int t = tid & 255;
       uint32_t e[4];
 #pragma unroll
       for (int p = 0; p < 4; ++p)
-        e[p] = (((tid >> (2 * p)) & 1) ? 0x0000ffffu : 0u) | (((tid >> (2 * p + 1)) & 1) ? 0xffff0000u : 0u);
-      lut[tid] = uint4{e[0], e[1], e[2], e[3]};
+        e[p] = (((t >> (2 * p)) & 1) ? 0x0000ffffu : 0u) | (((t >> (2 * p + 1)) & 1) ? 0xffff0000u : 0u);
+      lut[t] = uint4{e[0], e[1], e[2], e[3]};
     }
-    // (the slab loop's first barrier orders these writes before the first read)
-    wgd_phase<0>(a, s0, min(s1, nsc), u0, dbase, Xt, bt, lut, gs, acc);
-    if (s1 > nsc) {
-      __syncthreads();   // the clean phase's last compute is done with its LDS buffer
-      wgd_phase<1>(a, max(s0, nsc) - nsc, s1 - nsc, u0, dbase, Xt, bt, lut, gs, acc);
+    // slab 0 of each group into buffer 0; its ring slot reloads slab WGD_DEPTH
+    if (mine > 0) wgd_stage(r[0], Xg);
+    int ul = r[0].ul;
+    uint32_t mw[2] = {r[0].mw[0], r[0].mw[1]};
+    wgd_load(a, tab, min(WGD_DEPTH, jlast), sfirst, dbase, wv, r[0]);
+    __syncthreads();
+    t1 = WGD_CLK();
+    // round j: read slab j's operands from buffer j&1 into registers | MFMAs of slab j-1 from
+    // the registers read in round j-1 (so they never wait on LDS) | stage slab j+1 into
+    // buffer (j+1)&1 from ring slot (j+1)%DEPTH and reload that slot with slab j+1+DEPTH |
+    // barrier
+    WgdFrag F;
+    auto round = [&](int jr, int k, bool prev, bool comp, bool stage) {
+      const unsigned long long c0 = WGD_CLK();
+      const int nk = (k + 1) % WGD_DEPTH;
+      WgdFrag Fn;
+      if (comp) Fn = wgd_fetch(Xg + (k & 1) * (DAD_SLAB * WGD_XP), mw, lut, gs, ul, wv);
+      if (prev) wgd_mma(F, acc);
+      F = Fn;
+      if (stage) wgd_stage(r[nk], Xg + ((k + 1) & 1) * (DAD_SLAB * WGD_XP));
+      ul = r[nk].ul;
+      mw[0] = r[nk].mw[0];
+      mw[1] = r[nk].mw[1];
+      wgd_load(a, tab, min(jr + 1 + WGD_DEPTH, jlast), sfirst, dbase, wv, r[nk]);
+      const unsigned long long c1 = WGD_CLK();
+      __syncthreads();
+      WGD_ACC(4, c1 - c0); WGD_ACC(5, WGD_CLK() - c1); WGD_ACC(8, 1);
+      (void)c0; (void)c1;
+    };
+    // round 0, then blocks of WGD_DEPTH rounds in which both groups have every step (no early
+    // exits: an exit inside the block would reach the loop header with a different load
+    // order and force vmcnt(0) there; ring slots are compile-time: j = 1 mod WGD_DEPTH at a
+    // block start), then the last rounds with per-group flags and the final MFMAs
+    round(0, 0, false, mine > 0, 1 < mine);
+    int j = 1;
+    for (; j + WGD_DEPTH <= cnt1 - 1; j += WGD_DEPTH) {
+#pragma unroll
+      for (int k = 0; k < WGD_DEPTH; ++k) round(j + k, k + 1, true, true, true);
     }
+#pragma unroll
+    for (int k = 0; k < WGD_DEPTH + 2; ++k)   // nround - j <= WGD_DEPTH + 1
+      if (j + k < nround) round(j + k, k + 1, j + k - 1 < mine, j + k < mine, j + k + 1 < mine);
+    if (nround - 1 < mine) wgd_mma(F, acc);
+    t2 = WGD_CLK();
   }
-  float* out = a.wpart + (size_t)split * DAD_H * DAD_D;
+  // exchange halves: group 0 finishes h tile 2w (+ group 1's partial), group 1 tile 2w+1
   const int kh = lane >> 5;
 #pragma unroll
   for (int m = 0; m < 2; ++m)
+    if (m != grp)
 #pragma unroll
-    for (int n = 0; n < 2; ++n)
+      for (int nn = 0; nn < 2; ++nn)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int h = (2 * wv + m) * 32 + dad_acc_row(r, kh);
-        out[(size_t)h * DAD_D + dbase + 32 * n + (lane & 31)] = acc[m][n][r];
-      }
+        for (int rr = 0; rr < 16; ++rr)
+          red[((2 * wv + m) * 32 + dad_acc_row(rr, kh)) * WGD_DB + 32 * nn + (lane & 31)] = acc[m][nn][rr];
+  __syncthreads();
+  float* out = a.wpart + (size_t)split * DAD_H * DAD_D;
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+    if (m == grp)
+#pragma unroll
+      for (int nn = 0; nn < 2; ++nn)
+#pragma unroll
+        for (int rr = 0; rr < 16; ++rr) {
+          const int h = (2 * wv + m) * 32 + dad_acc_row(rr, kh);
+          const int d = 32 * nn + (lane & 31);
+          out[(size_t)h * DAD_D + dbase + d] = acc[m][nn][rr] + red[h * WGD_DB + d];
+        }
+  WGD_ACC(0, t1 - t0); WGD_ACC(1, t2 - t1); WGD_ACC(2, WGD_CLK() - t2);
+  (void)t0; (void)t1; (void)t2;
 }
 
 // ---------------------------------------------------------------- reduce + squared norms
@@ -457,23 +534,39 @@ __device__ double extra_block(const DadReduceArgs& a, int e) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) w2[c] = a.student[DAD_OFF_W2 + c * DAD_H + h];
   float db = 0.0f, gw[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  for (int r = rg; r < nb; r += 16) {
-    float gv, kv = 1.0f;
-    if (fused) {
-      gv = fused_ge1(a, g.Bc, r, h, w2, &kv);
-    } else {
-      gv = a.ge[(size_t)r * DAD_H + h];
-      if (ecda) gv += a.ge_ecda[(size_t)r * DAD_H + h];
-    }
-    db += gv / fmaxf(a.vlen[r], 1.0f) * a.cnt_tot[(size_t)r * DAD_H + h];
-    if (fused) {
-      // dW2[c][h] = sum_u dL/dz[u][c] * dropout(e_u)[h]  (student clean / strong embeddings)
-      const bool strong = r >= g.Bc;
-      const int erow = strong ? g.Bn + r : r;   // strong row b lives at Bc + Bn + b
-      const float d = a.emb[(size_t)erow * DAD_H + h] * kv;
-      const f32x4 gz = *reinterpret_cast<const f32x4*>(a.gzb + (size_t)r * DAD_C);
+  // rows rg, rg + 16, ... in batches of 8 whose loads are all issued before any is used
+  // (index clamped, contribution masked): one memory round trip per batch, not per row
+  for (int r0 = rg; r0 < nb; r0 += 16 * 8) {
+    float gv[8], kv[8], rl[8], ct[8], em[8];
+    f32x4 gzv[8];
 #pragma unroll
-      for (int c = 0; c < 4; ++c) gw[c] += gz[c] * d;
+    for (int k = 0; k < 8; ++k) {
+      const int r = min(r0 + 16 * k, nb - 1);
+      kv[k] = 1.0f;
+      if (fused) {
+        gv[k] = fused_ge1(a, g.Bc, r, h, w2, &kv[k]);
+        const int erow = r >= g.Bc ? g.Bn + r : r;   // strong row b lives at Bc + Bn + b
+        em[k] = a.emb[(size_t)erow * DAD_H + h];
+        gzv[k] = *reinterpret_cast<const f32x4*>(a.gzb + (size_t)r * DAD_C);
+      } else {
+        gv[k] = a.ge[(size_t)r * DAD_H + h];
+        if (ecda) gv[k] += a.ge_ecda[(size_t)r * DAD_H + h];
+        em[k] = 0.0f;
+        gzv[k] = f32x4{};
+      }
+      rl[k] = a.vlen[r];
+      ct[k] = a.cnt_tot[(size_t)r * DAD_H + h];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (r0 + 16 * k >= nb) break;
+      db += gv[k] / fmaxf(rl[k], 1.0f) * ct[k];
+      if (fused) {
+        // dW2[c][h] = sum_u dL/dz[u][c] * dropout(e_u)[h]  (student clean / strong embeddings)
+        const float d = em[k] * kv[k];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) gw[c] += gzv[k][c] * d;
+      }
     }
   }
   xs[rg][hl][0] = db;

@@ -1,13 +1,15 @@
 """rocprofv3 outputs under gpurun_out/ -> one markdown report for profiles/.
 
-    python tools/profile_report.py <title> <out.md> [prof_dir] [pmc_dir]
+    python tools/profile_report.py <title> <out.md> [prof_dir] [pmc_dir] [out.json]
 
 prof_dir: `--kernel-trace --stats --output-format csv -o run` output (kernel stats + trace);
 pmc_dir:  tools/gpu_pmc.sh output (one sub-directory per counter pass).
 Sections: per-kernel duration stats, the last step's kernel timeline (start/end relative to
 that step's encoder launch, queue id), and per-launch PMC averages with HBM traffic
 (FETCH_SIZE x 2, the gfx950 half-count correction of MI355X_MICROARCH.md, + WRITE_SIZE; KB).
+out.json (optional): the per-kernel HBM bytes per launch that bench.py reports as roofline.traffic.
 """
+import json
 import collections
 import csv
 import os
@@ -45,6 +47,29 @@ def timeline(prof):
     return out
 
 
+def pmc_agg(pmc_dir):
+    agg = collections.defaultdict(list)
+    for name in sorted(os.listdir(pmc_dir)):
+        f = os.path.join(pmc_dir, name, "run_counter_collection.csv")
+        if not os.path.exists(f):
+            continue
+        for r in csv.DictReader(open(f)):
+            agg[(r["Kernel_Name"].split("(")[0], r["Counter_Name"])].append(float(r["Counter_Value"]))
+    return agg
+
+
+def pmc_json(pmc_dir, title):
+    agg = pmc_agg(pmc_dir)
+    out = {}
+    for k in sorted({k for k, _ in agg}):
+        f, w = agg.get((k, "FETCH_SIZE")), agg.get((k, "WRITE_SIZE"))
+        if f and w:
+            kb = 2 * sum(f) / len(f) + sum(w) / len(w)
+            out[k] = {"hbm_bytes_per_launch": kb * 1024.0, "fetch_kb_x2": 2 * sum(f) / len(f),
+                      "write_kb": sum(w) / len(w), "launches": len(f)}
+    return {"source": title, "units": "bytes per launch = (2 x FETCH_SIZE + WRITE_SIZE) KB x 1024", "kernels": out}
+
+
 def pmc(pmc_dir):
     agg = collections.defaultdict(list)
     for name in sorted(os.listdir(pmc_dir)):
@@ -80,6 +105,8 @@ def main():
     if os.path.isdir(pmc_dir):
         out += ["", "## PMC per launch (averages over launches; separate --pmc passes)", ""] + pmc(pmc_dir)
     open(dst, "w").write("\n".join(out) + "\n")
+    if len(sys.argv) > 5 and os.path.isdir(pmc_dir):
+        json.dump(pmc_json(pmc_dir, title), open(sys.argv[5], "w"), indent=1)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,39 @@
+"""Diagnostic: dad_wgrad_direct per-phase cycles (build variant 'stamps', -DDAD_PROBE_STAMPS;
+never the product library).  Runs bench-shaped steps and prints workgroup averages."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ.setdefault("DAD_LIB_VARIANT", "stamps")
+import bench  # noqa: E402
+
+PKG = bench.PKG
+
+
+def main():
+    B, T = 64, 300
+    model = PKG.SSRLModel().cuda()
+    P = bench.init_model_weights(model, seed=0)
+    step = PKG.DADStep(model, flavor="iemocap", precision="bf16", rng="counter", seed=1)
+    data = bench.make_batches(P, 2, B, T, seed=17, device=torch.device("cuda"))
+    for i in range(6):
+        step.step(data[i % 2][0], data[i % 2][1], 60)
+    torch.cuda.synchronize()
+    L = PKG.lib()
+    n = 256
+    buf = (ctypes.c_ulonglong * (10 * n))()
+    assert L.dad_probe_read_wgd_stamps(buf, n) == 0
+    e = np.frombuffer(buf, dtype=np.uint64).astype(np.float64).reshape(n, 10)
+    e = e[e[:, 8] > 0]
+    m = e.mean(0)
+    print("workgroups %d; cycles: prologue %.0f loop %.0f epilogue %.0f" % (len(e), m[0], m[1], m[2]))
+    print("per round (n=%.1f): compute+stage+load %.0f barrier %.0f" % (m[8], m[4] / m[8], m[5] / m[8]))
+
+
+if __name__ == "__main__":
+    main()
