@@ -18,7 +18,10 @@
 #define WGD_MAXU 64
 #define WGD_DEPTH 4
 #define WGD_XP 96
-#define WGD_THREADS 512   // two groups of 4 waves, one slab each per round (two waves per SIMD)
+#ifndef WGD_GROUPS
+#define WGD_GROUPS 2      // slab groups of 4 waves per workgroup (2: two waves per SIMD)
+#endif
+#define WGD_THREADS (256 * WGD_GROUPS)
 #define DAD_REDUCE_THREADS 256
 #define DAD_REDUCE_COLS 256                                  // dW1 floats per reduce block
 #define DAD_REDUCE_XBLK 16                                   // db1 / dW2 / totals blocks (16 hidden units each)

@@ -174,15 +174,16 @@ __global__ __launch_bounds__(DAD_WGRAD_THREADS) void dad_wgrad_f32(DadWgradArgs 
 //     disjoint bank quarters), read as k-major B fragments with ds_read_b64_tr_b16;
 //   G is never staged: each lane loads the ReLU' row masks (one u32 per h) of its own two
 //     hidden units straight into registers, and its A fragment (8 rows of one h) is byte
-//     (16 ks + 8 (lane/32)) of that mask,
-//     expanded through a 256-entry LDS table into four 0xFFFF/0 dword masks and AND-ed with
-//     bf16(dL/de_u[h] / len_u) in both halves: one table read and four ANDs per fragment.
+//     (16 ks + 8 (lane/32)) of that mask, expanded nibble by nibble through a 16-entry LDS
+//     table (conflict-free) into four 0xFFFF/0 dword masks and AND-ed with bf16(dL/de_u[h] /
+//     len_u) in both halves: two table reads and four ANDs per fragment.
 // Software pipeline, one barrier per round: round j computes slab j from one LDS buffer while
 // it stages slab j+1 into the other and issues the loads of slab j+1+WGD_DEPTH, all in one
 // basic block so the staging VALU fills the MFMA gaps.  dL/de_u[h] / len_u of the
 // workgroup's utterances is rebuilt in the prologue (fused_ge1) while the first loads are in
 // flight.  Output: one f32 partial slab per split, summed in fixed order by dad_reduce.
-static_assert(WGD_THREADS == 512 && DAD_H == 256, "dad_wgrad_direct: two groups of 256 threads, thread = h");
+static_assert(WGD_THREADS == 256 * WGD_GROUPS && DAD_H == 256, "dad_wgrad_direct: groups of 256 threads, thread = h");
+static_assert(WGD_GROUPS == 1 || WGD_GROUPS == 2, "dad_wgrad_direct: one or two slab groups");
 static_assert(WGD_DB == 64 && DAD_D % WGD_DB == 0, "dad_wgrad_direct: 8 threads x 8 columns per row");
 #ifdef DAD_PROBE_STAMPS
 // diagnostic build only: per-workgroup cycles of wave 0: [prologue, loop, epilogue, -,
@@ -230,8 +231,8 @@ struct WgdSlab {
   int ul, nvalid;
 };
 
-// Slab table of one group, one slab per lane: lane l (< 32) describes the group's slab j = l,
-// global slab s0 + grp + 2l (clean slabs first, then strong): its first x row (rows of the
+// Slab table of one group, one slab per lane: lane l describes the group's slab j = l,
+// global slab s0 + grp + WGD_GROUPS l (clean slabs first, then strong): its first x row (rows of the
 // bf16 copy: clean [b][Tc], then strong [b][Tn]) and (utterance slot << 8 | valid rows).
 // A load reads its slab's entry with v_readlane, so no cursor arithmetic runs per slab.
 struct WgdTable {
@@ -262,7 +263,7 @@ __device__ __forceinline__ void wgd_load(const DadWgradArgs& a, const WgdTable& 
   r.ul = info >> 8;
   const int row = min(tid >> 3, r.nvalid - 1);
   const __bf16* xb = a.xs_bf16 + (size_t)row0 * DAD_D + dbase;
-  const uint32_t* mb = a.bits + (size_t)(sfirst + 2 * j) * DAD_H;
+  const uint32_t* mb = a.bits + (size_t)(sfirst + WGD_GROUPS * j) * DAD_H;
 #ifdef DAD_PROBE_WGD_NOMEM
   // diagnostic build only: no HBM traffic in the slab loop
   for (int e = 0; e < 8; ++e) r.x[e] = (__bf16)(float)(row0 & 1023);
@@ -287,16 +288,20 @@ __device__ __forceinline__ void wgd_stage(const WgdSlab& r, __bf16* Xt) {
 }
 
 // A fragment of h tile ht, k rows 16 ks + 8 (lane/32) + 0..7: bit ? gb : 0 (bf16 bits).
-// lut[b] = the 0xFFFF/0 halfword masks of the 8 bits of b.
-__device__ __forceinline__ bf16x8 wgd_afrag(uint32_t mask, const uint4* lut, int ks, uint32_t gpair) {
+// lut[n] = the 0xFFFF/0 halfword masks of the 4 bits of nibble n (8 B): the 16-entry table
+// spans the 32 banks once, so a 32-lane half-wave's reads are conflict-free (equal entries
+// broadcast, different entries sit on different banks).
+__device__ __forceinline__ uint4 wgd_amask(uint32_t mask, const uint2* lut, int ks) {
   const int lane = threadIdx.x & 63;
 #ifdef DAD_PROBE_WGD_NOAFRAG
-  const uint4 m = uint4{mask, mask >> 1, mask >> 2, mask >> 3};
   (void)lut; (void)lane; (void)ks;
+  return uint4{mask, mask >> 1, mask >> 2, mask >> 3};
 #else
-  const uint4 m = lut[(mask >> (16 * ks + 8 * (lane >> 5))) & 0xffu];
+  const uint32_t byte = mask >> (16 * ks + 8 * (lane >> 5));
+  const uint2 lo = lut[byte & 15u];
+  const uint2 hi = lut[(byte >> 4) & 15u];
+  return uint4{lo.x, lo.y, hi.x, hi.y};
 #endif
-  return __builtin_bit_cast(bf16x8, uint4{m.x & gpair, m.y & gpair, m.z & gpair, m.w & gpair});
 }
 
 // one slab's operands for one wave: A (G) fragments a[ks][m], B (x) fragments b[ks][n]
@@ -304,30 +309,53 @@ struct WgdFrag {
   bf16x8 a[2][2], b[2][2];
 };
 
-__device__ __forceinline__ WgdFrag wgd_fetch(const __bf16* Xt, const uint32_t (&mk)[2], const uint4* lut,
-                                             const uint16_t* gs, int ul, int wv) {
-  WgdFrag f;
-  const int i = threadIdx.x & 31;
+// the LDS reads of one slab's operands, issued together at the start of a round: B fragments
+// (final), the A fragments' table masks and the dL/de pair (combined by wgd_finish at the
+// round's end, after the MFMAs have covered the read latency)
+struct WgdRaw {
+  bf16x8 b[2][2];
+  uint4 am[2][2];
   uint32_t gp[2];
+};
+
+__device__ __forceinline__ WgdRaw wgd_read(const __bf16* Xt, const uint32_t (&mk)[2], const uint2* lut,
+                                           const uint16_t* gs, int ul, int wv) {
+  WgdRaw w;
+  const int i = threadIdx.x & 31;
 #pragma unroll
-  for (int m = 0; m < 2; ++m) {
-    const uint32_t gb = gs[ul * DAD_H + (2 * wv + m) * 32 + i];
-    gp[m] = gb | (gb << 16);
-  }
+  for (int m = 0; m < 2; ++m) w.gp[m] = gs[ul * DAD_H + (2 * wv + m) * 32 + i];
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
 #ifdef DAD_PROBE_WGD_NOTR
       // diagnostic build only: B fragments without LDS reads
-      for (int e = 0; e < 8; ++e) f.b[ks][n][e] = __builtin_bit_cast(__bf16, (uint16_t)(mk[n] >> e));
+      for (int e = 0; e < 8; ++e) w.b[ks][n][e] = __builtin_bit_cast(__bf16, (uint16_t)(mk[n] >> e));
 #else
-      f.b[ks][n] = tr_frag(Xt, WGD_XP, 16 * ks, 32 * n);
+      w.b[ks][n] = tr_frag(Xt, WGD_XP, 16 * ks, 32 * n);
 #endif
     }
 #pragma unroll
-    for (int m = 0; m < 2; ++m) f.a[ks][m] = wgd_afrag(mk[m], lut, ks, gp[m]);
+    for (int m = 0; m < 2; ++m) w.am[ks][m] = wgd_amask(mk[m], lut, ks);
   }
+  return w;
+}
+
+__device__ __forceinline__ WgdFrag wgd_finish(const WgdRaw& w) {
+  WgdFrag f;
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    const uint32_t gpair = w.gp[m] | (w.gp[m] << 16);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const uint4 am = w.am[ks][m];
+      f.a[ks][m] = __builtin_bit_cast(bf16x8, uint4{am.x & gpair, am.y & gpair, am.z & gpair, am.w & gpair});
+    }
+  }
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) f.b[ks][n] = w.b[ks][n];
   return f;
 }
 
@@ -359,10 +387,10 @@ __device__ __forceinline__ int wgd_utt(const DadGeom& g, int s) {
 
 __global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct(DadWgradArgs a, DadReduceArgs ra) {
   DAD_GUARD_BLOCK(WGD_THREADS);
-  __shared__ __attribute__((aligned(16))) __bf16 Xt[2 * 2 * DAD_SLAB * WGD_XP];
-  __shared__ __attribute__((aligned(16))) uint4 lut[256];
+  __shared__ __attribute__((aligned(16))) __bf16 Xt[WGD_GROUPS * 2 * DAD_SLAB * WGD_XP];
+  __shared__ __attribute__((aligned(16))) uint2 lut[16];
   __shared__ __attribute__((aligned(16))) uint16_t gs[WGD_MAXU * DAD_H];
-  __shared__ __attribute__((aligned(16))) float red[DAD_H * WGD_DB];
+  __shared__ __attribute__((aligned(16))) float red[WGD_GROUPS == 2 ? DAD_H * WGD_DB : 1];
   const int tid = threadIdx.x;
   // wave-uniform by construction; readfirstlane lets the compiler keep the group's cursor
   // and flags in scalar registers
@@ -392,13 +420,14 @@ __global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct(DadWgradArgs 
   const unsigned long long t0 = WGD_CLK();
   unsigned long long t1 = t0, t2 = t0;
   if (s0 < s1) {
-    // group g takes slabs s0 + g, s0 + g + 2, ...; both groups run nround rounds (barriers)
+    // group g takes slabs s0 + g, s0 + g + WGD_GROUPS, ...; all groups run nround rounds
+    // (barriers); cntmin = the smallest group's slab count
     const int n = s1 - s0;
-    const int nround = (n + 1) >> 1;
-    const int mine = (n - grp + 1) >> 1;               // group 1 may have one slab fewer
-    const int cnt1 = n >> 1;
+    const int nround = (n + WGD_GROUPS - 1) / WGD_GROUPS;
+    const int mine = (n - grp + WGD_GROUPS - 1) / WGD_GROUPS;   // group 1 may have one slab fewer
+    const int cntmin = n / WGD_GROUPS;
     const int u0 = wgd_utt(g, s0), nu = wgd_utt(g, s1 - 1) - u0 + 1;
-    __bf16* Xg = Xt + grp * (2 * DAD_SLAB * WGD_XP);
+    __bf16* Xg = Xt + grp * (2 * DAD_SLAB * WGD_XP);   // this group's two LDS buffers
     // dL/de_u[h] / max(1, len_u) of this split's utterances (group 0, thread = h) as bf16; the
     // host bounds a split to WGD_MAXU slabs, hence utterances.  The first eight utterances'
     // vector loads go out before the slab prefetch, so their math never waits on it.
@@ -410,7 +439,7 @@ __global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct(DadWgradArgs 
       for (int k = 0; k < 8; ++k) ec0[k] = ra.ge_ecda[(size_t)(u0 + min(k, nu - 1)) * DAD_H + tid];
     }
     const int sfirst = s0 + grp;
-    const WgdTable tab = wgd_table(g, min(sfirst + 2 * (lane & 31), s1 - 1), u0);
+    const WgdTable tab = wgd_table(g, min(sfirst + WGD_GROUPS * lane, s1 - 1), u0);
     const int jlast = max(mine - 1, 0);
     WgdSlab r[WGD_DEPTH];
     // loads are unconditional (slab index clamped at the group's last slab): conditional
@@ -430,13 +459,14 @@ __global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct(DadWgradArgs 
         for (int k = 0; k < 8; ++k)
           if (ul0 + k < nu) gs[(ul0 + k) * DAD_H + tid] = __builtin_bit_cast(uint16_t, (__bf16)v[k]);
       }
-    } else {
-      const int t = tid & 255;
-      uint32_t e[4];
+    }
+    if (tid - 256 * (WGD_GROUPS - 1) < 16) {
+      const int t = tid - 256 * (WGD_GROUPS - 1);
+      uint32_t e[2];
 #pragma unroll
-      for (int p = 0; p < 4; ++p)
+      for (int p = 0; p < 2; ++p)
         e[p] = (((t >> (2 * p)) & 1) ? 0x0000ffffu : 0u) | (((t >> (2 * p + 1)) & 1) ? 0xffff0000u : 0u);
-      lut[t] = uint4{e[0], e[1], e[2], e[3]};
+      lut[t] = uint2{e[0], e[1]};
     }
     // slab 0 of each group into buffer 0; its ring slot reloads slab WGD_DEPTH
     if (mine > 0) wgd_stage(r[0], Xg);
@@ -453,15 +483,17 @@ __global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct(DadWgradArgs 
     auto round = [&](int jr, int k, bool prev, bool comp, bool stage) {
       const unsigned long long c0 = WGD_CLK();
       const int nk = (k + 1) % WGD_DEPTH;
-      WgdFrag Fn;
-      if (comp) Fn = wgd_fetch(Xg + (k & 1) * (DAD_SLAB * WGD_XP), mw, lut, gs, ul, wv);
+      WgdRaw R;
+      if (comp) R = wgd_read(Xg + (k & 1) * (DAD_SLAB * WGD_XP), mw, lut, gs, ul, wv);
+      __builtin_amdgcn_sched_barrier(0);   // reads first, their latency under the MFMAs
       if (prev) wgd_mma(F, acc);
-      F = Fn;
       if (stage) wgd_stage(r[nk], Xg + ((k + 1) & 1) * (DAD_SLAB * WGD_XP));
       ul = r[nk].ul;
       mw[0] = r[nk].mw[0];
       mw[1] = r[nk].mw[1];
       wgd_load(a, tab, min(jr + 1 + WGD_DEPTH, jlast), sfirst, dbase, wv, r[nk]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (comp) F = wgd_finish(R);
       const unsigned long long c1 = WGD_CLK();
       __syncthreads();
       WGD_ACC(4, c1 - c0); WGD_ACC(5, WGD_CLK() - c1); WGD_ACC(8, 1);
@@ -473,7 +505,7 @@ __global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct(DadWgradArgs 
     // block start), then the last rounds with per-group flags and the final MFMAs
     round(0, 0, false, mine > 0, 1 < mine);
     int j = 1;
-    for (; j + WGD_DEPTH <= cnt1 - 1; j += WGD_DEPTH) {
+    for (; j + WGD_DEPTH <= cntmin - 1; j += WGD_DEPTH) {
 #pragma unroll
       for (int k = 0; k < WGD_DEPTH; ++k) round(j + k, k + 1, true, true, true);
     }
@@ -483,28 +515,30 @@ __global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct(DadWgradArgs 
     if (nround - 1 < mine) wgd_mma(F, acc);
     t2 = WGD_CLK();
   }
-  // exchange halves: group 0 finishes h tile 2w (+ group 1's partial), group 1 tile 2w+1
   const int kh = lane >> 5;
-#pragma unroll
-  for (int m = 0; m < 2; ++m)
-    if (m != grp)
-#pragma unroll
-      for (int nn = 0; nn < 2; ++nn)
-#pragma unroll
-        for (int rr = 0; rr < 16; ++rr)
-          red[((2 * wv + m) * 32 + dad_acc_row(rr, kh)) * WGD_DB + 32 * nn + (lane & 31)] = acc[m][nn][rr];
-  __syncthreads();
   float* out = a.wpart + (size_t)split * DAD_H * DAD_D;
+  if constexpr (WGD_GROUPS == 2) {
+    // exchange halves: group 0 finishes h tile 2w (+ group 1's partial), group 1 tile 2w+1
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+      if (m != grp)
+#pragma unroll
+        for (int nn = 0; nn < 2; ++nn)
+#pragma unroll
+          for (int rr = 0; rr < 16; ++rr)
+            red[((2 * wv + m) * 32 + dad_acc_row(rr, kh)) * WGD_DB + 32 * nn + (lane & 31)] = acc[m][nn][rr];
+    __syncthreads();
+  }
 #pragma unroll
   for (int m = 0; m < 2; ++m)
-    if (m == grp)
+    if (WGD_GROUPS == 1 || m == grp)
 #pragma unroll
       for (int nn = 0; nn < 2; ++nn)
 #pragma unroll
         for (int rr = 0; rr < 16; ++rr) {
           const int h = (2 * wv + m) * 32 + dad_acc_row(rr, kh);
           const int d = 32 * nn + (lane & 31);
-          out[(size_t)h * DAD_D + dbase + d] = acc[m][nn][rr] + red[h * WGD_DB + d];
+          out[(size_t)h * DAD_D + dbase + d] = acc[m][nn][rr] + (WGD_GROUPS == 2 ? red[h * WGD_DB + d] : 0.0f);
         }
   WGD_ACC(0, t1 - t0); WGD_ACC(1, t2 - t1); WGD_ACC(2, WGD_CLK() - t2);
   (void)t0; (void)t1; (void)t2;
