@@ -20,18 +20,18 @@
 
 #ifdef DAD_PROBE_STAMPS
 // diagnostic build only: ECDA per-class phase wall clocks (100 MHz), 12 slots per class
-__device__ unsigned long long g_ecda_stamps[DAD_C * 12 + 12];   // + tail phases
+__device__ unsigned long long g_ecda_stamps[DAD_C * 16 + 12];   // 16 per class + tail phases
 extern "C" int dad_probe_read_ecda_stamps(void* host) {
   return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ecda_stamps), sizeof(g_ecda_stamps), 0, hipMemcpyDeviceToHost);
 }
 #define ECDA_STAMP(k) \
-  if (threadIdx.x == 0) g_ecda_stamps[blockIdx.x * 12 + (k)] = wall_clock64()
+  if (threadIdx.x == 0) g_ecda_stamps[blockIdx.x * 16 + (k)] = wall_clock64()
 __device__ __forceinline__ void g_ecda_stamps_n(int c, int n, int ns) {
-  g_ecda_stamps[c * 12 + 10] = (unsigned long long)n;
-  g_ecda_stamps[c * 12 + 11] = (unsigned long long)ns;
+  g_ecda_stamps[c * 16 + 10] = (unsigned long long)n;
+  g_ecda_stamps[c * 16 + 11] = (unsigned long long)ns;
 }
 #define TAIL_STAMP(k) \
-  if (threadIdx.x == 0) g_ecda_stamps[DAD_C * 12 + (k)] = wall_clock64()
+  if (threadIdx.x == 0) g_ecda_stamps[DAD_C * 16 + (k)] = wall_clock64()
 #else
 #define ECDA_STAMP(k)
 #define TAIL_STAMP(k)
@@ -431,8 +431,6 @@ __global__ __launch_bounds__(TAIL_THREADS) void dad_tail(DadTailArgs a) {
 
 #define ECDA_THREADS DAD_ECDA_THREADS
 static_assert(ECDA_THREADS % DAD_H == 0 && ECDA_THREADS >= DAD_H, "ECDA column groups");
-#define ECDA_GROUPS (ECDA_THREADS / DAD_H)   // column groups of 256 threads
-#define ECDA_BATCH 4                         // member rows per read-modify-write batch
 #define ECDA_NZ 80           // members staged in LDS (n <= 80); larger sets read global
 
 struct EcdaSmem {
@@ -448,6 +446,7 @@ struct EcdaSmem {
   int prd[DAD_MAX_BATCH];         // noisy pseudo-labels, -1 where not masked in
   float scr[DAD_MAX_BATCH];       // noisy certainty scores
   int wcount[ECDA_THREADS / 64];
+  float repg[DAD_H];              // repulsion grad of this class's noisy members, per hidden unit
 };
 
 __device__ __forceinline__ double ecda_block_sum_d(EcdaSmem& S, double v) {
@@ -533,30 +532,80 @@ template <bool STAGED>
 __device__ __forceinline__ float ecda_mmd_coef(EcdaSmem& S, const EcdaRows<STAGED>& R, int n, float* D) {
   const int tid = threadIdx.x;
   const int ns = R.ns;
-  // pairwise squared distances (I/utils.py:533-537).  Lane reads float4 (q + i + j) mod 64
-  // of both rows: consecutive pairs hit different LDS banks, and (i, j) / (j, i) sum in the
-  // same order, so D stays exactly symmetric.
+  // pairwise squared distances (I/utils.py:533-537), register-tiled: a work item is a 4x4
+  // block of member pairs over one slice of the 256 hidden units (ks slices per block, a
+  // power of two <= 16, as many as keep the workgroup busy).  Per float4 step a lane loads
+  // 8 rows' values and does 16 pairs' differences: 4x the arithmetic per LDS byte of a
+  // pair-per-lane loop.  The slice lanes of a block are adjacent and combined by a fixed
+  // butterfly; (i, j) and (j, i) run the same per-element order and the same butterfly
+  // (the slice rotation depends on bi + bj), so D stays exactly symmetric.
+  const int nb = (n + 3) >> 2, nblk = nb * nb;
+  int lks = 0;
+  while (lks < 4 && (2 << lks) * nblk <= ECDA_THREADS) ++lks;
+  const int ks = 1 << lks, qs = (DAD_H / 4) >> lks;   // slices per block, float4 steps per slice
+  const int nitem = nblk << lks;
   double part = 0.0;
-  for (int p = tid; p < n * n; p += ECDA_THREADS) {
-    const int i = p / n, j = p - i * n;
-    float d = 0.0f;
-    if (i != j) {
-      const f32x4* zi = reinterpret_cast<const f32x4*>(R.row(i));
-      const f32x4* zj = reinterpret_cast<const f32x4*>(R.row(j));
-      const int rot = (i + j) & 63;
-      f32x4 acc = f32x4{};            // four independent chains instead of one 256-long one
-#pragma unroll 4
-      for (int q = 0; q < DAD_H / 4; ++q) {
-        const int qq = (q + rot) & 63;
-        const f32x4 df = zj[qq] - zi[qq];
-        acc += df * df;
+  for (int it0 = 0; it0 < nitem; it0 += ECDA_THREADS) {   // uniform trip count: every lane shuffles
+    const int item = it0 + tid;
+    const bool on = item < nitem;
+    const int blk = on ? item >> lks : 0, sl = item & (ks - 1);
+    const int bi = blk / nb, bj = blk - bi * nb;
+    float acc[4][4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[p][q] = 0.0f;
+    if (on) {
+      const f32x4* zi[4];
+      const f32x4* zj[4];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        zi[p] = reinterpret_cast<const f32x4*>(R.row(min(4 * bi + p, n - 1))) + sl * qs;
+        zj[p] = reinterpret_cast<const f32x4*>(R.row(min(4 * bj + p, n - 1))) + sl * qs;
       }
-      d = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+      const int rot = bi + bj + sl;   // spreads the lanes of a wave over the banks
+      for (int q = 0; q < qs; ++q) {
+        const int qq = (q + rot) & (qs - 1);
+        f32x4 xi[4], xj[4];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          xi[p] = zi[p][qq];
+          xj[p] = zj[p][qq];
+        }
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const f32x4 df = xi[p] - xj[r];
+            acc[p][r] = acc[p][r] + df[0] * df[0];
+            acc[p][r] = acc[p][r] + df[1] * df[1];
+            acc[p][r] = acc[p][r] + df[2] * df[2];
+            acc[p][r] = acc[p][r] + df[3] * df[3];
+          }
+      }
     }
-    D[p] = d;
-    part += d;
+    for (int o = ks >> 1; o > 0; o >>= 1)
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[p][r] += __shfl_xor(acc[p][r], o, 64);
+    if (on && sl == 0) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = 4 * bi + p, j = 4 * bj + r;
+          if (i < n && j < n) {
+            const float d = i == j ? 0.0f : acc[p][r];
+            D[i * n + j] = d;
+            part += d;
+          }
+        }
+    }
   }
+  ECDA_STAMP(12);
   const double sumD = ecda_block_sum_d(S, part);
+  ECDA_STAMP(13);
   // detached bandwidth (I/utils.py:540-544): sum(D)/(n^2-n) / mul^(num//2), x mul^i
   float bw = (n > 1) ? (float)(sumD / (double)(n * n - n)) : 1.0f;
   bw = bw / 4.0f;
@@ -586,10 +635,12 @@ __device__ __forceinline__ float ecda_mmd_coef(EcdaSmem& S, const EcdaRows<STAGE
     else coef = 0.0f;   // the T x S block is not used by t_st
     D[p] = coef * dK;
   }
+  ECDA_STAMP(14);
   tss = ecda_block_sum_d(S, tss);
   ttt = ecda_block_sum_d(S, ttt);
   tst = ecda_block_sum_d(S, tst);
   const float mmd = (float)(tss / Wss + ttt / Wtt - 2.0 * (tst / Wst));
+  ECDA_STAMP(15);
   // symmetrise in place (each unordered pair owned by one thread)
   for (int p = tid; p < n * n; p += ECDA_THREADS) {
     const int i = p / n, j = p - i * n;
@@ -603,49 +654,51 @@ __device__ __forceinline__ float ecda_mmd_coef(EcdaSmem& S, const EcdaRows<STAGE
   return mmd;
 }
 
-// Embedding grads of the members into the ECDA part of dL/de (plain stores over the zeros
-// the tail wrote; a row belongs to at most one class), one column (hh = tid % 256) per
-// thread, members split over the ECDA_GROUPS column groups:
+// Embedding grads of the members into the ECDA part of dL/de (plain stores; a row belongs to
+// at most one class), register-tiled: a work item is 4 members x 4 hidden units (one float4
+// column chunk), so each member row chunk read from LDS serves 4 members' sums:
 //   g = mmd_scale * 2 sum_j Csym_ij (z_i - z_j)            (all members, if D)
-//     + comp_scale * (z_i - mu_c) + rep_g                    (noisy members)
+//     + comp_scale * (z_i - mu_c) + repg                     (noisy members)
 // comp_part accumulates sum ||z_i - mu_c||^2 over noisy members (when cent).
 template <bool STAGED>
 __device__ __forceinline__ void ecda_member_grads(EcdaSmem& S, const EcdaRows<STAGED>& R, int n, const float* D,
-                                                  float mmd_scale, const float* cent, float comp_scale, float rep_g,
-                                                  float* ge_c, float* ge_s, uint32_t* eflag, int B_,
-                                                  float& comp_part) {
-  const int hh = threadIdx.x & (DAD_H - 1);
-  const int grp = threadIdx.x / DAD_H;
+                                                  float mmd_scale, const float* cent, float comp_scale,
+                                                  const float* repg, float* ge_c, float* ge_s, uint32_t* eflag,
+                                                  int B_, float& comp_part) {
   const int ns = R.ns;
-  // group grp owns members grp, grp + G, grp + 2G, ...; ECDA_BATCH of them per batch
-  for (int m0 = grp; m0 < n; m0 += ECDA_BATCH * ECDA_GROUPS) {
+  const int nb = (n + 3) >> 2;
+  for (int item = threadIdx.x; item < nb * (DAD_H / 4); item += ECDA_THREADS) {
+    const int ib = item / (DAD_H / 4), hq = item - ib * (DAD_H / 4);
+    int m[4];
+    f32x4 zi[4], acc[4];
 #pragma unroll
-    for (int u = 0; u < ECDA_BATCH; ++u) {
-      const int m = m0 + u * ECDA_GROUPS;
-      if (m >= n) break;
-      float g = 0.0f;
-      float zi = 0.0f;
-      if (D || cent) zi = R.row(m)[hh];
-      if (D) {
-        float acc0 = 0.0f, acc1 = 0.0f;
-        int j = 0;
-        for (; j + 1 < n; j += 2) {
-          acc0 += D[m * n + j] * (zi - R.row(j)[hh]);
-          acc1 += D[m * n + j + 1] * (zi - R.row(j + 1)[hh]);
-        }
-        if (j < n) acc0 += D[m * n + j] * (zi - R.row(j)[hh]);
-        g = mmd_scale * (2.0f * (acc0 + acc1));
+    for (int p = 0; p < 4; ++p) {
+      m[p] = min(4 * ib + p, n - 1);
+      zi[p] = reinterpret_cast<const f32x4*>(R.row(m[p]))[hq];
+      acc[p] = f32x4{};
+    }
+    if (D) {
+      for (int j = 0; j < n; ++j) {
+        const f32x4 zj = reinterpret_cast<const f32x4*>(R.row(j))[hq];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) acc[p] += D[j * n + m[p]] * (zi[p] - zj);   // Csym[j][i] = Csym[i][j]
       }
-      if (m >= ns) {
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int mm = 4 * ib + p;
+      if (mm >= n) break;
+      f32x4 g = D ? mmd_scale * (2.0f * acc[p]) : f32x4{};
+      if (mm >= ns) {
         if (cent) {
-          const float df = zi - cent[hh];
-          comp_part += df * df;
+          const f32x4 df = zi[p] - reinterpret_cast<const f32x4*>(cent)[hq];
+          comp_part += ((df[0] * df[0] + df[1] * df[1]) + df[2] * df[2]) + df[3] * df[3];
           g += comp_scale * df;
         }
-        g += rep_g;
+        g += reinterpret_cast<const f32x4*>(repg)[hq];
       }
-      (m < ns ? ge_c : ge_s)[(size_t)S.idx[m] * DAD_H + hh] = g;
-      if (hh == 0) eflag[m < ns ? S.idx[m] : B_ + S.idx[m]] = 1u;
+      reinterpret_cast<f32x4*>((mm < ns ? ge_c : ge_s) + (size_t)S.idx[mm] * DAD_H)[hq] = g;
+      if (hq == 0) eflag[mm < ns ? S.idx[mm] : B_ + S.idx[mm]] = 1u;
     }
   }
 }
@@ -686,6 +739,7 @@ __global__ __launch_bounds__(ECDA_THREADS) void dad_ecda(DadEcdaArgs a) {
   if (!cfg.class_aware) {
     // global MMD ablation: all clean vs all masked noisy, unit weights (I/utils.py:633-650)
     if (c != 0) return;
+    if (tid < DAD_H) S.repg[tid] = 0.0f;   // no repulsion term (read after the compaction's barriers)
     int n = ecda_compact(S, B, 0, [](int) { return true; }, [](int) { return 1.0f; });
     const int ns = n;
     n = ecda_compact(S, Bn, n, [&](int i) { return S.prd[i] >= 0; }, [](int) { return 1.0f; });
@@ -699,7 +753,7 @@ __global__ __launch_bounds__(ECDA_THREADS) void dad_ecda(DadEcdaArgs a) {
         ecda_stage(S, R, n);
         const float mmd = ecda_mmd_coef(S, R, n, D);
         float unused = 0.0f;
-        ecda_member_grads(S, R, n, D, wscale, nullptr, 0.0f, 0.0f, ge_c, ge_s, a.eflag, B, unused);
+        ecda_member_grads(S, R, n, D, wscale, nullptr, 0.0f, S.repg, ge_c, ge_s, a.eflag, B, unused);
         if (tid == 0) { a.tail_terms[0] = mmd; a.tail_terms[DAD_T_ECDA_GATE - DAD_T_ECDA_TERM] = 1.0f; }
       };
       if (n <= ECDA_NZ) run(std::true_type{});
@@ -797,16 +851,19 @@ __global__ __launch_bounds__(ECDA_THREADS) void dad_ecda(DadEcdaArgs a) {
   }
   // repulsion grad of this class's noisy members (d rep / d mu_c, then 1/n_c per member)
   const bool rep_on = nvalid > 1 && S.cnt_noisy[c] > 0 && rep_coef != 0.0f;
-  float rep_g = 0.0f;
-  if (rep_on) {
-    const int hh = tid & (DAD_H - 1);
-    float gsum = 0.0f;
-    for (int q = 0; q < ncls; ++q) {
-      if (q == c || S.cnt_noisy[q] == 0) continue;
-      const float nd = pdist[c][q];
-      if (nd > 0.0f) gsum += (S.cent[c][hh] - S.cent[q][hh]) / nd;
+  if (tid < DAD_H) {
+    const int hh = tid;
+    float rep_g = 0.0f;
+    if (rep_on) {
+      float gsum = 0.0f;
+      for (int q = 0; q < ncls; ++q) {
+        if (q == c || S.cnt_noisy[q] == 0) continue;
+        const float nd = pdist[c][q];
+        if (nd > 0.0f) gsum += (S.cent[c][hh] - S.cent[q][hh]) / nd;
+      }
+      rep_g = wscale * rep_coef * (-gsum / (float)npairs / (float)S.cnt_noisy[c]);
     }
-    rep_g = wscale * rep_coef * (-gsum / (float)npairs / (float)S.cnt_noisy[c]);
+    S.repg[hh] = rep_g;   // read after the member compaction's barriers
   }
   if (!gated[c] && !rep_on) return;
   ECDA_STAMP(3);
@@ -839,7 +896,7 @@ __global__ __launch_bounds__(ECDA_THREADS) void dad_ecda(DadEcdaArgs a) {
     if (false)
 #endif
     ecda_member_grads(S, R, n, D, wscale * att_c, gated[c] ? S.cent[c] : nullptr,
-                      wscale * att_c * cfg.ecda_gamma * (2.0f / (float)nt), rep_g, ge_c, ge_s, a.eflag, B, cpart);
+                      wscale * att_c * cfg.ecda_gamma * (2.0f / (float)nt), S.repg, ge_c, ge_s, a.eflag, B, cpart);
   };
   if (n <= ECDA_NZ) run(std::true_type{});
   else run(std::false_type{});

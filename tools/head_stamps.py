@@ -25,18 +25,19 @@ def main():
         step.step(data[i % 2][0], data[i % 2][1], 60)
     torch.cuda.synchronize()
     L = PKG.lib()
-    ebuf = (ctypes.c_ulonglong * (4 * 12 + 12))()
+    ebuf = (ctypes.c_ulonglong * (4 * 16 + 12))()
     assert L.dad_probe_read_ecda_stamps(ebuf) == 0
     e = np.frombuffer(ebuf, dtype=np.uint64).astype(np.int64)
-    t0 = e[48]
+    t0 = e[64]
     rel = lambda v: (v - t0) / 100.0
     tn = ["end", "ce", "probs", "dacp", "kl", "outputs", "clsbwd"]
-    print("tail start 0 | " + "  ".join("%s %.2f" % (tn[k - 1], rel(e[48 + k])) for k in range(1, 8) if e[48 + k] > 0))
+    print("tail start 0 | " + "  ".join("%s %.2f" % (tn[k - 1], rel(e[64 + k])) for k in range(1, 8) if e[64 + k] > 0))
     names = ["start", "meta", "centroid", "gates", "zero", "compact", "stage", "mmd", "grads"]
     for c in range(4):
-        row = e[c * 12:c * 12 + 9]
+        row = e[c * 16:c * 16 + 16]
         parts = ["%s %.2f" % (names[k], rel(row[k])) for k in range(9) if row[k] > 0]
-        print("ecda class %d (n=%d ns=%d): %s" % (c, e[c * 12 + 10], e[c * 12 + 11], "  ".join(parts)))
+        sub = ["%s %.2f" % (nm, rel(row[k])) for k, nm in ((12, "dist"), (13, "sumD"), (14, "coef"), (15, "terms")) if row[k] > 0]
+        print("ecda class %d (n=%d ns=%d): %s | mmd: %s" % (c, e[c * 16 + 10], e[c * 16 + 11], "  ".join(parts), "  ".join(sub)))
 
 
 if __name__ == "__main__":
