@@ -1,0 +1,18 @@
+# Round profile: PMC passes (HBM traffic per kernel -> profiles/pmc_latest.json, read by
+# bench.py as roofline.traffic), the default bench line (with the CPU baseline), and a
+# rocprofv3 kernel-trace/stats run of bench.py; one markdown report.  TITLE names the report.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+TITLE=${TITLE:-profile}
+bash tools/gpu_pmc.sh > gpurun_out/pmc.log 2>&1 || { echo PMC_FAIL; tail -20 gpurun_out/pmc.log; exit 1; }
+python tools/profile_report.py "$TITLE" gpurun_out/report_pmc.md gpurun_out/none gpurun_out/pmc gpurun_out/pmc_latest.json || exit 1
+cp gpurun_out/pmc_latest.json profiles/pmc_latest.json
+timeout -k 10 600 python bench.py > gpurun_out/bench.log 2>&1 || { echo BENCH_FAIL; tail -30 gpurun_out/bench.log; exit 1; }
+grep '^{' gpurun_out/bench.log | tail -1 > gpurun_out/bench.json
+cat gpurun_out/bench.json
+cd /tmp
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run -- python "$GRAFT_REPO_ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --fp32-steps 0 > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1 || { echo PROF_FAIL; tail -20 "$GRAFT_REPO_ROOT/gpurun_out/prof.log"; exit 1; }
+cd "$GRAFT_REPO_ROOT"
+python tools/profile_report.py "$TITLE" gpurun_out/profile.md gpurun_out/prof gpurun_out/pmc && sed -n 1,14p gpurun_out/profile.md
