@@ -274,14 +274,19 @@ __device__ __forceinline__ void ws_convert(const Ctx& C, const Job& J, int w, in
         if constexpr (strong) {
           const f32x4 kp = *reinterpret_cast<const f32x4*>(fk + d);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = tzero ? 0.0f : v[e] * kp[e];
+          for (int e = 0; e < 4; ++e) v[e] = v[e] * kp[e];
         }
       }
-      bf16x4 o;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = (__bf16)v[e];
-      *reinterpret_cast<bf16x4*>(trow + 512 * k) = o;         // chunk 32k + (lane>>1), swizzled by row
-      if constexpr (KIND != KIND_WEAK) *reinterpret_cast<bf16x4*>((strong ? C.xsn : C.xs) + (size_t)grow * DAD_D + d) = o;
+      // two v_cvt_pk_bf16_f32 per 4 elements; the temporal zero selects the packed words
+      uint2 o = uint2{__builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{v[0], v[1]}, bf16x2)),
+                      __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{v[2], v[3]}, bf16x2))};
+      if constexpr (strong) o = tzero ? uint2{0u, 0u} : o;
+      *reinterpret_cast<uint2*>(trow + 512 * k) = o;           // chunk 32k + (lane>>1), swizzled by row
+      if constexpr (KIND != KIND_WEAK) {
+        // 32-bit byte offset from the uniform base (saddr store, no 64-bit address math)
+        const uint32_t boff = ((uint32_t)grow * (uint32_t)DAD_D + (uint32_t)d) * 2u;
+        *reinterpret_cast<uint2*>(reinterpret_cast<char*>(strong ? C.xsn : C.xs) + boff) = o;
+      }
       // one unit (4 elements, 2 Box-Muller pairs) per scheduling region: the wave's partner on
       // the SIMD covers its dependent latency, and nothing is hoisted across units
       __builtin_amdgcn_sched_barrier(0);
@@ -312,27 +317,34 @@ __device__ __forceinline__ bf16x8 afrag(const char* tile, const int (&aoff)[4]) 
   return *reinterpret_cast<const bf16x8*>(tile + aoff[KS & 3] + 256 * (KS >> 2));
 }
 
-// acc[t] = x_tile(16 rows) . W1[hw + 16t .. +15]^T over K = 768, the next k-step's A fragment
-// read while the current one's MFMAs issue.
+// acc[t] = x_tile(16 rows) . W1[hw + 16t .. +15]^T over K = 768.  A fragments are read
+// WS_LA k-steps ahead of their MFMAs: one k-step's MFMAs (NT x 16 cycles) are shorter than an
+// LDS read under load, so a one-step lookahead left every k-step waiting on its fragment.
+#ifndef WS_LA
+#define WS_LA 2   // 1 or 2
+#endif
+static_assert(WS_LA == 1 || WS_LA == 2, "A-fragment lookahead: 1 or 2 k-steps");
 template <class S, int KS>
 __device__ __forceinline__ void ws_mfma_from(const char* tile, const int (&aoff)[4], const bf16x8 (&wf)[S::NT][kKS],
-                                             f32x4 (&acc)[S::NT], bf16x8 xa) {
+                                             f32x4 (&acc)[S::NT], bf16x8 x0, bf16x8 x1) {
   if constexpr (KS < kKS) {
     bf16x8 xn;
-    if constexpr (KS + 1 < kKS) xn = afrag<KS + 1>(tile, aoff);
+    if constexpr (KS + WS_LA < kKS) xn = afrag<KS + WS_LA>(tile, aoff);
 #pragma unroll
     for (int t = 0; t < S::NT; ++t) {
       const bool agpr = S::AGPR_W && (t < 2 || (t == 2 && KS < 16));
-      if (agpr) mfma1<true, KS == 0>(acc[t], xa, wf[t][KS]);
-      else mfma1<false, KS == 0>(acc[t], xa, wf[t][KS]);
+      if (agpr) mfma1<true, KS == 0>(acc[t], x0, wf[t][KS]);
+      else mfma1<false, KS == 0>(acc[t], x0, wf[t][KS]);
     }
-    if constexpr (KS + 1 < kKS) ws_mfma_from<S, KS + 1>(tile, aoff, wf, acc, xn);
+    if constexpr (WS_LA == 1) ws_mfma_from<S, KS + 1>(tile, aoff, wf, acc, xn, xn);
+    else ws_mfma_from<S, KS + 1>(tile, aoff, wf, acc, x1, xn);
   }
 }
 template <class S>
 __device__ __forceinline__ void ws_mfma(const char* tile, const int (&aoff)[4], const bf16x8 (&wf)[S::NT][kKS],
                                         f32x4 (&acc)[S::NT]) {
-  ws_mfma_from<S, 0>(tile, aoff, wf, acc, afrag<0>(tile, aoff));
+  if constexpr (WS_LA == 1) ws_mfma_from<S, 0>(tile, aoff, wf, acc, afrag<0>(tile, aoff), afrag<0>(tile, aoff));
+  else ws_mfma_from<S, 0>(tile, aoff, wf, acc, afrag<0>(tile, aoff), afrag<1>(tile, aoff));
   // MFMA D -> VALU readers of the epilogue (hipcc pads nothing after an asm MFMA)
   if constexpr (S::NT == 4) asm volatile("s_nop 7\n\ts_nop 7" ::"v"(acc[0]), "v"(acc[1]), "v"(acc[2]), "v"(acc[3]));
   else asm volatile("s_nop 7\n\ts_nop 7" ::"v"(acc[0]), "v"(acc[1]));

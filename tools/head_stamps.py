@@ -32,7 +32,7 @@ def main():
     rel = lambda v: (v - t0) / 100.0
     tn = ["end", "ce", "probs", "dacp", "kl", "outputs", "clsbwd"]
     print("tail start 0 | " + "  ".join("%s %.2f" % (tn[k - 1], rel(e[64 + k])) for k in range(1, 8) if e[64 + k] > 0))
-    names = ["start", "meta", "centroid", "gates", "zero", "compact", "stage", "mmd", "grads"]
+    names = ["start", "meta", "centroid", "gates", "pdist", "compact", "stage", "mmd", "grads"]
     for c in range(4):
         row = e[c * 16:c * 16 + 16]
         parts = ["%s %.2f" % (names[k], rel(row[k])) for k in range(9) if row[k] > 0]

@@ -52,6 +52,13 @@ def main():
             print("        fit: clean sub-slab %.3f us, strong sub-slab %.3f us" % tuple(coef))
         print("        wave-0 cycles/sub-slab p50: wait %.0f  mfma %.0f  convert %.0f  epilogue %.0f  dma %.0f  barrier %.0f" %
               tuple(np.median(cyc, axis=0)))
+        if r == 0:
+            # per-kind phase cycles: least squares of each workgroup's phase sums on its sub-slab counts
+            sums = st[m, 4:10].astype(np.float64)
+            fit, *_ = np.linalg.lstsq(A, sums, rcond=None)
+            for kname, row in (("clean", fit[0]), ("strong", fit[1])):
+                print("        %-6s fit cycles/sub-slab: wait %.0f  mfma %.0f  convert %.0f  epilogue %.0f  dma %.0f  barrier %.0f"
+                      % ((kname,) + tuple(row)))
 
 
 def student_kinds(B, T, nt, ns, wstrong=1.47):
