@@ -1,5 +1,6 @@
 // Host side of the C ABI (include/dad.h): argument validation, workspace carving and the
 // kernel sequence of one DAD step.  Enqueue-only: no allocation, no synchronisation.
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -96,6 +97,14 @@ int side_stream(SideStream** out) {
   }
   *out = &ss;
   return DAD_OK;
+}
+
+// BF16 weight-gradient strategy: the direct GEMM after the losses (default), or the factorised
+// S_u GEMM on the side stream (DAD_WGRAD=su, read per step).  Measured on MI355X the
+// side-stream fork/join latency (~7 + ~12 us) cancels the overlap, so direct is the default.
+bool wgrad_direct() {
+  const char* e = getenv("DAD_WGRAD");
+  return !(e && strcmp(e, "su") == 0);
 }
 
 int device_cus(int* out) {
@@ -226,9 +235,10 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   }
   if (!do_backward) return DAD_OK;
 
-  // 2. FP32: the loss-independent factor of dW1 on the side stream, S_u = bits_u^T X_u per
-  //    utterance (clean rows, then the strong-augmented noisy rows), concurrent with 3-5.
-  //    BF16: the direct GEMM runs after ECDA (6), with dL/de folded into its A operand.
+  // 2. The loss-independent factor of dW1 on the side stream, S_u = bits_u^T X_u per
+  //    utterance (clean rows, then the strong-augmented noisy rows; BF16: the encoder's bf16
+  //    copies, S_u stored in bf16), concurrent with 3-5, for FP32 and for BF16 with DAD_WGRAD=su.
+  //    BF16 default: one direct GEMM after ECDA (6) with dL/de folded into its A operand.
   const int nutt = G.Bc + Bn;
   float* sbuf = ws_ptr<float>(workspace, L.sbuf);
   DadWgradArgs wa;
@@ -241,15 +251,23 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   wa.strong_std = cfg->strong_std; wa.feat_p = cfg->feat_p;
   wa.bits = bits; wa.ge = ge; wa.vlen = vlen; wa.xs_bf16 = xs_bf16;
   SideStream* side = nullptr;
-  if (!bf16) {
+  const bool factorised = !bf16 || !wgrad_direct();
+  if (factorised) {
     const int rc = side_stream(&side);
     if (rc) return rc;
     wa.splits = nutt; wa.per_utt = 1; wa.wpart = sbuf;
-    wa.ntiles = 6 * nutt;
-    const int sgrid = std::max(1, std::min(wa.ntiles, side->cus - kReservedCUs));
     DAD_TRY(hipEventRecord(side->fork, stream));
     DAD_TRY(hipStreamWaitEvent(side->s, side->fork, 0));
-    hipLaunchKernelGGL(dad_wgrad_f32, dim3(sgrid), dim3(DAD_WGRAD_THREADS), 0, side->s, wa);
+    if (bf16) {
+      wa.su = reinterpret_cast<__bf16*>(sbuf);
+      wa.ntiles = WGD_NDB * nutt;
+      const int sgrid = std::max(1, std::min(wa.ntiles, side->cus - kReservedCUs));
+      hipLaunchKernelGGL(dad_wgrad_su, dim3(sgrid), dim3(WGD_THREADS), 0, side->s, wa);
+    } else {
+      wa.ntiles = 6 * nutt;
+      const int sgrid = std::max(1, std::min(wa.ntiles, side->cus - kReservedCUs));
+      hipLaunchKernelGGL(dad_wgrad_f32, dim3(sgrid), dim3(DAD_WGRAD_THREADS), 0, side->s, wa);
+    }
     DAD_TRY(hipGetLastError());
     DAD_TRY(hipEventRecord(side->join, side->s));
   }
@@ -289,7 +307,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
     DAD_TRY(hipGetLastError());
   }
 
-  // 6. dW1 (BF16: direct split-K GEMM; FP32: join, then sum_u (dL/de_u / len_u) * S_u), db1,
+  // 6. dW1 (join, then sum_u (dL/de_u / len_u) * S_u; or the direct split-K GEMM), db1,
   //    dW2, loss totals, squared-norm partials
   DadReduceArgs ra;
   memset(&ra, 0, sizeof(ra));
@@ -302,7 +320,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   ra.key_drop1 = k.drop1; ra.key_drop2 = k.drop2; ra.p_drop = cfg->p_drop; ra.drop_scale = cfg->drop_scale;
   ra.ge = ge; ra.vlen = vlen; ra.cnt_tot = cnt_tot; ra.tailf = st->tail;
   ra.grad = st->grad; ra.normpart = normpart;
-  if (bf16) {
+  if (!factorised) {
     wa.splits = splits; wa.per_utt = 0;
     wa.wpart = ws_ptr<float>(workspace, L.wpart);
     wa.ntiles = WGD_NDB * splits;
@@ -314,6 +332,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   } else {
     DAD_TRY(hipStreamWaitEvent(stream, side->join, 0));
     ra.splits = nutt; ra.wpart = sbuf;
+    if (bf16) ra.su = wa.su;
     hipLaunchKernelGGL(dad_wsum, dim3(DAD_REDUCE_BLOCKS), dim3(DAD_REDUCE_THREADS), 0, stream, ra);
   }
   DAD_TRY(hipGetLastError());

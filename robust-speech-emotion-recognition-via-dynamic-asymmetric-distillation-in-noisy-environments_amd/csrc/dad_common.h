@@ -214,7 +214,7 @@ struct DadWs {
   size_t xs_bf16;    // bf16 [Bc*Tc + Bn*Tn][768]   BF16 mode: the student's MFMA input, clean rows then strong rows (wgrad operand)
   size_t w1bf;       // bf16 [H][D]                 modular encoder ops: bf16 copy of W1
   size_t gflat;      // f32 [DAD_GRAD_FLOATS]       modular encoder backward: scratch grad vector
-  size_t sbuf;       // f32 [Bc + Bn][H][D]         FP32 step: S_u = bits_u^T X_u, the loss-independent factor of dW1
+  size_t sbuf;       // [Bc + Bn][H][D]             S_u = bits_u^T X_u, the loss-independent factor of dW1 (f32; bf16 in BF16 mode)
   size_t bytes;
   int splits;
 };
@@ -225,10 +225,13 @@ static inline size_t dad_align(size_t x) { return (x + 255) & ~(size_t)255; }
 // splits.  BF16 (dad_wgrad_direct, 12 column blocks per split): 21 splits -> 252 workgroups,
 // one per CU, and never more than WGD_MAXU = 64 slabs per split (its dL/de table in LDS).
 // Both are bounded by the number of 32-row slabs.
+#ifndef WGD_SPLITS
+#define WGD_SPLITS 21   // x 12 column blocks = 252 workgroups (one per CU with 2 slab groups)
+#endif
 static inline int dad_wgd_min_splits(int total) { return (total + 63) / 64; }
 static inline int dad_auto_splits(const DadGeom& g, int precision, int warmup) {
   const int total = g.Bc * g.ncc + (warmup ? 0 : g.Bn * g.ncn);
-  const int target = precision == DAD_PREC_BF16 ? 21 : 64;
+  const int target = precision == DAD_PREC_BF16 ? WGD_SPLITS : 64;
   int s = total < target ? total : target;
   if (precision == DAD_PREC_BF16 && s < dad_wgd_min_splits(total)) s = dad_wgd_min_splits(total);
   return s;
@@ -256,7 +259,7 @@ static inline DadWs dad_ws_layout(const DadGeom& g, int splits, int precision, b
   w.xs_bf16 = off;  off = dad_align(off + (precision == DAD_PREC_BF16 ? 2 * ((size_t)g.Bc * g.Tc + (size_t)g.Bn * g.Tn) * DAD_D : 0));
   w.w1bf = off;     off = dad_align(off + 2 * (size_t)DAD_H * DAD_D);
   w.gflat = off;    off = dad_align(off + sizeof(float) * DAD_GRAD_FLOATS);
-  w.sbuf = off;     off = dad_align(off + (fused && precision != DAD_PREC_BF16 ? sizeof(float) * nb * DAD_H * DAD_D : 0));
+  w.sbuf = off;     off = dad_align(off + (fused ? (precision == DAD_PREC_BF16 ? 2 : sizeof(float)) * nb * DAD_H * DAD_D : 0));
   w.bytes = off;
   return w;
 }

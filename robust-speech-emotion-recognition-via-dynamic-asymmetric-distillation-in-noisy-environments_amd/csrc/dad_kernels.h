@@ -100,6 +100,7 @@ struct DadWgradArgs {
   float* wpart;
   int per_utt;         // 1: one split per utterance with G = ReLU' bits (S_u = bits_u^T X_u into wpart[u])
   int ntiles;          // column blocks x splits; workgroups stride over them (grid may be smaller)
+  __bf16* su;          // dad_wgrad_su: S_u = bits_u^T X_u, bf16 [Bc + Bn][H][D]
 };
 
 struct DadReduceArgs {
@@ -107,6 +108,7 @@ struct DadReduceArgs {
   int splits, warmup, want_norm;
   float w_kl, w_ecda;
   const float* wpart; const float* ge; const float* vlen; const float* cnt_tot;
+  const __bf16* su;           // dad_wsum (BF16 step): bf16 S_u instead of the fp32 wpart slabs
   const float* ge_ecda;       // ECDA part of dL/de, added where eflag is set
   // fused step: dL/de is not materialised; the classifier part is rebuilt per (utterance, h)
   // as keep(u,h) * sum_c W2[c][h] gzb[u][c] (nn.Linear + dropout backward, I/model.py:62-63)
@@ -135,6 +137,7 @@ __global__ void dad_tail(DadTailArgs a);
 __global__ void dad_ecda(DadEcdaArgs a);
 __global__ void dad_wgrad_f32(DadWgradArgs a);
 __global__ void dad_wgrad_direct(DadWgradArgs a, DadReduceArgs r);
+__global__ void dad_wgrad_su(DadWgradArgs a);
 __global__ void dad_wsum(DadReduceArgs a);
 __global__ void dad_reduce(DadReduceArgs a);
 __global__ void dad_norm(float* grad, float* normpart, float inv_world);

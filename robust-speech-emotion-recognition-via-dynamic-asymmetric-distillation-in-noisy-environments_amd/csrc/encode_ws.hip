@@ -232,6 +232,9 @@ __device__ __forceinline__ int live_rows(const Job& J, int half, int w) {
 // so the 3*RPW independent RNG chains interleave): rows past the utterance are converted as
 // copies of its last row (identical bytes to the same xs address), temporally masked rows
 // are selected to zero after the RNG.  Noise comes pre-scaled (dad_normal_pair_c).
+#ifndef WS_REGION
+#define WS_REGION 1
+#endif
 template <class S, int NOISE, int KIND, int HALF>
 __device__ __forceinline__ void ws_convert(const Ctx& C, const Job& J, int w, int lane_, const float* raw, char* tile,
                                            const float* fk) {
@@ -287,9 +290,10 @@ __device__ __forceinline__ void ws_convert(const Ctx& C, const Job& J, int w, in
         const uint32_t boff = ((uint32_t)grow * (uint32_t)DAD_D + (uint32_t)d) * 2u;
         *reinterpret_cast<uint2*>(reinterpret_cast<char*>(strong ? C.xsn : C.xs) + boff) = o;
       }
-      // one unit (4 elements, 2 Box-Muller pairs) per scheduling region: the wave's partner on
-      // the SIMD covers its dependent latency, and nothing is hoisted across units
-      __builtin_amdgcn_sched_barrier(0);
+      // WS_REGION units (4 elements, 2 Box-Muller pairs each) per scheduling region: the
+      // wave's partner on the SIMD covers the rest of the dependent latency, and nothing is
+      // hoisted across regions
+      if ((k + 1) % WS_REGION == 0 || k == 2) __builtin_amdgcn_sched_barrier(0);
     }
   }
 }

@@ -318,12 +318,13 @@ struct WgdRaw {
   uint32_t gp[2];
 };
 
+template <bool SU>
 __device__ __forceinline__ WgdRaw wgd_read(const __bf16* Xt, const uint32_t (&mk)[2], const uint2* lut,
                                            const uint16_t* gs, int ul, int wv) {
   WgdRaw w;
   const int i = threadIdx.x & 31;
 #pragma unroll
-  for (int m = 0; m < 2; ++m) w.gp[m] = gs[ul * DAD_H + (2 * wv + m) * 32 + i];
+  for (int m = 0; m < 2; ++m) w.gp[m] = SU ? 0x3f80u : gs[ul * DAD_H + (2 * wv + m) * 32 + i];   // SU: bf16 1.0
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
 #pragma unroll
@@ -385,29 +386,15 @@ __device__ __forceinline__ int wgd_utt(const DadGeom& g, int s) {
 
 }  // namespace
 
-__global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct(DadWgradArgs a, DadReduceArgs ra) {
-  DAD_GUARD_BLOCK(WGD_THREADS);
-  __shared__ __attribute__((aligned(16))) __bf16 Xt[WGD_GROUPS * 2 * DAD_SLAB * WGD_XP];
-  __shared__ __attribute__((aligned(16))) uint2 lut[16];
-  __shared__ __attribute__((aligned(16))) uint16_t gs[WGD_MAXU * DAD_H];
-  __shared__ __attribute__((aligned(16))) float red[WGD_GROUPS == 2 ? DAD_H * WGD_DB : 1];
+// one 256 h x WGD_DB d tile over slabs [s0, s1): fp32 partial (direct) or bf16 S_u (SU)
+template <bool SU>
+__device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceArgs& ra, int s0, int s1, int dbase,
+                                         float* outf, __bf16* outb, __bf16* Xt, const uint2* lut, uint16_t* gs,
+                                         float* red) {
   const int tid = threadIdx.x;
-  // wave-uniform by construction; readfirstlane lets the compiler keep the group's cursor
-  // and flags in scalar registers
   const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane((tid >> 6) & 3);
   const int grp = __builtin_amdgcn_readfirstlane(tid >> 8);
-  // XCD-aware tile order (grid is a multiple of 8; workgroups go round-robin over the 8
-  // XCDs): each XCD takes a consecutive run of tiles, so the column blocks of one split,
-  // which read the same ReLU' row masks, share an L2
-  const int per_xcd = gridDim.x >> 3;
-  const int tile = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
-  if (tile >= a.ntiles) return;
-  const int split = tile / WGD_NDB, dblk = tile - split * WGD_NDB;
-  const int dbase = dblk * WGD_DB;
   const DadGeom& g = a.g;
-  const int total = wg_total(a);
-  const int per = (total + a.splits - 1) / a.splits;
-  const int s0 = split * per, s1 = min(total, s0 + per);
   f32x16 acc[2][2];
 #pragma unroll
   for (int m = 0; m < 2; ++m)
@@ -432,7 +419,7 @@ __global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct(DadWgradArgs 
     // host bounds a split to WGD_MAXU slabs, hence utterances.  The first eight utterances'
     // vector loads go out before the slab prefetch, so their math never waits on it.
     float w2[4] = {0.0f, 0.0f, 0.0f, 0.0f}, ec0[8];
-    if (grp == 0) {
+    if (!SU && grp == 0) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) w2[c] = ra.student[DAD_OFF_W2 + c * DAD_H + tid];
 #pragma unroll
@@ -446,7 +433,7 @@ __global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct(DadWgradArgs 
     // loads make the compiler merge the paths' pending counts into a vmcnt(0) drain
 #pragma unroll
     for (int k = 0; k < WGD_DEPTH; ++k) wgd_load(a, tab, min(k, jlast), sfirst, dbase, wv, r[k]);
-    if (grp == 0) {
+    if (!SU && grp == 0) {
       for (int ul0 = 0; ul0 < nu; ul0 += 8) {
         float v[8];
 #pragma unroll
@@ -459,14 +446,6 @@ __global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct(DadWgradArgs 
         for (int k = 0; k < 8; ++k)
           if (ul0 + k < nu) gs[(ul0 + k) * DAD_H + tid] = __builtin_bit_cast(uint16_t, (__bf16)v[k]);
       }
-    }
-    if (tid - 256 * (WGD_GROUPS - 1) < 16) {
-      const int t = tid - 256 * (WGD_GROUPS - 1);
-      uint32_t e[2];
-#pragma unroll
-      for (int p = 0; p < 2; ++p)
-        e[p] = (((t >> (2 * p)) & 1) ? 0x0000ffffu : 0u) | (((t >> (2 * p + 1)) & 1) ? 0xffff0000u : 0u);
-      lut[t] = uint2{e[0], e[1]};
     }
     // slab 0 of each group into buffer 0; its ring slot reloads slab WGD_DEPTH
     if (mine > 0) wgd_stage(r[0], Xg);
@@ -484,7 +463,7 @@ __global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct(DadWgradArgs 
       const unsigned long long c0 = WGD_CLK();
       const int nk = (k + 1) % WGD_DEPTH;
       WgdRaw R;
-      if (comp) R = wgd_read(Xg + (k & 1) * (DAD_SLAB * WGD_XP), mw, lut, gs, ul, wv);
+      if (comp) R = wgd_read<SU>(Xg + (k & 1) * (DAD_SLAB * WGD_XP), mw, lut, gs, ul, wv);
       __builtin_amdgcn_sched_barrier(0);   // reads first, their latency under the MFMAs
       if (prev) wgd_mma(F, acc);
       if (stage) wgd_stage(r[nk], Xg + ((k + 1) & 1) * (DAD_SLAB * WGD_XP));
@@ -516,7 +495,6 @@ __global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct(DadWgradArgs 
     t2 = WGD_CLK();
   }
   const int kh = lane >> 5;
-  float* out = a.wpart + (size_t)split * DAD_H * DAD_D;
   if constexpr (WGD_GROUPS == 2) {
     // exchange halves: group 0 finishes h tile 2w (+ group 1's partial), group 1 tile 2w+1
 #pragma unroll
@@ -538,10 +516,66 @@ __global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct(DadWgradArgs 
         for (int rr = 0; rr < 16; ++rr) {
           const int h = (2 * wv + m) * 32 + dad_acc_row(rr, kh);
           const int d = 32 * nn + (lane & 31);
-          out[(size_t)h * DAD_D + dbase + d] = acc[m][nn][rr] + (WGD_GROUPS == 2 ? red[h * WGD_DB + d] : 0.0f);
+          const float v = acc[m][nn][rr] + (WGD_GROUPS == 2 ? red[h * WGD_DB + d] : 0.0f);
+          if constexpr (SU) outb[(size_t)h * DAD_D + dbase + d] = (__bf16)v;
+          else outf[(size_t)h * DAD_D + dbase + d] = v;
         }
+  if constexpr (WGD_GROUPS == 2) __syncthreads();   // red free for the next tile
   WGD_ACC(0, t1 - t0); WGD_ACC(1, t2 - t1); WGD_ACC(2, WGD_CLK() - t2);
   (void)t0; (void)t1; (void)t2;
+}
+
+// the 16-entry nibble table of the A-fragment masks (threads 0..15)
+__device__ __forceinline__ void wgd_lut(uint2* lut) {
+  const int t = threadIdx.x;
+  if (t < 16) {
+    uint32_t e[2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+      e[p] = (((t >> (2 * p)) & 1) ? 0x0000ffffu : 0u) | (((t >> (2 * p + 1)) & 1) ? 0xffff0000u : 0u);
+    lut[t] = uint2{e[0], e[1]};
+  }
+}
+
+__global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct(DadWgradArgs a, DadReduceArgs ra) {
+  DAD_GUARD_BLOCK(WGD_THREADS);
+  __shared__ __attribute__((aligned(16))) __bf16 Xt[WGD_GROUPS * 2 * DAD_SLAB * WGD_XP];
+  __shared__ __attribute__((aligned(16))) uint2 lut[16];
+  __shared__ __attribute__((aligned(16))) uint16_t gs[WGD_MAXU * DAD_H];
+  __shared__ __attribute__((aligned(16))) float red[WGD_GROUPS == 2 ? DAD_H * WGD_DB : 1];
+  // XCD-aware tile order (grid is a multiple of 8; workgroups go round-robin over the 8
+  // XCDs): each XCD takes a consecutive run of tiles, so the column blocks of one split,
+  // which read the same ReLU' row masks, share an L2
+  const int per_xcd = gridDim.x >> 3;
+  const int tile = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+  if (tile >= a.ntiles) return;
+  const int split = tile / WGD_NDB, dblk = tile - split * WGD_NDB;
+  const int total = wg_total(a);
+  const int per = (total + a.splits - 1) / a.splits;
+  const int s0 = split * per, s1 = min(total, s0 + per);
+  wgd_lut(lut);   // (the tile's first barrier orders it before the first read)
+  wgd_tile<false>(a, ra, s0, s1, dblk * WGD_DB, a.wpart + (size_t)split * DAD_H * DAD_D, nullptr, Xt, lut, gs, red);
+}
+
+// FP32-free loss-independent factor for the BF16 step: S_u = bits_u^T X_u (G = 0/1 exactly,
+// bf16 output) per (utterance, column block), persistent workgroups striding over the tiles.
+// Runs on a side stream concurrently with pool/tail/ECDA; dad_wsum applies dL/de_u / len_u.
+__global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_su(DadWgradArgs a) {
+  DAD_GUARD_BLOCK(WGD_THREADS);
+  __shared__ __attribute__((aligned(16))) __bf16 Xt[WGD_GROUPS * 2 * DAD_SLAB * WGD_XP];
+  __shared__ __attribute__((aligned(16))) uint2 lut[16];
+  __shared__ __attribute__((aligned(16))) float red[WGD_GROUPS == 2 ? DAD_H * WGD_DB : 1];
+  DadReduceArgs unused;
+  const DadGeom& g = a.g;
+  const int nsc = g.Bc * g.ncc;
+  wgd_lut(lut);
+  for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+    const int u = tile / WGD_NDB, dblk = tile - u * WGD_NDB;
+    const int s0 = u < g.Bc ? u * g.ncc : nsc + (u - g.Bc) * g.ncn;
+    const int s1 = s0 + (u < g.Bc ? g.ncc : g.ncn);
+    wgd_tile<true>(a, unused, s0, s1, dblk * WGD_DB, nullptr, a.su + (size_t)u * DAD_H * DAD_D, Xt, lut, nullptr,
+                   red);
+  }
 }
 
 // ---------------------------------------------------------------- reduce + squared norms
@@ -676,7 +710,8 @@ __global__ __launch_bounds__(DAD_REDUCE_THREADS) void dad_reduce(DadReduceArgs a
   }
 }
 
-// FP32 fused-step weight-gradient finish: dW1[h][d] = sum_u g_u[h] * S_u[h][d],
+// Factorised weight-gradient finish (FP32 S_u in wpart, or BF16 S_u in su):
+// dW1[h][d] = sum_u g_u[h] * S_u[h][d],
 // g_u[h] = dL/de_u[h] / max(1, len_u).  Blocks [0, NB): DAD_REDUCE_COLS columns of one
 // row h; thread = (float4 column, utterance group ug), utterances ug, ug+4, ... with eight
 // loads in flight, the four groups combined in fixed order (deterministic).  Blocks NB + e:
@@ -706,10 +741,23 @@ __global__ __launch_bounds__(DAD_REDUCE_THREADS) void dad_wsum(DadReduceArgs a) 
     f32x4 s = f32x4{};
     for (int u0 = ug; u0 < nutt; u0 += 4 * 8) {
       f32x4 v[8];
+      if (a.su) {
+        bf16x4 vb[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int u = min(u0 + 4 * k, nutt - 1);
-        v[k] = *reinterpret_cast<const f32x4*>(a.wpart + (size_t)u * DAD_H * DAD_D + off);
+        for (int k = 0; k < 8; ++k) {
+          const int u = min(u0 + 4 * k, nutt - 1);
+          vb[k] = *reinterpret_cast<const bf16x4*>(a.su + (size_t)u * DAD_H * DAD_D + off);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[k][e] = (float)vb[k][e];
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int u = min(u0 + 4 * k, nutt - 1);
+          v[k] = *reinterpret_cast<const f32x4*>(a.wpart + (size_t)u * DAD_H * DAD_D + off);
+        }
       }
 #pragma unroll
       for (int k = 0; k < 8; ++k)

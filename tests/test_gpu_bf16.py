@@ -81,3 +81,22 @@ def test_bf16_counter_steps_stay_finite():
         o = gh.run_step(step, inp, 40 + k, with_draws=False)
         assert all(np.isfinite(o[n]) for n in ("total_loss", "supervised_ce_loss", "consistency_loss", "ecda_loss"))
         assert all(np.all(np.isfinite(p)) for p in o["student"])
+
+
+def test_bf16_factorised_weight_gradient_matches_direct(monkeypatch):
+    """DAD_WGRAD=su (S_u = bits_u^T X_u on the side stream, then the dL/de-weighted sum) and
+    the default direct GEMM compute the same dW1 from the same bf16 operands."""
+    cfg = dad_oracle.make_cfg("iemocap")
+    inp = _problem(B=20, T=90, seed=8, Bn=18, Tn=110, ragged=True)
+    st = synth.make_state(8, 1)
+    outs = []
+    for mode in ("direct", "su"):
+        monkeypatch.setenv("DAD_WGRAD", mode)
+        step = gh.make_step(cfg, precision="bf16", rng="counter", seed=5)
+        gh.load_state(step, st)
+        outs.append(gh.run_step(step, inp, 60, with_draws=False))
+    d, s = outs
+    assert np.array_equal(d["mask"], s["mask"])
+    for gd, gs in zip(d["grads"], s["grads"]):
+        gh.close(gs, gd, BF16_TOL, "factorised vs direct grad")
+    assert _grad_cos(d["grads"], s["grads"]) > 0.999
