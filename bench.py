@@ -117,6 +117,56 @@ def cpu_baseline(B, T, steps, epoch, seconds=CPU_BASELINE_SECONDS):
                       "noise sampling; median %.3f s/step" % (len(times) - 1, sum(times[1:]), B, T, epoch, med)}
 
 
+def data_path_bench(step, B, T, epoch, dev, n_utt=1024, reps=40, steps=20):
+    """The device-resident data path (csrc/collate.hip): dad_collate of
+    a [B, T] batch from a FeatureStore of n_utt full-length utterances (n_utt*T*3 KB in HBM,
+    well past the caches), timed with HIP events on the launch stream; then the train step fed
+    by two DeviceLoaders over the store (clean + noisy collated every step, inside the clock)."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(3)
+    feats = torch.randn(n_utt * T, 768, device=dev, generator=g)
+    sizes = np.full(n_utt, T, np.int64)
+    offsets = np.arange(n_utt, dtype=np.int64) * T
+    labels = np.arange(n_utt, dtype=np.int64) % 4
+    store = PKG.data.FeatureStore(feats, sizes, offsets, labels, device=dev)
+    del feats
+    idx = [np.random.RandomState(k).choice(n_utt, B, replace=False) for k in range(reps)]
+    idx_d = [torch.from_numpy(i).to(dev) for i in idx]
+    for k in range(3):
+        store.collate(idx[k], index_d=idx_d[k], T=T)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for k in range(reps):
+        store.collate(idx[k], index_d=idx_d[k], T=T)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    nbytes = B * T * 768 * 4 * 2 + B * T + B * 16       # rows read + rows written + mask + labels
+    # the step with both batches collated on the device inside the timed region
+    clean = PKG.data.DeviceLoader(store, batch_size=B, shuffle=True)
+    noisy = PKG.data.DeviceLoader(store.subset(np.arange(n_utt), with_labels=False), batch_size=B, shuffle=True)
+    def epochs(loader):      # a new epoch (a new shuffle) whenever one runs out, as a trainer's epoch loop does
+        while True:
+            yield from loader
+
+    ci, ni = epochs(clean), epochs(noisy)
+    for _ in range(3):
+        step.step(next(ci), next(ni), epoch)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step.step(next(ci), next(ni), epoch)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    return {"kernel": "dad_collate_kernel", "store": "%d utterances x %d frames x 768 f32 (%.2f GB) resident in HBM"
+            % (n_utt, T, n_utt * T * 3072 / 1e9), "collate_ms": ms, "algorithmic_bytes_per_launch": nbytes,
+            "achieved_gbs": nbytes / (ms * 1e-3) / 1e9, "peak_gbs": HBM_PEAK_GBS,
+            "frac": nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "step_with_device_collate": {"value": B / dt, "unit": "utterances/s", "ms_per_step": dt * 1e3,
+                                         "steps": steps, "note": "clean + noisy batch collated per step"}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -129,6 +179,7 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--fp32-steps", type=int, default=10, help="also time the FP32 parity mode (N=1)")
+    ap.add_argument("--no-data-path", action="store_true", help="skip the device collate measurement (N=1)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -191,6 +242,9 @@ def main():
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t1) / args.fp32_steps
         fp32 = {"value": B / dt, "ms_per_step": dt * 1e3, "dtype": "f32"}
+    data_path = None
+    if rank == 0 and world == 1 and not args.no_data_path:
+        data_path = data_path_bench(step, B, T, args.epoch, dev)
 
     if rank != 0:
         if dist:
@@ -224,6 +278,8 @@ def main():
     }
     if fp32 is not None:
         line["fp32_mode"] = fp32
+    if data_path is not None:
+        line["data_path"] = data_path
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(B, T, args.cpu_steps, args.epoch)
     print(json.dumps(line), flush=True)

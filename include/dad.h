@@ -199,6 +199,27 @@ int dad_encoder_backward(const float* x, const uint8_t* pad, int B, int T, const
                          const float* b1, const float* de, float* dw1, float* db1,
                          void* workspace, void* stream);
 
+/* --- device-resident data path ---------------------------
+ * One padded batch gathered from a feature store resident in HBM.  Replaces the DataLoader's
+ * per-sample row slice + .float() (NoisyEmotionDatasetFromArrays.__getitem__,
+ * I/dataload_noisy.py:104-115; CleanEmotionDatasetFromArrays.__getitem__, I/dataload_clean.py:
+ * 170-176) and its collator (I/dataload_noisy.py:116-129, I/dataload_clean.py:177-193,
+ * C/dataload_casia_noisy.py:68-99):
+ *   store     [frames][768] features of the whole split, dtype DAD_STORE_*
+ *   offsets   [n_samples] int64 first frame of each sample; sizes [n_samples] int32 frames
+ *   index     [B] int64 sample indices of this batch (the sampler's order)
+ *   T         padded length, >= max(sizes[index]) (the collator's target_size)
+ *   feats     [B][T][768] f32 out: sample rows, zeros past each size
+ *   pad       [B][T] u8 out: 1 = padding (padding_mask[i, size:] = True)
+ *   labels_in [n_samples] int64, labels_out [B] int64: both null for an unlabeled loader
+ * An index outside [0, n_samples) yields an all-padding row and label -1 (no read). */
+#define DAD_STORE_F32 0
+#define DAD_STORE_F16 1
+#define DAD_STORE_BF16 2
+int dad_collate(const void* store, int store_dtype, const int64_t* offsets, const int32_t* sizes,
+                int64_t n_samples, const int64_t* index, int B, int T, float* feats, uint8_t* pad,
+                const int64_t* labels_in, int64_t* labels_out, void* stream);
+
 /* --- data-parallel gradient exchange (RCCL over xGMI) ------------------------------ */
 int dad_comm_unique_id_bytes(void);
 int dad_comm_get_unique_id(void* id_out);

@@ -14,9 +14,10 @@ from .config import FLAVOR_DEFAULTS, ConfigView, dad_config_for
 from .model import EmotionClassifier, Emotion2VecEncoder, SSRLModel
 from .step import DADStep
 from .dist import DPComm, ProcessGroupComm
+from .data import DeviceLoader, FeatureStore
 
 __all__ = ["SSRLModel", "Emotion2VecEncoder", "EmotionClassifier", "DADStep", "DPComm", "ProcessGroupComm", "ConfigView",
-           "dad_config_for", "FLAVOR_DEFAULTS", "build", "lib"]
+           "dad_config_for", "FLAVOR_DEFAULTS", "FeatureStore", "DeviceLoader", "build", "lib"]
 
 
 def build(verbose=True):
@@ -29,5 +30,5 @@ def lib():
 
 
 _sys.modules.setdefault("dad_amd", _sys.modules[__name__])
-for _m in ("_build", "_lib", "config", "model", "step", "dist"):
+for _m in ("_build", "_lib", "config", "model", "step", "dist", "data"):
     _sys.modules.setdefault("dad_amd." + _m, _sys.modules[__name__ + "." + _m])

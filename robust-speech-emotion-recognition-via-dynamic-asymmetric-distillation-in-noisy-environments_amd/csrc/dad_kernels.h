@@ -27,6 +27,7 @@
 #define DAD_REDUCE_XBLK 16                                   // db1 / dW2 / totals blocks (16 hidden units each)
 #define DAD_REDUCE_BLOCKS (DAD_H * DAD_D / DAD_REDUCE_COLS + DAD_REDUCE_XBLK)
 #define DAD_OPTIM_THREADS 256
+#define DAD_COLLATE_THREADS 256                              // device collate (4 waves, 2 rows each)
 #define DAD_GUARD_BLOCK(n) \
   if (blockDim.x != (n) || blockDim.y != 1 || blockDim.z != 1) return
 
@@ -129,6 +130,17 @@ struct DadOptimArgs {
   float* losses_out;
 };
 
+// device-resident data path (collate.hip)
+struct DadCollateArgs {
+  const void* store; int dtype;
+  const int64_t* offsets; const int32_t* sizes; long n_samples;
+  const int64_t* index; int B, T;
+  float* feats; uint8_t* pad;
+  const int64_t* labels_in; int64_t* labels_out;
+};
+
+__global__ void dad_collate_kernel(DadCollateArgs a);
+int dad_collate_grid(long B, long T);
 __global__ void dad_encode_f32(DadEncodeArgs a);
 __global__ void dad_encode_ws(DadEncodeArgs a);            // counter RNG
 __global__ void dad_encode_ws_explicit(DadEncodeArgs a);   // explicit noise tensors (parity)

@@ -211,7 +211,13 @@ __device__ __forceinline__ void dma_rows(const float* x, const Job& J, int half,
   for (int i = 0; i < S::RPW; ++i) {
     const int r = S::RPW * w + i;
     const int t = min(J.c * DAD_SLAB + half * kSub + r, J.T - 1);
+#ifdef DAD_PROBE_WS_L2
+    // diagnostic build only: kinds in the mask read one fixed 16-row block (L2 hits), which
+    // removes their HBM reads from the encoder's traffic
+    const float* src = x + (size_t)(((DAD_PROBE_WS_L2 >> J.kind) & 1) ? r : J.row0 + t) * DAD_D + 4 * lane;
+#else
     const float* src = x + (size_t)(J.row0 + t) * DAD_D + 4 * lane;
+#endif
     const uint32_t dst = __builtin_amdgcn_readfirstlane(stage_base + (uint32_t)(r * kRawRow));
 #pragma unroll
     for (int k = 0; k < 3; ++k) glds16(src + 256 * k, dst + 1024u * (uint32_t)k);

@@ -14,7 +14,10 @@ _KEYS = set(dad_oracle.FLAVOR_DEFAULTS["iemocap"])
 
 
 def variants():
-    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz")))
+    # step fixtures (gen_golden.py); the data-path fixtures data_*.npz (gen_data_golden.py) are
+    # replayed by test_data_cpu.py / test_gpu_data.py
+    return sorted(n for n in (os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz")))
+                  if not n.startswith("data_"))
 
 
 def load(name):

@@ -1,0 +1,159 @@
+"""Device-resident data path on the MI355X: the dad_collate gather (csrc/collate.hip, through
+the C ABI) against the reference loaders' golden outputs and the NumPy oracle.  Bit-exact:
+collation copies and widens, it does not round."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+import dadpkg
+from oracle import data_oracle as do
+from test_data_cpu import CASIA_LOADERS, IEMOCAP_LOADERS, _golden
+
+pytestmark = pytest.mark.gpu
+PKG = dadpkg.pkg()
+D = PKG.data
+
+
+def _compare(g, name, loader, seed, with_ids=True):
+    torch.manual_seed(seed)
+    shapes, pads, labs, sums, sumsqs, ids = [], [], [], [], [], []
+    for batch in loader:
+        x = batch["net_input"]["feats"].cpu().numpy().astype(np.float64)
+        shapes.append(x.shape[:2])
+        pads.append(batch["net_input"]["padding_mask"].cpu().numpy().reshape(-1))
+        lab = batch.get("labels")
+        labs.append(np.full(x.shape[0], -2, np.int64) if lab is None else lab.cpu().numpy())
+        sums.append(x.sum())
+        sumsqs.append((x * x).sum())
+        if with_ids:
+            ids.append(batch["id"].cpu().numpy())
+    np.testing.assert_array_equal(np.array(shapes), g[name + "_shapes"], err_msg=name)
+    np.testing.assert_array_equal(np.concatenate(pads), g[name + "_pad"], err_msg=name)
+    np.testing.assert_array_equal(np.concatenate(labs), g[name + "_labels"], err_msg=name)
+    np.testing.assert_array_equal(np.array(sums), g[name + "_sum"], err_msg=name)
+    np.testing.assert_array_equal(np.array(sumsqs), g[name + "_sumsq"], err_msg=name)
+    if with_ids:
+        np.testing.assert_array_equal(np.concatenate(ids), g[name + "_ids"], err_msg=name)
+
+
+def test_iemocap_device_loaders_match_reference(tmp_path):
+    g = _golden("data_iemocap")
+    seed, bs, fold = int(g["seed"]), int(g["batch_size"]), int(g["fold"])
+    do.write_synthetic_split(str(tmp_path), seed, n_utt=150, max_len=40, flavor="iemocap")
+    noisy = D.get_cv_dataloaders_noisy(str(tmp_path), bs, fold_id=fold)
+    clean = D.get_cv_dataloaders(str(tmp_path), bs, fold_id=fold)[:3]
+    for (name, _, _, _, s), ld in zip(IEMOCAP_LOADERS, list(noisy) + list(clean)):
+        _compare(g, name, ld, s)
+
+
+def test_casia_device_loaders_match_reference(tmp_path):
+    g = _golden("data_casia")
+    seed, bs, fold = int(g["seed"]), int(g["batch_size"]), int(g["fold"])
+    prefix = do.write_synthetic_split(str(tmp_path), seed, n_utt=90, max_len=30, flavor="casia")
+    np.random.seed(seed)
+    store, spk = D.load_casia_noisy_data(prefix)
+    loaders = D.create_casia_noisy_speaker_isolated_loaders(store, spk, fold, bs)
+    for (name, _, _, _, s), ld in zip(CASIA_LOADERS, loaders):
+        _compare(g, name, ld, s, with_ids=False)
+
+
+def _store(seed, n, max_len, dtype=torch.float32):
+    rs = np.random.RandomState(seed)
+    sizes = rs.randint(1, max_len + 1, size=n)
+    feats = rs.standard_normal((int(sizes.sum()), 768)).astype(np.float32)
+    offsets = np.concatenate([[0], np.cumsum(sizes)[:-1]])
+    labels = rs.randint(0, 4, size=n)
+    return feats, sizes, offsets, labels, D.FeatureStore(feats, sizes, offsets, labels, dtype=dtype)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16, torch.bfloat16])
+def test_collate_matches_oracle_each_store_dtype(dtype):
+    feats, sizes, offsets, labels, st = _store(21, 40, 33, dtype)
+    # the oracle gathers the store's values widened to f32 (Tensor.float())
+    ref_feats = torch.from_numpy(feats).to(dtype).float().numpy()
+    for index in ([3], [0, 1, 2, 3], list(range(39, -1, -3)), [7, 7, 7]):
+        got = st.collate(index)
+        ref = do.collate(ref_feats, sizes, offsets, labels, index)
+        np.testing.assert_array_equal(got["net_input"]["feats"].cpu().numpy(), ref["feats"])
+        np.testing.assert_array_equal(got["net_input"]["padding_mask"].cpu().numpy(), ref["padding_mask"])
+        np.testing.assert_array_equal(got["labels"].cpu().numpy(), ref["labels"])
+        np.testing.assert_array_equal(got["id"].cpu().numpy(), ref["id"])
+
+
+def test_collate_explicit_pad_length_and_unlabeled():
+    feats, sizes, offsets, labels, st = _store(22, 12, 9)
+    index = [4, 0, 11]
+    T = int(sizes[index].max()) + 5          # longer than the batch max: extra rows are padding
+    got = st.collate(index, T=T, with_labels=False)
+    ref = do.collate(feats, sizes, offsets, None, index)
+    x = got["net_input"]["feats"].cpu().numpy()
+    np.testing.assert_array_equal(x[:, :ref["feats"].shape[1]], ref["feats"])
+    assert not x[:, ref["feats"].shape[1]:].any()
+    assert got["net_input"]["padding_mask"].cpu().numpy()[:, ref["feats"].shape[1]:].all()
+    assert got["labels"] is None
+
+
+def test_collate_c_abi_out_of_range_index_is_padding():
+    feats, sizes, offsets, labels, st = _store(23, 10, 6)
+    L = PKG.lib()
+    index = torch.tensor([2, -1, 10, 5], dtype=torch.int64, device="cuda")
+    B, T = 4, 6
+    out = torch.full((B, T, 768), 7.0, device="cuda")
+    pad = torch.full((B, T), 9, dtype=torch.uint8, device="cuda")
+    lab = torch.full((B,), 9, dtype=torch.int64, device="cuda")
+    p = lambda t: ctypes.c_void_p(t.data_ptr())
+    rc = L.dad_collate(p(st.feats), 0, p(st.offsets_d), p(st.sizes_d), len(st), p(index), B, T, p(out), p(pad),
+                       p(st.labels_d), p(lab), torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    torch.cuda.synchronize()
+    x, m, y = out.cpu().numpy(), pad.cpu().numpy(), lab.cpu().numpy()
+    for i in (1, 2):
+        assert not x[i].any() and m[i].all() and y[i] == -1
+    ref = do.collate(feats, sizes, offsets, labels, [2, 5])
+    for i, j in ((0, 0), (3, 1)):
+        n = ref["feats"].shape[1]
+        np.testing.assert_array_equal(x[i, :n], ref["feats"][j])
+        assert not x[i, n:].any()
+        np.testing.assert_array_equal(m[i, :n], ref["padding_mask"][j])
+        assert m[i, n:].all() and y[i] == labels[[2, 5][j]]
+    # argument errors come back as codes, nothing is launched
+    assert L.dad_collate(None, 0, p(st.offsets_d), p(st.sizes_d), 10, p(index), B, T, p(out), p(pad), None, None,
+                         None) == 1001
+    assert L.dad_collate(p(st.feats), 5, p(st.offsets_d), p(st.sizes_d), 10, p(index), B, T, p(out), p(pad), None,
+                         None, None) == 1001
+    assert L.dad_collate(p(st.feats), 0, p(st.offsets_d), p(st.sizes_d), 10, p(index), 0, T, p(out), p(pad), None,
+                         None, None) == 1002
+
+
+def test_collate_bench_shape_bit_exact():
+    """The benchmark's shape: B=64, T=300 from a store of 160 utterances up to 300 frames."""
+    rs = np.random.RandomState(24)
+    sizes = rs.randint(200, 301, size=160)
+    sizes[rs.choice(160, 8, replace=False)] = 300
+    feats = rs.standard_normal((int(sizes.sum()), 768)).astype(np.float32)
+    offsets = np.concatenate([[0], np.cumsum(sizes)[:-1]])
+    st = D.FeatureStore(feats, sizes, offsets, rs.randint(0, 4, size=160))
+    index = rs.permutation(160)[:64]
+    index[0] = int(np.argmax(sizes))
+    got = st.collate(index)
+    ref = do.collate(feats, sizes, offsets, st.labels, index)
+    assert got["net_input"]["feats"].shape == (64, 300, 768)
+    np.testing.assert_array_equal(got["net_input"]["feats"].cpu().numpy(), ref["feats"])
+    np.testing.assert_array_equal(got["net_input"]["padding_mask"].cpu().numpy(), ref["padding_mask"])
+
+
+def test_device_batches_drive_the_step(tmp_path):
+    """The loaders' batches go straight into DADStep (the reference loop body)."""
+    do.write_synthetic_split(str(tmp_path), 31, n_utt=80, max_len=25, flavor="iemocap")
+    clean = D.get_cv_dataloaders(str(tmp_path), 8, fold_id=1)[0]
+    noisy = D.get_cv_dataloaders_noisy(str(tmp_path), 8, fold_id=1)[0]
+    model = PKG.SSRLModel().cuda()
+    step = PKG.DADStep(model, flavor="iemocap", precision="bf16", rng="counter", seed=2)
+    torch.manual_seed(0)
+    ci, ni = iter(clean), iter(noisy)
+    for _ in range(2):
+        losses = step.step(next(ci), next(ni), 60)
+    torch.cuda.synchronize()
+    assert all(np.isfinite(float(v)) for v in losses.values())
