@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define DAD_ABI_VERSION 1
+#define DAD_ABI_VERSION 2
 
 /* error codes (besides hipError_t values) */
 #define DAD_OK 0
@@ -128,6 +128,17 @@ typedef struct dad_batch {
   const int64_t* start;         /* [Bn] temporal-mask starts */
   const uint8_t* keep1;         /* [B][256] classifier dropout keep mask, clean pass */
   const uint8_t* keep2;         /* [Bn][256] classifier dropout keep mask, strong pass */
+  /* STORE MODE, per batch (rowc+lenc for the clean one, rown+lenn for the noisy one; NULL =
+   * padded): xc / xn point at a feature store [frames][768] (FeatureStore, the device-
+   * resident data path) instead of a padded [B][T][768] batch, and
+   * frame t < T of utterance b is store row rowc[b] + min(t, lenc[b] - 1) (rown/lenn for the
+   * noisy batch).  The encoder's LDS-DMA reads the rows in place: collation never copies the
+   * features.  mc / mn / yc keep their [B][T] / [B] meaning (dad_collate_index builds them
+   * together with rowc / lenc). */
+  const int64_t* rowc;          /* [B] store row of frame 0 of each clean utterance */
+  const int32_t* lenc;          /* [B] its frame count (rows >= it are padding) */
+  const int64_t* rown;          /* [Bn] */
+  const int32_t* lenn;          /* [Bn] */
 } dad_batch;
 
 /* Persistent training state, all caller-owned device buffers. */
@@ -219,6 +230,14 @@ int dad_encoder_backward(const float* x, const uint8_t* pad, int B, int T, const
 int dad_collate(const void* store, int store_dtype, const int64_t* offsets, const int32_t* sizes,
                 int64_t n_samples, const int64_t* index, int B, int T, float* feats, uint8_t* pad,
                 const int64_t* labels_in, int64_t* labels_out, void* stream);
+
+/* Store-mode batch index (see dad_batch): for each b, row_out[b] = offsets[index[b]],
+ * len_out[b] = sizes[index[b]] (0 and row 0 for an index outside [0, n_samples)),
+ * pad [B][T] and labels exactly as dad_collate writes them -- the collator's outputs without
+ * the feature copy. */
+int dad_collate_index(const int64_t* offsets, const int32_t* sizes, int64_t n_samples, const int64_t* index,
+                      int B, int T, int64_t* row_out, int32_t* len_out, uint8_t* pad,
+                      const int64_t* labels_in, int64_t* labels_out, void* stream);
 
 /* --- data-parallel gradient exchange (RCCL over xGMI) ------------------------------ */
 int dad_comm_unique_id_bytes(void);

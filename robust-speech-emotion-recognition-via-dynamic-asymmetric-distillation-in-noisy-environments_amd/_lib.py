@@ -54,7 +54,8 @@ class DadConfig(ctypes.Structure):
 
 class DadBatch(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in
-                ("xc", "mc", "yc", "xn", "mn", "nw", "ns", "u", "start", "keep1", "keep2")]
+                ("xc", "mc", "yc", "xn", "mn", "nw", "ns", "u", "start", "keep1", "keep2",
+                 "rowc", "lenc", "rown", "lenn")]
 
 
 class DadState(ctypes.Structure):
@@ -94,6 +95,9 @@ EXPORTS = {
     "dad_collate": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                    ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "dad_collate_index": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                         ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "dad_comm_unique_id_bytes": (ctypes.c_int, []),
     "dad_comm_get_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
     "dad_comm_init": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_void_p, ctypes.c_int]),

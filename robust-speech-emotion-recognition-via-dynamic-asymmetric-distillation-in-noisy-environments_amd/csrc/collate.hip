@@ -17,6 +17,8 @@
 // consecutive rows with all their loads issued before the first store (6 loads in flight per
 // lane); the store is read once per epoch, so its loads are non-temporal (they do not evict
 // the output the encoder reads next from L2).
+#include <cstring>
+
 #include "dad_common.h"
 #include "dad_kernels.h"
 
@@ -125,6 +127,22 @@ __global__ __launch_bounds__(DAD_COLLATE_THREADS) void dad_collate_kernel(DadCol
   }
 }
 
+// store-mode index: one thread per (b, t) pad byte; threads t == 0 also write row/len/label
+__global__ __launch_bounds__(256) void dad_collate_index_kernel(DadCollateArgs a, int64_t* row_out, int32_t* len_out) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)a.B * a.T) return;
+  const int b = (int)(i / a.T), t = (int)(i - (long)b * a.T);
+  const long s = a.index[b];
+  const bool ok = s >= 0 && s < a.n_samples;
+  const int size = ok ? a.sizes[s] : 0;
+  a.pad[i] = t < size ? 0 : 1;
+  if (t == 0) {
+    row_out[b] = size > 0 ? a.offsets[s] : 0;     // an empty sample reads nothing past the store
+    len_out[b] = size;
+    if (a.labels_out) a.labels_out[b] = ok ? a.labels_in[s] : -1;
+  }
+}
+
 int dad_collate_grid(long B, long T) {
   const long per = (long)kWaves * kRowsPerWave;
   return (int)((B * T + per - 1) / per);
@@ -143,6 +161,23 @@ extern "C" int dad_collate(const void* store, int store_dtype, const int64_t* of
   a.labels_in = labels_in; a.labels_out = labels_out;
   hipLaunchKernelGGL(dad_collate_kernel, dim3(dad_collate_grid(B, T)), dim3(DAD_COLLATE_THREADS), 0,
                      (hipStream_t)stream, a);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? DAD_OK : (int)e;
+}
+
+extern "C" int dad_collate_index(const int64_t* offsets, const int32_t* sizes, int64_t n_samples, const int64_t* index,
+                                 int B, int T, int64_t* row_out, int32_t* len_out, uint8_t* pad,
+                                 const int64_t* labels_in, int64_t* labels_out, void* stream) {
+  if (!offsets || !sizes || !index || !row_out || !len_out || !pad) return DAD_E_ARG;
+  if ((labels_in == nullptr) != (labels_out == nullptr)) return DAD_E_ARG;
+  if (B <= 0 || T <= 0 || n_samples <= 0) return DAD_E_SHAPE;
+  DadCollateArgs a;
+  memset(&a, 0, sizeof(a));
+  a.offsets = offsets; a.sizes = sizes; a.n_samples = (long)n_samples; a.index = index; a.B = B; a.T = T;
+  a.pad = pad; a.labels_in = labels_in; a.labels_out = labels_out;
+  const long n = (long)B * T;
+  hipLaunchKernelGGL(dad_collate_index_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, a,
+                     row_out, len_out);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? DAD_OK : (int)e;
 }

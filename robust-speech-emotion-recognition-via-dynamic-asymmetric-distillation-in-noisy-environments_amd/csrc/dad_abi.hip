@@ -179,6 +179,10 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   const bool explicit_rng = cfg->rng_mode == DAD_RNG_EXPLICIT;
   if (explicit_rng && cfg->p_drop > 0.0f && (!bt->keep1 || (!cfg->warmup && !bt->keep2))) return DAD_E_ARG;
   if (explicit_rng && !cfg->warmup && (!bt->nw || !bt->ns || !bt->u || !bt->start)) return DAD_E_ARG;
+  // store mode, per batch (clean and noisy independently): rows and lengths together
+  if ((bt->rowc == nullptr) != (bt->lenc == nullptr) || (bt->rown == nullptr) != (bt->lenn == nullptr))
+    return DAD_E_ARG;
+  const DadStoreRows src = {bt->rowc, bt->lenc, bt->rown, bt->lenn};
   hipStream_t stream = (hipStream_t)stream_;
   const DadGeom G = geom_of(cfg);
   const int Bn = cfg->warmup ? 0 : G.Bn;
@@ -205,7 +209,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   memset(&ea, 0, sizeof(ea));
   ea.g = G; ea.warmup = cfg->warmup;
   ea.mask_len = cfg->mask_len; ea.start_hi = cfg->start_hi;
-  ea.xc = bt->xc; ea.mc = bt->mc; ea.xn = bt->xn; ea.mn = bt->mn;
+  ea.xc = bt->xc; ea.mc = bt->mc; ea.xn = bt->xn; ea.mn = bt->mn; ea.src = src;
   ea.w1_student = st->student + DAD_OFF_W1; ea.b1_student = st->student + DAD_OFF_B1;
   ea.w1_teacher = st->teacher + DAD_OFF_W1; ea.b1_teacher = st->teacher + DAD_OFF_B1;
   ea.w1bf_student = reinterpret_cast<const __bf16*>(st->w1bf_student);
@@ -245,7 +249,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   memset(&wa, 0, sizeof(wa));
   wa.g = G; wa.warmup = cfg->warmup;
   wa.mask_len = cfg->mask_len; wa.start_hi = cfg->start_hi;
-  wa.xc = bt->xc; wa.xn = bt->xn;
+  wa.xc = bt->xc; wa.xn = bt->xn; wa.src = src;
   if (explicit_rng) { wa.ns = bt->ns; wa.u = bt->u; wa.start = bt->start; }
   wa.key_strong = k.strong; wa.key_feat = k.feat; wa.key_tstart = k.tstart;
   wa.strong_std = cfg->strong_std; wa.feat_p = cfg->feat_p;

@@ -108,6 +108,22 @@ __device__ __forceinline__ f32x4 dad_normal4(uint32_t key, uint32_t row, uint32_
   return z;
 }
 
+// Source rows of the feature tensors.  Padded mode: frame t of utterance b is row b*T + t of
+// the [B][T][768] batch.  Store mode (dad_batch.rowc..lenn set): row base[b] + min(t, len[b]-1)
+// of the feature store, so padding frames re-read the utterance's last frame (every consumer
+// masks them) and nothing is read past the utterance.  Noise / RNG indices always use the
+// padded row b*T + t, so both modes draw the same values.
+struct DadStoreRows {
+  const int64_t* rowc; const int32_t* lenc;
+  const int64_t* rown; const int32_t* lenn;
+};
+__device__ __forceinline__ size_t dad_src_row(const DadStoreRows& s, bool noisy, int b, int T, int t) {
+  const int64_t* base = noisy ? s.rown : s.rowc;
+  if (!base) return (size_t)b * T + t;
+  const int len = (noisy ? s.lenn : s.lenc)[b];
+  return (size_t)(base[b] + min(t, max(len, 1) - 1));
+}
+
 // W1 bf16 shadow layout = the B-fragment order of the W-stationary encoder (encode_ws.hip):
 // fragment ((w*4 + t)*24 + ks) is 64 lanes x 8 bf16, lane l holding
 // W1[h = 64w + 16t + (l & 15)][k = 32ks + 8(l >> 4) + j], so each wave loads its resident

@@ -36,6 +36,7 @@ struct DadEncodeArgs {
   int warmup, mask_len, start_hi;
   const float* xc; const uint8_t* mc;
   const float* xn; const uint8_t* mn;
+  DadStoreRows src;         // store mode (dad_batch.rowc..lenn) or all NULL
   const float* w1_student; const float* b1_student;
   const float* w1_teacher; const float* b1_teacher;
   const __bf16* w1bf_student; const __bf16* w1bf_teacher;
@@ -93,6 +94,7 @@ struct DadWgradArgs {
   DadGeom g;
   int warmup, splits, mask_len, start_hi;
   const float* xc; const float* xn;
+  DadStoreRows src;
   const float* ns; const float* u; const int64_t* start;
   uint32_t key_strong, key_feat, key_tstart;
   float strong_std, feat_p;

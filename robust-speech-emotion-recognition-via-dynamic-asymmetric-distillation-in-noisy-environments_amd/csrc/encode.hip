@@ -152,7 +152,7 @@ __global__ __launch_bounds__(DAD_ENC_F32_THREADS) void dad_encode_f32(DadEncodeA
   const uint8_t* pad = g.noisy ? a.mn : a.mc;
   const bool valid = tin && pad[g.row0 + t] == 0;
   const uint32_t vbits = (uint32_t)__ballot(valid);
-  const float* X = (g.noisy ? a.xn : a.xc) + (size_t)grow * DAD_D;
+  const float* X = (g.noisy ? a.xn : a.xc) + dad_src_row(a.src, g.noisy, g.b, g.T, tin ? t : 0) * DAD_D;
   bool tzero = false;
   if (g.noisy && a.mask_len > 0) {
     const int st = tmask_start(a, g.b);

@@ -77,6 +77,7 @@ struct Ctx {
   int nsc, nsn, Jc, Js;
   int mask_len, start_hi;
   const float* xc; const float* xn;
+  DadStoreRows src;
   const uint8_t* mc; const uint8_t* mn;
   const float* nw; const float* ns; const float* u; const int64_t* start;
   uint32_t key_weak, key_strong, key_feat, key_tstart;
@@ -94,7 +95,7 @@ __device__ __forceinline__ Ctx ctx_of(const DadEncodeArgs& a) {
   c.mcn = c.ncn > 1 ? 0xffffffffu / (uint32_t)c.ncn + 1u : 0u;
   c.Jc = c.nsc; c.Js = a.warmup ? 0 : c.nsn;
   c.mask_len = a.mask_len; c.start_hi = a.start_hi;
-  c.xc = a.xc; c.xn = a.xn; c.mc = a.mc; c.mn = a.mn;
+  c.xc = a.xc; c.xn = a.xn; c.src = a.src; c.mc = a.mc; c.mn = a.mn;
   c.nw = a.nw; c.ns = a.ns; c.u = a.u; c.start = a.start;
   c.key_weak = a.key_weak; c.key_strong = a.key_strong; c.key_feat = a.key_feat; c.key_tstart = a.key_tstart;
   c.wstd = a.weak_std; c.sstd = a.strong_std; c.feat_p = a.feat_p;
@@ -115,6 +116,8 @@ struct Job {
   long row0;        // [b][T] row of frame 0
   long sum_slab;    // part_sum slab
   long cnt_slab;    // part_cnt slab = ReLU' row-mask slab (student only)
+  long src0;        // source row of frame 0: row0, or the store row (store mode)
+  int srcT;         // source frames: T, or the utterance's length (store mode)
 };
 
 // job j of the workgroup's role list: teacher -> weak slab j; student -> clean slab j, then
@@ -131,6 +134,9 @@ __device__ __forceinline__ Job job_of(const Ctx& C, bool teacher, int j) {
   J.row0 = (long)J.b * J.T;
   J.sum_slab = teacher ? (long)C.nsc + s : (noisy ? (long)C.nsc + C.nsn + s : (long)s);
   J.cnt_slab = noisy ? (long)C.nsc + s : (long)s;
+  const int64_t* base = noisy ? C.src.rown : C.src.rowc;
+  J.src0 = base ? base[J.b] : J.row0;
+  J.srcT = base ? max((noisy ? C.src.lenn : C.src.lenc)[J.b], 1) : J.T;
   return J;
 }
 
@@ -203,21 +209,16 @@ struct Shape {
 };
 
 // DMA the wave's RPW rows of sub-slab (J, half) into a raw stage.  Frames past the
-// utterance are clamped to its last frame (masked out by the valid bits).
+// utterance (padded mode: past T; store mode: past its length) are clamped to its last
+// source frame (masked out by the valid bits).
 template <class S>
 __device__ __forceinline__ void dma_rows(const float* x, const Job& J, int half, int w, uint32_t stage_base,
                                          int lane) {
 #pragma unroll
   for (int i = 0; i < S::RPW; ++i) {
     const int r = S::RPW * w + i;
-    const int t = min(J.c * DAD_SLAB + half * kSub + r, J.T - 1);
-#ifdef DAD_PROBE_WS_L2
-    // diagnostic build only: kinds in the mask read one fixed 16-row block (L2 hits), which
-    // removes their HBM reads from the encoder's traffic
-    const float* src = x + (size_t)(((DAD_PROBE_WS_L2 >> J.kind) & 1) ? r : J.row0 + t) * DAD_D + 4 * lane;
-#else
-    const float* src = x + (size_t)(J.row0 + t) * DAD_D + 4 * lane;
-#endif
+    const int t = min(J.c * DAD_SLAB + half * kSub + r, J.srcT - 1);
+    const float* src = x + (size_t)(J.src0 + t) * DAD_D + 4 * lane;
     const uint32_t dst = __builtin_amdgcn_readfirstlane(stage_base + (uint32_t)(r * kRawRow));
 #pragma unroll
     for (int k = 0; k < 3; ++k) glds16(src + 256 * k, dst + 1024u * (uint32_t)k);

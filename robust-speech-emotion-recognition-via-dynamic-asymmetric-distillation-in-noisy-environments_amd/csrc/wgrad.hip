@@ -139,7 +139,7 @@ __global__ __launch_bounds__(DAD_WGRAD_THREADS) void dad_wgrad_f32(DadWgradArgs 
       const int t = q.c * DAD_SLAB + rr + kh;
       const bool tin = t < q.T;
       const size_t grow = q.row0 + (tin ? t : 0);
-      float x = tin ? X[grow * DAD_D + d] : 0.0f;
+      float x = tin ? X[dad_src_row(a.src, q.br, q.b, q.T, t) * DAD_D + d] : 0.0f;
       if (q.br && tin) {
         const float n = a.ns ? a.ns[grow * DAD_D + d] : dad_normal1(a.key_strong, (uint32_t)(grow * DAD_D + d));
         const float sn = n * a.strong_std;

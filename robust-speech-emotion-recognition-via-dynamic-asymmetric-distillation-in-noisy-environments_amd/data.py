@@ -129,21 +129,75 @@ class FeatureStore:
             _lib.ptr(self.feats), STORE_DTYPES[self.feats.dtype], _lib.ptr(self.offsets_d), _lib.ptr(self.sizes_d),
             len(self), _lib.ptr(index_d), B, T, _lib.ptr(feats), _lib.ptr(pad),
             _lib.ptr(self.labels_d if lab is not None else None), _lib.ptr(lab), s.cuda_stream), "dad_collate")
+        return self._pack(index_d, feats, pad, lab, style)
+
+    def batch_index(self, index, index_d=None, T=None, style="iemocap", with_labels=True, stream=None):
+        """Store-mode batch (no feature copy): the collator's dict with net_input['feats'] a
+        StoreFeats over this store; padding mask and labels as collate() writes them
+        (dad_collate_index)."""
+        index = np.asarray(index, dtype=np.int64).reshape(-1)
+        B = len(index)
+        if B == 0:
+            return {}
+        if index.min() < 0 or index.max() >= len(self):
+            raise IndexError("sample index out of range [0, %d)" % len(self))
+        if T is None:
+            T = int(self.sizes[index].max())
+        if index_d is None:
+            index_d = torch.from_numpy(index).to(self.device, non_blocking=True)
+        rows = torch.empty(B, dtype=torch.int64, device=self.device)
+        lens = torch.empty(B, dtype=torch.int32, device=self.device)
+        pad = torch.empty(B, T, dtype=torch.uint8, device=self.device)
+        lab = None
+        if with_labels and self.labels_d is not None:
+            lab = torch.empty(B, dtype=torch.int64, device=self.device)
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        _lib.check(_lib.lib().dad_collate_index(
+            _lib.ptr(self.offsets_d), _lib.ptr(self.sizes_d), len(self), _lib.ptr(index_d), B, T, _lib.ptr(rows),
+            _lib.ptr(lens), _lib.ptr(pad), _lib.ptr(self.labels_d if lab is not None else None), _lib.ptr(lab),
+            s.cuda_stream), "dad_collate_index")
+        return self._pack(index_d, StoreFeats(self, index, index_d, rows, lens, T), pad, lab, style)
+
+    @staticmethod
+    def _pack(index_d, feats, pad, lab, style):
         net_input = {"feats": feats, "padding_mask": pad.view(torch.bool)}
         if style == "casia":           # C/dataload_casia_noisy.py:93-106: no 'id'; 'labels' only when labeled
             return {"net_input": net_input, **({"labels": lab} if lab is not None else {})}
         return {"id": index_d, "net_input": net_input, "labels": lab}
 
 
+class StoreFeats:
+    """net_input['feats'] of a store-mode batch: B utterances of a FeatureStore at padded
+    length T, NOT copied -- DADStep hands the store and the per-utterance rows/lengths to the
+    encoder, whose LDS-DMA reads the rows in place (dad_batch store mode, include/dad.h).
+    .shape is the padded batch's; .materialize() returns the padded f32 tensor (dad_collate)."""
+
+    def __init__(self, store, index, index_d, rows, lens, T):
+        self.store, self.index, self.index_d, self.rows, self.lens = store, index, index_d, rows, lens
+        self.shape = torch.Size((len(index), T, 768))
+        self.dtype = torch.float32
+        self.device = store.device
+
+    def dim(self):
+        return 3
+
+    def materialize(self):
+        return self.store.collate(self.index, index_d=self.index_d, T=self.shape[1],
+                                  with_labels=False)["net_input"]["feats"]
+
+
 class DeviceLoader:
     """torch DataLoader(dataset, batch_size, shuffle, collate_fn=dataset.collator) over a
     FeatureStore, collating on the device.  `style`: 'iemocap' (the I/ collators' dict, with
     'id') or 'casia' (C/ and E/ noisy collators: no 'id', 'labels' only when labeled);
-    `with_labels`: False for the reference's unlabeled SSL training loaders."""
+    `with_labels`: False for the reference's unlabeled SSL training loaders; `fused`: yield
+    store-mode batches (StoreFeats, no feature copy) that DADStep feeds to the encoder's
+    row gather -- the padded feature tensor never exists."""
 
     def __init__(self, store, batch_size=1, shuffle=False, generator=None, drop_last=False, style="iemocap",
-                 with_labels=True):
+                 with_labels=True, fused=False):
         self.store = store
+        self.fused = fused
         self.dataset = store
         self.batch_size = batch_size
         self.style = style
@@ -187,8 +241,9 @@ class _DeviceLoaderIter:
         k = self._k
         self._k += 1
         b = self._batches[k]
-        return L.store.collate(b, index_d=self._index_d[self._starts[k]:self._starts[k + 1]], T=self._T[k],
-                               style=L.style, with_labels=L.with_labels)
+        fn = L.store.batch_index if L.fused else L.store.collate
+        return fn(b, index_d=self._index_d[self._starts[k]:self._starts[k + 1]], T=self._T[k], style=L.style,
+                  with_labels=L.with_labels)
 
 
 # ------------------------------------------------------------------- reference file formats

@@ -19,13 +19,26 @@ import torch
 
 from . import _lib
 from .config import ConfigView, dad_config_for
+from .data import StoreFeats
 
 PRECISIONS = {"fp32": _lib.PREC_FP32, "bf16": _lib.PREC_BF16}
 
 
 def _dev_batch(batch, device, labels=True):
+    """(x, pad, y, rows, lens): a padded batch, or a store-mode batch (data.StoreFeats: x is the
+    feature store and rows/lens locate each utterance in it, dad_batch.rowc..lenn)."""
     ni = batch["net_input"]
-    x = ni["feats"].to(device=device, dtype=torch.float32, non_blocking=True).contiguous()
+    feats = ni["feats"]
+    rows = lens = None
+    if isinstance(feats, StoreFeats):
+        if feats.store.feats.dtype == torch.float32 and feats.device == device:
+            x, rows, lens = feats.store.feats, feats.rows, feats.lens
+        else:                      # the encoders read f32 rows: other stores are widened by dad_collate
+            x = feats.materialize().to(device)
+        pad = ni["padding_mask"].to(device=device).contiguous().view(torch.uint8)
+        y = batch["labels"].to(device=device, dtype=torch.int64).contiguous() if labels else None
+        return x, pad, y, rows, lens
+    x = feats.to(device=device, dtype=torch.float32, non_blocking=True).contiguous()
     pm = ni.get("padding_mask")
     if pm is None:
         pad = torch.zeros(x.shape[0], x.shape[1], dtype=torch.uint8, device=device)
@@ -36,7 +49,7 @@ def _dev_batch(batch, device, labels=True):
         y = batch["labels"].to(device=device, dtype=torch.int64, non_blocking=True).contiguous()
     if x.dim() != 3 or x.shape[2] != 768:
         raise ValueError("feats must be [B, T, 768], got %s" % (tuple(x.shape),))
-    return x, pad, y
+    return x, pad, y, None, None
 
 
 class _StepLossFn(torch.autograd.Function):
@@ -197,22 +210,27 @@ class DADStep:
     def _prepare(self, clean_batch, noisy_batch, epoch, lr, draws):
         """Device batch + POD structs for one step (shared by step() and train_step())."""
         dev = self.device
-        xc, mc, yc = _dev_batch(clean_batch, dev)
+        xc, mc, yc, rc, lc = _dev_batch(clean_batch, dev)
         warm = epoch < self.view.WARMUP_EPOCHS
+        rn = ln = None
         if noisy_batch is not None:
-            xn, mn, _ = _dev_batch(noisy_batch, dev, labels=False)
-            Bn, Tn = xn.shape[0], xn.shape[1]
+            xn, mn, _, rn, ln = _dev_batch(noisy_batch, dev, labels=False)
+            Bn, Tn = mn.shape[0], mn.shape[1]
         elif warm:
             xn = mn = None
             Bn, Tn = 0, 0
         else:
             raise ValueError("post-warm-up steps need a noisy batch")
-        Bc, Tc = xc.shape[0], xc.shape[1]
+        Bc, Tc = mc.shape[0], mc.shape[1]
         cfg = self.make_config(Bc, Tc, Bn, Tn, epoch, lr=lr)
         bt = _lib.DadBatch()
         bt.xc, bt.mc, bt.yc = xc.data_ptr(), mc.data_ptr(), yc.data_ptr()
+        if rc is not None:
+            bt.rowc, bt.lenc = rc.data_ptr(), lc.data_ptr()
         if xn is not None:
             bt.xn, bt.mn = xn.data_ptr(), mn.data_ptr()
+            if rn is not None:
+                bt.rown, bt.lenn = rn.data_ptr(), ln.data_ptr()
         keep = []
         if self.rng_mode == _lib.RNG_EXPLICIT:
             if draws is None:
@@ -232,7 +250,7 @@ class DADStep:
         st = self._state_struct(Bn, Bc)
         self._loss_vec = torch.empty(4, device=dev)          # written by the optimizer/commit kernel
         st.losses = self._loss_vec.data_ptr()
-        self._keepalive = (xc, mc, yc, xn, mn, keep)
+        self._keepalive = (xc, mc, yc, xn, mn, keep, rc, lc, rn, ln)
         return cfg, bt, st
 
     def step(self, clean_batch, noisy_batch, epoch, lr=None, draws=None):

@@ -8,6 +8,8 @@ import pytest
 import torch
 
 import dadpkg
+import gpu_harness as gh
+from oracle import dad_oracle, synth
 from oracle import data_oracle as do
 from test_data_cpu import CASIA_LOADERS, IEMOCAP_LOADERS, _golden
 
@@ -144,16 +146,70 @@ def test_collate_bench_shape_bit_exact():
     np.testing.assert_array_equal(got["net_input"]["padding_mask"].cpu().numpy(), ref["padding_mask"])
 
 
-def test_device_batches_drive_the_step(tmp_path):
-    """The loaders' batches go straight into DADStep (the reference loop body)."""
-    do.write_synthetic_split(str(tmp_path), 31, n_utt=80, max_len=25, flavor="iemocap")
-    clean = D.get_cv_dataloaders(str(tmp_path), 8, fold_id=1)[0]
-    noisy = D.get_cv_dataloaders_noisy(str(tmp_path), 8, fold_id=1)[0]
-    model = PKG.SSRLModel().cuda()
-    step = PKG.DADStep(model, flavor="iemocap", precision="bf16", rng="counter", seed=2)
-    torch.manual_seed(0)
-    ci, ni = iter(clean), iter(noisy)
-    for _ in range(2):
-        losses = step.step(next(ci), next(ni), 60)
+def _step_outputs(step, clean, noisy, epoch, draws, Bc, Bn):
+    losses = step.step(clean, noisy, epoch, draws=draws)
     torch.cuda.synchronize()
-    assert all(np.isfinite(float(v)) for v in losses.values())
+    out = {k: v.detach().cpu().numpy() for k, v in step.outputs(Bc, Bn).items() if torch.is_tensor(v)}
+    out.update({k: np.float32(float(v)) for k, v in losses.items()})
+    out["student"] = step.model.student_flat.detach().cpu().numpy()
+    out["teacher"] = step.model.teacher_flat.detach().cpu().numpy()
+    out["dacp"] = step.dacp.cpu().numpy()
+    return out
+
+
+@pytest.mark.parametrize("precision,rng", [("fp32", "explicit"), ("bf16", "explicit"), ("bf16", "counter")])
+def test_store_mode_step_equals_padded_step(precision, rng):
+    """Store mode (the encoder gathers rows straight from the FeatureStore, no padded copy)
+    computes exactly what the padded batch computes: same losses, logits, embeddings, updated
+    student/teacher and DACP state, bit for bit (padding frames are masked everywhere)."""
+    cfg = dad_oracle.make_cfg("iemocap")
+    rs = np.random.RandomState(40)
+    sizes = rs.randint(5, 38, size=48)
+    feats = rs.standard_normal((int(sizes.sum()), 768)).astype(np.float32) * 0.5
+    offsets = np.concatenate([[0], np.cumsum(sizes)[:-1]])
+    st = D.FeatureStore(feats, sizes, offsets, rs.randint(0, 4, size=48))
+    ic, inn = rs.choice(48, 12, replace=False), rs.choice(48, 10, replace=False)
+    Tc, Tn = int(sizes[ic].max()), int(sizes[inn].max())
+    draws = None
+    if rng == "explicit":
+        draws = {"nw": rs.standard_normal((10, Tn, 768)).astype(np.float32),
+                 "ns": rs.standard_normal((10, Tn, 768)).astype(np.float32),
+                 "u": rs.rand(768).astype(np.float32), "start": rs.randint(0, max(1, Tn - 4), size=10),
+                 "keep1": rs.rand(12, 256) > 0.1, "keep2": rs.rand(10, 256) > 0.1}
+    state = synth.make_state(40, 1)
+    outs = []
+    for mode in ("padded", "store"):
+        step = gh.make_step(cfg, precision=precision, rng=rng, seed=9)
+        gh.load_state(step, state)
+        mk = st.collate if mode == "padded" else st.batch_index
+        clean, noisy = mk(ic), mk(inn, with_labels=False)
+        if mode == "store":
+            assert isinstance(clean["net_input"]["feats"], D.StoreFeats)
+        outs.append(_step_outputs(step, clean, noisy, 60, draws, 12, 10))
+    a, b = outs
+    assert set(a) == set(b)
+    for k in a:
+        np.testing.assert_array_equal(b[k], a[k], err_msg=k)
+
+
+def test_device_batches_drive_the_step(tmp_path):
+    """The loaders' batches go straight into DADStep (the reference loop body); fused loaders
+    (store mode) give the same training trajectory as collating loaders."""
+    do.write_synthetic_split(str(tmp_path), 31, n_utt=80, max_len=25, flavor="iemocap")
+    res = []
+    for fused in (False, True):
+        clean = D.get_cv_dataloaders(str(tmp_path), 8, fold_id=1)[0]
+        noisy = D.get_cv_dataloaders_noisy(str(tmp_path), 8, fold_id=1)[0]
+        clean.fused = noisy.fused = fused
+        torch.manual_seed(1)
+        model = PKG.SSRLModel().cuda()
+        step = PKG.DADStep(model, flavor="iemocap", precision="bf16", rng="counter", seed=2)
+        torch.manual_seed(0)
+        ci, ni = iter(clean), iter(noisy)
+        for _ in range(3):
+            losses = step.step(next(ci), next(ni), 60)
+        torch.cuda.synchronize()
+        assert all(np.isfinite(float(v)) for v in losses.values())
+        res.append((np.array([float(v) for v in losses.values()]), model.student_flat.detach().cpu().numpy()))
+    np.testing.assert_array_equal(res[0][0], res[1][0])
+    np.testing.assert_array_equal(res[0][1], res[1][1])
