@@ -242,6 +242,9 @@ __device__ __forceinline__ int live_rows(const Job& J, int half, int w) {
 #ifndef WS_REGION
 #define WS_REGION 1
 #endif
+#ifndef WS_PRIO
+#define WS_PRIO 0      // static s_setprio 1 for: 0 no wave, 1 waves WAVES/2.., 2 waves ..WAVES/2-1
+#endif
 template <class S, int NOISE, int KIND, int HALF>
 __device__ __forceinline__ void ws_convert(const Ctx& C, const Job& J, int w, int lane_, const float* raw, char* tile,
                                            const float* fk) {
@@ -538,6 +541,11 @@ __device__ __forceinline__ void ws_loop(const Ctx& C, const int j0, const int Q,
     (void)c0; (void)c1; (void)c2; (void)c3; (void)c4; (void)c5;
 #endif
   };
+#if WS_PRIO == 1
+  if (w >= WAVES / 2) __builtin_amdgcn_s_setprio(1);   // the second-dispatched half loses arbitration by age
+#elif WS_PRIO == 2
+  if (w < WAVES / 2) __builtin_amdgcn_s_setprio(1);
+#endif
   dma(0);
   dma(1);
   wait_vm_sw<S::kDma>(Q > 1 ? S::kDma : 0);   // sub-slab 0 landed

@@ -9,7 +9,7 @@ cd /tmp
 for v in product ${VARIANTS:-}; do
   lv="$v"; [ "$v" = product ] && lv=""
   DAD_LIB_VARIANT="$lv" timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
-    -d "$R/gpurun_out/abprof/$v" -o run -- python "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --fp32-steps 0 \
+    -d "$R/gpurun_out/abprof/$v" -o run -- python "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --fp32-steps 0 --no-data-path \
     > "$R/gpurun_out/abprof/$v.log" 2>&1 || { tail -20 "$R/gpurun_out/abprof/$v.log"; exit 1; }
   echo "== $v"
   python - "$R/gpurun_out/abprof/$v/run_kernel_stats.csv" <<'PY'
