@@ -239,6 +239,15 @@ int dad_collate_index(const int64_t* offsets, const int32_t* sizes, int64_t n_sa
                       int B, int T, int64_t* row_out, int32_t* len_out, uint8_t* pad,
                       const int64_t* labels_in, int64_t* labels_out, void* stream);
 
+/* --- eval path ------------------------------------------------
+ * SSRLModel.predict's classifier in eval mode (I/model.py:225-245) on embeddings e [B][256]
+ * from dad_encoder_forward, with what validation (I/train.py:522-564) and anchor calibration
+ * (I/train.py:317-357) read from it: logits [B][4], softmax probs [B][4], the DACP certainty
+ * score [B] (DACPManager.calculate_certainty_scores, I/utils.py:401-430; use_entropy selects
+ * max_prob * (1 - H/log2 C) or max_prob) and the argmax pred [B].  Outputs may be NULL. */
+int dad_predict_head(const float* e, int B, const float* w2, const float* b2, int use_entropy,
+                     float* logits, float* probs, float* score, int64_t* pred, void* stream);
+
 /* --- data-parallel gradient exchange (RCCL over xGMI) ------------------------------ */
 int dad_comm_unique_id_bytes(void);
 int dad_comm_get_unique_id(void* id_out);

@@ -14,10 +14,10 @@ _KEYS = set(dad_oracle.FLAVOR_DEFAULTS["iemocap"])
 
 
 def variants():
-    # step fixtures (gen_golden.py); the data-path fixtures data_*.npz (gen_data_golden.py) are
-    # replayed by test_data_cpu.py / test_gpu_data.py
+    # step fixtures (gen_golden.py); the data-path / eval-path fixtures data_*.npz, eval_*.npz
+    # (gen_data_golden.py) are replayed by test_data_cpu.py, test_gpu_data.py, test_gpu_eval.py
     return sorted(n for n in (os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz")))
-                  if not n.startswith("data_"))
+                  if not n.startswith(("data_", "eval_")))
 
 
 def load(name):
