@@ -1,0 +1,66 @@
+"""Epoch-level state on the MI355X (checkpoint.py): a run resumed from a checkpoint continues
+bit for bit like the uninterrupted run, and train_epoch drives the device loaders through the
+fused step with the DACP epoch-end update."""
+import numpy as np
+import pytest
+import torch
+
+import dadpkg
+import gpu_harness as gh
+from oracle import dad_oracle, synth
+from oracle import data_oracle as do
+
+pytestmark = pytest.mark.gpu
+PKG = dadpkg.pkg()
+CK = PKG.checkpoint
+
+
+def _batches(seed, k):
+    rs = np.random.RandomState(seed)
+    sizes = rs.randint(8, 40, size=64)
+    feats = rs.standard_normal((int(sizes.sum()), 768)).astype(np.float32)
+    offsets = np.concatenate([[0], np.cumsum(sizes)[:-1]])
+    st = PKG.data.FeatureStore(feats, sizes, offsets, rs.randint(0, 4, size=64))
+    return [(st.collate(rs.choice(64, 12, replace=False)), st.collate(rs.choice(64, 10, replace=False), with_labels=False))
+            for _ in range(k)]
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_resume_from_checkpoint_is_bit_exact(tmp_path, precision):
+    cfg = dad_oracle.make_cfg("iemocap")
+    data = _batches(50, 4)
+    state = synth.make_state(50, 1)
+    a = gh.make_step(cfg, precision=precision, rng="counter", seed=4)
+    gh.load_state(a, state)
+    for i in range(2):
+        a.step(*data[i], 60)
+    path = str(tmp_path / "ck.pth")
+    CK.save_checkpoint(path, 60, a.model, a, clean_results={"confusion_matrix": np.eye(4, dtype=np.int64)})
+    b = gh.make_step(cfg, precision=precision, rng="counter", seed=4)
+    CK.load_checkpoint(path, b.model, b)
+    for i in range(2, 4):
+        la, lb = a.step(*data[i], 60), b.step(*data[i], 60)
+    torch.cuda.synchronize()
+    for k in la:
+        assert float(la[k]) == float(lb[k]), k
+    for x, y in ((a.model.student_flat, b.model.student_flat), (a.model.teacher_flat, b.model.teacher_flat),
+                 (a.exp_avg, b.exp_avg), (a.exp_avg_sq, b.exp_avg_sq), (a.dacp, b.dacp)):
+        assert torch.equal(x, y)
+    assert a.adam_step == b.adam_step == int(state["nstep"]) + 4
+
+
+def test_train_epoch_runs_loaders_and_epoch_end(tmp_path):
+    do.write_synthetic_split(str(tmp_path), 61, n_utt=90, max_len=30, flavor="iemocap")
+    clean = PKG.data.get_cv_dataloaders(str(tmp_path), 8, fold_id=2)[0]
+    noisy = PKG.data.get_cv_dataloaders_noisy(str(tmp_path), 8, fold_id=2)[0]
+    torch.manual_seed(0)
+    model = PKG.SSRLModel().cuda()
+    step = PKG.DADStep(model, flavor="iemocap", precision="bf16", rng="counter", seed=1)
+    q0 = step.class_quality_scores.clone()
+    avg = CK.train_epoch(step, clean, noisy, 40)
+    assert set(avg) >= {"total_loss", "supervised_ce_loss", "consistency_loss", "ecda_loss"}
+    assert all(np.isfinite(v) for v in avg.values())
+    assert step.adam_step == min(len(clean), len(noisy))
+    assert not torch.equal(step.class_quality_scores, q0)   # DACP quality updated at epoch end
+    warm = CK.train_epoch(step, clean, noisy, 3)              # warm-up: no epoch-end update
+    assert np.isfinite(warm["total_loss"])
