@@ -122,3 +122,10 @@ def make_state(problem_seed, step, C=N_CLS, tau_range=(0.55, 0.9)):
     Q = rs.uniform(0.3, 0.7, size=C).astype(f)
     return dict(student=[x.astype(f) for x in stud], teacher=[x.astype(f) for x in teach],
                 exp_avg=m, exp_avg_sq=v, nstep=nstep, tau=tau, Q=Q)
+
+
+def base_weights(seed):
+    """BaseModel (IP/model.py:4-21) weights for the pre-training fixtures: init_weights(seed)
+    with the classifier scaled back to nn.Linear's range (W2 / 40)."""
+    W1, b1, W2, b2, _ = init_weights(seed)
+    return W1, b1, (W2 / 40.0).astype(W2.dtype), b2

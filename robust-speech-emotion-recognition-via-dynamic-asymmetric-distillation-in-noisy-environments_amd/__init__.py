@@ -15,7 +15,7 @@ from .model import EmotionClassifier, Emotion2VecEncoder, SSRLModel
 from .step import DADStep
 from .dist import DPComm, ProcessGroupComm
 from .data import DeviceLoader, FeatureStore
-from . import checkpoint, evaluate
+from . import checkpoint, evaluate, pretrain
 
 __all__ = ["SSRLModel", "Emotion2VecEncoder", "EmotionClassifier", "DADStep", "DPComm", "ProcessGroupComm", "ConfigView",
            "dad_config_for", "FLAVOR_DEFAULTS", "FeatureStore", "DeviceLoader", "build", "lib"]
@@ -31,5 +31,5 @@ def lib():
 
 
 _sys.modules.setdefault("dad_amd", _sys.modules[__name__])
-for _m in ("_build", "_lib", "config", "model", "step", "dist", "data", "evaluate", "checkpoint"):
+for _m in ("_build", "_lib", "config", "model", "step", "dist", "data", "evaluate", "checkpoint", "pretrain"):
     _sys.modules.setdefault("dad_amd." + _m, _sys.modules[__name__ + "." + _m])

@@ -17,7 +17,7 @@ def variants():
     # step fixtures (gen_golden.py); the data-path / eval-path fixtures data_*.npz, eval_*.npz
     # (gen_data_golden.py) are replayed by test_data_cpu.py, test_gpu_data.py, test_gpu_eval.py
     return sorted(n for n in (os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz")))
-                  if not n.startswith(("data_", "eval_")))
+                  if not n.startswith(("data_", "eval_", "pretrain_")))
 
 
 def load(name):
