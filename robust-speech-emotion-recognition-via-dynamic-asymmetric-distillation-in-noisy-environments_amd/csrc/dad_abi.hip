@@ -328,11 +328,12 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
     wa.splits = splits; wa.per_utt = 0;
     wa.wpart = ws_ptr<float>(workspace, L.wpart);
     wa.ntiles = WGD_NDB * splits;
-    const int grid = (wa.ntiles + 7) / 8 * 8;   // multiple of 8: XCD-aware tile order
+    // multiple of 8 (XCD-aware tile order) with WGD_XWG spare workgroups for the extra blocks
+    const int grid = (wa.ntiles + WGD_XWG + 7) / 8 * 8;
     hipLaunchKernelGGL(dad_wgrad_direct, dim3(grid), dim3(WGD_THREADS), 0, stream, wa, ra);
     DAD_TRY(hipGetLastError());
     ra.splits = splits; ra.wpart = wa.wpart;
-    hipLaunchKernelGGL(dad_reduce, dim3(DAD_REDUCE_BLOCKS), dim3(DAD_REDUCE_THREADS), 0, stream, ra);
+    hipLaunchKernelGGL(dad_reduce, dim3(DAD_REDUCE_BLOCKS - DAD_REDUCE_XBLK), dim3(DAD_REDUCE_THREADS), 0, stream, ra);
   } else {
     DAD_TRY(hipStreamWaitEvent(stream, side->join, 0));
     ra.splits = nutt; ra.wpart = sbuf;

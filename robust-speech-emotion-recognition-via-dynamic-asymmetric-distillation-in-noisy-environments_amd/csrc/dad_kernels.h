@@ -22,6 +22,7 @@
 #define WGD_GROUPS 2      // slab groups of 4 waves per workgroup (2: two waves per SIMD)
 #endif
 #define WGD_THREADS (256 * WGD_GROUPS)
+#define WGD_XWG 4         // spare dad_wgrad_direct workgroups that run dad_reduce's extra blocks
 #define DAD_REDUCE_THREADS 256
 #define DAD_REDUCE_COLS 256                                  // dW1 floats per reduce block
 #define DAD_REDUCE_XBLK 16                                   // db1 / dW2 / totals blocks (16 hidden units each)

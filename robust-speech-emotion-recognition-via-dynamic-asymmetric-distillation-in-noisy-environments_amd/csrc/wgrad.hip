@@ -537,6 +537,8 @@ __device__ __forceinline__ void wgd_lut(uint2* lut) {
   }
 }
 
+__device__ double extra_block(const DadReduceArgs& a, int e, int tid, float (*xs)[16][6]);
+
 __global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct(DadWgradArgs a, DadReduceArgs ra) {
   DAD_GUARD_BLOCK(WGD_THREADS);
   __shared__ __attribute__((aligned(16))) __bf16 Xt[WGD_GROUPS * 2 * DAD_SLAB * WGD_XP];
@@ -548,7 +550,30 @@ __global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct(DadWgradArgs 
   // which read the same ReLU' row masks, share an L2
   const int per_xcd = gridDim.x >> 3;
   const int tile = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
-  if (tile >= a.ntiles) return;
+  if (tile >= a.ntiles) {
+    // The first WGD_XWG spare workgroups do dad_reduce's extra blocks (db1, dW2, loss totals):
+    // their inputs are ready before this launch and the work then overlaps the GEMM instead of
+    // trailing the reduction.  Two extra blocks at a time, one per 256-thread half, combining
+    // in the (otherwise unused) x-tile LDS.
+    const int xi = tile - a.ntiles;
+    if (xi >= WGD_XWG) return;
+    static_assert(sizeof(Xt) >= 2 * 16 * 16 * 6 * sizeof(float), "extra-block scratch fits the x tile");
+    __shared__ double wred[WGD_THREADS / 64];
+    const int half = threadIdx.x >> 8, htid = threadIdx.x & 255;
+    float (*xs)[16][6] = reinterpret_cast<float (*)[16][6]>(Xt) + 16 * half;
+    constexpr int per_wg = DAD_REDUCE_XBLK / WGD_XWG;
+    constexpr int NB = DAD_REDUCE_BLOCKS - DAD_REDUCE_XBLK;
+    for (int r = 0; r < per_wg; r += 2) {
+      const int e = xi * per_wg + r + half;
+      const double v = dad_wave_sum_d(extra_block(ra, e, htid, xs));
+      if ((threadIdx.x & 63) == 0) wred[threadIdx.x >> 6] = v;
+      __syncthreads();
+      if (htid == 0 && ra.want_norm)
+        ra.normpart[NB + e] = (float)(((wred[4 * half] + wred[4 * half + 1]) + wred[4 * half + 2]) + wred[4 * half + 3]);
+      __syncthreads();
+    }
+    return;
+  }
   const int split = tile / WGD_NDB, dblk = tile - split * WGD_NDB;
   const int total = wg_total(a);
   const int per = (total + a.splits - 1) / a.splits;
@@ -588,9 +613,8 @@ __global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_su(DadWgradArgs a) {
 // the 16 row groups are combined in fixed order (deterministic).
 static_assert(DAD_REDUCE_THREADS == 256 && DAD_H == 16 * DAD_REDUCE_XBLK, "extra blocks: 16 h x 16 row groups");
 
-__device__ double extra_block(const DadReduceArgs& a, int e) {
-  __shared__ float xs[16][16][6];
-  const int tid = threadIdx.x;
+// run by 256 threads (tid = 0..255 of a workgroup or of half of one), combining in xs
+__device__ double extra_block(const DadReduceArgs& a, int e, int tid, float (*xs)[16][6]) {
   const int hl = tid & 15, rg = tid >> 4;
   const int h = 16 * e + hl;
   const DadGeom& g = a.g;
@@ -683,6 +707,12 @@ __global__ __launch_bounds__(DAD_REDUCE_THREADS) void dad_reduce(DadReduceArgs a
   const int tid = threadIdx.x;
   constexpr int NB = DAD_REDUCE_BLOCKS - DAD_REDUCE_XBLK;
   double sq = 0.0;
+#ifdef DAD_PROBE_RED_NOMAIN
+  if (blockIdx.x < NB) return;     // diagnostic build only
+#endif
+#ifdef DAD_PROBE_RED_NOEXTRA
+  if (blockIdx.x >= NB) return;    // diagnostic build only
+#endif
   if (blockIdx.x < NB) {
     const int col = tid & (DAD_REDUCE_COLS / 4 - 1), kg = tid / (DAD_REDUCE_COLS / 4);
     const size_t e0 = (size_t)blockIdx.x * DAD_REDUCE_COLS + (size_t)col * 4;
@@ -697,7 +727,8 @@ __global__ __launch_bounds__(DAD_REDUCE_THREADS) void dad_reduce(DadReduceArgs a
       for (int e = 0; e < 4; ++e) sq += (double)t[e] * t[e];
     }
   } else {
-    sq = extra_block(a, blockIdx.x - NB);
+    __shared__ float xsx[16][16][6];
+    sq = extra_block(a, blockIdx.x - NB, tid, xsx);
   }
   if (!a.want_norm) return;
   double v = dad_wave_sum_d(sq);
@@ -771,7 +802,8 @@ __global__ __launch_bounds__(DAD_REDUCE_THREADS) void dad_wsum(DadReduceArgs a) 
       for (int e = 0; e < 4; ++e) sq += (double)t[e] * t[e];
     }
   } else {
-    sq = extra_block(a, blockIdx.x - NB);
+    __shared__ float xsx[16][16][6];
+    sq = extra_block(a, blockIdx.x - NB, tid, xsx);
   }
   if (!a.want_norm) return;
   double v = dad_wave_sum_d(sq);
