@@ -7,6 +7,7 @@ DataLoaders for these without touching the loop:
   get_cv_dataloaders (clean)                                        I/dataload_clean.py:222-293
   get_cv_dataloaders_noisy                                          I/dataload_noisy.py:159-231
   load_casia_noisy_data, create_casia_noisy_speaker_isolated_loaders C/dataload_casia_noisy.py:109-292
+  load_emodb_noisy_data, create_emodb_noisy_speaker_isolated_loaders E/dataload_emodb_noisy.py:20-345
 
 What changes is where the bytes live.  The reference slices each sample out of a host NumPy
 array, widens it to f32 and pads the batch in a Python loop (I/dataload_noisy.py:104-129),
@@ -353,5 +354,39 @@ def create_casia_noisy_speaker_isolated_loaders(store, speakers, fold, batch_siz
     tr = np.where(np.isin(speakers, [s for s in spk if s not in [test_spk, val_spk]]))[0]
     np.random.shuffle(tr)
     va, te = np.where(speakers == val_spk)[0], np.where(speakers == test_spk)[0]
+    mk = lambda idx, lab, sh: DeviceLoader(store.subset(idx, with_labels=lab), batch_size, shuffle=sh, style="casia")
+    return mk(tr, False, True), mk(tr, False, True), mk(va, True, False), mk(te, True, False)
+
+
+EMODB_SPEAKERS = ['03', '08', '09', '10', '11', '12', '13', '14', '15', '16']   # E/dataload_emodb_noisy.py:21
+
+
+def get_emodb_fold_speakers(fold_id):
+    """E/dataload_emodb_noisy.py:23-47: (8 train speakers, val = next speaker, test = speaker[fold])."""
+    if fold_id < 0 or fold_id >= 10:
+        raise ValueError(f"fold_id must be between 0 and 9, got {fold_id}")
+    test_spk, val_spk = EMODB_SPEAKERS[fold_id], EMODB_SPEAKERS[(fold_id + 1) % 10]
+    return [s for s in EMODB_SPEAKERS if s not in [test_spk, val_spk]], val_spk, test_spk
+
+
+def load_emodb_noisy_data(feature_path, label_dict=CASIA_LABEL_DICT, device=None, dtype=None):
+    """E/dataload_emodb_noisy.py:140-189: same files as CASIA (.npy/.lengths/.lbl/.spk)."""
+    return load_casia_noisy_data(feature_path, label_dict, device=device, dtype=dtype)
+
+
+def create_emodb_noisy_speaker_isolated_loaders(store, speakers, fold, batch_size):
+    """E/dataload_emodb_noisy.py:191-342: speakers matched on the part after the last '_'
+    ('emodb_spk_03' -> '03'); 10 folds; the train indices shuffled with the global NumPy RNG;
+    batches without 'id', the two train loaders unlabeled."""
+    if fold < 0 or fold >= 10:
+        raise ValueError(f"fold must be in 0-9, got {fold}")
+    tr_spk, va_spk, te_spk = get_emodb_fold_speakers(fold)
+    ids = np.array([s.split("_")[-1] for s in speakers])
+    tr = np.where(np.isin(ids, tr_spk))[0]
+    va, te = np.where(ids == va_spk)[0], np.where(ids == te_spk)[0]
+    np.random.shuffle(tr)
+    for name, idx in (("train", tr), ("val", va), ("test", te)):
+        if len(idx) == 0:
+            raise ValueError("no samples for the %s subset" % name)
     mk = lambda idx, lab, sh: DeviceLoader(store.subset(idx, with_labels=lab), batch_size, shuffle=sh, style="casia")
     return mk(tr, False, True), mk(tr, False, True), mk(va, True, False), mk(te, True, False)

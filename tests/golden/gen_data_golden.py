@@ -34,6 +34,7 @@ CASES = {
     # name: (tree, flavor, seed, n_utt, max_len, batch_size, fold)
     "data_iemocap": ("IEMOCAP/DAD-train-IEMOCAP", "iemocap", 5, 150, 40, 16, 2),
     "data_casia": ("CASIA/DAD-train-CASIA", "casia", 6, 90, 30, 8, 1),
+    "data_emodb": ("EMODB/DAD-train-EMODB", "emodb", 8, 160, 30, 8, 4),
 }
 
 
@@ -89,11 +90,13 @@ def run_case(name, out_path):
             for k, (ln, ld) in enumerate(zip(("clean_train", "clean_val", "clean_test"), (tr, va, te))):
                 _record(out, ln, ld, 200 + k)
         else:
-            import dataload_casia_noisy
+            mod = __import__("dataload_casia_noisy" if flavor == "casia" else "dataload_emodb_noisy")
             np.random.seed(seed)                # the train-index shuffle uses the global NumPy RNG
-            ds = dataload_casia_noisy.load_casia_noisy_data(prefix, {"angry": 0, "happy": 1, "neutral": 2, "sad": 3})
-            loaders = dataload_casia_noisy.create_casia_noisy_speaker_isolated_loaders(
-                ds, fold, bs, ["angry", "happy", "neutral", "sad"])
+            load = mod.load_casia_noisy_data if flavor == "casia" else mod.load_emodb_noisy_data
+            make = (mod.create_casia_noisy_speaker_isolated_loaders if flavor == "casia"
+                    else mod.create_emodb_noisy_speaker_isolated_loaders)
+            ds = load(prefix, {"angry": 0, "happy": 1, "neutral": 2, "sad": 3})
+            loaders = make(ds, fold, bs, ["angry", "happy", "neutral", "sad"])
             for k, (ln, ld) in enumerate(zip(("noisy_student", "noisy_teacher", "noisy_val", "noisy_test"), loaders)):
                 _record(out, ln, ld, 300 + k)
     np.savez_compressed(out_path, **out)

@@ -85,6 +85,27 @@ def test_oracle_casia_loaders_match_reference(tmp_path):
         _check_loader(g, name, sub, _torch_batches(len(idx), bs, shuffle, s), style_ids=False)
 
 
+def test_oracle_emodb_loaders_match_reference(tmp_path):
+    g = _golden("data_emodb")
+    seed, bs, fold = int(g["seed"]), int(g["batch_size"]), int(g["fold"])
+    prefix = do.write_synthetic_split(str(tmp_path), seed, n_utt=160, max_len=30, flavor="emodb")
+    np.random.seed(seed)
+    d = do.load_casia_noisy_data(prefix)            # E/ reads the same four files
+    tr, va, te = do.emodb_speaker_split(d["speakers"], fold)
+    splits = {"train": tr, "val": va, "test": te}
+    for name, part, shuffle, labeled, s in CASIA_LOADERS:
+        idx = splits[part]
+        sub = do.make_subset(d["feats"], d["sizes"], d["offsets"], d["labels"] if labeled else None, idx)
+        _check_loader(g, name, sub, _torch_batches(len(idx), bs, shuffle, s), style_ids=False)
+
+
+def test_product_emodb_folds_match_oracle():
+    for f in range(10):
+        assert PKG.data.get_emodb_fold_speakers(f)[1:] == (do.EMODB_SPEAKERS[(f + 1) % 10], do.EMODB_SPEAKERS[f])
+    with pytest.raises(ValueError):
+        PKG.data.get_emodb_fold_speakers(10)
+
+
 def test_product_parsers_match_oracle(tmp_path):
     D = PKG.data
     prefix = do.write_synthetic_split(str(tmp_path), 9, n_utt=60, max_len=12, flavor="iemocap")

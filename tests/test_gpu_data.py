@@ -61,6 +61,17 @@ def test_casia_device_loaders_match_reference(tmp_path):
         _compare(g, name, ld, s, with_ids=False)
 
 
+def test_emodb_device_loaders_match_reference(tmp_path):
+    g = _golden("data_emodb")
+    seed, bs, fold = int(g["seed"]), int(g["batch_size"]), int(g["fold"])
+    prefix = do.write_synthetic_split(str(tmp_path), seed, n_utt=160, max_len=30, flavor="emodb")
+    np.random.seed(seed)
+    store, spk = D.load_emodb_noisy_data(prefix)
+    loaders = D.create_emodb_noisy_speaker_isolated_loaders(store, spk, fold, bs)
+    for (name, _, _, _, s), ld in zip(CASIA_LOADERS, loaders):
+        _compare(g, name, ld, s, with_ids=False)
+
+
 def _store(seed, n, max_len, dtype=torch.float32):
     rs = np.random.RandomState(seed)
     sizes = rs.randint(1, max_len + 1, size=n)
