@@ -287,6 +287,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   pa.p_drop = cfg->p_drop; pa.drop_scale = cfg->drop_scale;
   pa.emb = st->emb; pa.vlen = vlen; pa.logits = st->logits;
   pa.part_cnt = part_cnt; pa.cnt_tot = cnt_tot;
+  pa.eflag = eflag; pa.tail_terms = st->tail + DAD_T_ECDA_TERM;
   hipLaunchKernelGGL(dad_pool, dim3(G.Bc + Bn), dim3(DAD_POOL_THREADS), 0, stream, pa);
   DAD_TRY(hipGetLastError());
 
@@ -298,17 +299,22 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   ta.key_drop1 = k.drop1; ta.key_drop2 = k.drop2;
   ta.dacp = st->dacp; ta.tailf = st->tail; ta.ge = ge; ta.ge_ecda = ge_ecda; ta.grad = st->grad;
   ta.gzb = gzb; ta.eflag = eflag;
-  hipLaunchKernelGGL(dad_tail, dim3(1), dim3(DAD_TAIL_THREADS), 0, stream, ta);
-  DAD_TRY(hipGetLastError());
-
-  // 5. ECDA (class-aware MMD + compactness + repulsion) and its embedding grads
-  if (!cfg->warmup) {
-    DadEcdaArgs ca;
-    memset(&ca, 0, sizeof(ca));
-    ca.cfg = *cfg; ca.yc = bt->yc; ca.emb = st->emb; ca.tailf = st->tail;
-    ca.tail_terms = st->tail + DAD_T_ECDA_TERM; ca.ge = ge_ecda; ca.scratch = ecda_scratch; ca.eflag = eflag;
-    hipLaunchKernelGGL(dad_ecda, dim3(DAD_C), dim3(DAD_ECDA_THREADS), 0, stream, ca);
+  // 5. ECDA (class-aware MMD + compactness + repulsion) and its embedding grads: after the
+  //    warm-up, in the same launch as the tail (block 0 = tail, blocks 1..C = classes)
+  DadEcdaArgs ca;
+  memset(&ca, 0, sizeof(ca));
+  ca.cfg = *cfg; ca.yc = bt->yc; ca.emb = st->emb; ca.tailf = st->tail;
+  ca.tail_terms = st->tail + DAD_T_ECDA_TERM; ca.ge = ge_ecda; ca.scratch = ecda_scratch; ca.eflag = eflag;
+  if (!cfg->warmup && DAD_FUSED_TAIL) {
+    hipLaunchKernelGGL(dad_tail_ecda, dim3(1 + DAD_C), dim3(DAD_TAIL_THREADS), 0, stream, ta, ca);
     DAD_TRY(hipGetLastError());
+  } else {
+    hipLaunchKernelGGL(dad_tail, dim3(1), dim3(DAD_TAIL_THREADS), 0, stream, ta);
+    DAD_TRY(hipGetLastError());
+    if (!cfg->warmup) {
+      hipLaunchKernelGGL(dad_ecda, dim3(DAD_C), dim3(DAD_ECDA_THREADS), 0, stream, ca);
+      DAD_TRY(hipGetLastError());
+    }
   }
 
   // 6. dW1 (join, then sum_u (dL/de_u / len_u) * S_u; or the direct split-K GEMM), db1,

@@ -10,6 +10,12 @@
 #define DAD_POOL_THREADS 256
 #define DAD_TAIL_THREADS 512
 #define DAD_ECDA_THREADS 512
+// 1: the tail and ECDA run as one launch (dad_tail_ecda): block 0 is the tail, blocks 1..C
+// re-derive the DACP mask themselves and go straight on to ECDA (no kernel boundary and no
+// round trip of the mask through HBM).  0: dad_tail then dad_ecda (A/B builds).
+#ifndef DAD_FUSED_TAIL
+#define DAD_FUSED_TAIL 1
+#endif
 #define DAD_WGRAD_THREADS 256
 // dad_wgrad_direct (BF16): 64-column blocks, slab-range splits of at most WGD_MAXU slabs,
 // WGD_DEPTH slabs in flight per group, x tile row pitch WGD_XP bf16 (192 B)
@@ -62,6 +68,8 @@ struct DadPoolArgs {
   float p_drop, drop_scale;
   float* emb; float* vlen; float* logits;
   const float* part_cnt; float* cnt_tot;
+  uint32_t* eflag;        // [Bc+Bn] ECDA row flags, zeroed here (ECDA flags the rows it writes)
+  float* tail_terms;      // per-class ECDA terms + gates, zeroed here (block 0)
 };
 
 struct DadTailArgs {
@@ -76,7 +84,7 @@ struct DadTailArgs {
   float* ge;              // [Bc+Bn][H] dL/de (CE/KL part)
   float* ge_ecda;         // [Bc+Bn][H] modular path only (fused step: ge_ecda rows are flagged)
   float* gzb;             // [Bc+Bn][C] dL/dz per utterance (clean | strong)
-  uint32_t* eflag;        // [Bc+Bn]    zeroed here; ECDA flags the rows it writes
+  uint32_t* eflag;        // [Bc+Bn]    (zeroed by dad_pool; ECDA flags the rows it writes)
   float* grad;            // flat grads (W2, b2 written here) + extras
 };
 
@@ -150,6 +158,7 @@ __global__ void dad_encode_ws_explicit(DadEncodeArgs a);   // explicit noise ten
 __global__ void dad_pool(DadPoolArgs a);
 __global__ void dad_tail(DadTailArgs a);
 __global__ void dad_ecda(DadEcdaArgs a);
+__global__ void dad_tail_ecda(DadTailArgs ta, DadEcdaArgs ca);
 __global__ void dad_wgrad_f32(DadWgradArgs a);
 __global__ void dad_wgrad_direct(DadWgradArgs a, DadReduceArgs r);
 __global__ void dad_wgrad_su(DadWgradArgs a);

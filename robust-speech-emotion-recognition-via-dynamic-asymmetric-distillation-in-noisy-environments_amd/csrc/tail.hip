@@ -25,7 +25,7 @@ extern "C" int dad_probe_read_ecda_stamps(void* host) {
   return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ecda_stamps), sizeof(g_ecda_stamps), 0, hipMemcpyDeviceToHost);
 }
 #define ECDA_STAMP(k) \
-  if (threadIdx.x == 0) g_ecda_stamps[blockIdx.x * 16 + (k)] = wall_clock64()
+  if (threadIdx.x == 0) g_ecda_stamps[(gridDim.x > DAD_C ? blockIdx.x - 1 : blockIdx.x) * 16 + (k)] = wall_clock64()
 __device__ __forceinline__ void g_ecda_stamps_n(int c, int n, int ns) {
   g_ecda_stamps[c * 16 + 10] = (unsigned long long)n;
   g_ecda_stamps[c * 16 + 11] = (unsigned long long)ns;
@@ -142,6 +142,10 @@ __global__ __launch_bounds__(DAD_POOL_THREADS) void dad_pool(DadPoolArgs a) {
   // active-row count per (utterance, h) of the branch that gets a gradient (clean / strong)
   a.cnt_tot[(size_t)(noisy ? g.Bc + b : b) * DAD_H + h] = cnt;
   if (h == 0) a.vlen[blk] = len;
+  // ECDA row flag of this utterance (clean b / noisy Bc + b = blk) and the per-class ECDA
+  // terms and gates start at zero: the ECDA workgroups write only what they own
+  if (h == 0) a.eflag[blk] = 0u;
+  if (blk == 0 && h < 2 * DAD_C) a.tail_terms[h] = 0.0f;
   if (l == 0)
     for (int k = 0; k < nbr; ++k)
       for (int c = 0; c < 4; ++c) zred[k * 4 + c][w] = zp[k][c];
@@ -181,25 +185,128 @@ __device__ __forceinline__ void block_sum4_d(double (&v)[4], double (*red)[4]) {
   }
 }
 
-__global__ __launch_bounds__(TAIL_THREADS) void dad_tail(DadTailArgs a) {
-  DAD_GUARD_BLOCK(TAIL_THREADS);
+struct TailSmem {
+  double dred[16];
+  double dred4[TAIL_THREADS / 64][4];
+  float fred[16];
+  float gz[2][DAD_MAX_BATCH][DAD_C];       // dL/dz clean, strong
+  float sq[DAD_MAX_BATCH][DAD_C];          // teacher probs
+  float ss[DAD_MAX_BATCH];                 // certainty scores
+  int sp[DAD_MAX_BATCH];                   // pseudo labels
+  float sm[DAD_MAX_BATCH];                 // mask
+  float srt[DAD_C][DAD_MAX_BATCH];         // per-class sorted scores
+  int ncls[DAD_C];
+  float tau_new[DAD_C];
+  float dstate[20];                        // DACP state: tau | Q | (sums) | (counts) | anchors
+};
+
+// teacher probs (I/train.py:409-410), certainty score and pseudo-label (I/utils.py:400-428)
+__device__ __forceinline__ void teacher_certainty(const float (&z)[4], const dad_config& cfg, float (&q)[4],
+                                                  float& s, int& pred) {
+  float m = -INFINITY;
+  for (int c = 0; c < 4; ++c) m = fmaxf(m, z[c]);
+  float e[4], se = 0.0f;
+  for (int c = 0; c < 4; ++c) { e[c] = expf(z[c] - m); se += e[c]; }
+  float mx = -1.0f;
+  pred = 0;
+  for (int c = 0; c < 4; ++c) {
+    q[c] = e[c] / se;
+    if (q[c] > mx) { mx = q[c]; pred = c; }
+  }
+  s = mx;
+  if (cfg.use_dacp && cfg.use_entropy) {
+    float ent = 0.0f;
+    for (int c = 0; c < 4; ++c) ent += q[c] * log2f(q[c] + 1e-8f);
+    ent = -ent;
+    s = mx * (1.0f - ent / 2.0f);   // log2(NUM_CLASSES) = 2
+  }
+}
+
+// DACPManager.calculate_mask thresholds (I/utils.py:449-507): per-class ranks of the scores,
+// torch.quantile(linear) of each class, sigmoid class weights, floored + EMA-blended tau.
+// Entry: ncls[] zeroed and ss/sp visible (barrier done by the caller).  Exit: tau_new[] and
+// wc[] valid in all threads.  tf/extras (nullable): the per-step outputs of the tail block.
+// Shared by the tail block and the ECDA blocks of dad_tail_ecda, so both derive the same mask.
+__device__ __forceinline__ void dacp_thresholds(const dad_config& cfg, int Bn, const float* ss, const int* sp,
+                                                float (*srt)[DAD_MAX_BATCH], int* ncls, const float* dstate,
+                                                float* tau_new, float* wcs, float* tf, float* extras) {
+  const int tid = threadIdx.x;
+  // rank of each score inside its pseudo-label class (ties by index): 16 threads per
+  // utterance, each counting a strided share of the others, combined by a 16-lane sum
+  {
+    const int bb = tid >> 4, part = tid & 15;
+    for (int b0 = 0; b0 < Bn; b0 += TAIL_THREADS / 16) {
+      const int b = b0 + bb;
+      int cnt = 0, c = 0;
+      float sv = 0.0f;
+      if (b < Bn) {
+        c = sp[b];
+        sv = ss[b];
+        for (int k = part; k < Bn; k += 16) {
+          const float o = ss[k];
+          cnt += (sp[k] == c && (o < sv || (o == sv && k < b))) ? 1 : 0;
+        }
+      }
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 16);
+      if (b < Bn && part == 0) {
+        srt[c][cnt] = sv;
+        atomicAdd(&ncls[c], 1);
+      }
+    }
+  }
+  __syncthreads();
+  if (tid < DAD_C) {
+    const int c = tid;
+    const float* Qs = dstate + 4;
+    const float qmean = (((Qs[0] + Qs[1]) + Qs[2]) + Qs[3]) / 4.0f;
+    const float wc = 1.0f / (1.0f + expf(-(cfg.dacp_k * (Qs[c] - qmean))));
+    const int n = ncls[c];
+    float that;
+    if (n > 0) {
+      // torch.quantile(linear): rank = q*(n-1) in f32, lerp(below, above, rank-floor)
+      const float rank = cfg.dacp_gamma * (float)(n - 1);
+      const int lo = (int)rank;
+      const int hi = (int)ceilf(rank);
+      const float wgt = rank - (float)lo;
+      const float vlo = srt[c][lo], vhi = srt[c][hi];
+      that = wgt < 0.5f ? vlo + wgt * (vhi - vlo) : vhi - (vhi - vlo) * (1.0f - wgt);
+    } else {
+      that = dstate[c];
+    }
+    const float adj = cfg.dacp_lambda * (wc - 0.5f);
+    const float fl = fmaxf(that + adj, dstate[16 + c]);
+    const float tn = cfg.dacp_alpha * dstate[c] + cfg.dacp_one_m_alpha * fl;
+    tau_new[c] = tn;
+    wcs[c] = wc;
+    if (tf) {
+      tf[DAD_T_W + c] = wc;
+      tf[DAD_T_TAU_BEFORE + c] = dstate[c];
+      tf[DAD_T_TAU_AFTER + c] = tn;
+      tf[DAD_T_FLOORED + c] = fl;
+      tf[DAD_T_TAU_HAT + c] = that;
+      extras[0 + c] = fl;
+    }
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void tail_block(const DadTailArgs& a, TailSmem& T) {
   TAIL_STAMP(0);
   const dad_config& cfg = a.cfg;
   const int B = cfg.B;                       // clean utterances
   const int Bn = cfg.warmup ? 0 : cfg.Bn;    // noisy utterances
   const int tid = threadIdx.x;
-  __shared__ double dred[16];
-  __shared__ double dred4[TAIL_THREADS / 64][4];
-  __shared__ float fred[16];
-  __shared__ float gz[2][DAD_MAX_BATCH][DAD_C];       // dL/dz clean, strong
-  __shared__ float sq[DAD_MAX_BATCH][DAD_C];          // teacher probs
-  __shared__ float ss[DAD_MAX_BATCH];                 // certainty scores
-  __shared__ int sp[DAD_MAX_BATCH];                   // pseudo labels
-  __shared__ float sm[DAD_MAX_BATCH];                 // mask
-  __shared__ float srt[DAD_C][DAD_MAX_BATCH];         // per-class sorted scores
-  __shared__ int ncls[DAD_C];
-  __shared__ float tau_new[DAD_C];
-  __shared__ float dstate[20];                        // DACP state: tau | Q | (sums) | (counts) | anchors
+  double* dred = T.dred;
+  auto& dred4 = T.dred4;
+  float* fred = T.fred;
+  auto& gz = T.gz;
+  auto& sq = T.sq;
+  float* ss = T.ss;
+  int* sp = T.sp;
+  float* sm = T.sm;
+  float* dstate = T.dstate;
+  float wc_unused[DAD_C];
 
   float* tf = a.tailf;
   float* extras = a.grad + DAD_NPARAM;
@@ -243,92 +350,24 @@ __global__ __launch_bounds__(TAIL_THREADS) void dad_tail(DadTailArgs a) {
   if (!cfg.warmup) {
     // ---- teacher probs (I/train.py:409-410) and certainty (I/utils.py:400-428)
     for (int b = tid; b < Bn; b += TAIL_THREADS) {
-      float z[4], m = -INFINITY;
+      float z[4], q[4], s;
+      int pred;
       if (b == tid) { z[0] = zt[0]; z[1] = zt[1]; z[2] = zt[2]; z[3] = zt[3]; }
       else for (int c = 0; c < 4; ++c) z[c] = z1[b * 4 + c];
-      for (int c = 0; c < 4; ++c) m = fmaxf(m, z[c]);
-      float e[4], se = 0.0f;
-      for (int c = 0; c < 4; ++c) { e[c] = expf(z[c] - m); se += e[c]; }
-      float q[4], mx = -1.0f;
-      int pred = 0;
-      for (int c = 0; c < 4; ++c) {
-        q[c] = e[c] / se;
-        sq[b][c] = q[c];
-        if (q[c] > mx) { mx = q[c]; pred = c; }
-      }
-      float s = mx;
-      if (cfg.use_dacp && cfg.use_entropy) {
-        float ent = 0.0f;
-        for (int c = 0; c < 4; ++c) ent += q[c] * log2f(q[c] + 1e-8f);
-        ent = -ent;
-        s = mx * (1.0f - ent / 2.0f);   // log2(NUM_CLASSES) = 2
-      }
+      teacher_certainty(z, cfg, q, s, pred);
+      for (int c = 0; c < 4; ++c) sq[b][c] = q[c];
       ss[b] = s;
       sp[b] = pred;
     }
-    if (tid < DAD_C) ncls[tid] = 0;
+    if (tid < DAD_C) T.ncls[tid] = 0;
     __syncthreads();
     TAIL_STAMP(3);
     if (cfg.use_dacp) {
       // ---- DACPManager.calculate_mask (I/utils.py:449-507)
-      // rank of each score inside its pseudo-label class (ties by index): 16 threads per
-      // utterance, each counting a strided share of the others, combined by a 16-lane sum
-      {
-        const int bb = tid >> 4, part = tid & 15;
-        for (int b0 = 0; b0 < Bn; b0 += TAIL_THREADS / 16) {
-          const int b = b0 + bb;
-          int cnt = 0, c = 0;
-          float sv = 0.0f;
-          if (b < Bn) {
-            c = sp[b];
-            sv = ss[b];
-            for (int k = part; k < Bn; k += 16) {
-              const float o = ss[k];
-              cnt += (sp[k] == c && (o < sv || (o == sv && k < b))) ? 1 : 0;
-            }
-          }
-#pragma unroll
-          for (int o = 8; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 16);
-          if (b < Bn && part == 0) {
-            srt[c][cnt] = sv;
-            atomicAdd(&ncls[c], 1);
-          }
-        }
-      }
-      __syncthreads();
-      if (tid < DAD_C) {
-        const int c = tid;
-        const float* Qs = dstate + 4;
-        const float qmean = (((Qs[0] + Qs[1]) + Qs[2]) + Qs[3]) / 4.0f;
-        const float wc = 1.0f / (1.0f + expf(-(cfg.dacp_k * (Qs[c] - qmean))));
-        const int n = ncls[c];
-        float that;
-        if (n > 0) {
-          // torch.quantile(linear): rank = q*(n-1) in f32, lerp(below, above, rank-floor)
-          const float rank = cfg.dacp_gamma * (float)(n - 1);
-          const int lo = (int)rank;
-          const int hi = (int)ceilf(rank);
-          const float wgt = rank - (float)lo;
-          const float vlo = srt[c][lo], vhi = srt[c][hi];
-          that = wgt < 0.5f ? vlo + wgt * (vhi - vlo) : vhi - (vhi - vlo) * (1.0f - wgt);
-        } else {
-          that = dstate[c];
-        }
-        const float adj = cfg.dacp_lambda * (wc - 0.5f);
-        const float fl = fmaxf(that + adj, dstate[16 + c]);
-        const float tn = cfg.dacp_alpha * dstate[c] + cfg.dacp_one_m_alpha * fl;
-        tau_new[c] = tn;
-        tf[DAD_T_W + c] = wc;
-        tf[DAD_T_TAU_BEFORE + c] = dstate[c];
-        tf[DAD_T_TAU_AFTER + c] = tn;
-        tf[DAD_T_FLOORED + c] = fl;
-        tf[DAD_T_TAU_HAT + c] = that;
-        extras[0 + c] = fl;
-      }
-      __syncthreads();
+      dacp_thresholds(cfg, Bn, ss, sp, T.srt, T.ncls, dstate, T.tau_new, wc_unused, tf, extras);
       // mask, and the epoch statistics for update_class_quality_scores_epoch
       // (I/utils.py:503-505): per-class score sums and counts, fixed-order block reduction
-      for (int b = tid; b < Bn; b += TAIL_THREADS) sm[b] = ss[b] >= tau_new[sp[b]] ? 1.0f : 0.0f;
+      for (int b = tid; b < Bn; b += TAIL_THREADS) sm[b] = ss[b] >= T.tau_new[sp[b]] ? 1.0f : 0.0f;
       double st4[4] = {0.0, 0.0, 0.0, 0.0}, ct4[4] = {0.0, 0.0, 0.0, 0.0};
       for (int b = tid; b < Bn; b += TAIL_THREADS)
 #pragma unroll
@@ -398,7 +437,6 @@ __global__ __launch_bounds__(TAIL_THREADS) void dad_tail(DadTailArgs a) {
     tf[DAD_T_MSUM] = msum;
     tf[DAD_T_KL_ON] = (float)kl_on;
     tf[DAD_T_ECDA_ON] = (kl_on && cfg.ecda_on) ? 1.0f : 0.0f;
-    for (int c = 0; c < 4; ++c) { tf[DAD_T_ECDA_TERM + c] = 0.0f; tf[DAD_T_ECDA_GATE + c] = 0.0f; }
   }
   __syncthreads();
   TAIL_STAMP(6);
@@ -409,7 +447,6 @@ __global__ __launch_bounds__(TAIL_THREADS) void dad_tail(DadTailArgs a) {
   for (int b = tid; b < Bn; b += TAIL_THREADS)
     *reinterpret_cast<f32x4*>(a.gzb + (size_t)(B + b) * DAD_C) =
         f32x4{gz[1][b][0], gz[1][b][1], gz[1][b][2], gz[1][b][3]};
-  for (int b = tid; b < B + Bn; b += TAIL_THREADS) a.eflag[b] = 0u;
   double b2s[4] = {0.0, 0.0, 0.0, 0.0};
   for (int b = tid; b < B; b += TAIL_THREADS)
 #pragma unroll
@@ -421,6 +458,12 @@ __global__ __launch_bounds__(TAIL_THREADS) void dad_tail(DadTailArgs a) {
   TAIL_STAMP(7);
   if (tid < 4) a.grad[DAD_OFF_B2 + tid] = (float)b2s[tid];
   TAIL_STAMP(1);
+}
+
+__global__ __launch_bounds__(TAIL_THREADS) void dad_tail(DadTailArgs a) {
+  DAD_GUARD_BLOCK(TAIL_THREADS);
+  __shared__ TailSmem T;
+  tail_block(a, T);
 }
 
 // ------------------------------------------------------------------------------ ECDA
@@ -707,32 +750,80 @@ __device__ __forceinline__ void ecda_member_grads(EcdaSmem& S, const EcdaRows<ST
   }
 }
 
-__global__ __launch_bounds__(ECDA_THREADS) void dad_ecda(DadEcdaArgs a) {
-  DAD_GUARD_BLOCK(ECDA_THREADS);
-  __shared__ EcdaSmem S;
-  __shared__ float pdist[DAD_C][DAD_C];
+// DACP state and thresholds of the fused prefix (dad_tail_ecda's ECDA blocks)
+struct EcdaPrefix {
+  float dstate[20];
+  int ncls[DAD_C];
+  float tau_new[DAD_C];
+  float wc[DAD_C];
+  float fred[16];
+};
+
+// One class of ECDA.  FUSED: the DACP mask, scores and class weights are derived here from
+// the teacher logits by the same code as the tail block (teacher_certainty, dacp_thresholds),
+// instead of being read back from the tail's outputs.
+template <bool FUSED>
+__device__ __forceinline__ void ecda_block(const DadEcdaArgs& a, const int c, EcdaSmem& S, float (&pdist)[DAD_C][DAD_C],
+                                           const DadTailArgs* ta, EcdaPrefix& P) {
   const dad_config& cfg = a.cfg;
   const int B = cfg.B, Bn = cfg.Bn;
-  const int c = blockIdx.x, tid = threadIdx.x;
+  const int tid = threadIdx.x;
   const float* tf = a.tailf;
   ECDA_STAMP(0);
-  const float ecda_on = tf[DAD_T_ECDA_ON];   // branched on after the metadata loads are issued
-  const float* score = tf + DAD_TAIL_HDR;
-  const float* predf = tf + DAD_TAIL_HDR + Bn;
-  const float* mask = tf + DAD_TAIL_HDR + 2 * Bn;
   const float* emb_c = a.emb;
   const float* emb_s = a.emb + (size_t)(B + Bn) * DAD_H;
   float* ge_c = a.ge;
   float* ge_s = a.ge + (size_t)B * DAD_H;
   float* scratch = a.scratch + (size_t)c * (B + Bn) * (B + Bn);
   const float wscale = cfg.w_ecda;
-  // stage per-sample metadata (masked-out noisy samples get pseudo-label -1)
-  for (int b = tid; b < B; b += ECDA_THREADS) S.lab[b] = (int)a.yc[b];
-  for (int b = tid; b < Bn; b += ECDA_THREADS) {
-    S.prd[b] = mask[b] > 0.0f ? (int)predf[b] : -1;   // noisy_mask>thr re-cast: I/utils.py:573-576
-    S.scr[b] = score[b];
+  float ecda_on;
+  const float* w;   // DACP class weights
+  if constexpr (FUSED) {
+    // every global input up front: teacher logits, DACP state, clean labels
+    const float* z1 = ta->logits + (size_t)B * DAD_C;
+    f32x4 zt = f32x4{};
+    if (tid < Bn) zt = reinterpret_cast<const f32x4*>(z1)[tid];
+    if (tid >= ECDA_THREADS - 20) P.dstate[tid - (ECDA_THREADS - 20)] = ta->dacp[tid - (ECDA_THREADS - 20)];
+    for (int b = tid; b < B; b += ECDA_THREADS) S.lab[b] = (int)a.yc[b];
+    for (int b = tid; b < Bn; b += ECDA_THREADS) {
+      float z[4], q[4], sc;
+      int pred;
+      if (b == tid) { z[0] = zt[0]; z[1] = zt[1]; z[2] = zt[2]; z[3] = zt[3]; }
+      else for (int k = 0; k < 4; ++k) z[k] = z1[b * 4 + k];
+      teacher_certainty(z, cfg, q, sc, pred);
+      S.scr[b] = sc;
+      S.prd[b] = pred;
+    }
+    if (tid < DAD_C) { P.ncls[tid] = 0; S.cnt_clean[tid] = 0; S.cnt_noisy[tid] = 0; }
+    __syncthreads();
+    // masked-out noisy samples get pseudo-label -1 (noisy_mask>thr re-cast: I/utils.py:573-576)
+    if (cfg.use_dacp) {
+      dacp_thresholds(cfg, Bn, S.scr, S.prd, reinterpret_cast<float(*)[DAD_MAX_BATCH]>(S.z), P.ncls, P.dstate,
+                      P.tau_new, P.wc, nullptr, nullptr);
+      for (int b = tid; b < Bn; b += ECDA_THREADS) S.prd[b] = S.scr[b] >= P.tau_new[S.prd[b]] ? S.prd[b] : -1;
+    } else {
+      for (int b = tid; b < Bn; b += ECDA_THREADS) S.prd[b] = S.scr[b] >= cfg.fixed_thr ? S.prd[b] : -1;
+      if (tid < DAD_C) P.wc[tid] = 1.0f;
+    }
+    float mpart = 0.0f;
+    for (int b = tid; b < Bn; b += ECDA_THREADS) mpart += S.prd[b] >= 0 ? 1.0f : 0.0f;
+    const float msum = block_sum_f(mpart, P.fred);   // the tail's mask sum (exact: a count)
+    ecda_on = (msum > 1.0f && cfg.ecda_on) ? 1.0f : 0.0f;   // I/train.py:444
+    w = P.wc;
+  } else {
+    ecda_on = tf[DAD_T_ECDA_ON];   // branched on after the metadata loads are issued
+    w = tf + DAD_T_W;
+    const float* score = tf + DAD_TAIL_HDR;
+    const float* predf = tf + DAD_TAIL_HDR + Bn;
+    const float* mask = tf + DAD_TAIL_HDR + 2 * Bn;
+    // stage per-sample metadata (masked-out noisy samples get pseudo-label -1)
+    for (int b = tid; b < B; b += ECDA_THREADS) S.lab[b] = (int)a.yc[b];
+    for (int b = tid; b < Bn; b += ECDA_THREADS) {
+      S.prd[b] = mask[b] > 0.0f ? (int)predf[b] : -1;   // noisy_mask>thr re-cast: I/utils.py:573-576
+      S.scr[b] = score[b];
+    }
+    if (tid < DAD_C) { S.cnt_clean[tid] = 0; S.cnt_noisy[tid] = 0; }
   }
-  if (tid < DAD_C) { S.cnt_clean[tid] = 0; S.cnt_noisy[tid] = 0; }
   __syncthreads();
   ECDA_STAMP(1);
   if (ecda_on == 0.0f) return;   // no row flagged: the ECDA part of dL/de is zero
@@ -805,7 +896,6 @@ __global__ __launch_bounds__(ECDA_THREADS) void dad_ecda(DadEcdaArgs a) {
   __syncthreads();
   ECDA_STAMP(2);
   // class attention (I/utils.py:597-599)
-  const float* w = tf + DAD_T_W;
   float att[DAD_C];
   if (cfg.use_dacp) {
     const float wmean = (((w[0] + w[1]) + w[2]) + w[3]) / 4.0f;
@@ -913,4 +1003,26 @@ __global__ __launch_bounds__(ECDA_THREADS) void dad_ecda(DadEcdaArgs a) {
     g_ecda_stamps_n(c, n, ns);
     a.tail_terms[DAD_T_ECDA_GATE - DAD_T_ECDA_TERM + c] = 1.0f;
   }
+}
+
+__global__ __launch_bounds__(ECDA_THREADS) void dad_ecda(DadEcdaArgs a) {
+  DAD_GUARD_BLOCK(ECDA_THREADS);
+  __shared__ EcdaSmem S;
+  __shared__ float pdist[DAD_C][DAD_C];
+  __shared__ EcdaPrefix P;
+  ecda_block<false>(a, blockIdx.x, S, pdist, nullptr, P);
+}
+
+// block 0: the tail (losses, DACP outputs, dL/dz); blocks 1..C: ECDA class blockIdx.x - 1,
+// which re-derives the DACP mask itself and so does not wait for block 0.  The two roles
+// write disjoint outputs (dad_pool zeroed the ECDA flags and terms).  LDS: one union.
+static_assert(DAD_TAIL_THREADS == DAD_ECDA_THREADS, "dad_tail_ecda: one block size for both roles");
+__global__ __launch_bounds__(TAIL_THREADS) void dad_tail_ecda(DadTailArgs ta, DadEcdaArgs ca) {
+  DAD_GUARD_BLOCK(TAIL_THREADS);
+  __shared__ union U {
+    TailSmem t;
+    struct E { EcdaSmem s; float pdist[DAD_C][DAD_C]; EcdaPrefix p; } e;
+  } u;
+  if (blockIdx.x == 0) tail_block(ta, u.t);
+  else ecda_block<true>(ca, (int)blockIdx.x - 1, u.e.s, u.e.pdist, &ta, u.e.p);
 }
