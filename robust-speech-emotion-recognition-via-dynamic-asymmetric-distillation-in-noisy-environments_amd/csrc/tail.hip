@@ -593,11 +593,14 @@ __device__ __forceinline__ float ecda_mmd_coef(EcdaSmem& S, const EcdaRows<STAGE
     const bool on = item < nitem;
     const int blk = on ? item >> lks : 0, sl = item & (ks - 1);
     const int bi = blk / nb, bj = blk - bi * nb;
-    float acc[4][4];
+    // packed accumulators: (sum over even dims, sum over odd dims) of each pair, so the
+    // squares accumulate by v_pk_fma_f32 (half the VALU issues of scalar FMAs); (i, j) and
+    // (j, i) see exactly negated differences, hence identical squares and sums
+    f32x2 acc2[4][4];
 #pragma unroll
     for (int p = 0; p < 4; ++p)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) acc[p][q] = 0.0f;
+      for (int q = 0; q < 4; ++q) acc2[p][q] = f32x2{0.0f, 0.0f};
     if (on) {
       const f32x4* zi[4];
       const f32x4* zj[4];
@@ -620,13 +623,17 @@ __device__ __forceinline__ float ecda_mmd_coef(EcdaSmem& S, const EcdaRows<STAGE
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const f32x4 df = xi[p] - xj[r];
-            acc[p][r] = acc[p][r] + df[0] * df[0];
-            acc[p][r] = acc[p][r] + df[1] * df[1];
-            acc[p][r] = acc[p][r] + df[2] * df[2];
-            acc[p][r] = acc[p][r] + df[3] * df[3];
+            const f32x2 lo = f32x2{df[0], df[1]}, hi = f32x2{df[2], df[3]};
+            acc2[p][r] = __builtin_elementwise_fma(lo, lo, acc2[p][r]);
+            acc2[p][r] = __builtin_elementwise_fma(hi, hi, acc2[p][r]);
           }
       }
     }
+    float acc[4][4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[p][r] = acc2[p][r][0] + acc2[p][r][1];
     for (int o = ks >> 1; o > 0; o >>= 1)
 #pragma unroll
       for (int p = 0; p < 4; ++p)
@@ -728,7 +735,10 @@ __device__ __forceinline__ void ecda_member_grads(EcdaSmem& S, const EcdaRows<ST
       for (int j = 0; j < n; ++j) {
         const f32x4 zj = reinterpret_cast<const f32x4*>(R.row(j))[hq];
 #pragma unroll
-        for (int p = 0; p < 4; ++p) acc[p] += D[j * n + m[p]] * (zi[p] - zj);   // Csym[j][i] = Csym[i][j]
+        for (int p = 0; p < 4; ++p) {   // Csym[j][i] = Csym[i][j]; packed sub + packed FMA
+          const float cji = D[j * n + m[p]];
+          acc[p] = __builtin_elementwise_fma(f32x4{cji, cji, cji, cji}, zi[p] - zj, acc[p]);
+        }
       }
     }
 #pragma unroll
