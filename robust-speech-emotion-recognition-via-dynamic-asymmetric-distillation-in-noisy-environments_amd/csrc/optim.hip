@@ -34,10 +34,31 @@ __global__ void dad_commit_kernel(dad_config cfg, const float* grad, float* dacp
   dacp_commit(cfg, grad, dacp, tid);
 }
 
-// Elementwise clip + Adam + EMA over this block's 1024 parameters.  __restrict__ (no-alias
-// scopes once inlined) lets all four elements' loads issue before the first store.
-__device__ __forceinline__ void adam_ema_update(const dad_config& cfg, float coef, size_t n0,
-                                                const float* __restrict__ grad, float* __restrict__ student,
+// Elementwise clip + Adam + EMA over this block's 1024 parameters, 4 per thread
+// (i = n0 + 256k + tid).  The operands are loaded before the clip coefficient is known, so
+// the loads overlap the global-norm reduction; the stores follow once it is.
+struct AdamOperands {
+  float g[4], p[4], m[4], v[4], t[4];
+};
+
+__device__ __forceinline__ void adam_load(size_t n0, const float* __restrict__ grad, const float* __restrict__ student,
+                                          const float* __restrict__ teacher, const float* __restrict__ exp_avg,
+                                          const float* __restrict__ exp_avg_sq, AdamOperands& o) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const size_t i = n0 + (size_t)k * 256 + tid;
+    if (i >= DAD_NPARAM) break;
+    o.g[k] = grad[i];
+    o.p[k] = student[i];
+    o.m[k] = exp_avg[i];
+    o.v[k] = exp_avg_sq[i];
+    o.t[k] = teacher[i];
+  }
+}
+
+__device__ __forceinline__ void adam_ema_apply(const dad_config& cfg, float coef, size_t n0, const AdamOperands& o,
+                                               float* __restrict__ student,
                                                 float* __restrict__ teacher, float* __restrict__ exp_avg,
                                                 float* __restrict__ exp_avg_sq, __bf16* __restrict__ w1bf_s,
                                                 __bf16* __restrict__ w1bf_t) {
@@ -46,19 +67,19 @@ __device__ __forceinline__ void adam_ema_update(const dad_config& cfg, float coe
   for (int k = 0; k < 4; ++k) {
     const size_t i = n0 + (size_t)k * 256 + tid;
     if (i >= DAD_NPARAM) break;
-    float g = grad[i] * coef;
-    float p = student[i];
+    float g = o.g[k] * coef;
+    float p = o.p[k];
     g = g + cfg.weight_decay * p;                               // grad.add(param, alpha=wd)
-    float m = exp_avg[i];
+    float m = o.m[k];
     m = m + cfg.one_m_beta1 * (g - m);                          // exp_avg.lerp_(grad, 1-beta1)
-    float v = exp_avg_sq[i];
+    float v = o.v[k];
     v = v * cfg.beta2 + cfg.one_m_beta2 * g * g;                // mul_(beta2).addcmul_(g, g, 1-beta2)
     const float denom = sqrtf(v) / cfg.bc2_sqrt + cfg.adam_eps;
     p = p + (-cfg.lr_step_size) * (m / denom);                  // addcdiv_(m, denom, -step_size)
     exp_avg[i] = m;
     exp_avg_sq[i] = v;
     student[i] = p;
-    float t = teacher[i];
+    float t = o.t[k];
     if (!cfg.warmup) {
       t = t * cfg.ema_m + p * cfg.ema_one_m;
       teacher[i] = t;
@@ -77,6 +98,9 @@ __global__ __launch_bounds__(DAD_OPTIM_THREADS) void dad_optim(DadOptimArgs a) {
   __shared__ double nred[DAD_OPTIM_THREADS / 64];
   const dad_config& cfg = a.cfg;
   const int tid = threadIdx.x;
+  const size_t n0 = (size_t)blockIdx.x * 1024;
+  AdamOperands o;
+  adam_load(n0, a.grad, a.student, a.teacher, a.exp_avg, a.exp_avg_sq, o);
   // global norm from the squared-norm partials: all threads load, fixed-order combine
   double s = 0.0;
   for (int k = tid; k < a.nnorm; k += DAD_OPTIM_THREADS) s += (double)a.normpart[k];
@@ -103,8 +127,7 @@ __global__ __launch_bounds__(DAD_OPTIM_THREADS) void dad_optim(DadOptimArgs a) {
   }
   if (blockIdx.x == 0) dacp_commit(cfg, a.grad, a.dacp, tid);
   __syncthreads();
-  adam_ema_update(cfg, coef_s, (size_t)blockIdx.x * 1024, a.grad, a.student, a.teacher, a.exp_avg, a.exp_avg_sq,
-                  a.w1bf_student, a.w1bf_teacher);
+  adam_ema_apply(cfg, coef_s, n0, o, a.student, a.teacher, a.exp_avg, a.exp_avg_sq, a.w1bf_student, a.w1bf_teacher);
 }
 
 // DACPManager.update_class_quality_scores_epoch (I/utils.py:430-447)

@@ -101,19 +101,21 @@ __global__ __launch_bounds__(DAD_POOL_THREADS) void dad_pool(DadPoolArgs a) {
   const size_t cslab0 = noisy ? nsc + (size_t)b * g.ncn : (size_t)b * g.ncc;
   float ssum[2] = {0.0f, 0.0f};
   float cnt = 0.0f;
-  // slab partials in batches of 8 slabs, every load of a batch issued before the sums
-  // (index clamped, contribution masked; summed in slab order as before)
-  for (int c0 = 0; c0 < nc; c0 += 8) {
-    float p0[8], p1[8], pc[8];
+  // slab partials in batches of POOL_BATCH slabs, every load of a batch issued before the
+  // sums (index clamped, contribution masked; summed in slab order).  16 slabs of 32 rows
+  // cover T <= 512 frames in one round trip.
+  constexpr int POOL_BATCH = 16;
+  for (int c0 = 0; c0 < nc; c0 += POOL_BATCH) {
+    float p0[POOL_BATCH], p1[POOL_BATCH], pc[POOL_BATCH];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < POOL_BATCH; ++k) {
       const int c = min(c0 + k, nc - 1);
       p0[k] = a.part_sum[(slab0[0] + c) * DAD_H + h];
       p1[k] = noisy ? a.part_sum[(slab0[1] + c) * DAD_H + h] : 0.0f;
       pc[k] = a.part_cnt[(cslab0 + c) * DAD_H + h];
     }
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < POOL_BATCH; ++k) {
       if (c0 + k >= nc) break;
       ssum[0] += p0[k];
       ssum[1] += p1[k];
