@@ -235,3 +235,28 @@ def test_train_step_shim_with_reference_loop_body():
     np.testing.assert_allclose(step.dacp[0:4].cpu().numpy(), r["tau_after"], atol=1e-6)
     # a fused step afterwards sees the caller-updated parameters (bf16 shadows refreshed)
     assert step._shadow_dirty
+
+
+@pytest.mark.parametrize("class_aware", [True, False], ids=["class_aware", "global_mmd"])
+def test_large_member_sets_match_oracle(class_aware):
+    """Large batches: ECDA member sets beyond the LDS-staged size (ECDA_NZ = 80 rows in
+    csrc/tail.hip), so the member rows and the distance matrix go through the global-memory
+    path of dad_tail_ecda's class blocks; the DACP ranks span several 512-thread rounds."""
+    cfg = dad_oracle.make_cfg("iemocap", USE_CLASS_AWARE_MMD=class_aware)
+    B = 200 if class_aware else 96
+    inp = _problem(B, 6, seed=9, snr=20.0)
+    if class_aware:
+        inp["yc"] = np.zeros_like(inp["yc"])          # one class holds every clean utterance
+    st = synth.make_state(4, 1, tau_range=(0.0, 0.01))   # low thresholds: most noisy rows masked in
+    step = gh.make_step(cfg)
+    orc = dad_oracle.DADOracle(*synth.init_weights(4)[:4], cfg)
+    gh.load_state(step, st)
+    orc.load_state(st)
+    o = gh.run_step(step, inp, 60)
+    r = orc.step(inp, 60)
+    assert r["ecda_loss"] != 0.0 and int(np.sum(r["mask"])) > 80
+    for k in ("total_loss", "supervised_ce_loss", "consistency_loss", "ecda_loss"):
+        _cmp_loss(o[k], r[k], (class_aware, k))
+    np.testing.assert_array_equal(o["mask"], r["mask"])
+    for k, (a, b_) in enumerate(zip(o["grads"], r["grads"])):
+        gh.close_grad(a, b_, "large B grad %d" % k)
