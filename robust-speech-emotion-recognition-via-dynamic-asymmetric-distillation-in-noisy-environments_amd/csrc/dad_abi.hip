@@ -1,5 +1,6 @@
 // Host side of the C ABI (include/dad.h): argument validation, workspace carving and the
 // kernel sequence of one DAD step.  Enqueue-only: no allocation, no synchronisation.
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -122,7 +123,21 @@ int device_cus(int* out) {
 // kWsWeak, strong kWsStrong -- the augmentation RNG dominates a noisy slab), more
 // workgroups than CUs only when a range would exceed DAD_ENC_WS_MAXJ jobs.
 constexpr float kWsWeak = 1.03f, kWsStrong = 1.47f;   // measured (tools/ws_stamps.py fit)
+// DAD_WS_WEIGHTS="weak,strong" overrides the two costs (tuning runs; read once per process)
+struct WsWeights { float weak, strong; };
+WsWeights ws_weights() {
+  static const WsWeights w = [] {
+    WsWeights v{kWsWeak, kWsStrong};
+    if (const char* e = getenv("DAD_WS_WEIGHTS")) {
+      float a = 0.0f, b = 0.0f;
+      if (sscanf(e, "%f,%f", &a, &b) == 2 && a > 0.0f && b > 0.0f) v = WsWeights{a, b};
+    }
+    return v;
+  }();
+  return w;
+}
 void ws_split(const DadGeom& G, int Bn, int cus, int& nt, int& ns) {
+  const float kWsWeak = ws_weights().weak, kWsStrong = ws_weights().strong;
   const int Jt = Bn * G.ncn, Jc = G.Bc * G.ncc, Js = Jt;
   if (Jt == 0) {
     nt = 0;
@@ -226,7 +241,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
       const int rc = device_cus(&cus);
       if (rc) return rc;
       ws_split(G, Bn, cus, ea.ws_nt, ea.ws_ns);
-      ea.ws_wstrong = kWsStrong;
+      ea.ws_wstrong = ws_weights().strong;
       if (ea.ws_nt + ea.ws_ns > 0) {
         if (explicit_rng) hipLaunchKernelGGL(dad_encode_ws_explicit, dim3(ea.ws_nt + ea.ws_ns), dim3(DAD_ENC_WS_THREADS), 0,
                                              stream, ea);
@@ -491,7 +506,7 @@ int encoder_forward_impl(const float* x, const uint8_t* pad, int B, int T, const
     const int rc = device_cus(&cus);
     if (rc) return rc;
     ws_split(G, 0, cus, ea.ws_nt, ea.ws_ns);
-    ea.ws_wstrong = kWsStrong;
+    ea.ws_wstrong = ws_weights().strong;
     hipLaunchKernelGGL(dad_encode_ws, dim3(ea.ws_nt + ea.ws_ns), dim3(DAD_ENC_WS_THREADS), 0, stream, ea);
   } else {
     hipLaunchKernelGGL(dad_encode_f32, egrid, dim3(DAD_ENC_F32_THREADS), 0, stream, ea);
