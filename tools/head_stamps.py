@@ -1,4 +1,4 @@
-"""Diagnostic: dad_tail / dad_ecda phase timeline (build variant 'stamps', -DDAD_PROBE_STAMPS;
+"""Diagnostic: dad_tail_ecda phase timeline (tail block and ECDA class blocks) (build variant 'stamps', -DDAD_PROBE_STAMPS;
 never the product library).  Runs bench-shaped steps and prints the last step's phases."""
 import ctypes
 import os
