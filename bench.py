@@ -19,6 +19,7 @@ import json
 import math
 import os
 import statistics
+import subprocess
 import sys
 import time
 
@@ -176,6 +177,52 @@ def data_path_bench(step, B, T, epoch, dev, n_utt=1024, reps=40, steps=20):
             "step_with_device_collate": collated, "step_with_store_gather": fused}
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` without a launcher: N rank processes of this script, one per GPU,
+    with the torchrun environment (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*).  This parent
+    never touches the GPU.  If a rank fails, the others are stopped (by PID) and the first
+    non-zero exit code is returned."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        time.sleep(0.2)
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:
+                    q.kill()
+    return rc
+
+
+def flavor_view(args):
+    """The step's config for the workload: the dataset flavour's defaults (config.py), with
+    CASIA's DACP + ECDA forced on for BASELINE config 4 (C/config_casia.py:85-86 overridden)."""
+    ov = {}
+    if args.force_ecda:
+        ov.update(USE_DACP=True, USE_ECDA=True)
+    return PKG.ConfigView(None, flavor=args.flavor, **ov)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -185,29 +232,55 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--frames", type=int, default=300)
     ap.add_argument("--epoch", type=int, default=60)
+    ap.add_argument("--flavor", default="iemocap", choices=["iemocap", "casia", "emodb"])
+    ap.add_argument("--force-ecda", action="store_true", help="USE_DACP=USE_ECDA=True (CASIA, BASELINE config 4)")
+    ap.add_argument("--snr", type=float, default=5.0, help="SNR (dB) of the synthetic noisy branch")
+    ap.add_argument("--comm", default="rccl", choices=["rccl", "gloo"],
+                    help="gradient all-reduce transport for N > 1 (gloo lets ranks share one GPU)")
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--fp32-steps", type=int, default=10, help="also time the FP32 parity mode (N=1)")
     ap.add_argument("--no-data-path", action="store_true", help="skip the device collate measurement (N=1)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    if world != args.gpus:
+        print("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world), file=sys.stderr)
+        sys.exit(2)
+    ndev = torch.cuda.device_count()
+    if args.comm == "rccl" and world > 1 and local >= ndev:
+        print("bench.py: rank %d has no GPU of its own (%d visible); RCCL needs one GPU per rank "
+              "(--comm gloo shares)" % (local, ndev), file=sys.stderr)
+        sys.exit(2)
+    dev = torch.device("cuda", local % max(ndev, 1))
+    torch.cuda.set_device(dev)
     dist = None
     if world > 1:
+        import datetime
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        # control plane (barriers, the max-over-ranks clock, RCCL id broadcast) on gloo; the
+        # data path's one collective is the step's own all-reduce (RCCL through the C ABI)
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=300))
     PKG.lib()
     B, T = args.batch, args.frames
 
     model = PKG.SSRLModel().to(dev)
     P = init_model_weights(model, seed=0)
-    comm = PKG.DPComm.from_torch_distributed() if world > 1 else None
-    step = PKG.DADStep(model, flavor="iemocap", precision=args.precision, rng="counter", seed=1000 + rank, comm=comm)
-    data = make_batches(P, N_BATCHES, B, T, seed=17 + rank, device=dev)
+    comm = None
+    if world > 1:
+        comm = PKG.DPComm.from_torch_distributed() if args.comm == "rccl" else PKG.ProcessGroupComm()
+    ranks_seen = comm.ranks_seen(dev) if comm is not None else 1
+    if ranks_seen != args.gpus:
+        print("bench.py: the %s transport connected %d ranks, expected %d" % (args.comm, ranks_seen, args.gpus),
+              file=sys.stderr)
+        sys.exit(3)
+    view = flavor_view(args)
+    step = PKG.DADStep(model, view, precision=args.precision, rng="counter", seed=1000 + rank, comm=comm)
+    data = make_batches(P, N_BATCHES, B, T, seed=17 + rank, device=dev, snr_db=args.snr)
     torch.cuda.synchronize()
 
     def run(n, events=None):
@@ -221,9 +294,9 @@ def main():
         step.kernel_events = None
 
     run(args.warmup)
+    torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    torch.cuda.synchronize()
     events = []
     t0 = time.perf_counter()
     run(args.steps, events)
@@ -232,16 +305,17 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     losses = {k: float(v) for k, v in step.losses().items()}
     msum = float(step.outputs(B, B)["msum"])
+    ecda_on = float(step.outputs(B, B)["ecda_on"])
     enc_ms = statistics.mean(a.elapsed_time(b) for a, b in events)
 
     fp32 = None
     if rank == 0 and world == 1 and args.fp32_steps > 0 and args.precision == "bf16":
-        s32 = PKG.DADStep(model, flavor="iemocap", precision="fp32", rng="counter", seed=5)
+        s32 = PKG.DADStep(model, view, precision="fp32", rng="counter", seed=5)
         for i in range(3):
             s32.step(data[i % 4][0], data[i % 4][1], args.epoch)
         torch.cuda.synchronize()
@@ -256,6 +330,8 @@ def main():
         data_path = data_path_bench(step, B, T, args.epoch, dev)
 
     if rank != 0:
+        if comm is not None:
+            comm.close()
         if dist:
             dist.destroy_process_group()
         return
@@ -269,21 +345,29 @@ def main():
     t_roof = max(flops / (peak_tf * 1e12), enc_bytes / (HBM_PEAK_GBS * 1e9))
     enc_kernel = "dad_encode_ws" if args.precision == "bf16" else "dad_encode_f32"
     traffic, traffic_src = pmc_traffic(enc_kernel)
+    if args.flavor == "iemocap":
+        workload = ("IEMOCAP DAD train step (configs[%d]): batch=64/GPU, T=300x768 synthetic emotion2vec-shaped "
+                    "features, post-warm-up epoch %d (CE+KL+ECDA active), counter-RNG augmentation in-kernel"
+                    % (1 if world == 1 else 2, args.epoch))
+    else:
+        workload = ("%s DAD train step%s: batch=%d/GPU, T=%dx768 synthetic features, noisy branch at SNR %g dB, "
+                    "post-warm-up epoch %d, counter-RNG augmentation in-kernel"
+                    % (args.flavor.upper(), " (configs[3]: DACP+ECDA forced on; SCL is 0 in the reference)"
+                       if args.force_ecda else "", B, T, args.snr, args.epoch))
     line = {
         "metric": METRIC, "value": value, "unit": "utterances/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": args.precision, "data": "synthetic",
-        "config": {"workload": "IEMOCAP DAD train step (configs[1]): batch=64/GPU, T=300x768 synthetic "
-                               "emotion2vec-shaped features, post-warm-up epoch %d (CE+KL+ECDA active), "
-                               "counter-RNG augmentation in-kernel" % args.epoch,
+        "config": {"workload": workload, "flavor": args.flavor, "snr_db": args.snr,
                    "global_batch": B * world, "per_gpu_batch": B, "seq_len": T, "feature_dim": 768,
                    "parallelism": "dp%d" % world},
+        "comm": {"transport": args.comm if world > 1 else None, "ranks_seen": ranks_seen},
         "roofline": {"bound": "hbm", "kernel": enc_kernel, "achieved": enc_gbs,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": enc_gbs / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": traffic_src, "avg_launch_ms": enc_ms, "algorithmic_bytes_per_launch": enc_bytes},
         "step_roofline": {"t_roof_us": t_roof * 1e6, "t_step_us": ms * 1e3, "frac": t_roof / (ms * 1e-3),
                           "flops_per_step": flops, "bytes_per_step": enc_bytes, "mfma_peak_tflops": peak_tf},
-        "losses_last_step": losses, "mask_sum_last_step": msum,
+        "losses_last_step": losses, "mask_sum_last_step": msum, "ecda_on_last_step": ecda_on,
     }
     if fp32 is not None:
         line["fp32_mode"] = fp32
@@ -292,6 +376,8 @@ def main():
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(B, T, args.cpu_steps, args.epoch)
     print(json.dumps(line), flush=True)
+    if comm is not None:
+        comm.close()
     if dist:
         dist.destroy_process_group()
 

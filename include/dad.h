@@ -254,6 +254,11 @@ int dad_comm_get_unique_id(void* id_out);
 int dad_comm_init(void** comm, int nranks, const void* id, int rank);
 /* in-place SUM all-reduce of state->grad (DAD_GRAD_FLOATS floats) on `stream` */
 int dad_comm_allreduce_grad(void* comm, const dad_state* st, void* stream);
+/* ranks in the communicator (ncclCommCount) */
+int dad_comm_count(void* comm, int* nranks);
+/* in-place SUM all-reduce of n floats on `stream` (bench/test probe: a buffer of ones
+ * all-reduced gives the number of ranks the transport actually connected) */
+int dad_comm_allreduce_f32(void* comm, float* buf, size_t n, void* stream);
 int dad_comm_destroy(void* comm);
 
 #ifdef __cplusplus

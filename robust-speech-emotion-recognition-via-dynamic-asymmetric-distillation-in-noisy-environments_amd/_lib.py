@@ -105,6 +105,8 @@ EXPORTS = {
     "dad_comm_get_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
     "dad_comm_init": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_void_p, ctypes.c_int]),
     "dad_comm_allreduce_grad": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(DadState), ctypes.c_void_p]),
+    "dad_comm_count": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
+    "dad_comm_allreduce_f32": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
     "dad_comm_destroy": (ctypes.c_int, [ctypes.c_void_p]),
 }
 

@@ -41,6 +41,18 @@ int dad_comm_allreduce_grad(void* comm, const dad_state* st, void* stream) {
   return DAD_OK;
 }
 
+int dad_comm_count(void* comm, int* nranks) {
+  if (!comm || !nranks) return DAD_E_ARG;
+  return ncclCommCount((ncclComm_t)comm, nranks) == ncclSuccess ? DAD_OK : DAD_E_COMM;
+}
+
+int dad_comm_allreduce_f32(void* comm, float* buf, size_t n, void* stream) {
+  if (!comm || (!buf && n)) return DAD_E_ARG;
+  if (ncclAllReduce(buf, buf, n, ncclFloat32, ncclSum, (ncclComm_t)comm, (hipStream_t)stream) != ncclSuccess)
+    return DAD_E_COMM;
+  return DAD_OK;
+}
+
 int dad_comm_destroy(void* comm) {
   if (!comm) return DAD_E_ARG;
   return ncclCommDestroy((ncclComm_t)comm) == ncclSuccess ? DAD_OK : DAD_E_COMM;

@@ -47,6 +47,24 @@ class DPComm:
             return
         _lib.check(_lib.lib().dad_comm_allreduce_grad(self._comm, state_struct, stream), "dad_comm_allreduce_grad")
 
+    def ranks_seen(self, device=None):
+        """Ranks the RCCL transport actually connected: a float 1.0 per rank SUM-all-reduced
+        through the communicator (checked against ncclCommCount)."""
+        if self._comm is None:
+            return 1
+        L = _lib.lib()
+        cnt = ctypes.c_int(0)
+        _lib.check(L.dad_comm_count(self._comm, ctypes.byref(cnt)), "dad_comm_count")
+        dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        one = torch.ones(1, device=dev)
+        stream = torch.cuda.current_stream(dev)
+        _lib.check(L.dad_comm_allreduce_f32(self._comm, one.data_ptr(), 1, stream.cuda_stream),
+                   "dad_comm_allreduce_f32")
+        seen = int(round(float(one.item())))
+        if seen != cnt.value:
+            raise _lib.DadError("RCCL all-reduce saw %d ranks, communicator has %d" % (seen, cnt.value))
+        return seen
+
     def close(self):
         if self._comm is not None:
             _lib.lib().dad_comm_destroy(self._comm)
@@ -74,6 +92,12 @@ class ProcessGroupComm:
         if grad is None:
             raise ValueError("ProcessGroupComm needs the grad tensor")
         self._dist.all_reduce(grad, op=self._dist.ReduceOp.SUM, group=self.group)
+
+    def ranks_seen(self, device=None):
+        """Ranks the process group actually connected (a 1 per rank, SUM-all-reduced)."""
+        one = torch.ones(1)
+        self._dist.all_reduce(one, op=self._dist.ReduceOp.SUM, group=self.group)
+        return int(round(float(one.item())))
 
     def close(self):
         pass

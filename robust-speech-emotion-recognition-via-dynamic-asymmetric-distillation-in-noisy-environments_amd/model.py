@@ -120,6 +120,7 @@ class SSRLModel(nn.Module):
             self.load_complete_pretrained_weights(pretrained_path)
         self._init_teacher_network()
         self.ema_momentum = g("EMA_MOMENTUM", 0.99)
+        self.param_writes = 0      # parameter writes by kernels outside a DADStep (shadow refresh key)
 
     @staticmethod
     def _plist(enc, cls):
@@ -189,6 +190,7 @@ class SSRLModel(nn.Module):
                                               float(torch.tensor(1.0 - m).float()),
                                               torch.cuda.current_stream(self._student_flat.device).cuda_stream),
                    "dad_teacher_ema")
+        self.param_writes += 1
 
     def predict(self, x, padding_mask=None, use_teacher=False):
         """Eval-mode logits (I/model.py:225-245)."""

@@ -141,11 +141,22 @@ class DADStep:
         a = torch.as_tensor(anchors, dtype=torch.float32).to(self.device)
         self.dacp[16:20].copy_(a)
 
+    def _param_key(self):
+        """Identity + write count of the model's flat parameter vectors.  Writes through the
+        parameter views (load_state_dict, optimizer steps, copy_) bump the shared version
+        counter; kernel writes made outside this step (SSRLModel.update_teacher_ema) bump
+        `model.param_writes`; `.to()` rebinds the storage."""
+        m = self.model
+        s, t = m.student_flat, m.teacher_flat
+        return (s.data_ptr(), t.data_ptr(), s._version, t._version, getattr(m, "param_writes", 0))
+
     def refresh_shadow(self):
-        """Re-derive the bf16 W1 shadows after the caller changed the model's parameters."""
+        """Re-derive the bf16 W1 shadows after the caller changed the model's parameters
+        (step() also does this by itself whenever `_param_key` changed)."""
         st = self._state_struct(0)
         _lib.check(_lib.lib().dad_refresh_shadow(st, self._stream()), "dad_refresh_shadow")
         self._shadow_dirty = False
+        self._shadow_key = self._param_key()
 
     def state_dict(self):
         return {"exp_avg": self.exp_avg.clone(), "exp_avg_sq": self.exp_avg_sq.clone(),
@@ -255,7 +266,7 @@ class DADStep:
 
     def step(self, clean_batch, noisy_batch, epoch, lr=None, draws=None):
         """One full training step; returns the reference's loss dict as 0-d device tensors."""
-        if self._shadow_dirty:
+        if self._shadow_dirty or self._param_key() != self._shadow_key:
             self.refresh_shadow()
         cfg, bt, st = self._prepare(clean_batch, noisy_batch, epoch, lr, draws)
         ws = self._workspace(cfg)

@@ -100,3 +100,47 @@ def test_bf16_factorised_weight_gradient_matches_direct(monkeypatch):
     for gd, gs in zip(d["grads"], s["grads"]):
         gh.close(gs, gd, BF16_TOL, "factorised vs direct grad")
     assert _grad_cos(d["grads"], s["grads"]) > 0.999
+
+
+def test_bf16_shadow_follows_parameter_changes():
+    """Parameters changed after the DADStep exists (load_state_dict, update_teacher_ema) must
+    reach the bf16 W1 shadows of the next step: same result as a freshly constructed step."""
+    import torch
+    cfg = dad_oracle.make_cfg("iemocap")
+    inp = _problem(B=16, T=60, seed=12, ragged=True)
+    st = synth.make_state(12, 1)
+    other = synth.make_state(13, 1)
+    a = gh.make_step(cfg, precision="bf16", rng="counter", seed=9)
+    gh.load_state(a, st)
+    gh.run_step(a, inp, 60, with_draws=False)           # shadows now derived from the updated st params
+    m = a.model
+    sd = {k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in zip(
+        ["student_encoder.pre_net.weight", "student_encoder.pre_net.bias", "student_classifier.fc_layer.weight",
+         "student_classifier.fc_layer.bias", "teacher_encoder.pre_net.weight", "teacher_encoder.pre_net.bias",
+         "teacher_classifier.fc_layer.weight", "teacher_classifier.fc_layer.bias"],
+        list(other["student"]) + list(other["teacher"]))}
+    m.load_state_dict(sd)                                # no refresh_shadow() call on purpose
+    m.update_teacher_ema()
+    a.global_step = 0
+    with torch.no_grad():
+        a.exp_avg.copy_(torch.from_numpy(gh.flat(other["exp_avg"])))
+        a.exp_avg_sq.copy_(torch.from_numpy(gh.flat(other["exp_avg_sq"])))
+        a.dacp[0:4].copy_(torch.from_numpy(np.asarray(other["tau"], np.float32)))
+        a.dacp[4:8].copy_(torch.from_numpy(np.asarray(other["Q"], np.float32)))
+        a.dacp[8:16].zero_()
+    a.adam_step = int(other["nstep"])
+    b = gh.make_step(cfg, precision="bf16", rng="counter", seed=9)
+    with torch.no_grad():
+        b.model.student_flat.copy_(m.student_flat)
+        b.model.teacher_flat.copy_(m.teacher_flat)
+        b.exp_avg.copy_(a.exp_avg)
+        b.exp_avg_sq.copy_(a.exp_avg_sq)
+        b.dacp.copy_(a.dacp)
+    b.adam_step = a.adam_step
+    b.refresh_shadow()
+    oa = gh.run_step(a, inp, 60, with_draws=False)
+    ob = gh.run_step(b, inp, 60, with_draws=False)
+    for k in ("e_clean", "e_teacher", "e_strong", "z_strong"):
+        np.testing.assert_array_equal(oa[k], ob[k], err_msg=k)
+    for pa, pb in zip(oa["student"], ob["student"]):
+        np.testing.assert_array_equal(pa, pb)

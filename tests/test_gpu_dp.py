@@ -1,12 +1,19 @@
 """Data-parallel HIP step, world_size 2 on the one-GPU box: two ranks share cuda:0 and
 exchange the step's [grads | tau' | sums | counts | losses] buffer with ProcessGroupComm over
 gloo.  That runs the kernels' DP path (dad_norm rank-mean, replicated clip/Adam/EMA, DACP
-commit of the mean tau'); the RCCL transport itself (DPComm) is exercised by the driver's
-multi-GPU bench.  Each rank checks itself against the oracle's DP step on its own shard.
+commit of the mean tau').  Each rank checks itself against the oracle's DP step on its own
+shard.  RCCL cannot put two ranks on one GPU, so the RCCL transport (DPComm) with more than
+one rank runs only where the node has a GPU per rank (the driver's multi-GPU bench, which
+reports the ranks RCCL connected); here it is covered with one rank (test_gpu_rccl.py).
+The last test drives `bench.py --gpus 2 --comm gloo` end to end: the launcher spawns both
+ranks itself and the line must report two ranks.
 """
+import json
 import multiprocessing as mp
 import os
 import socket
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -95,3 +102,20 @@ def test_dp_step_two_ranks_match_oracle():
             if p.exitcode is None:
                 p.kill()
     assert res == {0: "ok", 1: "ok"}, res
+
+
+def test_bench_spawns_ranks_gloo():
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--comm", "gloo",
+                        "--steps", "5", "--warmup", "2", "--no-cpu-baseline", "--no-data-path", "--fp32-steps", "0"],
+                       cwd=root, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2
+    assert line["config"]["parallelism"] == "dp2"
+    assert line["config"]["global_batch"] == 128
+    assert line["comm"] == {"transport": "gloo", "ranks_seen": 2}
+    assert line["value"] > 0 and line["ecda_on_last_step"] == 1.0

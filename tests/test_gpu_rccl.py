@@ -1,8 +1,10 @@
 """The RCCL transport of the data-parallel step (csrc/rccl_dp.hip through the C ABI) on the
 one-GPU box: a single-rank communicator is created from a fresh unique id, the step's
 [grads | extras] buffer is SUM-all-reduced in place on the step's stream (the identity for
-one rank, bit for bit), and the communicator is destroyed.  The multi-rank exchange itself
-runs in the driver's multi-GPU bench; the DP arithmetic is covered by test_gpu_dp.py."""
+one rank, bit for bit), the rank probe (ncclCommCount + an all-reduced 1.0) reports one rank,
+and the communicator is destroyed.  RCCL refuses two ranks on one GPU, so the multi-rank
+exchange runs only in the driver's multi-GPU bench (whose line reports `comm.ranks_seen`);
+the DP arithmetic is covered by test_gpu_dp.py over gloo."""
 import ctypes
 
 import pytest
@@ -33,6 +35,7 @@ def test_single_rank_rccl_allreduce_is_identity():
     assert L.dad_comm_allreduce_grad(handle, st, stream) == 0
     torch.cuda.synchronize()
     assert torch.equal(step.grad, before)
+    assert comm.ranks_seen() == 1
     assert L.dad_comm_init(ctypes.byref(ctypes.c_void_p()), 0, uid, 0) == 1001     # argument check
     comm.close()
     assert comm._comm is None
