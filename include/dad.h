@@ -248,6 +248,27 @@ int dad_collate_index(const int64_t* offsets, const int32_t* sizes, int64_t n_sa
 int dad_predict_head(const float* e, int B, const float* w2, const float* b2, int use_entropy,
                      float* logits, float* probs, float* score, int64_t* pred, void* stream);
 
+/* --- counter-RNG draws (diagnostics, distribution tests) ------------------------------
+ * The random draws the throughput mode (DAD_RNG_COUNTER) makes inside the step kernels for
+ * the step described by cfg (seed, counter = global step, B / Bn / Tn, stds, p, mask
+ * geometry), computed by the same device functions the kernels call.  Elements
+ * [first, first + n) of one stream, as float:
+ *   DAD_DRAW_WEAK       weak-aug noise std*N of element i of the [Bn][Tn][768] tensor
+ *                       (DataAugmentation.weak_augment's randn_like * std, I/utils.py:330)
+ *   DAD_DRAW_STRONG     strong-aug noise (I/utils.py:338)
+ *   DAD_DRAW_FEAT_KEEP  feature keep flag 1/0 of channel d < 768 (rand(D) > p, I/utils.py:343)
+ *   DAD_DRAW_TSTART     temporal-mask start of utterance b < Bn (randint, I/utils.py:370)
+ *   DAD_DRAW_KEEP1      classifier dropout factor (0 or 1/(1-p)) of element b*256+h, b < B
+ *                       (student_classifier dropout, clean pass, I/train.py:400)
+ *   DAD_DRAW_KEEP2      same, strong pass, b < Bn (I/train.py:440) */
+#define DAD_DRAW_WEAK 1
+#define DAD_DRAW_STRONG 2
+#define DAD_DRAW_FEAT_KEEP 3
+#define DAD_DRAW_TSTART 4
+#define DAD_DRAW_KEEP1 5
+#define DAD_DRAW_KEEP2 6
+int dad_rng_draws(const dad_config* cfg, int which, uint64_t first, size_t n, float* out, void* stream);
+
 /* --- data-parallel gradient exchange (RCCL over xGMI) ------------------------------ */
 int dad_comm_unique_id_bytes(void);
 int dad_comm_get_unique_id(void* id_out);

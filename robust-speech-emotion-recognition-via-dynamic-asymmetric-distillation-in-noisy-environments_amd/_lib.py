@@ -17,6 +17,7 @@ DAD_DACP_FLOATS = 20
 DAD_TAIL_HDR = 64
 DAD_MAX_BATCH = 1024
 PREC_FP32, PREC_BF16 = 0, 1
+DRAW_WEAK, DRAW_STRONG, DRAW_FEAT_KEEP, DRAW_TSTART, DRAW_KEEP1, DRAW_KEEP2 = range(1, 7)
 RNG_EXPLICIT, RNG_COUNTER = 0, 1
 
 # tail header slots (dad.h DAD_T_*)
@@ -101,6 +102,8 @@ EXPORTS = {
     "dad_predict_head": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p]),
+    "dad_rng_draws": (ctypes.c_int, [ctypes.POINTER(DadConfig), ctypes.c_int, ctypes.c_uint64, ctypes.c_size_t,
+                                     ctypes.c_void_p, ctypes.c_void_p]),
     "dad_comm_unique_id_bytes": (ctypes.c_int, []),
     "dad_comm_get_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
     "dad_comm_init": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_void_p, ctypes.c_int]),

@@ -450,6 +450,64 @@ int dad_refresh_shadow(const dad_state* st, void* stream_) {
   return DAD_OK;
 }
 
+// ------------------------------------------------------------------ counter-RNG draws
+}  // extern "C"
+
+namespace {
+
+// The throughput mode's random draws, by the device functions the step kernels call
+// (dad_common.h): elements [first, first + n) of stream `which`.
+__global__ __launch_bounds__(256) void dad_draws_kernel(int which, uint32_t key, uint64_t first, size_t n, float sd,
+                                                        float p, float scale, int start_hi, float* out) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t e = first + i;
+  float v = 0.0f;
+  switch (which) {
+    case DAD_DRAW_WEAK:
+    case DAD_DRAW_STRONG: {
+      float z0, z1;
+      dad_aug_noise_pair(key, (uint32_t)(e >> 1), sd, z0, z1);
+      v = (e & 1) ? z1 : z0;
+      break;
+    }
+    case DAD_DRAW_FEAT_KEEP: v = dad_feat_keep(nullptr, key, (int)e, p); break;
+    case DAD_DRAW_TSTART: v = (float)dad_tstart_at(key, (int)e, start_hi); break;
+    default:   // DAD_DRAW_KEEP1 / KEEP2: element b * 256 + h
+      v = keep_value(nullptr, key, (int)(e / DAD_H), (int)(e % DAD_H), p, scale);
+      break;
+  }
+  out[i] = v;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dad_rng_draws(const dad_config* cfg, int which, uint64_t first, size_t n, float* out, void* stream) {
+  if (!cfg || (!out && n)) return DAD_E_ARG;
+  const Keys k = keys_of(cfg);
+  uint32_t key = 0;
+  float sd = 0.0f, p = 0.0f;
+  uint64_t limit = 0;
+  const uint64_t noise = (uint64_t)cfg->Bn * (uint64_t)cfg->Tn * DAD_D;
+  switch (which) {
+    case DAD_DRAW_WEAK: key = k.weak; sd = cfg->weak_std; limit = noise; break;
+    case DAD_DRAW_STRONG: key = k.strong; sd = cfg->strong_std; limit = noise; break;
+    case DAD_DRAW_FEAT_KEEP: key = k.feat; p = cfg->feat_p; limit = DAD_D; break;
+    case DAD_DRAW_TSTART: key = k.tstart; limit = (uint64_t)cfg->Bn; break;
+    case DAD_DRAW_KEEP1: key = k.drop1; p = cfg->p_drop; limit = (uint64_t)cfg->B * DAD_H; break;
+    case DAD_DRAW_KEEP2: key = k.drop2; p = cfg->p_drop; limit = (uint64_t)cfg->Bn * DAD_H; break;
+    default: return DAD_E_ARG;
+  }
+  if (first + n > limit || limit > 0xffffffffull * 2) return DAD_E_SHAPE;
+  if (n == 0) return DAD_OK;
+  hipLaunchKernelGGL(dad_draws_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, which,
+                     key, first, n, sd, p, cfg->drop_scale, cfg->start_hi, out);
+  DAD_TRY(hipGetLastError());
+  return DAD_OK;
+}
+
 // ----------------------------------------------------------------- modular encoder ops
 size_t dad_encoder_workspace_bytes(int B, int T) {
   if (B < 1 || T < 1) return 0;

@@ -137,6 +137,26 @@ __device__ __forceinline__ float dad_uniform_at(uint32_t key, uint32_t idx) {
   return dad_u01(dad_rng32(idx, key));
 }
 
+// Augmentation noise std*N of elements 2*pair, 2*pair+1 as the BF16 encoder adds it: the scale
+// folded into the Box-Muller radius constant (c = -2 ln2 std^2).
+__device__ __forceinline__ void dad_aug_noise_pair(uint32_t key, uint32_t pair, float sd, float& z0, float& z1) {
+  dad_normal_pair_c(key, pair, DAD_NEG2LN2 * sd * sd, z0, z1);
+}
+
+// Temporal-mask start of utterance b: uniform in [0, start_hi) (I/utils.py:370,
+// randint(0, max(1, Tmax - mask_len + 1))) by a 32x32 -> 64-bit multiply-high.
+__device__ __forceinline__ int dad_tstart_at(uint32_t key, int b, int start_hi) {
+  const uint32_t h = dad_rng32((uint32_t)b, key);
+  return (int)(((uint64_t)h * (uint64_t)start_hi) >> 32);
+}
+
+// Strong-augmentation feature keep flag of channel d (I/utils.py:343: rand(D) > dropout_rate,
+// one [768] mask per call, no rescale); u = the explicit draw or the counter uniform.
+__device__ __forceinline__ float dad_feat_keep(const float* u, uint32_t key, int d, float p) {
+  const float v = u ? u[d] : dad_uniform_at(key, (uint32_t)d);
+  return v > p ? 1.0f : 0.0f;
+}
+
 // classifier dropout keep factor of (utterance b, hidden unit h): nn.Dropout(p) in training
 // mode, inverted scaling (I/model.py:54-64); explicit mask (parity) or counter RNG
 __device__ __forceinline__ float keep_value(const uint8_t* keep, uint32_t key, int b, int h, float p, float scale) {

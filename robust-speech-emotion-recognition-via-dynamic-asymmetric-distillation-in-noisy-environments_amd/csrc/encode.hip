@@ -46,14 +46,12 @@ __device__ __forceinline__ EncodeGeom encode_geom(const DadEncodeArgs& a, int wi
 // Temporal-mask start for utterance b (I/utils.py:370: randint(0, max(1, Tmax-mlen+1))).
 __device__ __forceinline__ int tmask_start(const DadEncodeArgs& a, int b) {
   if (a.start) return (int)a.start[b];
-  uint32_t h = dad_rng32((uint32_t)b, a.key_tstart);
-  return (int)(((uint64_t)h * (uint64_t)a.start_hi) >> 32);
+  return dad_tstart_at(a.key_tstart, b, a.start_hi);
 }
 
 // Feature-dropout keep flag for channel d (I/utils.py:343: rand(D) > dropout_rate).
 __device__ __forceinline__ float feat_keep(const DadEncodeArgs& a, int d) {
-  float u = a.u ? a.u[d] : dad_uniform_at(a.key_feat, (uint32_t)d);
-  return u > a.feat_p ? 1.0f : 0.0f;
+  return dad_feat_keep(a.u, a.key_feat, d, a.feat_p);
 }
 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }

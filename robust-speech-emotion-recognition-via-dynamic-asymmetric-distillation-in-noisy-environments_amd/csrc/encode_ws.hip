@@ -166,8 +166,7 @@ __device__ __forceinline__ void job_range(const Ctx& C, int wg, int nt, int ns, 
 template <int NOISE>
 __device__ __forceinline__ int tstart_of(const Ctx& C, int b) {
   if (NOISE && C.start) return (int)C.start[b];
-  const uint32_t h = dad_rng32((uint32_t)b, C.key_tstart);
-  return (int)(((uint64_t)h * (uint64_t)C.start_hi) >> 32);
+  return dad_tstart_at(C.key_tstart, b, C.start_hi);
 }
 
 // LDS-DMA: 16 B per lane of `src` into LDS at lds_dst + 16 * lane (M0 = wave-uniform base).
@@ -253,7 +252,6 @@ __device__ __forceinline__ void ws_convert(const Ctx& C, const Job& J, int w, in
   const int st = (strong && C.mask_len > 0) ? tstart_of<NOISE>(C, J.b) : -(1 << 30);
   const uint32_t key = strong ? C.key_strong : C.key_weak;
   const float sd = strong ? C.sstd : C.wstd;
-  const float cscale = DAD_NEG2LN2 * sd * sd;
   const float* nsrc = strong ? C.ns : C.nw;
 #pragma unroll
   for (int i = 0; i < S::RPW; ++i) {
@@ -276,8 +274,8 @@ __device__ __forceinline__ void ws_convert(const Ctx& C, const Job& J, int w, in
         } else {
           const uint32_t p = ((uint32_t)grow * (uint32_t)DAD_D + (uint32_t)d) >> 1;
           float z0, z1, z2, z3;
-          dad_normal_pair_c(key, p, cscale, z0, z1);
-          dad_normal_pair_c(key, p + 1u, cscale, z2, z3);
+          dad_aug_noise_pair(key, p, sd, z0, z1);
+          dad_aug_noise_pair(key, p + 1u, sd, z2, z3);
           n = f32x4{z0, z1, z2, z3};
         }
         // reference op order: x + std*N, then * feature mask, then temporal zero
@@ -583,8 +581,7 @@ __device__ __forceinline__ void encode_ws_body(const DadEncodeArgs& a, char* sme
   uint32_t* vb = reinterpret_cast<uint32_t*>(smem + kOffVB);
   if (!teacher)
     for (int d = tid; d < DAD_D; d += S::kThreads) {
-      const float u = C.u ? C.u[d] : dad_uniform_at(C.key_feat, (uint32_t)d);
-      fk[d] = u > C.feat_p ? 1.0f : 0.0f;     // I/utils.py:343 (rand(D) > p)
+      fk[d] = dad_feat_keep(C.u, C.key_feat, d, C.feat_p);     // I/utils.py:343 (rand(D) > p)
     }
   for (int p = tid; p < nj * DAD_SLAB; p += S::kThreads) {
     const Job J = job_of(C, teacher, j0 + p / DAD_SLAB);

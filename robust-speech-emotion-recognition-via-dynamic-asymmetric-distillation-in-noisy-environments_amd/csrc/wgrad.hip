@@ -22,13 +22,11 @@ namespace {
 
 __device__ __forceinline__ int wg_tstart(const DadWgradArgs& a, int b) {
   if (a.start) return (int)a.start[b];
-  const uint32_t h = dad_rng32((uint32_t)b, a.key_tstart);
-  return (int)(((uint64_t)h * (uint64_t)a.start_hi) >> 32);
+  return dad_tstart_at(a.key_tstart, b, a.start_hi);
 }
 
 __device__ __forceinline__ float wg_featkeep(const DadWgradArgs& a, int d) {
-  const float u = a.u ? a.u[d] : dad_uniform_at(a.key_feat, (uint32_t)d);
-  return u > a.feat_p ? 1.0f : 0.0f;
+  return dad_feat_keep(a.u, a.key_feat, d, a.feat_p);
 }
 
 // slab s of the weight-gradient row list: clean slabs first, then strong (noisy) slabs

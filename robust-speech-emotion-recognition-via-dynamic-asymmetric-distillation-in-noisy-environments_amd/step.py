@@ -344,6 +344,25 @@ class DADStep:
             "grad": self.grad[:_lib.DAD_NPARAM], "nb": nb,
         }
 
+    _DRAWS = {"weak": _lib.DRAW_WEAK, "strong": _lib.DRAW_STRONG, "feat_keep": _lib.DRAW_FEAT_KEEP,
+              "tstart": _lib.DRAW_TSTART, "keep1": _lib.DRAW_KEEP1, "keep2": _lib.DRAW_KEEP2}
+
+    def counter_draws(self, which, Bc, Tc, Bn, Tn, epoch=60, counter=None, first=0, n=None):
+        """The counter-RNG draws a step with this geometry makes in-kernel (dad_rng_draws):
+        'weak' / 'strong' noise (std * N per element of [Bn, Tn, 768]), 'feat_keep' [768],
+        'tstart' [Bn], 'keep1' [Bc*256] / 'keep2' [Bn*256] classifier dropout factors.
+        `counter` defaults to the next step's (self.global_step).  Diagnostics only."""
+        cfg = self.make_config(Bc, Tc, Bn, Tn, epoch)
+        if counter is not None:
+            cfg.counter = int(counter) & (2 ** 64 - 1)
+        size = {"weak": Bn * Tn * 768, "strong": Bn * Tn * 768, "feat_keep": 768, "tstart": Bn,
+                "keep1": Bc * 256, "keep2": Bn * 256}[which]
+        n = size - first if n is None else n
+        out = torch.empty(max(n, 0), device=self.device)
+        _lib.check(_lib.lib().dad_rng_draws(cfg, self._DRAWS[which], first, n, _lib.ptr(out), self._stream()),
+                   "dad_rng_draws")
+        return out
+
     def epoch_end(self):
         """DACPManager.update_class_quality_scores_epoch (I/utils.py:430-447), on device."""
         cfg = self.make_config(1, 1, 1, 1, self.view.WARMUP_EPOCHS)

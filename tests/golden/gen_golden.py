@@ -48,6 +48,16 @@ VARIANTS = {
     "iemocap_t300": dict(tree="IEMOCAP", B=8, T=300, seed=41),
     "emodb_hi_tau": dict(tree="EMODB", B=8, T=20, seed=33, tau_range=[0.96, 0.995]),
     "iemocap_b64": dict(tree="IEMOCAP", B=64, T=40, seed=51),
+    # the bench geometry (BASELINE configs[1]): one warm-up and two full-weight steps
+    "iemocap_b64_t300": dict(tree="IEMOCAP", B=64, T=300, seed=61, schedule=[0, 60, 60, "epoch_end"]),
+    # BASELINE configs[3]: CASIA with DACP + ECDA forced on (C/config_casia.py:85-86 overridden),
+    # noisy branch at SNR 0 / 5 / 10 dB
+    "casia_ecda_snr0": dict(tree="CASIA", B=16, T=40, seed=71, snr_db=0.0,
+                            overrides=dict(USE_DACP=True, USE_ECDA=True)),
+    "casia_ecda_snr5": dict(tree="CASIA", B=16, T=40, seed=73, snr_db=5.0,
+                            overrides=dict(USE_DACP=True, USE_ECDA=True)),
+    "casia_ecda_snr10": dict(tree="CASIA", B=16, T=40, seed=72, snr_db=10.0,
+                             overrides=dict(USE_DACP=True, USE_ECDA=True)),
 }
 
 W1_SAMPLE = 1024          # sampled entries of the [256,768] tensors stored per step
@@ -198,7 +208,7 @@ def run_variant(name, out_path):
     step = 0
     torch.randn_like, torch.rand, torch.randint = fake_randn_like, fake_rand, fake_randint
     try:
-        for item in SCHEDULE:
+        for item in spec.get("schedule", SCHEDULE):
             if item == "epoch_end":
                 Q0 = synth.make_state(seed, step, C, tuple(spec.get("tau_range", (0.55, 0.9))))["Q"]
                 tr.dacp_manager.class_quality_scores = torch.from_numpy(Q0.copy())
@@ -209,7 +219,7 @@ def run_variant(name, out_path):
                 continue
             epoch = item
             pre = "s%d_" % step
-            inp = synth.make_step_inputs(seed, step, B, T)
+            inp = synth.make_step_inputs(seed, step, B, T, snr_db=spec.get("snr_db", 5.0))
             st = synth.make_state(seed, step, C, tuple(spec.get("tau_range", (0.55, 0.9))))
             with torch.no_grad():
                 for p_, a in zip(student_params, st["student"]):

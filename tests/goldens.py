@@ -44,7 +44,7 @@ def problem(spec):
 
 
 def step_inputs(spec, step):
-    return synth.make_step_inputs(spec["seed"], step, spec["B"], spec["T"])
+    return synth.make_step_inputs(spec["seed"], step, spec["B"], spec["T"], snr_db=spec.get("snr_db", 5.0))
 
 
 def rel_err(a, b):
