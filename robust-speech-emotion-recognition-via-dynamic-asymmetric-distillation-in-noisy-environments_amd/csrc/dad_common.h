@@ -31,13 +31,14 @@ __device__ __forceinline__ int dad_nchunk(int T) { return (T + DAD_SLAB - 1) / D
 // ---------------------------------------------------------------------------------
 // Counter-based RNG (production mode).  Each random value is a pure function of
 // (seed, step counter, stream, element index), so the weight-gradient kernel can
-// regenerate the strong augmentation instead of storing it.  Per value: the
-// "lowbias32" integer mixer (two 32-bit multiplies) with the 32-bit stream key
-// injected between its two rounds, so different streams are different bijections of
-// the element index (not shifted copies of one sequence).  The stream key is derived
-// on the host from (seed, counter, stream) with splitmix64 (dad_stream_key).
-// Philox4x32-10 costs ~40 quarter-rate multiplies per 4 outputs, which made the
-// augmentation VALU-bound ("RNG").
+// regenerate the strong augmentation instead of storing it.  Per value: the three-round
+// "triple32" integer mixer (three 32-bit multiplies) with the 32-bit stream key injected
+// after its first round, so different streams are different bijections of the element
+// index (not shifted copies of one sequence) and two full rounds follow the key.  (A
+// two-round mixer keyed between its rounds left adjacent elements correlated at ~2x the iid
+// spread over 1.5e7 samples: tests/test_gpu_rng.py.)  The stream key is derived on the host
+// from (seed, counter, stream) with splitmix64 (dad_stream_key).  Philox4x32-10 costs ~40
+// quarter-rate multiplies per 4 outputs, which made the augmentation VALU-bound.
 enum DadStream {
   DAD_RNG_WEAK = 1,      // teacher weak-aug noise      (I/utils.py:330)
   DAD_RNG_STRONG = 2,    // student strong-aug noise    (I/utils.py:338)
@@ -49,12 +50,14 @@ enum DadStream {
 
 __host__ __device__ __forceinline__ uint32_t dad_rng32(uint32_t i, uint32_t key) {
   uint32_t x = i;
-  x ^= x >> 16;
-  x *= 0x7feb352du;
+  x ^= x >> 17;
+  x *= 0xed5ad4bbu;
   x ^= key;
+  x ^= x >> 11;
+  x *= 0xac4c1b51u;
   x ^= x >> 15;
-  x *= 0x846ca68bu;
-  x ^= x >> 16;
+  x *= 0x31848babu;
+  x ^= x >> 14;
   return x;
 }
 
