@@ -248,6 +248,47 @@ int dad_collate_index(const int64_t* offsets, const int32_t* sizes, int64_t n_sa
 int dad_predict_head(const float* e, int B, const float* w2, const float* b2, int use_entropy,
                      float* logits, float* probs, float* score, int64_t* pred, void* stream);
 
+/* --- the reference's helper types as operators (I/utils.py:317-652) -------------------
+ * For trainer code that drives DataAugmentation / DACPManager / ECDALoss itself (the
+ * train_step shim's callers, anchor calibration, I/train.py:334,341).  Same device functions
+ * as the fused step.
+ *
+ * DataAugmentation.weak_augment (strong = 0, I/utils.py:328-331) / strong_augment (strong = 1,
+ * I/utils.py:333-375) of x [B][T][D] (a [T][D] input is B = 1; 1-D or > 3-D inputs are
+ * passed with mask_len 0, as the reference masks only 2-D / 3-D data):
+ *   out = x + std * N;  strong: * (u[d] > feat_p) (one [D] mask, no rescale; skipped when
+ *   feat_p <= 0), then frames [start_b, start_b + mask_len) of utterance b zeroed, start_b
+ *   uniform in [0, max(1, T - mask_len + 1)).
+ * Draws: explicit (noise [B][T][D] standard normals, u [D] uniforms, start [B]) or, for NULL,
+ * the counter streams of (seed, counter) -- with D = 768 the values the fused step draws. */
+int dad_augment(const float* x, int B, int T, int D, int strong, float noise_std, float feat_p, int mask_len,
+                uint64_t seed, uint64_t counter, const float* noise, const float* u, const int64_t* start,
+                float* out, void* stream);
+/* DACPManager.calculate_certainty_scores (I/utils.py:400-428): probs [B][4] -> score [B],
+ * pred [B] (first argmax); use_entropy = USE_ENTROPY_IN_SCORE.  Outputs may be NULL. */
+int dad_certainty_scores(const float* probs, int B, int use_entropy, float* score, int64_t* pred, void* stream);
+/* DACPManager.calculate_mask (I/utils.py:449-507): teacher probs [Bn][4] and the 20-float
+ * DACP state (tau | Q | epoch score sums | counts | calibrated anchors, DAD_DACP_FLOATS) ->
+ * mask [Bn] (1 = confident), score [Bn], pred [Bn], class_weights [4] (W_c); updates tau
+ * (EMA of the floored thresholds) and the epoch sums / counts in place, as the reference
+ * updates its fields.  Reads cfg: dacp_gamma (from the epoch), dacp_k, dacp_lambda,
+ * dacp_alpha / one_m_alpha, use_entropy.  score / pred / class_weights may be NULL. */
+int dad_dacp_mask(const dad_config* cfg, const float* probs, int Bn, float* dacp, uint8_t* mask, float* score,
+                  int64_t* pred, float* class_weights, void* stream);
+/* ECDALoss.forward (I/utils.py:565-652) + its gradients: clean [B][256], noisy [Bn][256]
+ * embeddings, clean_labels [B], noisy_labels [Bn] (teacher pseudo-labels), noisy_mask [Bn]
+ * (1 = confident), noisy_scores [Bn], class_weights [n_weights] (DACP's [4] W_c, or the
+ * fixed-threshold branch's ones(Bn), I/train.py:420).  loss [1] (device) = the class-aware sum
+ * (or the global-MMD ablation when cfg->class_aware = 0); grad_clean [B][256] / grad_noisy
+ * [Bn][256] = d loss / d embeddings (rows outside every member set are 0; may be NULL).
+ * Reads cfg: class_aware, ecda_att_lambda, ecda_gamma, ecda_delta.
+ * workspace: dad_ecda_workspace_bytes(B, Bn). */
+size_t dad_ecda_workspace_bytes(int B, int Bn);
+int dad_ecda_loss(const dad_config* cfg, const float* clean, int B, const float* noisy, int Bn,
+                  const int64_t* clean_labels, const int64_t* noisy_labels, const uint8_t* noisy_mask,
+                  const float* noisy_scores, const float* class_weights, int n_weights, float* loss,
+                  float* grad_clean, float* grad_noisy, void* workspace, void* stream);
+
 /* --- counter-RNG draws (diagnostics, distribution tests) ------------------------------
  * The random draws the throughput mode (DAD_RNG_COUNTER) makes inside the step kernels for
  * the step described by cfg (seed, counter = global step, B / Bn / Tn, stds, p, mask

@@ -15,10 +15,11 @@ from .model import EmotionClassifier, Emotion2VecEncoder, SSRLModel
 from .step import DADStep
 from .dist import DPComm, ProcessGroupComm
 from .data import DeviceLoader, FeatureStore
+from .utils import DACPManager, DataAugmentation, ECDALoss
 from . import checkpoint, evaluate, pretrain
 
 __all__ = ["SSRLModel", "Emotion2VecEncoder", "EmotionClassifier", "DADStep", "DPComm", "ProcessGroupComm", "ConfigView",
-           "dad_config_for", "FLAVOR_DEFAULTS", "FeatureStore", "DeviceLoader", "build", "lib"]
+           "dad_config_for", "FLAVOR_DEFAULTS", "FeatureStore", "DeviceLoader", "DataAugmentation", "DACPManager", "ECDALoss", "build", "lib"]
 
 
 def build(verbose=True):
@@ -31,5 +32,5 @@ def lib():
 
 
 _sys.modules.setdefault("dad_amd", _sys.modules[__name__])
-for _m in ("_build", "_lib", "config", "model", "step", "dist", "data", "evaluate", "checkpoint", "pretrain"):
+for _m in ("_build", "_lib", "config", "model", "step", "dist", "data", "utils", "evaluate", "checkpoint", "pretrain"):
     _sys.modules.setdefault("dad_amd." + _m, _sys.modules[__name__ + "." + _m])

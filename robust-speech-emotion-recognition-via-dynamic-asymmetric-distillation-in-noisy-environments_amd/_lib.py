@@ -102,6 +102,19 @@ EXPORTS = {
     "dad_predict_head": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p]),
+    "dad_augment": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                   ctypes.c_float, ctypes.c_float, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64,
+                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "dad_certainty_scores": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_void_p]),
+    "dad_dacp_mask": (ctypes.c_int, [ctypes.POINTER(DadConfig), ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_void_p]),
+    "dad_ecda_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int, ctypes.c_int]),
+    "dad_ecda_loss": (ctypes.c_int, [ctypes.POINTER(DadConfig), ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                     ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "dad_rng_draws": (ctypes.c_int, [ctypes.POINTER(DadConfig), ctypes.c_int, ctypes.c_uint64, ctypes.c_size_t,
                                      ctypes.c_void_p, ctypes.c_void_p]),
     "dad_comm_unique_id_bytes": (ctypes.c_int, []),

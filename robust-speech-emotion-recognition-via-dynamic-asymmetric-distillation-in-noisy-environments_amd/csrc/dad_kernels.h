@@ -169,6 +169,15 @@ __global__ void dad_optim(DadOptimArgs a);
 __global__ void dad_commit_kernel(dad_config cfg, const float* grad, float* dacp, float* tailf, float* losses_out);
 __global__ void dad_epoch_end_kernel(float* dacp, float beta, float one_m_beta);
 __global__ void dad_shadow_kernel(const float* student, const float* teacher, __bf16* ws, __bf16* wt);
+// helper-type drop-ins (DACPManager / ECDALoss, tail.hip; DataAugmentation, utils_abi.hip)
+__global__ void dad_certainty_kernel(const float* probs, int B, int use_entropy, float* score, int64_t* pred);
+__global__ void dad_dacp_mask_kernel(dad_config cfg, const float* probs, int Bn, float* dacp, uint8_t* mask,
+                                     float* score, int64_t* pred, float* wout);
+__global__ void dad_ecda_prep_kernel(const float* clean, int B, const float* noisy, int Bn, const int64_t* noisy_labels,
+                                     const uint8_t* noisy_mask, const float* noisy_scores, const float* class_weights,
+                                     int nw, float* emb, float* tailf, uint32_t* eflag);
+__global__ void dad_ecda_finish_kernel(int B, int Bn, const float* tailf, const float* ge, const uint32_t* eflag,
+                                       float* loss, float* gclean, float* gnoisy);
 
 // offsets inside the flat parameter vector [W1 | b1 | W2 | b2]
 #define DAD_OFF_W1 0

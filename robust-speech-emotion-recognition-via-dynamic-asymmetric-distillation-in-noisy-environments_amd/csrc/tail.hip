@@ -202,26 +202,33 @@ struct TailSmem {
   float dstate[20];                        // DACP state: tau | Q | (sums) | (counts) | anchors
 };
 
-// teacher probs (I/train.py:409-410), certainty score and pseudo-label (I/utils.py:400-428)
+// DACPManager.calculate_certainty_scores (I/utils.py:400-428) of one probability row:
+// pseudo-label = first argmax, score = max_prob * (1 - H / log2 C) with
+// H = -sum q log2(q + 1e-8) (log2(NUM_CLASSES) = 2), or max_prob without the entropy term
+__device__ __forceinline__ void certainty_from_probs(const float (&q)[4], bool entropy, float& s, int& pred) {
+  float mx = -1.0f;
+  pred = 0;
+  for (int c = 0; c < 4; ++c)
+    if (q[c] > mx) { mx = q[c]; pred = c; }
+  s = mx;
+  if (entropy) {
+    float ent = 0.0f;
+    for (int c = 0; c < 4; ++c) ent += q[c] * log2f(q[c] + 1e-8f);
+    ent = -ent;
+    s = mx * (1.0f - ent / 2.0f);
+  }
+}
+
+// teacher probs (I/train.py:409-410), certainty score and pseudo-label (I/utils.py:400-428);
+// the fixed-threshold branch (I/train.py:417-420) uses max_prob
 __device__ __forceinline__ void teacher_certainty(const float (&z)[4], const dad_config& cfg, float (&q)[4],
                                                   float& s, int& pred) {
   float m = -INFINITY;
   for (int c = 0; c < 4; ++c) m = fmaxf(m, z[c]);
   float e[4], se = 0.0f;
   for (int c = 0; c < 4; ++c) { e[c] = expf(z[c] - m); se += e[c]; }
-  float mx = -1.0f;
-  pred = 0;
-  for (int c = 0; c < 4; ++c) {
-    q[c] = e[c] / se;
-    if (q[c] > mx) { mx = q[c]; pred = c; }
-  }
-  s = mx;
-  if (cfg.use_dacp && cfg.use_entropy) {
-    float ent = 0.0f;
-    for (int c = 0; c < 4; ++c) ent += q[c] * log2f(q[c] + 1e-8f);
-    ent = -ent;
-    s = mx * (1.0f - ent / 2.0f);   // log2(NUM_CLASSES) = 2
-  }
+  for (int c = 0; c < 4; ++c) q[c] = e[c] / se;
+  certainty_from_probs(q, cfg.use_dacp && cfg.use_entropy, s, pred);
 }
 
 // DACPManager.calculate_mask thresholds (I/utils.py:449-507): per-class ranks of the scores,
@@ -1037,4 +1044,100 @@ __global__ __launch_bounds__(TAIL_THREADS) void dad_tail_ecda(DadTailArgs ta, Da
   } u;
   if (blockIdx.x == 0) tail_block(ta, u.t);
   else ecda_block<true>(ca, (int)blockIdx.x - 1, u.e.s, u.e.pdist, &ta, u.e.p);
+}
+
+// ------------------------------------------------------------- helper-type drop-ins
+// DACPManager.calculate_certainty_scores (I/utils.py:400-428): one thread per row of probs.
+__global__ __launch_bounds__(256) void dad_certainty_kernel(const float* probs, int B, int use_entropy, float* score,
+                                                            int64_t* pred) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= B) return;
+  const f32x4 v = reinterpret_cast<const f32x4*>(probs)[b];
+  const float q[4] = {v[0], v[1], v[2], v[3]};
+  float s;
+  int p;
+  certainty_from_probs(q, use_entropy != 0, s, p);
+  if (score) score[b] = s;
+  if (pred) pred[b] = p;
+}
+
+// DACPManager.calculate_mask (I/utils.py:449-507) on teacher probabilities, one workgroup:
+// the tail block's own thresholds (dacp_thresholds) and mask, then the state update the fused
+// step commits in dad_optim (tau EMA, epoch score sums and counts).  dacp = the 20-float state
+// (tau | Q | sums | counts | anchors).
+__global__ __launch_bounds__(TAIL_THREADS) void dad_dacp_mask_kernel(dad_config cfg, const float* probs, int Bn,
+                                                                      float* dacp, uint8_t* mask, float* score,
+                                                                      int64_t* pred, float* wout) {
+  DAD_GUARD_BLOCK(TAIL_THREADS);
+  __shared__ TailSmem T;
+  const int tid = threadIdx.x;
+  if (tid < 20) T.dstate[tid] = dacp[tid];
+  for (int b = tid; b < Bn; b += TAIL_THREADS) {
+    const f32x4 v = reinterpret_cast<const f32x4*>(probs)[b];
+    const float q[4] = {v[0], v[1], v[2], v[3]};
+    certainty_from_probs(q, cfg.use_entropy != 0, T.ss[b], T.sp[b]);
+  }
+  if (tid < DAD_C) T.ncls[tid] = 0;
+  __syncthreads();
+  float wc[DAD_C];
+  dacp_thresholds(cfg, Bn, T.ss, T.sp, T.srt, T.ncls, T.dstate, T.tau_new, wc, nullptr, nullptr);
+  double st4[4] = {0.0, 0.0, 0.0, 0.0}, ct4[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int b = tid; b < Bn; b += TAIL_THREADS) {
+    const int p = T.sp[b];
+    mask[b] = T.ss[b] >= T.tau_new[p] ? 1 : 0;
+    if (score) score[b] = T.ss[b];
+    if (pred) pred[b] = p;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      st4[c] += p == c ? (double)T.ss[b] : 0.0;
+      ct4[c] += p == c ? 1.0 : 0.0;
+    }
+  }
+  block_sum4_d(st4, T.dred4);
+  block_sum4_d(ct4, T.dred4);
+  if (tid < DAD_C) {
+    dacp[tid] = T.tau_new[tid];
+    dacp[8 + tid] += (float)st4[tid];
+    dacp[12 + tid] += (float)ct4[tid];
+    if (wout) wout[tid] = wc[tid];
+  }
+}
+
+// ECDALoss.forward (I/utils.py:565-652) on caller embeddings: stage them in the step's layout
+// (emb rows [clean | - | noisy], tail header + per-sample score / pred / mask) for dad_ecda.
+__global__ __launch_bounds__(256) void dad_ecda_prep_kernel(const float* clean, int B, const float* noisy, int Bn,
+                                                            const int64_t* noisy_labels, const uint8_t* noisy_mask,
+                                                            const float* noisy_scores, const float* class_weights,
+                                                            int nw, float* emb, float* tailf, uint32_t* eflag) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const size_t nc = (size_t)B * DAD_H, nn = (size_t)Bn * DAD_H;
+  if (i < nc) emb[i] = clean[i];
+  if (i < nn) emb[(size_t)(B + Bn) * DAD_H + i] = noisy[i];
+  if (i < DAD_TAIL_HDR) {
+    float v = 0.0f;
+    if (i >= DAD_T_W && i < DAD_T_W + DAD_C) v = (int)(i - DAD_T_W) < nw ? class_weights[i - DAD_T_W] : 1.0f;
+    if (i == DAD_T_ECDA_ON) v = 1.0f;
+    tailf[i] = v;
+  }
+  if (i < (size_t)Bn) {
+    tailf[DAD_TAIL_HDR + i] = noisy_scores[i];
+    tailf[DAD_TAIL_HDR + Bn + i] = (float)noisy_labels[i];
+    tailf[DAD_TAIL_HDR + 2 * Bn + i] = noisy_mask[i] ? 1.0f : 0.0f;
+  }
+  if (i < (size_t)(B + Bn)) eflag[i] = 0u;
+}
+
+// loss = sum of the per-class terms (class-aware: ((t0 + t1) + t2) + t3, the reference's
+// accumulation order; global MMD: t0), grads = the member rows dad_ecda wrote, zero elsewhere
+__global__ __launch_bounds__(256) void dad_ecda_finish_kernel(int B, int Bn, const float* tailf, const float* ge,
+                                                              const uint32_t* eflag, float* loss, float* gclean,
+                                                              float* gnoisy) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const size_t nc = (size_t)B * DAD_H, nn = (size_t)Bn * DAD_H;
+  if (i == 0 && loss) {
+    const float* t = tailf + DAD_T_ECDA_TERM;
+    *loss = ((t[0] + t[1]) + t[2]) + t[3];
+  }
+  if (gclean && i < nc) gclean[i] = eflag[i / DAD_H] ? ge[i] : 0.0f;
+  if (gnoisy && i < nn) gnoisy[i] = eflag[B + i / DAD_H] ? ge[nc + i] : 0.0f;
 }
