@@ -23,7 +23,12 @@ PKG = dadpkg.pkg()
 
 DACP_VARIANTS = [n for n in goldens.variants() if not n.endswith(("fixed_thr", "fixed_ecda")) and
                  not n.startswith("casia_default")]
-ECDA_VARIANTS = [n for n in goldens.variants() if n not in ("casia_default", "iemocap_fixed_thr")]
+def _has_ecda(name):
+    d = goldens.load(name)[0]
+    return any(float(d["s%d_ecda_loss" % s]) != 0.0 for s in range(int(d["n_steps"])))
+
+
+ECDA_VARIANTS = [n for n in goldens.variants() if _has_ecda(n)]
 
 
 def _cuda(a, dtype=None):
