@@ -36,7 +36,7 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BF16_PEAK_TFLOPS = 2500.0      # dense bf16 MFMA
 FP32_PEAK_TFLOPS = 157.3       # f32 MFMA == f32 vector rate
 EVENT_EVERY = 4                # timed steps per encoder event pair
-CPU_BASELINE_SECONDS = 15.0    # bounded CPU sample (oracle steps until this much CPU time)
+CPU_BASELINE_SECONDS = 15.0    # bounded CPU sample (PyTorch-CPU steps until this much time)
 N_BATCHES = 8                  # distinct resident batches cycled by the timed steps: 8 x 118 MB of f32
                                # features, past the 256 MB infinity cache, so encoder reads come from HBM
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_latest.json")   # tools/profile_report.py --json
@@ -91,33 +91,56 @@ def pmc_traffic(kernel):
         return None, None
 
 
-def cpu_baseline(B, T, steps, epoch, seconds=CPU_BASELINE_SECONDS):
-    """The NumPy oracle (CPU restatement of the reference step) on this host's cores: at least
-    `steps` steps after one warm-up, continuing until `seconds` of steps have run."""
-    from oracle import dad_oracle, synth
+def _cpu_model():
     try:
-        import threadpoolctl
-        info = threadpoolctl.threadpool_info()
-        cores = max([i.get("num_threads", 1) for i in info if i.get("user_api") == "blas"] or [1])
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_baseline(B, T, steps, epoch, seconds=CPU_BASELINE_SECONDS):
+    """The PyTorch-CPU step (oracle/torch_cpu.py: the reference's step on the same ATen ops,
+    calibrated against the imported reference in profiles/r02_cpu_calibration.json) on this
+    host: torch's intra-op pool sized to the job's CPU share (OMP_NUM_THREADS, else every CPU
+    in the affinity mask); at least `steps` steps after 2 warm-ups, until `seconds` of steps."""
+    from oracle import dad_oracle, synth, torch_cpu
+    host_cpus = len(os.sched_getaffinity(0))
+    threads = int(os.environ.get("OMP_NUM_THREADS") or host_cpus)
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        cfg = dad_oracle.make_cfg("iemocap")
+        W1, b1, W2, b2, _ = synth.init_weights(0)
+        st = torch_cpu.TorchCPUStep(W1, b1, W2, b2, cfg)
+        times = []
+        k = 0
+        while k < steps + 2 or (sum(times[2:]) < seconds and k < 200):
+            inp = synth.make_step_inputs(0, k, B, T, ragged=False)
+            t0 = time.perf_counter()
+            st.step(inp, epoch)
+            times.append(time.perf_counter() - t0)
+            k += 1
+    finally:
+        torch.set_num_threads(prev)
+    med = statistics.median(times[2:])
+    out = {"value": B / med, "unit": "utterances/s", "cores": threads, "kind": "port",
+           "host_cpus": host_cpus, "cpu_model": _cpu_model(),
+           "sample": "%d steps (after 2 warm-ups, %.1f s) of the PyTorch-CPU DAD step (oracle/torch_cpu.py), B=%d "
+                     "T=%d epoch %d, torch RNG; median %.3f s/step" % (len(times) - 2, sum(times[2:]), B, T, epoch, med)}
+    try:
+        cal = json.load(open(os.path.join(ROOT, "profiles", "r02_cpu_calibration.json")))
+        rows = cal["by_threads"]
+        near = min(rows, key=lambda n: abs(int(n) - threads))
+        r = rows[near]["ratio_port_over_reference"]
+        out["calibration"] = {"ratio_port_over_reference": r, "at_threads": int(near),
+                              "container_cpu": cal.get("cpu_model"), "source": "profiles/r02_cpu_calibration.json",
+                              "reference_equivalent_value": out["value"] * r}
     except Exception:
-        cores = os.cpu_count() or 1
-    cfg = dad_oracle.make_cfg("iemocap")
-    W1, b1, W2, b2, _ = synth.init_weights(0)
-    orc = dad_oracle.DADOracle(W1, b1, W2, b2, cfg)
-    rng = np.random.default_rng(0)
-    times = []
-    k = 0
-    while k < steps + 1 or (sum(times[1:]) < seconds and k < 200):
-        inp = synth.make_step_inputs(0, k, B, T, ragged=False)
-        inp = {n: inp[n] for n in ("xc", "mc", "yc", "xn", "mn", "yn")}    # draws sampled inside (like randn)
-        t0 = time.perf_counter()
-        orc.step(inp, epoch, rng=rng)
-        times.append(time.perf_counter() - t0)
-        k += 1
-    med = statistics.median(times[1:])
-    return {"value": B / med, "unit": "utterances/s", "cores": int(cores), "kind": "port",
-            "sample": "%d steps (after 1 warm-up, %.1f s) of the NumPy oracle DAD step, B=%d T=%d epoch %d incl. "
-                      "noise sampling; median %.3f s/step" % (len(times) - 1, sum(times[1:]), B, T, epoch, med)}
+        out["calibration"] = None
+    return out
 
 
 def data_path_bench(step, B, T, epoch, dev, n_utt=1024, reps=40, steps=20):
