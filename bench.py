@@ -200,6 +200,138 @@ def data_path_bench(step, B, T, epoch, dev, n_utt=1024, reps=40, steps=20):
             "step_with_device_collate": collated, "step_with_store_gather": fused}
 
 
+# ------------------------------------------------------------------ BASELINE configs[4]: mixed corpora
+CORPORA = {   # synthetic stand-ins with each corpus's utterance count and fold structure
+    "iemocap": {"sessions": [1085, 1023, 1151, 1031, 1241]},           # I/config.py:36, 5 session folds
+    "casia": {"speakers": ["spk_%d" % k for k in range(4)], "n": 5996},  # 4 speaker folds
+    "emodb": {"n": 535},                                                 # 10 speakers, LOSO folds
+}
+
+
+def _synthetic_store(P, labels, sizes, sigma, dev, gen):
+    """FeatureStore of utterances x[t] = P[y] + sigma_u * N(0, 1), all on the device."""
+    sizes = np.asarray(sizes, np.int64)
+    offsets = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
+    n_rows = int(sizes.sum())
+    feats = torch.empty(n_rows, 768, device=dev)
+    row_utt = torch.repeat_interleave(torch.arange(len(sizes), device=dev), torch.from_numpy(sizes).to(dev))
+    lab_d = torch.from_numpy(np.asarray(labels, np.int64)).to(dev)
+    sig_d = torch.as_tensor(sigma, dtype=torch.float32, device=dev).reshape(-1).expand(len(sizes))
+    chunk = 1 << 18
+    for r0 in range(0, n_rows, chunk):
+        u = row_utt[r0:r0 + chunk]
+        feats[r0:r0 + len(u)] = P[lab_d[u]] + sig_d[u, None] * torch.randn(len(u), 768, device=dev, generator=gen)
+    st = PKG.data.FeatureStore.__new__(PKG.data.FeatureStore)
+    st.feats = feats
+    st._init_index(dev, sizes, offsets, labels)
+    return st
+
+
+def mixed_corpora(P, dev, seed, snr_db, t_min=100, t_max=300):
+    """Clean and noisy unions of synthetic IEMOCAP + CASIA + EMODB stores (fused-loader ready),
+    with the per-corpus fold metadata: returns (clean, noisy, starts, meta)."""
+    rs = np.random.RandomState(seed)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(seed)
+    Pd = P.to(dev)
+    cleans, noisys, meta = [], [], {}
+    for name in ("iemocap", "casia", "emodb"):
+        c = CORPORA[name]
+        if name == "iemocap":
+            sess = np.concatenate([np.full(n, k + 1) for k, n in enumerate(c["sessions"])])
+            n = len(sess)
+            meta[name] = sess
+        elif name == "casia":
+            n = c["n"]
+            meta[name] = np.array(c["speakers"])[np.arange(n) % 4]
+        else:
+            n = c["n"]
+            meta[name] = np.array(["emodb_spk_" + s for s in PKG.data.EMODB_SPEAKERS])[np.arange(n) % 10]
+        labels = rs.permutation(np.arange(n) % 4)
+        sizes = rs.randint(t_min, t_max + 1, size=n)
+        sig_n = (0.5 + 10 ** (-snr_db / 20)) * rs.uniform(0.5, 2.5, size=n)
+        cleans.append(_synthetic_store(Pd, labels, sizes, np.full(n, 0.5), dev, gen))
+        noisys.append(_synthetic_store(Pd, labels, sizes, sig_n, dev, gen))
+    clean, starts = PKG.data.FeatureStore.concat(cleans)
+    noisy, _ = PKG.data.FeatureStore.concat(noisys)
+    del cleans, noisys
+    return clean, noisy, starts, meta
+
+
+def mixed_fold_train(starts, meta, k):
+    """Fold k of the K-fold sweep: the union of IEMOCAP session fold (k mod 5) + 1, CASIA speaker
+    fold k mod 4 and EMODB speaker fold k mod 10 training utterances (data.py fold rules)."""
+    d = PKG.data
+    tr = [d.iemocap_fold_split(meta["iemocap"], k % 5 + 1)[0], d.casia_fold_split(meta["casia"], k % 4)[0],
+          d.emodb_fold_split(meta["emodb"], k % 10)[0]]
+    return np.concatenate([s + t for s, t in zip(starts, tr)])
+
+
+def run_mixed(args, model, dev, rank, world, dist, comm):
+    """BASELINE configs[4]: mixed IEMOCAP+CASIA+EMODB batches, K-fold throughput sweep.  Every
+    step's clean and noisy batches mix utterances of the three corpora (fused store-mode
+    loaders over the unions of the fold's training splits, variable lengths); the DAD config
+    rotates over the three flavours per batch.  One timed segment per fold."""
+    P = init_model_weights(model, seed=0)
+    clean, noisy, starts, meta = mixed_corpora(P, dev, seed=23, snr_db=args.snr)
+    views = [PKG.ConfigView(None, flavor="iemocap"), PKG.ConfigView(None, flavor="casia", USE_DACP=True, USE_ECDA=True),
+             PKG.ConfigView(None, flavor="emodb")]
+    step = PKG.DADStep(model, views[0], precision=args.precision, rng="counter", seed=1000 + rank, comm=comm)
+    B = args.batch
+
+    def batches(store, labeled, seed):
+        g = torch.Generator()
+        g.manual_seed(seed)
+        while True:
+            yield from PKG.data.DeviceLoader(store, batch_size=B, shuffle=True, generator=g, fused=True,
+                                             with_labels=labeled)
+
+    folds, events = [], []
+    n = 0
+    for k in range(args.folds):
+        tr = mixed_fold_train(starts, meta, k)
+        ci = batches(clean.subset(tr), True, 1000 * k + rank)
+        ni = batches(noisy.subset(tr, with_labels=False), False, 1000 * k + 500 + rank)
+
+        def run(nsteps, timed):
+            rows = 0
+            utts = 0
+            nonlocal n
+            for i in range(nsteps):
+                c, nb = next(ci), next(ni)
+                step.view = views[n % 3]
+                n += 1
+                step.kernel_events = events if (timed and i % EVENT_EVERY == 0) else None
+                if timed:
+                    for b in (c, nb):
+                        f = b["net_input"]["feats"]
+                        rows += int(f.store.sizes[f.index].sum())
+                    utts += c["net_input"]["feats"].shape[0]
+                step.step(c, nb, args.epoch)
+            step.kernel_events = None
+            return rows, utts
+        run(args.warmup if k == 0 else 3, False)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        t0 = time.perf_counter()
+        rows, utts = run(args.steps, True)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if dist:
+            t = torch.tensor([el], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+            u = torch.tensor([utts], dtype=torch.float64)
+            dist.all_reduce(u)
+            utts = int(u.item())
+        folds.append({"fold": k, "train_utterances": int(len(tr)), "seconds": el, "utterances": utts,
+                      "value": utts / el, "avg_valid_frames_per_step": rows / args.steps})
+    return step, folds, events
+
+
 def _free_port():
     import socket
     s = socket.socket()
@@ -258,6 +390,9 @@ def main():
     ap.add_argument("--flavor", default="iemocap", choices=["iemocap", "casia", "emodb"])
     ap.add_argument("--force-ecda", action="store_true", help="USE_DACP=USE_ECDA=True (CASIA, BASELINE config 4)")
     ap.add_argument("--snr", type=float, default=5.0, help="SNR (dB) of the synthetic noisy branch")
+    ap.add_argument("--mixed", action="store_true",
+                    help="BASELINE configs[4]: mixed IEMOCAP+CASIA+EMODB batches, K-fold sweep (--folds)")
+    ap.add_argument("--folds", type=int, default=5)
     ap.add_argument("--comm", default="rccl", choices=["rccl", "gloo"],
                     help="gradient all-reduce transport for N > 1 (gloo lets ranks share one GPU)")
     ap.add_argument("--cpu-steps", type=int, default=3)
@@ -301,43 +436,56 @@ def main():
         print("bench.py: the %s transport connected %d ranks, expected %d" % (args.comm, ranks_seen, args.gpus),
               file=sys.stderr)
         sys.exit(3)
-    view = flavor_view(args)
-    step = PKG.DADStep(model, view, precision=args.precision, rng="counter", seed=1000 + rank, comm=comm)
-    data = make_batches(P, N_BATCHES, B, T, seed=17 + rank, device=dev, snr_db=args.snr)
-    torch.cuda.synchronize()
-
-    def run(n, events=None):
-        # encoder-launch events on every EVENT_EVERY-th step of the timed region only: a
-        # timing event pair costs a few microseconds of stream time, which would otherwise
-        # be charged to every step
-        for i in range(n):
-            step.kernel_events = events if (events is not None and i % EVENT_EVERY == 0) else None
-            c, nb = data[i % len(data)]
-            step.step(c, nb, args.epoch)
-        step.kernel_events = None
-
-    run(args.warmup)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
     events = []
-    t0 = time.perf_counter()
-    run(args.steps, events)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    folds = None
+    if args.mixed:
+        step, folds, events = run_mixed(args, model, dev, rank, world, dist, comm)
+        elapsed = sum(f["seconds"] for f in folds)
+        total_utts = sum(f["utterances"] for f in folds)
+        timed_steps = args.steps * args.folds
+        rows_per_step = statistics.mean(f["avg_valid_frames_per_step"] for f in folds)
+        view = step.view
+    else:
+        view = flavor_view(args)
+        step = PKG.DADStep(model, view, precision=args.precision, rng="counter", seed=1000 + rank, comm=comm)
+        data = make_batches(P, N_BATCHES, B, T, seed=17 + rank, device=dev, snr_db=args.snr)
+        torch.cuda.synchronize()
+
+        def run(n, events=None):
+            # encoder-launch events on every EVENT_EVERY-th step of the timed region only: a
+            # timing event pair costs a few microseconds of stream time, which would otherwise
+            # be charged to every step
+            for i in range(n):
+                step.kernel_events = events if (events is not None and i % EVENT_EVERY == 0) else None
+                c, nb = data[i % len(data)]
+                step.step(c, nb, args.epoch)
+            step.kernel_events = None
+
+        run(args.warmup)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        t0 = time.perf_counter()
+        run(args.steps, events)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        if dist:
+            t = torch.tensor([elapsed], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        timed_steps = args.steps
+        total_utts = B * world * args.steps
+        rows_per_step = 2 * B * T
     losses = {k: float(v) for k, v in step.losses().items()}
-    msum = float(step.outputs(B, B)["msum"])
-    ecda_on = float(step.outputs(B, B)["ecda_on"])
+    nbc = step._last_shape
+    msum = float(step.outputs(*nbc)["msum"])
+    ecda_on = float(step.outputs(*nbc)["ecda_on"])
     enc_ms = statistics.mean(a.elapsed_time(b) for a, b in events)
 
     fp32 = None
-    if rank == 0 and world == 1 and args.fp32_steps > 0 and args.precision == "bf16":
+    if rank == 0 and world == 1 and args.fp32_steps > 0 and args.precision == "bf16" and not args.mixed:
         s32 = PKG.DADStep(model, view, precision="fp32", rng="counter", seed=5)
         for i in range(3):
             s32.step(data[i % 4][0], data[i % 4][1], args.epoch)
@@ -349,7 +497,7 @@ def main():
         dt = (time.perf_counter() - t1) / args.fp32_steps
         fp32 = {"value": B / dt, "ms_per_step": dt * 1e3, "dtype": "f32"}
     data_path = None
-    if rank == 0 and world == 1 and not args.no_data_path:
+    if rank == 0 and world == 1 and not args.no_data_path and not args.mixed:
         data_path = data_path_bench(step, B, T, args.epoch, dev)
 
     if rank != 0:
@@ -358,17 +506,22 @@ def main():
         if dist:
             dist.destroy_process_group()
         return
-    ms = elapsed / args.steps * 1e3
-    value = B * world * args.steps / elapsed
-    rows = B * T
-    enc_bytes = 2 * rows * 768 * 4                      # clean + noisy fp32 features, read once
+    ms = elapsed / timed_steps * 1e3
+    value = total_utts / elapsed
+    rows = rows_per_step / 2                            # valid frames per batch (clean = noisy count here)
+    enc_bytes = int(rows_per_step * 768 * 4)            # clean + noisy fp32 features, read once
     enc_gbs = enc_bytes / (enc_ms * 1e-3) / 1e9
     flops = 2 * 768 * 256 * (2 * rows + 3 * rows)       # 5 encoder-sized contractions / step
     peak_tf = BF16_PEAK_TFLOPS if args.precision == "bf16" else FP32_PEAK_TFLOPS
     t_roof = max(flops / (peak_tf * 1e12), enc_bytes / (HBM_PEAK_GBS * 1e9))
     enc_kernel = "dad_encode_ws" if args.precision == "bf16" else "dad_encode_f32"
     traffic, traffic_src = pmc_traffic(enc_kernel)
-    if args.flavor == "iemocap":
+    if args.mixed:
+        workload = ("IEMOCAP+CASIA+EMODB mixed-batch DAD step (configs[4]): batch=%d/GPU of utterances from all three "
+                    "corpora (synthetic stores with each corpus's utterance count and fold structure, %d-%d frames), "
+                    "DAD config rotating IEMOCAP / CASIA (DACP+ECDA) / EMODB per batch, %d-fold sweep, fused "
+                    "store-mode loaders, epoch %d, counter-RNG augmentation" % (B, 100, 300, args.folds, args.epoch))
+    elif args.flavor == "iemocap":
         workload = ("IEMOCAP DAD train step (configs[%d]): batch=64/GPU, T=300x768 synthetic emotion2vec-shaped "
                     "features, post-warm-up epoch %d (CE+KL+ECDA active), counter-RNG augmentation in-kernel"
                     % (1 if world == 1 else 2, args.epoch))
@@ -381,7 +534,7 @@ def main():
         "metric": METRIC, "value": value, "unit": "utterances/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": args.precision, "data": "synthetic",
-        "config": {"workload": workload, "flavor": args.flavor, "snr_db": args.snr,
+        "config": {"workload": workload, "flavor": "mixed" if args.mixed else args.flavor, "snr_db": args.snr,
                    "global_batch": B * world, "per_gpu_batch": B, "seq_len": T, "feature_dim": 768,
                    "parallelism": "dp%d" % world},
         "comm": {"transport": args.comm if world > 1 else None, "ranks_seen": ranks_seen},
@@ -392,6 +545,8 @@ def main():
                           "flops_per_step": flops, "bytes_per_step": enc_bytes, "mfma_peak_tflops": peak_tf},
         "losses_last_step": losses, "mask_sum_last_step": msum, "ecda_on_last_step": ecda_on,
     }
+    if folds is not None:
+        line["folds"] = folds
     if fp32 is not None:
         line["fp32_mode"] = fp32
     if data_path is not None:

@@ -92,6 +92,27 @@ class FeatureStore:
     def __len__(self):
         return len(self.sizes)
 
+    @classmethod
+    def concat(cls, stores):
+        """One store over several (e.g. IEMOCAP + CASIA + EMODB for mixed batches): frames
+        concatenated in HBM (one device copy), offsets shifted, labels kept.  Sample i of
+        stores[k] becomes sample starts[k] + i; returns (store, starts)."""
+        if not stores:
+            raise ValueError("no stores")
+        dev = stores[0].device
+        dtype = stores[0].feats.dtype
+        if any(st.feats.dtype != dtype or st.device != dev for st in stores):
+            raise ValueError("stores must share dtype and device")
+        out = cls.__new__(cls)
+        out.feats = torch.cat([st.feats for st in stores], 0)
+        base = np.cumsum([0] + [st.feats.shape[0] for st in stores])[:-1]
+        starts = np.cumsum([0] + [len(st) for st in stores])
+        labeled = all(st.labels is not None for st in stores)
+        out._init_index(dev, np.concatenate([st.sizes for st in stores]),
+                        np.concatenate([st.offsets + b for st, b in zip(stores, base)]),
+                        np.concatenate([st.labels for st in stores]) if labeled else None)
+        return out, starts[:-1]
+
     def subset(self, indices, with_labels=True):
         """create_subset (I/dataload_noisy.py:193-205, C/dataload_casia_noisy.py:200-224): the
         samples `indices` in that order, sharing this store's rows (no copy)."""
@@ -269,6 +290,28 @@ def load_emotion2vec_dataset(data_path, labels="emo", min_length=3, max_length=N
                     names.append(name)
             offset += n
     return npy, np.asarray(sizes), np.asarray(offsets), (None if ignore_labels else names)
+
+
+def iemocap_fold_split(session_ids, fold_id):
+    """(train, val, test) sample indices of an IEMOCAP session fold (I/dataload_noisy.py:44-65,
+    193-205)."""
+    return _session_subsets(np.asarray(session_ids), fold_id)
+
+
+def casia_fold_split(speakers, fold):
+    """(train, val, test) indices of a CASIA speaker fold (C/dataload_casia_noisy.py:175-182),
+    train in index order (the loaders shuffle)."""
+    spk = np.unique(speakers)
+    test_spk, val_spk = spk[fold % len(spk)], spk[(fold + 1) % len(spk)]
+    tr = np.where(~np.isin(speakers, [test_spk, val_spk]))[0]
+    return tr, np.where(speakers == val_spk)[0], np.where(speakers == test_spk)[0]
+
+
+def emodb_fold_split(speakers, fold):
+    """(train, val, test) indices of an EMODB leave-one-speaker-out fold (E/dataload_emodb_noisy.py:23-47)."""
+    tr_spk, va_spk, te_spk = get_emodb_fold_speakers(fold)
+    ids = np.array([str(s).split("_")[-1] for s in speakers])
+    return np.where(np.isin(ids, tr_spk))[0], np.where(ids == va_spk)[0], np.where(ids == te_spk)[0]
 
 
 def get_session_ids(data_path, num_samples):

@@ -200,6 +200,7 @@ class DADStep:
             b = self._buffers_for(Bc, Bn)
             s.tail, s.emb, s.logits = b["tail"].data_ptr(), b["emb"].data_ptr(), b["logits"].data_ptr()
             self._last = b
+            self._last_shape = (Bc, Bn)
         return s
 
     def _workspace(self, cfg):
