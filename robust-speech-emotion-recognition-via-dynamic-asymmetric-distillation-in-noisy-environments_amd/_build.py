@@ -14,7 +14,7 @@ LIB_DIR = os.path.join(PKG_DIR, "lib")
 OBJ_DIR = os.path.join(PKG_DIR, "build")
 LIB_PATH = os.path.join(LIB_DIR, "libdad_hip.so")
 SOURCES = ["encode.hip", "encode_ws.hip", "tail.hip", "wgrad.hip", "optim.hip", "dad_abi.hip", "rccl_dp.hip", "collate.hip", "eval.hip", "utils_abi.hip"]
-HEADERS = ["dad_common.h", "dad_kernels.h", os.path.join("..", "..", "include", "dad.h")]
+HEADERS = ["dad_common.h", "dad_kernels.h", "dad_probe.h", os.path.join("..", "..", "include", "dad.h")]
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")
 ARCH = os.environ.get("DAD_OFFLOAD_ARCH", "gfx950")

@@ -32,23 +32,26 @@
 
 #include "dad_common.h"
 #include "dad_kernels.h"
+#include "dad_probe.h"
 
-#ifdef DAD_PROBE_STAMPS
-// diagnostic build only (never the product library): per-workgroup wave-0 timeline
-// [start, after prologue, end (100 MHz wall clock), role<<16 | sub-slabs]
-__device__ unsigned long long g_ws_stamps[4096 * 10];
-// [4..9]: wave-0 cycles summed over the loop in: DMA wait, MFMA, convert, epilogue, DMA issue, barrier
-#define WS_CLK() __builtin_amdgcn_s_memtime()
-extern "C" int dad_probe_read_ws_stamps(void* host, int n) {
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ws_stamps), sizeof(unsigned long long) * 10 * n, 0,
-                                  hipMemcpyDeviceToHost);
-}
+// per-workgroup wave-0 timeline of the stamps build (dad_probe.h): [start, after prologue, end
+// (100 MHz wall clock), role<<16 | sub-slabs, then wave-0 cycles summed over the loop in: DMA
+// wait, MFMA, convert, epilogue, DMA issue, barrier]
+DAD_PROBE_BUFFER(ws_stamps, 4096 * 10)
+#define WS_CLK() DAD_PROBE_CLK()
 #define WS_STAMP(k, v) \
-  if (threadIdx.x == 0 && blockIdx.x < 4096) g_ws_stamps[blockIdx.x * 10 + (k)] = (v)
-#else
-#define WS_STAMP(k, v)
-#define WS_CLK() 0ull
-#endif
+  if (threadIdx.x == 0 && blockIdx.x < 4096) DAD_PROBE_SET(ws_stamps, blockIdx.x * 10 + (k), (v))
+#define WS_PHASES(c0, c1, c2, c3, c4, c5)                                                    \
+  do {                                                                                       \
+    const unsigned long long c6_ = WS_CLK();                                                 \
+    if (DAD_PROBE_ON && threadIdx.x == 0 && blockIdx.x < 4096) {                             \
+      const int i_ = blockIdx.x * 10;                                                        \
+      DAD_PROBE_ADD(ws_stamps, i_ + 4, c1 - c0); DAD_PROBE_ADD(ws_stamps, i_ + 5, c2 - c1);  \
+      DAD_PROBE_ADD(ws_stamps, i_ + 6, c3 - c2); DAD_PROBE_ADD(ws_stamps, i_ + 7, c4 - c3);  \
+      DAD_PROBE_ADD(ws_stamps, i_ + 8, c5 - c4); DAD_PROBE_ADD(ws_stamps, i_ + 9, c6_ - c5); \
+    }                                                                                        \
+    (void)c0; (void)c1; (void)c2; (void)c3; (void)c4; (void)c5; (void)c6_;                   \
+  } while (0)
 
 namespace {
 
@@ -513,9 +516,7 @@ __device__ __forceinline__ void ws_loop(const Ctx& C, const int j0, const int Q,
         ws_mfma<S>(H ? tile1 : tile0, aoff, wf, acc);
       } else {
         ws_mfma<S>(H ? tile1 : tile0, aoff, wf, acc);
-#ifdef DAD_PROBE_STAMPS
-        asm volatile("s_nop 0" ::"v"(acc[0]), "v"(acc[S::NT - 1]));
-#endif
+        DAD_PROBE_FENCE2(acc[0], acc[S::NT - 1]);
         c2 = WS_CLK();
         convert(std::integral_constant<int, 1 - H>{}, Jn);
       }
@@ -529,15 +530,7 @@ __device__ __forceinline__ void ws_loop(const Ctx& C, const int j0, const int Q,
     dma(q + 3);
     const unsigned long long c5 = WS_CLK();
     lds_barrier();
-#ifdef DAD_PROBE_STAMPS
-    const unsigned long long c6 = WS_CLK();
-    if (threadIdx.x == 0 && blockIdx.x < 4096) {
-      unsigned long long* g = g_ws_stamps + blockIdx.x * 10;
-      g[4] += c1 - c0; g[5] += c2 - c1; g[6] += c3 - c2; g[7] += c4 - c3; g[8] += c5 - c4; g[9] += c6 - c5;
-    }
-#else
-    (void)c0; (void)c1; (void)c2; (void)c3; (void)c4; (void)c5;
-#endif
+    WS_PHASES(c0, c1, c2, c3, c4, c5);
   };
 #if WS_PRIO == 1
   if (w >= WAVES / 2) __builtin_amdgcn_s_setprio(1);   // the second-dispatched half loses arbitration by age
@@ -561,11 +554,8 @@ __device__ __forceinline__ void ws_loop(const Ctx& C, const int j0, const int Q,
 template <int WAVES, int NOISE>
 __device__ __forceinline__ void encode_ws_body(const DadEncodeArgs& a, char* smem) {
   using S = Shape<WAVES>;
-  WS_STAMP(0, wall_clock64());
-#ifdef DAD_PROBE_STAMPS
-  if (threadIdx.x == 0 && blockIdx.x < 4096)
-    for (int k = 4; k < 10; ++k) g_ws_stamps[blockIdx.x * 10 + k] = 0;
-#endif
+  WS_STAMP(0, DAD_PROBE_WALL());
+  for (int k = 4; DAD_PROBE_ON && k < 10; ++k) WS_STAMP(k, 0);
   const Ctx C = ctx_of(a);
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -605,10 +595,10 @@ __device__ __forceinline__ void encode_ws_body(const DadEncodeArgs& a, char* sme
   for (int t = 0; t < S::NT; ++t) bh[t] = bias[hw + 16 * t + (lane & 15)];
   __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): W1 and bias resident (a wait the compiler sees)
   lds_barrier();                        // fk / vb visible (no DMA in flight yet)
-  WS_STAMP(1, wall_clock64());
+  WS_STAMP(1, DAD_PROBE_WALL());
   if (teacher) ws_loop<WAVES, NOISE, true>(C, j0, 2 * nj, w, lane, smem, sbase, wf, bh, fk, vb);
   else ws_loop<WAVES, NOISE, false>(C, j0, 2 * nj, w, lane, smem, sbase, wf, bh, fk, vb);
-  WS_STAMP(2, wall_clock64());
+  WS_STAMP(2, DAD_PROBE_WALL());
   WS_STAMP(3, ((unsigned long long)teacher << 16) | (unsigned long long)(2 * nj));
 }
 

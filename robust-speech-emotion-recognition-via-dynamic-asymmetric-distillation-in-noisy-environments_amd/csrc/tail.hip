@@ -17,26 +17,17 @@
 
 #include "dad_common.h"
 #include "dad_kernels.h"
+#include "dad_probe.h"
 
-#ifdef DAD_PROBE_STAMPS
-// diagnostic build only: ECDA per-class phase wall clocks (100 MHz), 12 slots per class
-__device__ unsigned long long g_ecda_stamps[DAD_C * 16 + 12];   // 16 per class + tail phases
-extern "C" int dad_probe_read_ecda_stamps(void* host) {
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ecda_stamps), sizeof(g_ecda_stamps), 0, hipMemcpyDeviceToHost);
-}
+// ECDA per-class phase wall clocks (100 MHz) of the stamps build (dad_probe.h): 16 slots per
+// class, then the tail block's phases
+DAD_PROBE_BUFFER(ecda_stamps, DAD_C * 16 + 12)
 #define ECDA_STAMP(k) \
-  if (threadIdx.x == 0) g_ecda_stamps[(gridDim.x > DAD_C ? blockIdx.x - 1 : blockIdx.x) * 16 + (k)] = wall_clock64()
-__device__ __forceinline__ void g_ecda_stamps_n(int c, int n, int ns) {
-  g_ecda_stamps[c * 16 + 10] = (unsigned long long)n;
-  g_ecda_stamps[c * 16 + 11] = (unsigned long long)ns;
-}
+  if (threadIdx.x == 0) DAD_PROBE_SET(ecda_stamps, (gridDim.x > DAD_C ? blockIdx.x - 1 : blockIdx.x) * 16 + (k), DAD_PROBE_WALL())
+#define ECDA_STAMP_SIZES(c, n, ns) \
+  do { DAD_PROBE_SET(ecda_stamps, (c) * 16 + 10, (n)); DAD_PROBE_SET(ecda_stamps, (c) * 16 + 11, (ns)); } while (0)
 #define TAIL_STAMP(k) \
-  if (threadIdx.x == 0) g_ecda_stamps[DAD_C * 16 + (k)] = wall_clock64()
-#else
-#define ECDA_STAMP(k)
-#define TAIL_STAMP(k)
-#define g_ecda_stamps_n(c, n, ns)
-#endif
+  if (threadIdx.x == 0) DAD_PROBE_SET(ecda_stamps, DAD_C * 16 + (k), DAD_PROBE_WALL())
 
 #define TAIL_THREADS DAD_TAIL_THREADS
 
@@ -846,9 +837,6 @@ __device__ __forceinline__ void ecda_block(const DadEcdaArgs& a, const int c, Ec
   __syncthreads();
   ECDA_STAMP(1);
   if (ecda_on == 0.0f) return;   // no row flagged: the ECDA part of dL/de is zero
-#ifdef DAD_PROBE_ECDA_EXIT0
-  return;
-#endif
 
   if (!cfg.class_aware) {
     // global MMD ablation: all clean vs all masked noisy, unit weights (I/utils.py:633-650)
@@ -998,17 +986,10 @@ __device__ __forceinline__ void ecda_block(const DadEcdaArgs& a, const int c, Ec
       D = ST ? S.dm : scratch;
       ecda_stage(S, R, n);
       ECDA_STAMP(6);
-#ifdef DAD_PROBE_ECDA_NOMMD
-      D = nullptr;
-#else
       mmd = ecda_mmd_coef(S, R, n, D);
-#endif
       ECDA_STAMP(7);
     }
     // compactness (I/utils.py:614-616): mean_j ||z_j - mu||^2, grad (2/nt)(z_j - mu)
-#ifdef DAD_PROBE_ECDA_NOGRAD
-    if (false)
-#endif
     ecda_member_grads(S, R, n, D, wscale * att_c, gated[c] ? S.cent[c] : nullptr,
                       wscale * att_c * cfg.ecda_gamma * (2.0f / (float)nt), S.repg, ge_c, ge_s, a.eflag, B, cpart);
   };
@@ -1019,7 +1000,7 @@ __device__ __forceinline__ void ecda_block(const DadEcdaArgs& a, const int c, Ec
   const float comp = ecda_block_sum_f(S, cpart) / (float)nt;
   if (tid == 0) {
     a.tail_terms[c] = att_c * (mmd + cfg.ecda_gamma * comp + cfg.ecda_delta * rep);
-    g_ecda_stamps_n(c, n, ns);
+    ECDA_STAMP_SIZES(c, n, ns);
     a.tail_terms[DAD_T_ECDA_GATE - DAD_T_ECDA_TERM + c] = 1.0f;
   }
 }

@@ -17,6 +17,7 @@
 // scale folded into the A operand (one GEMM, no S_u round trip through HBM).
 #include "dad_common.h"
 #include "dad_kernels.h"
+#include "dad_probe.h"
 
 namespace {
 
@@ -183,21 +184,12 @@ __global__ __launch_bounds__(DAD_WGRAD_THREADS) void dad_wgrad_f32(DadWgradArgs 
 static_assert(WGD_THREADS == 256 * WGD_GROUPS && DAD_H == 256, "dad_wgrad_direct: groups of 256 threads, thread = h");
 static_assert(WGD_GROUPS == 1 || WGD_GROUPS == 2, "dad_wgrad_direct: one or two slab groups");
 static_assert(WGD_DB == 64 && DAD_D % WGD_DB == 0, "dad_wgrad_direct: 8 threads x 8 columns per row");
-#ifdef DAD_PROBE_STAMPS
-// diagnostic build only: per-workgroup cycles of wave 0: [prologue, loop, epilogue, -,
-// sum over rounds of: compute+stage+load, barrier, -, -, rounds]
-__device__ unsigned long long g_wgd_stamps[512 * 10];
-extern "C" int dad_probe_read_wgd_stamps(void* host, int n) {
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wgd_stamps), sizeof(unsigned long long) * 10 * n, 0,
-                                  hipMemcpyDeviceToHost);
-}
-#define WGD_CLK() __builtin_amdgcn_s_memtime()
+// per-workgroup cycles of wave 0 in the stamps build (dad_probe.h): [prologue, loop, epilogue,
+// -, sum over rounds of: compute+stage+load, barrier, -, -, rounds]
+DAD_PROBE_BUFFER(wgd_stamps, 512 * 10)
+#define WGD_CLK() DAD_PROBE_CLK()
 #define WGD_ACC(k, v) \
-  if (threadIdx.x == 0 && blockIdx.x < 512) g_wgd_stamps[blockIdx.x * 10 + (k)] += (v)
-#else
-#define WGD_CLK() 0ull
-#define WGD_ACC(k, v)
-#endif
+  if (threadIdx.x == 0 && blockIdx.x < 512) DAD_PROBE_ADD(wgd_stamps, blockIdx.x * 10 + (k), (v))
 namespace {
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -262,18 +254,10 @@ __device__ __forceinline__ void wgd_load(const DadWgradArgs& a, const WgdTable& 
   const int row = min(tid >> 3, r.nvalid - 1);
   const __bf16* xb = a.xs_bf16 + (size_t)row0 * DAD_D + dbase;
   const uint32_t* mb = a.bits + (size_t)(sfirst + WGD_GROUPS * j) * DAD_H;
-#ifdef DAD_PROBE_WGD_NOMEM
-  // diagnostic build only: no HBM traffic in the slab loop
-  for (int e = 0; e < 8; ++e) r.x[e] = (__bf16)(float)(row0 & 1023);
-  r.mw[0] = (uint32_t)row0 * 2654435761u;
-  r.mw[1] = r.mw[0] >> 3;
-  (void)xb; (void)mb; (void)row;
-#else
   r.x = *reinterpret_cast<const bf16x8*>(xb + row * DAD_D + (tid & 7) * 8);
   // masks of h = 32 (2 wv + m) + lane % 32 (both 32-lane halves load the same words)
 #pragma unroll
   for (int m = 0; m < 2; ++m) r.mw[m] = mb[(2 * wv + m) * 32 + (tid & 31)];
-#endif
 }
 
 __device__ __forceinline__ void wgd_stage(const WgdSlab& r, __bf16* Xt) {
@@ -291,15 +275,10 @@ __device__ __forceinline__ void wgd_stage(const WgdSlab& r, __bf16* Xt) {
 // broadcast, different entries sit on different banks).
 __device__ __forceinline__ uint4 wgd_amask(uint32_t mask, const uint2* lut, int ks) {
   const int lane = threadIdx.x & 63;
-#ifdef DAD_PROBE_WGD_NOAFRAG
-  (void)lut; (void)lane; (void)ks;
-  return uint4{mask, mask >> 1, mask >> 2, mask >> 3};
-#else
   const uint32_t byte = mask >> (16 * ks + 8 * (lane >> 5));
   const uint2 lo = lut[byte & 15u];
   const uint2 hi = lut[(byte >> 4) & 15u];
   return uint4{lo.x, lo.y, hi.x, hi.y};
-#endif
 }
 
 // one slab's operands for one wave: A (G) fragments a[ks][m], B (x) fragments b[ks][n]
@@ -327,12 +306,7 @@ __device__ __forceinline__ WgdRaw wgd_read(const __bf16* Xt, const uint32_t (&mk
   for (int ks = 0; ks < 2; ++ks) {
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
-#ifdef DAD_PROBE_WGD_NOTR
-      // diagnostic build only: B fragments without LDS reads
-      for (int e = 0; e < 8; ++e) w.b[ks][n][e] = __builtin_bit_cast(__bf16, (uint16_t)(mk[n] >> e));
-#else
       w.b[ks][n] = tr_frag(Xt, WGD_XP, 16 * ks, 32 * n);
-#endif
     }
 #pragma unroll
     for (int m = 0; m < 2; ++m) w.am[ks][m] = wgd_amask(mk[m], lut, ks);
@@ -359,12 +333,6 @@ __device__ __forceinline__ WgdFrag wgd_finish(const WgdRaw& w) {
 }
 
 __device__ __forceinline__ void wgd_mma(const WgdFrag& f, f32x16 (&acc)[2][2]) {
-#ifdef DAD_PROBE_WGD_NOMFMA
-  // diagnostic build only: operands fetched, no MFMAs
-  asm volatile("" ::"v"(f.a[0][0]), "v"(f.a[0][1]), "v"(f.a[1][0]), "v"(f.a[1][1]), "v"(f.b[0][0]), "v"(f.b[0][1]),
-               "v"(f.b[1][0]), "v"(f.b[1][1]));
-  (void)acc;
-#elif !defined(DAD_PROBE_WGD_NOCOMP)
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -372,9 +340,6 @@ __device__ __forceinline__ void wgd_mma(const WgdFrag& f, f32x16 (&acc)[2][2]) {
 #pragma unroll
       for (int n = 0; n < 2; ++n)
         acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[ks][m], f.b[ks][n], acc[m][n], 0, 0, 0);
-#else
-  (void)f; (void)acc;
-#endif
 }
 
 __device__ __forceinline__ int wgd_utt(const DadGeom& g, int s) {
@@ -398,10 +363,8 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
   for (int m = 0; m < 2; ++m)
 #pragma unroll
     for (int n = 0; n < 2; ++n) acc[m][n] = f32x16{};
-#ifdef DAD_PROBE_STAMPS
-  if (tid == 0 && blockIdx.x < 512)
-    for (int k = 0; k < 10; ++k) g_wgd_stamps[blockIdx.x * 10 + k] = 0;
-#endif
+  for (int k = 0; DAD_PROBE_ON && k < 10; ++k)
+    if (tid == 0 && blockIdx.x < 512) DAD_PROBE_SET(wgd_stamps, blockIdx.x * 10 + k, 0);
   const unsigned long long t0 = WGD_CLK();
   unsigned long long t1 = t0, t2 = t0;
   if (s0 < s1) {
@@ -705,12 +668,6 @@ __global__ __launch_bounds__(DAD_REDUCE_THREADS) void dad_reduce(DadReduceArgs a
   const int tid = threadIdx.x;
   constexpr int NB = DAD_REDUCE_BLOCKS - DAD_REDUCE_XBLK;
   double sq = 0.0;
-#ifdef DAD_PROBE_RED_NOMAIN
-  if (blockIdx.x < NB) return;     // diagnostic build only
-#endif
-#ifdef DAD_PROBE_RED_NOEXTRA
-  if (blockIdx.x >= NB) return;    // diagnostic build only
-#endif
   if (blockIdx.x < NB) {
     const int col = tid & (DAD_REDUCE_COLS / 4 - 1), kg = tid / (DAD_REDUCE_COLS / 4);
     const size_t e0 = (size_t)blockIdx.x * DAD_REDUCE_COLS + (size_t)col * 4;

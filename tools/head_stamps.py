@@ -26,7 +26,7 @@ def main():
     torch.cuda.synchronize()
     L = PKG.lib()
     ebuf = (ctypes.c_ulonglong * (4 * 16 + 12))()
-    assert L.dad_probe_read_ecda_stamps(ebuf) == 0
+    assert L.dad_probe_read_ecda_stamps(ebuf, len(ebuf)) == 0
     e = np.frombuffer(ebuf, dtype=np.uint64).astype(np.int64)
     t0 = e[64]
     rel = lambda v: (v - t0) / 100.0

@@ -27,7 +27,7 @@ def main():
     L = PKG.lib()
     n = 256
     buf = (ctypes.c_ulonglong * (10 * n))()
-    assert L.dad_probe_read_wgd_stamps(buf, n) == 0
+    assert L.dad_probe_read_wgd_stamps(buf, 10 * n) == 0
     e = np.frombuffer(buf, dtype=np.uint64).astype(np.float64).reshape(n, 10)
     e = e[e[:, 8] > 0]
     m = e.mean(0)

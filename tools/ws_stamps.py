@@ -28,7 +28,7 @@ def main():
     L = PKG.lib()
     n = 256
     buf = (ctypes.c_ulonglong * (10 * n))()
-    assert L.dad_probe_read_ws_stamps(buf, n) == 0
+    assert L.dad_probe_read_ws_stamps(buf, 10 * n) == 0
     st = np.frombuffer(buf, dtype=np.uint64).reshape(n, 10).astype(np.int64)
     st = st[st[:, 0] > 0]
     t0 = st[:, 0].min()
