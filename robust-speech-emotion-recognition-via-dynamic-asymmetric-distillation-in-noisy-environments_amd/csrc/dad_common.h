@@ -171,6 +171,15 @@ __device__ __forceinline__ float keep_value(const uint8_t* keep, uint32_t key, i
 }
 
 
+// LDS-DMA: 16 B per lane of `src` into LDS at lds_dst + 16 * lane (M0 = wave-uniform LDS
+// byte address).  Inline asm: the compiler neither counts it in its vmcnt waits nor drains it
+// at barriers; the caller waits for it (s_waitcnt vmcnt) before reading the LDS bytes.
+__device__ __forceinline__ void dad_glds16(const void* src, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(src), "s"(lds_dst) : "memory");
+}
+
 // ---------------------------------------------------------------------------------
 // wave helpers (wave64).  Sums use DPP (row_shr 1/2/4/8 inside each 16-lane row, then
 // row_bcast:15 / row_bcast:31 across rows; lane 63 ends with the total, broadcast by

@@ -22,7 +22,9 @@
 #define WGD_DB 64
 #define WGD_NDB (DAD_D / WGD_DB)
 #define WGD_MAXU 64
-#define WGD_DEPTH 4
+#ifndef WGD_DEPTH
+#define WGD_DEPTH 4       // slabs whose loads are in flight per group
+#endif
 #define WGD_XP 96
 #ifndef WGD_GROUPS
 #define WGD_GROUPS 2      // slab groups of 4 waves per workgroup (2: two waves per SIMD)

@@ -172,14 +172,6 @@ __device__ __forceinline__ int tstart_of(const Ctx& C, int b) {
   return dad_tstart_at(C.key_tstart, b, C.start_hi);
 }
 
-// LDS-DMA: 16 B per lane of `src` into LDS at lds_dst + 16 * lane (M0 = wave-uniform base).
-// Inline asm: hipcc neither counts it nor drains it at barriers; the kernel counts it.
-__device__ __forceinline__ void glds16(const void* src, uint32_t lds_dst) {
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(src), "s"(lds_dst) : "memory");
-}
-
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
@@ -223,7 +215,7 @@ __device__ __forceinline__ void dma_rows(const float* x, const Job& J, int half,
     const float* src = x + (size_t)(J.src0 + t) * DAD_D + 4 * lane;
     const uint32_t dst = __builtin_amdgcn_readfirstlane(stage_base + (uint32_t)(r * kRawRow));
 #pragma unroll
-    for (int k = 0; k < 3; ++k) glds16(src + 256 * k, dst + 1024u * (uint32_t)k);
+    for (int k = 0; k < 3; ++k) dad_glds16(src + 256 * k, dst + 1024u * (uint32_t)k);
   }
 }
 

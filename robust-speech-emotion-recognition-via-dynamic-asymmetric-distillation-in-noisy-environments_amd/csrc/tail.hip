@@ -21,13 +21,18 @@
 
 // ECDA per-class phase wall clocks (100 MHz) of the stamps build (dad_probe.h): 16 slots per
 // class, then the tail block's phases
-DAD_PROBE_BUFFER(ecda_stamps, DAD_C * 16 + 12)
+#define ECDA_SLOTS 24
+DAD_PROBE_BUFFER(ecda_stamps, DAD_C * ECDA_SLOTS + 16)
 #define ECDA_STAMP(k) \
-  if (threadIdx.x == 0) DAD_PROBE_SET(ecda_stamps, (gridDim.x > DAD_C ? blockIdx.x - 1 : blockIdx.x) * 16 + (k), DAD_PROBE_WALL())
+  if (threadIdx.x == 0) DAD_PROBE_SET(ecda_stamps, (gridDim.x > DAD_C ? blockIdx.x - 1 : blockIdx.x) * ECDA_SLOTS + (k), DAD_PROBE_WALL())
 #define ECDA_STAMP_SIZES(c, n, ns) \
-  do { DAD_PROBE_SET(ecda_stamps, (c) * 16 + 10, (n)); DAD_PROBE_SET(ecda_stamps, (c) * 16 + 11, (ns)); } while (0)
+  do { DAD_PROBE_SET(ecda_stamps, (c) * ECDA_SLOTS + 10, (n)); DAD_PROBE_SET(ecda_stamps, (c) * ECDA_SLOTS + 11, (ns)); } while (0)
 #define TAIL_STAMP(k) \
-  if (threadIdx.x == 0) DAD_PROBE_SET(ecda_stamps, DAD_C * 16 + (k), DAD_PROBE_WALL())
+  if (threadIdx.x == 0) DAD_PROBE_SET(ecda_stamps, DAD_C * ECDA_SLOTS + (k), DAD_PROBE_WALL())
+// shader-clock cycles at the tail block's start / end (slots 12 / 13): with the wall-clock
+// stamps 0 / 1 they give the clock the block ran at
+#define TAIL_CYCLES(k) \
+  if (threadIdx.x == 0) DAD_PROBE_SET(ecda_stamps, DAD_C * ECDA_SLOTS + (k), DAD_PROBE_CLK())
 
 #define TAIL_THREADS DAD_TAIL_THREADS
 
@@ -227,9 +232,11 @@ __device__ __forceinline__ void teacher_certainty(const float (&z)[4], const dad
 // Entry: ncls[] zeroed and ss/sp visible (barrier done by the caller).  Exit: tau_new[] and
 // wc[] valid in all threads.  tf/extras (nullable): the per-step outputs of the tail block.
 // Shared by the tail block and the ECDA blocks of dad_tail_ecda, so both derive the same mask.
+template <int SRT = DAD_MAX_BATCH>
 __device__ __forceinline__ void dacp_thresholds(const dad_config& cfg, int Bn, const float* ss, const int* sp,
-                                                float (*srt)[DAD_MAX_BATCH], int* ncls, const float* dstate,
-                                                float* tau_new, float* wcs, float* tf, float* extras) {
+                                                float (*srt)[SRT], int* ncls, const float* dstate,
+                                                float* tau_new, float* wcs, float* tf, float* extras,
+                                                bool stamp = false) {
   const int tid = threadIdx.x;
   // rank of each score inside its pseudo-label class (ties by index): 16 threads per
   // utterance, each counting a strided share of the others, combined by a 16-lane sum
@@ -242,7 +249,19 @@ __device__ __forceinline__ void dacp_thresholds(const dad_config& cfg, int Bn, c
       if (b < Bn) {
         c = sp[b];
         sv = ss[b];
-        for (int k = part; k < Bn; k += 16) {
+        int k = part;
+        for (; k + 48 < Bn; k += 64) {   // four candidates per LDS round trip
+          float o[4];
+          int pc[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) { o[u] = ss[k + 16 * u]; pc[u] = sp[k + 16 * u]; }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int kk = k + 16 * u;
+            cnt += (pc[u] == c && (o[u] < sv || (o[u] == sv && kk < b))) ? 1 : 0;
+          }
+        }
+        for (; k < Bn; k += 16) {
           const float o = ss[k];
           cnt += (sp[k] == c && (o < sv || (o == sv && k < b))) ? 1 : 0;
         }
@@ -256,6 +275,7 @@ __device__ __forceinline__ void dacp_thresholds(const dad_config& cfg, int Bn, c
     }
   }
   __syncthreads();
+  if (stamp) TAIL_STAMP(8);
   if (tid < DAD_C) {
     const int c = tid;
     const float* Qs = dstate + 4;
@@ -289,10 +309,12 @@ __device__ __forceinline__ void dacp_thresholds(const dad_config& cfg, int Bn, c
     }
   }
   __syncthreads();
+  if (stamp) TAIL_STAMP(9);
 }
 
 __device__ __forceinline__ void tail_block(const DadTailArgs& a, TailSmem& T) {
   TAIL_STAMP(0);
+  TAIL_CYCLES(12);
   const dad_config& cfg = a.cfg;
   const int B = cfg.B;                       // clean utterances
   const int Bn = cfg.warmup ? 0 : cfg.Bn;    // noisy utterances
@@ -364,7 +386,7 @@ __device__ __forceinline__ void tail_block(const DadTailArgs& a, TailSmem& T) {
     TAIL_STAMP(3);
     if (cfg.use_dacp) {
       // ---- DACPManager.calculate_mask (I/utils.py:449-507)
-      dacp_thresholds(cfg, Bn, ss, sp, T.srt, T.ncls, dstate, T.tau_new, wc_unused, tf, extras);
+      dacp_thresholds(cfg, Bn, ss, sp, T.srt, T.ncls, dstate, T.tau_new, wc_unused, tf, extras, true);
       // mask, and the epoch statistics for update_class_quality_scores_epoch
       // (I/utils.py:503-505): per-class score sums and counts, fixed-order block reduction
       for (int b = tid; b < Bn; b += TAIL_THREADS) sm[b] = ss[b] >= T.tau_new[sp[b]] ? 1.0f : 0.0f;
@@ -375,8 +397,10 @@ __device__ __forceinline__ void tail_block(const DadTailArgs& a, TailSmem& T) {
           st4[c] += sp[b] == c ? (double)ss[b] : 0.0;
           ct4[c] += sp[b] == c ? 1.0 : 0.0;
         }
+      TAIL_STAMP(10);
       block_sum4_d(st4, dred4);
       block_sum4_d(ct4, dred4);
+      TAIL_STAMP(11);
       if (tid < DAD_C) {
         extras[4 + tid] = (float)st4[tid];
         extras[8 + tid] = (float)ct4[tid];
@@ -457,6 +481,7 @@ __device__ __forceinline__ void tail_block(const DadTailArgs& a, TailSmem& T) {
   block_sum4_d(b2s, dred4);
   TAIL_STAMP(7);
   if (tid < 4) a.grad[DAD_OFF_B2 + tid] = (float)b2s[tid];
+  TAIL_CYCLES(13);
   TAIL_STAMP(1);
 }
 
@@ -474,15 +499,19 @@ __global__ __launch_bounds__(TAIL_THREADS) void dad_tail(DadTailArgs a) {
 
 #define ECDA_THREADS DAD_ECDA_THREADS
 static_assert(ECDA_THREADS % DAD_H == 0 && ECDA_THREADS >= DAD_H, "ECDA column groups");
-#define ECDA_NZ 80           // members staged in LDS (n <= 80); larger sets read global
+#define ECDA_NZ 80                          // members staged in LDS (n <= 80); larger sets read global
+#define ECDA_NG (ECDA_THREADS / 64)         // row groups (one wave each) of the centroid pass
+#define ECDA_PRE_U 8                        // rows per group held in registers from kernel entry
+#define ECDA_PRE (ECDA_NG * ECDA_PRE_U)     // batches of at most this many rows prefetch every row
 
 struct EcdaSmem {
   float z[ECDA_NZ * DAD_H];       // staged member embeddings (before that: centroid partials)
   float dm[ECDA_NZ * ECDA_NZ];    // pairwise distances, then symmetric MMD coefficients
   int idx[2 * DAD_MAX_BATCH];     // member list: [0,ns) clean rows, [ns,n) noisy rows
   float wt[2 * DAD_MAX_BATCH];    // member weights
+  int pos[2 * ECDA_PRE];          // inverse of idx (prefetch path): clean row b -> [b], noisy row b -> [ECDA_PRE + b]
   float cent[DAD_C][DAD_H];
-  double dred[ECDA_THREADS / 64];
+  double dred[ECDA_THREADS / 64][3];
   float fred[ECDA_THREADS / 64];
   int cnt_clean[DAD_C], cnt_noisy[DAD_C];
   int lab[DAD_MAX_BATCH];         // clean labels
@@ -492,14 +521,24 @@ struct EcdaSmem {
   float repg[DAD_H];              // repulsion grad of this class's noisy members, per hidden unit
 };
 
-__device__ __forceinline__ double ecda_block_sum_d(EcdaSmem& S, double v) {
-  v = dad_wave_sum_d(v);
+// fixed-order block reduction of NV doubles (one barrier pair for all), valid in all threads
+template <int NV>
+__device__ __forceinline__ void ecda_block_sum_d(EcdaSmem& S, double (&v)[NV]) {
+  static_assert(NV <= 3, "dred holds 3 values per wave");
+#pragma unroll
+  for (int k = 0; k < NV; ++k) v[k] = dad_wave_sum_d(v[k]);
   __syncthreads();
-  if ((threadIdx.x & 63) == 0) S.dred[threadIdx.x >> 6] = v;
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int k = 0; k < NV; ++k) S.dred[threadIdx.x >> 6][k] = v[k];
   __syncthreads();
-  double s = 0.0;
-  for (int k = 0; k < ECDA_THREADS / 64; ++k) s += S.dred[k];
-  return s;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    double s = 0.0;
+#pragma unroll
+    for (int w = 0; w < ECDA_THREADS / 64; ++w) s += S.dred[w][k];
+    v[k] = s;
+  }
 }
 
 __device__ __forceinline__ float ecda_block_sum_f(EcdaSmem& S, float v) {
@@ -508,30 +547,36 @@ __device__ __forceinline__ float ecda_block_sum_f(EcdaSmem& S, float v) {
   if ((threadIdx.x & 63) == 0) S.fred[threadIdx.x >> 6] = v;
   __syncthreads();
   float s = 0.0f;
+#pragma unroll
   for (int k = 0; k < ECDA_THREADS / 64; ++k) s += S.fred[k];
   return s;
 }
 
 // Ordered block-wide compaction: appends every i in [0, n) with flag(i) to S.idx (and
-// weight(i) to S.wt) after position `base`, in ascending i.  Returns the new length.
+// weight(i) to S.wt) after position `base`, in ascending i; inv (nullable) gets i's position.
+// Returns the new length.
 template <typename Flag, typename Wgt>
-__device__ int ecda_compact(EcdaSmem& S, int n, int base, Flag flag, Wgt weight) {
+__device__ int ecda_compact(EcdaSmem& S, int n, int base, Flag flag, Wgt weight, int* inv) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   for (int c0 = 0; c0 < n; c0 += ECDA_THREADS) {
     const int i = c0 + tid;
     const bool f = i < n && flag(i);
+    const float wi = f ? weight(i) : 0.0f;   // in flight across the barrier
     const uint64_t bal = __ballot(f);
     if (lane == 0) S.wcount[w] = __popcll(bal);
     __syncthreads();
     int pre = 0, tot = 0;
+#pragma unroll
     for (int k = 0; k < ECDA_THREADS / 64; ++k) {
-      if (k < w) pre += S.wcount[k];
-      tot += S.wcount[k];
+      const int ck = S.wcount[k];
+      pre += k < w ? ck : 0;
+      tot += ck;
     }
     if (f) {
       const int pos = base + pre + __popcll(bal & ((1ull << lane) - 1ull));
       S.idx[pos] = i;
-      S.wt[pos] = weight(i);
+      S.wt[pos] = wi;
+      if (inv) inv[i] = pos;
     }
     base += tot;
     __syncthreads();
@@ -554,48 +599,89 @@ struct EcdaRows {
   }
 };
 
-template <bool STAGED>
-__device__ __forceinline__ void ecda_stage(EcdaSmem& S, const EcdaRows<STAGED>& R, int n) {
-  if constexpr (STAGED) {
+// staging from global rows (no prefetch: batches above ECDA_PRE rows)
+__device__ __forceinline__ void ecda_stage_global(EcdaSmem& S, const float* emb_c, const float* emb_s, int ns, int n) {
 #pragma unroll 4
-    for (int k = threadIdx.x; k < n * (DAD_H / 4); k += ECDA_THREADS) {
-      const int a = k / (DAD_H / 4), q = k - a * (DAD_H / 4);
-      const float* src = (a < R.ns ? R.emb_c : R.emb_s) + (size_t)S.idx[a] * DAD_H;
-      reinterpret_cast<f32x4*>(S.z)[k] = reinterpret_cast<const f32x4*>(src)[q];
-    }
+  for (int k = threadIdx.x; k < n * (DAD_H / 4); k += ECDA_THREADS) {
+    const int a = k / (DAD_H / 4), q = k - a * (DAD_H / 4);
+    const float* src = (a < ns ? emb_c : emb_s) + (size_t)S.idx[a] * DAD_H;
+    reinterpret_cast<f32x4*>(S.z)[k] = reinterpret_cast<const f32x4*>(src)[q];
   }
   __syncthreads();
+}
+
+// upper-triangle index t of an m x m matrix (row-major, diagonal included) -> (i, j), i <= j
+__device__ __forceinline__ void ecda_tri(int t, int m, int& i, int& j) {
+  const float b = 2.0f * (float)m + 1.0f;
+  int r = (int)((b - sqrtf(fmaxf(b * b - 8.0f * (float)t, 0.0f))) * 0.5f);
+  r = r < 0 ? 0 : (r >= m ? m - 1 : r);
+  while (r > 0 && r * m - r * (r - 1) / 2 > t) --r;               // float rounding fix-ups
+  while (r + 1 < m && (r + 1) * m - (r + 1) * r / 2 <= t) ++r;
+  i = r;
+  j = t - (r * m - r * (r - 1) / 2) + r;
+}
+
+// recursive-halving reduce-scatter of 16 per-lane values over KS adjacent slice lanes (KS <= 16):
+// afterwards lane sl holds in v[0 .. 16/KS) the slice sums of values [base, base + 16/KS),
+// base returned.  Every value is summed by the same tree over the slices (up to operand order
+// of each add, which is commutative), so equal inputs give bit-equal sums in any lane.
+template <int O, int M>
+__device__ __forceinline__ void ecda_rs_level(float (&v)[16], int sl, int& base) {
+  if constexpr (O > 0) {
+    constexpr int HALF = M / 2;
+    const bool up = (sl & O) != 0;
+#pragma unroll
+    for (int t = 0; t < HALF; ++t) {
+      const float send = up ? v[t] : v[HALF + t];
+      const float keep = up ? v[HALF + t] : v[t];
+      v[t] = keep + __shfl_xor(send, O, 64);
+    }
+    base += up ? HALF : 0;
+    ecda_rs_level<O / 2, HALF>(v, sl, base);
+  }
+}
+template <int KS>
+__device__ __forceinline__ int ecda_reduce_scatter(float (&v)[16], int sl) {
+  int base = 0;
+  ecda_rs_level<KS / 2, 16>(v, sl, base);
+  return base;
 }
 
 // mmd = t_ss + t_tt - 2 t_st of _gaussian_kernel (I/utils.py:521-563) over members
 // [0, ns) (clean embeddings) and [ns, n) (strong embeddings).  Leaves the symmetric
 // coefficient matrix Csym = dmmd/dD + (dmmd/dD)^T in D, so that
 // dmmd/dz_i = 2 sum_j Csym_ij (z_i - z_j).  Returns mmd (valid in all threads).
-template <bool STAGED>
-__device__ __forceinline__ float ecda_mmd_coef(EcdaSmem& S, const EcdaRows<STAGED>& R, int n, float* D) {
+template <class RW>
+__device__ __forceinline__ float ecda_mmd_coef(EcdaSmem& S, const RW& R, int n, float* D) {
   const int tid = threadIdx.x;
   const int ns = R.ns;
-  // pairwise squared distances (I/utils.py:533-537), register-tiled: a work item is a 4x4
-  // block of member pairs over one slice of the 256 hidden units (ks slices per block, a
-  // power of two <= 16, as many as keep the workgroup busy).  Per float4 step a lane loads
-  // 8 rows' values and does 16 pairs' differences: 4x the arithmetic per LDS byte of a
-  // pair-per-lane loop.  The slice lanes of a block are adjacent and combined by a fixed
-  // butterfly; (i, j) and (j, i) run the same per-element order and the same butterfly
-  // (the slice rotation depends on bi + bj), so D stays exactly symmetric.
-  const int nb = (n + 3) >> 2, nblk = nb * nb;
-  int lks = 0;
-  while (lks < 4 && (2 << lks) * nblk <= ECDA_THREADS) ++lks;
+  // pairwise squared distances (I/utils.py:533-537), register-tiled over the upper triangle:
+  // a work item is a 4x4 block (bi <= bj) of member pairs over one slice of the 256 hidden
+  // units.  Per float4 step a lane loads 8 rows' values and does 16 pairs' differences.  The
+  // slices per block (ks, a power of two) are chosen for the least per-SIMD time given the
+  // round-robin wave placement; the slice lanes of a block are adjacent and combined by a
+  // fixed butterfly.  Each block writes D[i][j] and D[j][i] from one value, and a diagonal
+  // block computes (p, r) and (r, p) from exactly negated differences, so D is symmetric.
+  const int nb = (n + 3) >> 2, nblk = nb * (nb + 1) / 2;
+  // slices per block: least per-SIMD time, in units of 1/32 float4 step (a step: 8 row loads
+  // and 64 packed VALU ops per lane; a reduce-scatter shuffle ~1/32 of that; 1/2 step setup)
+  int lks = 0, best = 1 << 30;
+  for (int l = 0; l <= 4; ++l) {
+    const int waves = ((nblk << l) + 63) >> 6;
+    const int cost = ((waves + 3) >> 2) * (((DAD_H / 4) >> l) * 32 + (16 - (16 >> l)) + 16);
+    if (cost < best) { best = cost; lks = l; }
+  }
   const int ks = 1 << lks, qs = (DAD_H / 4) >> lks;   // slices per block, float4 steps per slice
   const int nitem = nblk << lks;
   double part = 0.0;
   for (int it0 = 0; it0 < nitem; it0 += ECDA_THREADS) {   // uniform trip count: every lane shuffles
     const int item = it0 + tid;
     const bool on = item < nitem;
-    const int blk = on ? item >> lks : 0, sl = item & (ks - 1);
-    const int bi = blk / nb, bj = blk - bi * nb;
+    const int sl = item & (ks - 1);
+    int bi = 0, bj = 0;
+    if (on) ecda_tri(item >> lks, nb, bi, bj);
     // packed accumulators: (sum over even dims, sum over odd dims) of each pair, so the
-    // squares accumulate by v_pk_fma_f32 (half the VALU issues of scalar FMAs); (i, j) and
-    // (j, i) see exactly negated differences, hence identical squares and sums
+    // squares accumulate by v_pk_fma_f32 (half the VALU issues of scalar FMAs)
     f32x2 acc2[4][4];
 #pragma unroll
     for (int p = 0; p < 4; ++p)
@@ -629,82 +715,98 @@ __device__ __forceinline__ float ecda_mmd_coef(EcdaSmem& S, const EcdaRows<STAGE
           }
       }
     }
-    float acc[4][4];
+    float v[16];
 #pragma unroll
     for (int p = 0; p < 4; ++p)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc[p][r] = acc2[p][r][0] + acc2[p][r][1];
-    for (int o = ks >> 1; o > 0; o >>= 1)
+      for (int r = 0; r < 4; ++r) v[4 * p + r] = acc2[p][r][0] + acc2[p][r][1];
+    // combine the slices: lane sl ends with pairs [base, base + 16/ks) of the block
+    int base = 0;
+    switch (lks) {
+      case 0: break;
+      case 1: base = ecda_reduce_scatter<2>(v, sl); break;
+      case 2: base = ecda_reduce_scatter<4>(v, sl); break;
+      case 3: base = ecda_reduce_scatter<8>(v, sl); break;
+      default: base = ecda_reduce_scatter<16>(v, sl); break;
+    }
+    if (on) {
+      const int m = 16 >> lks;
 #pragma unroll
-      for (int p = 0; p < 4; ++p)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[p][r] += __shfl_xor(acc[p][r], o, 64);
-    if (on && sl == 0) {
-#pragma unroll
-      for (int p = 0; p < 4; ++p)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int i = 4 * bi + p, j = 4 * bj + r;
-          if (i < n && j < n) {
-            const float d = i == j ? 0.0f : acc[p][r];
-            D[i * n + j] = d;
-            part += d;
-          }
+      for (int t = 0; t < 16; ++t) {
+        if (t >= m) break;
+        const int k = base + t, p = k >> 2, r = k & 3;
+        const int i = 4 * bi + p, j = 4 * bj + r;
+        if (i < n && j < n && (bi < bj || p <= r)) {
+          const float d = i == j ? 0.0f : v[t];
+          D[i * n + j] = d;
+          D[j * n + i] = d;
+          part += i == j ? 0.0 : 2.0 * (double)d;
         }
+      }
     }
   }
   ECDA_STAMP(12);
-  const double sumD = ecda_block_sum_d(S, part);
+  double sd[1] = {part};
+  ecda_block_sum_d<1>(S, sd);
   ECDA_STAMP(13);
   // detached bandwidth (I/utils.py:540-544): sum(D)/(n^2-n) / mul^(num//2), x mul^i
-  float bw = (n > 1) ? (float)(sumD / (double)(n * n - n)) : 1.0f;
+  float bw = (n > 1) ? (float)(sd[0] / (double)(n * n - n)) : 1.0f;
   bw = bw / 4.0f;
-  float bws[5];
   float ibw[5];   // reciprocals: one division per bandwidth instead of ten per pair
-  for (int m = 0; m < 5; ++m) {
-    bws[m] = bw * (float)(1 << m) + 1e-8f;
-    ibw[m] = 1.0f / bws[m];
-  }
+#pragma unroll
+  for (int m = 0; m < 5; ++m) ibw[m] = 1.0f / (bw * (float)(1 << m) + 1e-8f);
   // weight normalisers (I/utils.py:552-557)
   double wsum_t = 0.0;
-  for (int a = ns; a < n; ++a) wsum_t += S.wt[a];
+  {
+    int a = ns;
+    for (; a + 8 <= n; a += 8) {   // eight weights per LDS round trip, summed in index order
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = S.wt[a + u];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) wsum_t += v[u];
+    }
+    for (; a < n; ++a) wsum_t += S.wt[a];
+  }
   const float Wss = (float)ns * (float)ns + 1e-8f;
   const float Wtt = (float)(wsum_t * wsum_t) + 1e-8f;
   const float Wst = (float)((double)ns * wsum_t) + 1e-8f;
-  // terms and coefficients C_ij = dmmd/dK_ij * dK_ij/dD_ij (stored over D)
-  double tss = 0.0, ttt = 0.0, tst = 0.0;
-  for (int p = tid; p < n * n; p += ECDA_THREADS) {
-    const int i = p / n, j = p - i * n;
-    const float d = D[p];
+  // terms and the symmetric coefficients Csym_ij = C_ij + C_ji, C = dmmd/dK * dK/dD, one
+  // unordered pair per work item (K and dK computed once for (i, j) and (j, i))
+  double t3[3] = {0.0, 0.0, 0.0};   // t_ss, t_tt, t_st numerators
+  const int npair = n * (n + 1) / 2;
+  for (int t = tid; t < npair; t += ECDA_THREADS) {
+    int i, j;
+    ecda_tri(t, n, i, j);
+    const float d = D[i * n + j];
     float K = 0.0f, dK = 0.0f;
+#pragma unroll
     for (int m = 0; m < 5; ++m) {
       const float e = __expf(-d * ibw[m]);
       K += e;
       dK -= e * ibw[m];
     }
-    float coef;
-    if (i < ns && j < ns) { tss += K; coef = 1.0f / Wss; }
-    else if (i >= ns && j >= ns) { const float ww = S.wt[i] * S.wt[j]; ttt += (double)K * ww; coef = ww / Wtt; }
-    else if (i < ns) { tst += (double)K * S.wt[j]; coef = -2.0f * S.wt[j] / Wst; }
-    else coef = 0.0f;   // the T x S block is not used by t_st
-    D[p] = coef * dK;
+    const double mult = i == j ? 1.0 : 2.0;   // (i, j) and (j, i) of the sums
+    float cs;
+    if (j < ns) {                               // both clean
+      t3[0] += mult * (double)K;
+      cs = (i == j ? 1.0f : 2.0f) / Wss;
+    } else if (i >= ns) {                       // both noisy
+      const float ww = S.wt[i] * S.wt[j];
+      t3[1] += mult * ((double)K * ww);
+      cs = (i == j ? 1.0f : 2.0f) * ww / Wtt;
+    } else {                                    // (i, j) in S x T; (j, i) in T x S is unused by t_st
+      t3[2] += (double)K * S.wt[j];
+      cs = -2.0f * S.wt[j] / Wst;
+    }
+    const float v = cs * dK;
+    D[i * n + j] = v;
+    D[j * n + i] = v;
   }
   ECDA_STAMP(14);
-  tss = ecda_block_sum_d(S, tss);
-  ttt = ecda_block_sum_d(S, ttt);
-  tst = ecda_block_sum_d(S, tst);
-  const float mmd = (float)(tss / Wss + ttt / Wtt - 2.0 * (tst / Wst));
+  ecda_block_sum_d<3>(S, t3);   // its barriers also publish D
+  const float mmd = (float)(t3[0] / Wss + t3[1] / Wtt - 2.0 * (t3[2] / Wst));
   ECDA_STAMP(15);
-  // symmetrise in place (each unordered pair owned by one thread)
-  for (int p = tid; p < n * n; p += ECDA_THREADS) {
-    const int i = p / n, j = p - i * n;
-    if (i < j) {
-      const float v = D[i * n + j] + D[j * n + i];
-      D[i * n + j] = v;
-      D[j * n + i] = v;
-    }
-  }
-  __syncthreads();
   return mmd;
 }
 
@@ -714,8 +816,8 @@ __device__ __forceinline__ float ecda_mmd_coef(EcdaSmem& S, const EcdaRows<STAGE
 //   g = mmd_scale * 2 sum_j Csym_ij (z_i - z_j)            (all members, if D)
 //     + comp_scale * (z_i - mu_c) + repg                     (noisy members)
 // comp_part accumulates sum ||z_i - mu_c||^2 over noisy members (when cent).
-template <bool STAGED>
-__device__ __forceinline__ void ecda_member_grads(EcdaSmem& S, const EcdaRows<STAGED>& R, int n, const float* D,
+template <class RW>
+__device__ __forceinline__ void ecda_member_grads(EcdaSmem& S, const RW& R, int n, const float* D,
                                                   float mmd_scale, const float* cent, float comp_scale,
                                                   const float* repg, float* ge_c, float* ge_s, uint32_t* eflag,
                                                   int B_, float& comp_part) {
@@ -732,10 +834,27 @@ __device__ __forceinline__ void ecda_member_grads(EcdaSmem& S, const EcdaRows<ST
       acc[p] = f32x4{};
     }
     if (D) {
-      for (int j = 0; j < n; ++j) {
+      // four members j per round: every LDS read of the round issued before its FMAs
+      int j = 0;
+      for (; j + 4 <= n; j += 4) {
+        f32x4 zj[4];
+        float cj[4][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          zj[u] = reinterpret_cast<const f32x4*>(R.row(j + u))[hq];
+#pragma unroll
+          for (int p = 0; p < 4; ++p) cj[u][p] = D[(j + u) * n + m[p]];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int p = 0; p < 4; ++p)   // Csym[j][i] = Csym[i][j]; packed sub + packed FMA
+            acc[p] = __builtin_elementwise_fma(f32x4{cj[u][p], cj[u][p], cj[u][p], cj[u][p]}, zi[p] - zj[u], acc[p]);
+      }
+      for (; j < n; ++j) {
         const f32x4 zj = reinterpret_cast<const f32x4*>(R.row(j))[hq];
 #pragma unroll
-        for (int p = 0; p < 4; ++p) {   // Csym[j][i] = Csym[i][j]; packed sub + packed FMA
+        for (int p = 0; p < 4; ++p) {
           const float cji = D[j * n + m[p]];
           acc[p] = __builtin_elementwise_fma(f32x4{cji, cji, cji, cji}, zi[p] - zj, acc[p]);
         }
@@ -772,12 +891,16 @@ struct EcdaPrefix {
 // One class of ECDA.  FUSED: the DACP mask, scores and class weights are derived here from
 // the teacher logits by the same code as the tail block (teacher_certainty, dacp_thresholds),
 // instead of being read back from the tail's outputs.
+// Batches of at most ECDA_PRE rows per side load every embedding row into registers at entry
+// (wave g holds rows g, g + 8, ... of column chunk lane), in flight during the metadata phase;
+// the centroid pass and the member staging then need no global round trip.
 template <bool FUSED>
 __device__ __forceinline__ void ecda_block(const DadEcdaArgs& a, const int c, EcdaSmem& S, float (&pdist)[DAD_C][DAD_C],
                                            const DadTailArgs* ta, EcdaPrefix& P) {
   const dad_config& cfg = a.cfg;
   const int B = cfg.B, Bn = cfg.Bn;
   const int tid = threadIdx.x;
+  const int g = tid >> 6, lq = tid & 63;
   const float* tf = a.tailf;
   ECDA_STAMP(0);
   const float* emb_c = a.emb;
@@ -788,13 +911,23 @@ __device__ __forceinline__ void ecda_block(const DadEcdaArgs& a, const int c, Ec
   const float wscale = cfg.w_ecda;
   float ecda_on;
   const float* w;   // DACP class weights
-  if constexpr (FUSED) {
-    // every global input up front: teacher logits, DACP state, clean labels
-    const float* z1 = ta->logits + (size_t)B * DAD_C;
+  const bool pre = B <= ECDA_PRE && Bn <= ECDA_PRE;
+  f32x4 pc[ECDA_PRE_U], ps[ECDA_PRE_U];
+  if (FUSED) {
+    // teacher logits first: the DACP prefix waits on them
     f32x4 zt = f32x4{};
+    const float* z1 = ta->logits + (size_t)B * DAD_C;
     if (tid < Bn) zt = reinterpret_cast<const f32x4*>(z1)[tid];
     if (tid >= ECDA_THREADS - 20) P.dstate[tid - (ECDA_THREADS - 20)] = ta->dacp[tid - (ECDA_THREADS - 20)];
     for (int b = tid; b < B; b += ECDA_THREADS) S.lab[b] = (int)a.yc[b];
+    if (pre) {
+#pragma unroll
+      for (int u = 0; u < ECDA_PRE_U; ++u) {
+        const int b = g + ECDA_NG * u;
+        pc[u] = b < B ? reinterpret_cast<const f32x4*>(emb_c + (size_t)b * DAD_H)[lq] : f32x4{};
+        ps[u] = b < Bn ? reinterpret_cast<const f32x4*>(emb_s + (size_t)b * DAD_H)[lq] : f32x4{};
+      }
+    }
     for (int b = tid; b < Bn; b += ECDA_THREADS) {
       float z[4], q[4], sc;
       int pred;
@@ -832,27 +965,61 @@ __device__ __forceinline__ void ecda_block(const DadEcdaArgs& a, const int c, Ec
       S.prd[b] = mask[b] > 0.0f ? (int)predf[b] : -1;   // noisy_mask>thr re-cast: I/utils.py:573-576
       S.scr[b] = score[b];
     }
+    if (pre) {
+#pragma unroll
+      for (int u = 0; u < ECDA_PRE_U; ++u) {
+        const int b = g + ECDA_NG * u;
+        pc[u] = b < B ? reinterpret_cast<const f32x4*>(emb_c + (size_t)b * DAD_H)[lq] : f32x4{};
+        ps[u] = b < Bn ? reinterpret_cast<const f32x4*>(emb_s + (size_t)b * DAD_H)[lq] : f32x4{};
+      }
+    }
     if (tid < DAD_C) { S.cnt_clean[tid] = 0; S.cnt_noisy[tid] = 0; }
   }
   __syncthreads();
   ECDA_STAMP(1);
   if (ecda_on == 0.0f) return;   // no row flagged: the ECDA part of dL/de is zero
 
+  // member rows into S.z at their compacted positions: from the registers (prefetch), or
+  // from global rows through S.idx
+  auto stage = [&](int ns, int n) {
+    ECDA_STAMP(19);
+    if (pre) {
+      // every position read before the first store (one LDS round trip); -1: not a member
+      int pcl[ECDA_PRE_U], pno[ECDA_PRE_U];
+#pragma unroll
+      for (int u = 0; u < ECDA_PRE_U; ++u) {
+        const int b = g + ECDA_NG * u;   // < ECDA_PRE: S.pos rows past B / Bn stay -1
+        pcl[u] = S.pos[b];
+        pno[u] = S.pos[ECDA_PRE + b];
+      }
+#pragma unroll
+      for (int u = 0; u < ECDA_PRE_U; ++u) {
+        if (pcl[u] >= 0) reinterpret_cast<f32x4*>(&S.z[pcl[u] * DAD_H])[lq] = pc[u];
+        if (pno[u] >= 0) reinterpret_cast<f32x4*>(&S.z[pno[u] * DAD_H])[lq] = ps[u];
+      }
+      __syncthreads();
+    } else {
+      ecda_stage_global(S, emb_c, emb_s, ns, n);
+    }
+  };
+  int* inv = pre ? S.pos : nullptr;
+
   if (!cfg.class_aware) {
     // global MMD ablation: all clean vs all masked noisy, unit weights (I/utils.py:633-650)
     if (c != 0) return;
     if (tid < DAD_H) S.repg[tid] = 0.0f;   // no repulsion term (read after the compaction's barriers)
-    int n = ecda_compact(S, B, 0, [](int) { return true; }, [](int) { return 1.0f; });
+    if (pre && tid < 2 * ECDA_PRE) S.pos[tid] = -1;
+    int n = ecda_compact(S, B, 0, [](int) { return true; }, [](int) { return 1.0f; }, inv);
     const int ns = n;
-    n = ecda_compact(S, Bn, n, [&](int i) { return S.prd[i] >= 0; }, [](int) { return 1.0f; });
+    n = ecda_compact(S, Bn, n, [&](int i) { return S.prd[i] >= 0; }, [](int) { return 1.0f; },
+                     inv ? inv + ECDA_PRE : nullptr);
     const int nt = n - ns;
-    const bool gate = ns >= 2 && nt >= 2;
-    if (gate) {
+    if (ns >= 2 && nt >= 2) {
       auto run = [&](auto staged_tag) {
         constexpr bool ST = decltype(staged_tag)::value;
         const EcdaRows<ST> R{emb_c, emb_s, S, ns};
         float* D = ST ? S.dm : scratch;
-        ecda_stage(S, R, n);
+        if constexpr (ST) stage(ns, n);
         const float mmd = ecda_mmd_coef(S, R, n, D);
         float unused = 0.0f;
         ecda_member_grads(S, R, n, D, wscale, nullptr, 0.0f, S.repg, ge_c, ge_s, a.eflag, B, unused);
@@ -872,48 +1039,74 @@ __device__ __forceinline__ void ecda_block(const DadEcdaArgs& a, const int c, Ec
     if (S.lab[b] >= 0 && S.lab[b] < ncls) atomicAdd(&S.cnt_clean[S.lab[b]], 1);
   for (int b = tid; b < Bn; b += ECDA_THREADS)
     if (S.prd[b] >= 0 && S.prd[b] < ncls) atomicAdd(&S.cnt_noisy[S.prd[b]], 1);
-  // noisy centroids of every class (needed for the repulsion term): four utterance groups
-  // x 64 float4 columns, all loads of a group in flight, partials combined in fixed order
+  if (pre && tid < 2 * ECDA_PRE) S.pos[tid] = -1;
+  ECDA_STAMP(16);
+  // noisy centroids of every class (needed for the repulsion term): row group g (one wave) x
+  // 64 float4 columns, partials combined in fixed group order
   {
     float* part = S.z;   // [NG groups][C][H], before the members are staged
-    constexpr int NG = ECDA_THREADS / 64;
-    static_assert(NG * DAD_C * DAD_H <= ECDA_NZ * DAD_H, "centroid partials must fit in S.z");
-    const int g = tid >> 6, q = tid & 63;
+    static_assert(ECDA_NG * DAD_C * DAD_H <= ECDA_NZ * DAD_H, "centroid partials must fit in S.z");
     f32x4 cs[DAD_C];
 #pragma unroll
     for (int k = 0; k < DAD_C; ++k) cs[k] = f32x4{};
+    if (pre) {
+      int pk[ECDA_PRE_U];
+#pragma unroll
+      for (int u = 0; u < ECDA_PRE_U; ++u) {   // all pseudo-labels first (one LDS round trip)
+        const int b = g + ECDA_NG * u;
+        pk[u] = S.prd[b < Bn ? b : 0];
+        pk[u] = b < Bn ? pk[u] : -1;
+      }
+#pragma unroll
+      for (int u = 0; u < ECDA_PRE_U; ++u)
+#pragma unroll
+        for (int k = 0; k < DAD_C; ++k) cs[k] += pk[u] == k ? ps[u] : f32x4{};
+    } else {
 #pragma unroll 4
-    for (int b = g; b < Bn; b += NG) {
-      const int pk = S.prd[b];
-      const f32x4 e = reinterpret_cast<const f32x4*>(emb_s + (size_t)b * DAD_H)[q];
+      for (int b = g; b < Bn; b += ECDA_NG) {
+        const int pk = S.prd[b];
+        const f32x4 e = reinterpret_cast<const f32x4*>(emb_s + (size_t)b * DAD_H)[lq];
 #pragma unroll
-      for (int k = 0; k < DAD_C; ++k) cs[k] += pk == k ? e : f32x4{};
+        for (int k = 0; k < DAD_C; ++k) cs[k] += pk == k ? e : f32x4{};
+      }
     }
+    ECDA_STAMP(17);
 #pragma unroll
-    for (int k = 0; k < DAD_C; ++k) reinterpret_cast<f32x4*>(part + (g * DAD_C + k) * DAD_H)[q] = cs[k];
+    for (int k = 0; k < DAD_C; ++k) reinterpret_cast<f32x4*>(part + (g * DAD_C + k) * DAD_H)[lq] = cs[k];
     __syncthreads();
+    ECDA_STAMP(18);
     for (int e = tid; e < DAD_C * DAD_H; e += ECDA_THREADS) {
       const int k = e / DAD_H, hh = e & (DAD_H - 1);
       float sk = 0.0f;
 #pragma unroll
-      for (int gg = 0; gg < NG; ++gg) sk += part[(gg * DAD_C + k) * DAD_H + hh];
+      for (int gg = 0; gg < ECDA_NG; ++gg) sk += part[(gg * DAD_C + k) * DAD_H + hh];
       S.cent[k][hh] = S.cnt_noisy[k] > 0 ? sk / (float)S.cnt_noisy[k] : 0.0f;
     }
   }
   __syncthreads();
   ECDA_STAMP(2);
+  // per-class counts into registers (one LDS round trip for all of them)
+  int cn[DAD_C], cc[DAD_C];
+#pragma unroll
+  for (int k = 0; k < DAD_C; ++k) { cn[k] = S.cnt_noisy[k]; cc[k] = S.cnt_clean[k]; }
   // class attention (I/utils.py:597-599)
   float att[DAD_C];
   if (cfg.use_dacp) {
-    const float wmean = (((w[0] + w[1]) + w[2]) + w[3]) / 4.0f;
-    for (int k = 0; k < DAD_C; ++k) att[k] = expf(cfg.ecda_att_lambda * (wmean - w[k]));
+    float wk[DAD_C];
+#pragma unroll
+    for (int k = 0; k < DAD_C; ++k) wk[k] = w[k];
+    const float wmean = (((wk[0] + wk[1]) + wk[2]) + wk[3]) / 4.0f;
+#pragma unroll
+    for (int k = 0; k < DAD_C; ++k) att[k] = expf(cfg.ecda_att_lambda * (wmean - wk[k]));
   } else {
+#pragma unroll
     for (int k = 0; k < DAD_C; ++k) att[k] = 1.0f;
   }
   const float att_c = att[c];
   // repulsion over valid centroids (I/utils.py:582-595)
   int nvalid = 0;
-  for (int k = 0; k < ncls; ++k) nvalid += S.cnt_noisy[k] > 0;
+#pragma unroll
+  for (int k = 0; k < DAD_C; ++k) nvalid += (k < ncls && cn[k] > 0) ? 1 : 0;
   const int npairs = nvalid * (nvalid - 1) / 2;
   {
     // 16 (p, q) pairs x 256 dims over all threads: 32 threads per pair, 8 dims each,
@@ -924,11 +1117,13 @@ __device__ __forceinline__ void ecda_block(const DadEcdaArgs& a, const int c, Ec
       const int p = pair / DAD_C, q = pair % DAD_C;
       const int lo = p < q ? p : q, hi = p < q ? q : p;
       if (p < ncls && q < ncls && S.cnt_noisy[p] > 0 && S.cnt_noisy[q] > 0 && p != q) {
+        const f32x4* a0 = reinterpret_cast<const f32x4*>(&S.cent[lo][l32 * (DAD_H / 32)]);
+        const f32x4* a1 = reinterpret_cast<const f32x4*>(&S.cent[hi][l32 * (DAD_H / 32)]);
+        const f32x4 x0 = a0[0], x1 = a0[1], y0 = a1[0], y1 = a1[1];
+        const float v[8] = {x0[0] - y0[0], x0[1] - y0[1], x0[2] - y0[2], x0[3] - y0[3],
+                            x1[0] - y1[0], x1[1] - y1[1], x1[2] - y1[2], x1[3] - y1[3]};
 #pragma unroll
-        for (int k = 0; k < DAD_H / 32; ++k) {
-          const float df = S.cent[lo][l32 * (DAD_H / 32) + k] - S.cent[hi][l32 * (DAD_H / 32) + k];
-          d += df * df;
-        }
+        for (int k = 0; k < 8; ++k) d += v[k] * v[k];
       }
     }
 #pragma unroll
@@ -937,33 +1132,45 @@ __device__ __forceinline__ void ecda_block(const DadEcdaArgs& a, const int c, Ec
   }
   __syncthreads();
   ECDA_STAMP(4);
+  float pd[DAD_C][DAD_C];
+#pragma unroll
+  for (int p = 0; p < DAD_C; ++p)
+#pragma unroll
+    for (int q = 0; q < DAD_C; ++q) pd[p][q] = pdist[p][q];
   float rep = 0.0f;
   if (nvalid > 1) {
     float sp = 0.0f;
-    for (int p = 0; p < ncls; ++p)
-      for (int q = p + 1; q < ncls; ++q)
-        if (S.cnt_noisy[p] > 0 && S.cnt_noisy[q] > 0) sp += pdist[p][q];
+#pragma unroll
+    for (int p = 0; p < DAD_C; ++p)
+#pragma unroll
+      for (int q = p + 1; q < DAD_C; ++q)
+        if (q < ncls && cn[p] > 0 && cn[q] > 0) sp += pd[p][q];
     rep = -sp / (float)npairs;
   }
   bool gated[DAD_C];
   float rep_coef = 0.0f;
+#pragma unroll
   for (int k = 0; k < DAD_C; ++k) {
-    gated[k] = k < ncls && S.cnt_clean[k] >= 2 && S.cnt_noisy[k] >= 2;   // I/utils.py:609-610
+    gated[k] = k < ncls && cc[k] >= 2 && cn[k] >= 2;   // I/utils.py:609-610
     if (gated[k]) rep_coef += att[k] * cfg.ecda_delta;
   }
   // repulsion grad of this class's noisy members (d rep / d mu_c, then 1/n_c per member)
-  const bool rep_on = nvalid > 1 && S.cnt_noisy[c] > 0 && rep_coef != 0.0f;
+  const bool rep_on = nvalid > 1 && cn[c] > 0 && rep_coef != 0.0f;
   if (tid < DAD_H) {
     const int hh = tid;
     float rep_g = 0.0f;
     if (rep_on) {
+      float ce[DAD_C];
+#pragma unroll
+      for (int q = 0; q < DAD_C; ++q) ce[q] = S.cent[q][hh];
       float gsum = 0.0f;
-      for (int q = 0; q < ncls; ++q) {
-        if (q == c || S.cnt_noisy[q] == 0) continue;
-        const float nd = pdist[c][q];
-        if (nd > 0.0f) gsum += (S.cent[c][hh] - S.cent[q][hh]) / nd;
+#pragma unroll
+      for (int q = 0; q < DAD_C; ++q) {
+        if (q == c || q >= ncls || cn[q] == 0) continue;
+        const float nd = pd[c][q];
+        if (nd > 0.0f) gsum += (ce[c] - ce[q]) / nd;
       }
-      rep_g = wscale * rep_coef * (-gsum / (float)npairs / (float)S.cnt_noisy[c]);
+      rep_g = wscale * rep_coef * (-gsum / (float)npairs / (float)cn[c]);
     }
     S.repg[hh] = rep_g;   // read after the member compaction's barriers
   }
@@ -971,30 +1178,30 @@ __device__ __forceinline__ void ecda_block(const DadEcdaArgs& a, const int c, Ec
   ECDA_STAMP(3);
   // members of class c: clean (label c, weight 1) then masked noisy (pseudo-label c, weight = score);
   // a class below the gate only needs its noisy members (repulsion)
-  int n = gated[c] ? ecda_compact(S, B, 0, [&](int i) { return S.lab[i] == c; }, [](int) { return 1.0f; }) : 0;
+  int n = gated[c] ? ecda_compact(S, B, 0, [&](int i) { return S.lab[i] == c; }, [](int) { return 1.0f; }, inv) : 0;
   ECDA_STAMP(5);
   const int ns = n;
-  n = ecda_compact(S, Bn, n, [&](int i) { return S.prd[i] == c; }, [&](int i) { return S.scr[i]; });
+  n = ecda_compact(S, Bn, n, [&](int i) { return S.prd[i] == c; }, [&](int i) { return S.scr[i]; },
+                   inv ? inv + ECDA_PRE : nullptr);
   const int nt = n - ns;
   float mmd = 0.0f;
   float cpart = 0.0f;
-  auto run = [&](auto staged_tag) {
-    constexpr bool ST = decltype(staged_tag)::value;
-    const EcdaRows<ST> R{emb_c, emb_s, S, ns};
+  auto run = [&](auto R, float* Dbuf) {
+    constexpr bool ST = std::is_same_v<decltype(R), EcdaRows<true>>;
     float* D = nullptr;
     if (gated[c]) {
-      D = ST ? S.dm : scratch;
-      ecda_stage(S, R, n);
+      D = Dbuf;
+      if constexpr (ST) stage(ns, n);
       ECDA_STAMP(6);
       mmd = ecda_mmd_coef(S, R, n, D);
       ECDA_STAMP(7);
-    }
+    }   // (a repulsion-only class needs no member rows: g = repg)
     // compactness (I/utils.py:614-616): mean_j ||z_j - mu||^2, grad (2/nt)(z_j - mu)
     ecda_member_grads(S, R, n, D, wscale * att_c, gated[c] ? S.cent[c] : nullptr,
                       wscale * att_c * cfg.ecda_gamma * (2.0f / (float)nt), S.repg, ge_c, ge_s, a.eflag, B, cpart);
   };
-  if (n <= ECDA_NZ) run(std::true_type{});
-  else run(std::false_type{});
+  if (n <= ECDA_NZ) run(EcdaRows<true>{emb_c, emb_s, S, ns}, S.dm);
+  else run(EcdaRows<false>{emb_c, emb_s, S, ns}, scratch);
   if (!gated[c]) return;
   ECDA_STAMP(8);
   const float comp = ecda_block_sum_f(S, cpart) / (float)nt;
@@ -1007,10 +1214,8 @@ __device__ __forceinline__ void ecda_block(const DadEcdaArgs& a, const int c, Ec
 
 __global__ __launch_bounds__(ECDA_THREADS) void dad_ecda(DadEcdaArgs a) {
   DAD_GUARD_BLOCK(ECDA_THREADS);
-  __shared__ EcdaSmem S;
-  __shared__ float pdist[DAD_C][DAD_C];
-  __shared__ EcdaPrefix P;
-  ecda_block<false>(a, blockIdx.x, S, pdist, nullptr, P);
+  __shared__ struct { EcdaSmem s; float pdist[DAD_C][DAD_C]; EcdaPrefix p; } u;
+  ecda_block<false>(a, blockIdx.x, u.s, u.pdist, nullptr, u.p);
 }
 
 // block 0: the tail (losses, DACP outputs, dL/dz); blocks 1..C: ECDA class blockIdx.x - 1,

@@ -21,23 +21,41 @@ def main():
     P = bench.init_model_weights(model, seed=0)
     step = PKG.DADStep(model, flavor="iemocap", precision="bf16", rng="counter", seed=1)
     data = bench.make_batches(P, 2, B, T, seed=17, device=torch.device("cuda"))
-    for i in range(8):
-        step.step(data[i % 2][0], data[i % 2][1], 60)
-    torch.cuda.synchronize()
+    S = 24  # slots per ECDA class (tail.hip ECDA_SLOTS)
     L = PKG.lib()
-    ebuf = (ctypes.c_ulonglong * (4 * 16 + 12))()
-    assert L.dad_probe_read_ecda_stamps(ebuf, len(ebuf)) == 0
-    e = np.frombuffer(ebuf, dtype=np.uint64).astype(np.int64)
-    t0 = e[64]
-    rel = lambda v: (v - t0) / 100.0
+    reps = int(os.environ.get("STAMP_REPS", "15"))
+    raw = []
+    for r in range(reps):   # the last step of a 4-step burst, reps times
+        for i in range(4):
+            step.step(data[i % 2][0], data[i % 2][1], 60)
+        torch.cuda.synchronize()
+        ebuf = (ctypes.c_ulonglong * (4 * S + 16))()
+        assert L.dad_probe_read_ecda_stamps(ebuf, len(ebuf)) == 0
+        raw.append(np.frombuffer(ebuf, dtype=np.uint64).astype(np.int64))
+    raw = np.stack(raw[2:] if reps > 4 else raw)
+    t0 = raw[:, 4 * S:4 * S + 1]
+    relm = np.median((raw - t0) / 100.0, axis=0)        # us after the tail block's start, median
+    setm = np.all(raw > 0, axis=0)
+    last = raw[-1]
+    on = lambda k: bool(setm[k])
+    rel = lambda k: relm[k]
+    T = 4 * S
     tn = ["end", "ce", "probs", "dacp", "kl", "outputs", "clsbwd"]
-    print("tail start 0 | " + "  ".join("%s %.2f" % (tn[k - 1], rel(e[64 + k])) for k in range(1, 8) if e[64 + k] > 0))
+    print("median of %d steps" % raw.shape[0])
+    print("tail start 0 | " + "  ".join("%s %.2f" % (tn[k - 1], rel(T + k)) for k in range(1, 8) if on(T + k)))
+    if on(T + 13) and on(T + 12):
+        ghz = np.median((raw[:, T + 13] - raw[:, T + 12]) / ((raw[:, T + 1] - raw[:, T]) * 10.0))
+        print("  tail block clock: %.2f GHz" % ghz)
+    dn = ["dacp-ranks", "dacp-thresholds", "mask", "epoch-sums"]
+    print("  tail dacp detail: " + "  ".join("%s %.2f" % (dn[k - 8], rel(T + k)) for k in range(8, 12) if on(T + k)))
     names = ["start", "meta", "centroid", "gates", "pdist", "compact", "stage", "mmd", "grads"]
     for c in range(4):
-        row = e[c * 16:c * 16 + 16]
-        parts = ["%s %.2f" % (names[k], rel(row[k])) for k in range(9) if row[k] > 0]
-        sub = ["%s %.2f" % (nm, rel(row[k])) for k, nm in ((12, "dist"), (13, "sumD"), (14, "coef"), (15, "terms")) if row[k] > 0]
-        print("ecda class %d (n=%d ns=%d): %s | mmd: %s" % (c, e[c * 16 + 10], e[c * 16 + 11], "  ".join(parts), "  ".join(sub)))
+        o = c * S
+        parts = ["%s %.2f" % (names[k], rel(o + k)) for k in range(9) if on(o + k)]
+        sub = ["%s %.2f" % (nm, rel(o + k)) for k, nm in ((12, "dist"), (13, "sumD"), (14, "coef"), (15, "terms"),
+                                                          (16, "cnt"), (17, "cpart"), (18, "cbar"), (19, "stage0"))
+               if on(o + k)]
+        print("ecda class %d (n=%d ns=%d): %s | sub: %s" % (c, last[o + 10], last[o + 11], "  ".join(parts), "  ".join(sub)))
 
 
 if __name__ == "__main__":
