@@ -26,8 +26,11 @@
 //
 // Pipeline per wave (iteration q = sub-slab q of the workgroup's range):
 //   wait for the wave's own DMA of sub-slab q+1 (counted vmcnt: the stores and the youngest
-//   DMA batch stay in flight) -> MFMA(q) with convert(q+1) -> epilogue(q) -> DMA of sub-slab
-//   q+3 into the raw stage convert(q+1) just freed -> barrier.
+//   DMA batch stay in flight) -> MFMA(q) with convert(q+1)'s units issued between its k-steps
+//   -> epilogue(q) -> DMA of sub-slab q+3 into the raw stage convert(q+1) just freed -> barrier.
+// A sub-slab without a valid row (e.g. rows 304..319 of a 300-frame utterance) is neither
+// converted nor multiplied.  The first two sub-slabs' DMAs are issued ahead of the resident W1
+// load, so sub-slab 0 is converted while W1 streams in.
 #include <type_traits>
 
 #include "dad_common.h"
@@ -240,64 +243,114 @@ __device__ __forceinline__ int live_rows(const Job& J, int half, int w) {
 #define WS_PRIO 0      // static s_setprio 1 for: 0 no wave, 1 waves WAVES/2.., 2 waves ..WAVES/2-1
 #endif
 template <class S, int NOISE, int KIND, int HALF>
-__device__ __forceinline__ void ws_convert(const Ctx& C, const Job& J, int w, int lane_, const float* raw, char* tile,
-                                           const float* fk) {
-  constexpr bool strong = KIND == KIND_STRONG;
-  const int lane = opaque(lane_);
-  const int st = (strong && C.mask_len > 0) ? tstart_of<NOISE>(C, J.b) : -(1 << 30);
-  const uint32_t key = strong ? C.key_strong : C.key_weak;
-  const float sd = strong ? C.sstd : C.wstd;
-  const float* nsrc = strong ? C.ns : C.nw;
-#pragma unroll
-  for (int i = 0; i < S::RPW; ++i) {
+struct WsConv {
+  static constexpr bool strong = KIND == KIND_STRONG;
+  static constexpr int kUnits = 3 * S::RPW;   // (row i, 256-column chunk k) units of 4 elements per lane
+  const Ctx& C;
+  const Job& J;
+  int w, lane;
+  const float* raw;
+  char* tile;
+  const float* fk;
+  int st;
+  uint32_t key;
+  float sd;
+  const float* nsrc;
+  __device__ __forceinline__ WsConv(const Ctx& C_, const Job& J_, int w_, int lane_, const float* raw_, char* tile_,
+                                    const float* fk_)
+      : C(C_), J(J_), w(w_), lane(opaque(lane_)), raw(raw_), tile(tile_), fk(fk_) {
+    st = (strong && C.mask_len > 0) ? tstart_of<NOISE>(C, J.b) : -(1 << 30);
+    key = strong ? C.key_strong : C.key_weak;
+    sd = strong ? C.sstd : C.wstd;
+    nsrc = strong ? C.ns : C.nw;
+  }
+  // unit U: row i = U / 3 of the wave's rows, chunk k = U % 3 (columns 256k + 4 lane .. +3)
+  template <int U>
+  __device__ __forceinline__ void unit() const {
+    constexpr int i = U / 3, k = U % 3;
     const int r = S::RPW * w + i;                               // row within the sub-slab (w uniform)
     const int t = min(J.c * DAD_SLAB + HALF * kSub + r, J.T - 1);
     const long grow = J.row0 + t;
     const bool tzero = t >= st && t < st + C.mask_len;          // I/utils.py:365-372 (padded Tmax)
     const float* rrow = raw + r * DAD_D + 4 * lane;
     char* trow = tile + r * kTileRow + 16 * ((lane >> 1) ^ (r & 15)) + 8 * (lane & 1);
+    const int d = 256 * k + 4 * lane;
+    f32x4 v = *reinterpret_cast<const f32x4*>(rrow + 256 * k);
+    if constexpr (KIND != KIND_CLEAN) {
+      f32x4 n;
+      if constexpr (NOISE) {
+        n = *reinterpret_cast<const f32x4*>(nsrc + (size_t)grow * DAD_D + d);
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int d = 256 * k + 4 * lane;
-      f32x4 v = *reinterpret_cast<const f32x4*>(rrow + 256 * k);
-      if constexpr (KIND != KIND_CLEAN) {
-        f32x4 n;
-        if constexpr (NOISE) {
-          n = *reinterpret_cast<const f32x4*>(nsrc + (size_t)grow * DAD_D + d);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) n[e] *= sd;
-        } else {
-          const uint32_t p = ((uint32_t)grow * (uint32_t)DAD_D + (uint32_t)d) >> 1;
-          float z0, z1, z2, z3;
-          dad_aug_noise_pair(key, p, sd, z0, z1);
-          dad_aug_noise_pair(key, p + 1u, sd, z2, z3);
-          n = f32x4{z0, z1, z2, z3};
-        }
-        // reference op order: x + std*N, then * feature mask, then temporal zero
-        // (I/utils.py:330,338-344,365-372)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = v[e] + n[e];
-        if constexpr (strong) {
-          const f32x4 kp = *reinterpret_cast<const f32x4*>(fk + d);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = v[e] * kp[e];
-        }
+        for (int e = 0; e < 4; ++e) n[e] *= sd;
+      } else {
+        const uint32_t p = ((uint32_t)grow * (uint32_t)DAD_D + (uint32_t)d) >> 1;
+        float z0, z1, z2, z3;
+        dad_aug_noise_pair(key, p, sd, z0, z1);
+        dad_aug_noise_pair(key, p + 1u, sd, z2, z3);
+        n = f32x4{z0, z1, z2, z3};
       }
-      // two v_cvt_pk_bf16_f32 per 4 elements; the temporal zero selects the packed words
-      uint2 o = uint2{__builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{v[0], v[1]}, bf16x2)),
-                      __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{v[2], v[3]}, bf16x2))};
-      if constexpr (strong) o = tzero ? uint2{0u, 0u} : o;
-      *reinterpret_cast<uint2*>(trow + 512 * k) = o;           // chunk 32k + (lane>>1), swizzled by row
-      if constexpr (KIND != KIND_WEAK) {
-        // 32-bit byte offset from the uniform base (saddr store, no 64-bit address math)
-        const uint32_t boff = ((uint32_t)grow * (uint32_t)DAD_D + (uint32_t)d) * 2u;
-        *reinterpret_cast<uint2*>(reinterpret_cast<char*>(strong ? C.xsn : C.xs) + boff) = o;
+      // reference op order: x + std*N, then * feature mask, then temporal zero
+      // (I/utils.py:330,338-344,365-372)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = v[e] + n[e];
+      if constexpr (strong) {
+        const f32x4 kp = *reinterpret_cast<const f32x4*>(fk + d);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = v[e] * kp[e];
       }
-      // WS_REGION units (4 elements, 2 Box-Muller pairs each) per scheduling region: the
-      // wave's partner on the SIMD covers the rest of the dependent latency, and nothing is
-      // hoisted across regions
-      if ((k + 1) % WS_REGION == 0 || k == 2) __builtin_amdgcn_sched_barrier(0);
     }
+    // two v_cvt_pk_bf16_f32 per 4 elements; the temporal zero selects the packed words
+    uint2 o = uint2{__builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{v[0], v[1]}, bf16x2)),
+                    __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{v[2], v[3]}, bf16x2))};
+    if constexpr (strong) o = tzero ? uint2{0u, 0u} : o;
+    *reinterpret_cast<uint2*>(trow + 512 * k) = o;             // chunk 32k + (lane>>1), swizzled by row
+    if constexpr (KIND != KIND_WEAK) {
+      // 32-bit byte offset from the uniform base (saddr store, no 64-bit address math)
+      const uint32_t boff = ((uint32_t)grow * (uint32_t)DAD_D + (uint32_t)d) * 2u;
+      *reinterpret_cast<uint2*>(reinterpret_cast<char*>(strong ? C.xsn : C.xs) + boff) = o;
+    }
+  }
+  template <int U = 0>
+  __device__ __forceinline__ void all() const {
+    if constexpr (U < kUnits) {
+      unit<U>();
+      // WS_REGION units per scheduling region: the wave's partner on the SIMD covers the rest
+      // of the dependent latency, and nothing is hoisted across regions
+      if constexpr ((U % 3 + 1) % WS_REGION == 0 || U % 3 == 2) __builtin_amdgcn_sched_barrier(0);
+      all<U + 1>();
+    }
+  }
+};
+// no conversion riding along an MFMA pass
+struct WsNoConv {
+  static constexpr int kUnits = 0;
+  template <int U>
+  __device__ __forceinline__ void unit() const {}
+};
+
+// Convert the wave's rows of sub-slab (J, HALF): raw stage -> bf16 tile; CLEAN / STRONG also store
+// the bf16 row to HBM for the weight gradient.  Straight-line code per KIND (one basic block,
+// so the 3*RPW independent RNG chains interleave): rows past the utterance are converted as
+// copies of its last row (identical bytes to the same xs address), temporally masked rows
+// are selected to zero after the RNG.  Noise comes pre-scaled (dad_normal_pair_c).
+template <class S, int NOISE, int KIND, int HALF>
+__device__ __forceinline__ void ws_convert(const Ctx& C, const Job& J, int w, int lane_, const float* raw, char* tile,
+                                           const float* fk) {
+  WsConv<S, NOISE, KIND, HALF>(C, J, w, lane_, raw, tile, fk).all();
+}
+
+// bf16 copies of an empty sub-slab's rows that lie inside the utterance (padded frames): zeros.
+// Rows past the utterance alias its last row's copy and are left alone.
+template <class S, int HALF>
+__device__ __forceinline__ void ws_zero_xs(const Ctx& C, const Job& J, int w, int lane) {
+  __bf16* xs = J.kind == KIND_STRONG ? C.xsn : C.xs;
+#pragma unroll
+  for (int i = 0; i < S::RPW; ++i) {
+    const int t = J.c * DAD_SLAB + HALF * kSub + S::RPW * w + i;
+    if (t >= J.T) break;
+    const uint32_t boff = ((uint32_t)(J.row0 + t) * (uint32_t)DAD_D + 4u * (uint32_t)lane) * 2u;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) *reinterpret_cast<uint2*>(reinterpret_cast<char*>(xs) + boff + 512u * k) = uint2{0u, 0u};
   }
 }
 
@@ -328,12 +381,18 @@ __device__ __forceinline__ bf16x8 afrag(const char* tile, const int (&aoff)[4]) 
 // WS_LA k-steps ahead of their MFMAs: one k-step's MFMAs (NT x 16 cycles) are shorter than an
 // LDS read under load, so a one-step lookahead left every k-step waiting on its fragment.
 #ifndef WS_LA
-#define WS_LA 2   // 1 or 2
+#define WS_LA 1   // 1 or 2 (2 with the interleaved conversion spills W1 fragments)
 #endif
 static_assert(WS_LA == 1 || WS_LA == 2, "A-fragment lookahead: 1 or 2 k-steps");
-template <class S, int KS>
+// CV: conversion units of the next sub-slab riding along the MFMA chain (WS_INTERLEAVE): unit
+// u is issued after k-step (u + 1) * kKS / kUnits - 1, between scheduling barriers, so the
+// VALU work of the RNG fills the matrix pipe's cycles inside ONE wave.
+#ifndef WS_INTERLEAVE
+#define WS_INTERLEAVE 1   // measured 0.6-0.8 us per launch faster than the MFMA-then-convert order alone
+#endif
+template <class S, int KS, class CV>
 __device__ __forceinline__ void ws_mfma_from(const char* tile, const int (&aoff)[4], const bf16x8 (&wf)[S::NT][kKS],
-                                             f32x4 (&acc)[S::NT], bf16x8 x0, bf16x8 x1) {
+                                             f32x4 (&acc)[S::NT], bf16x8 x0, bf16x8 x1, const CV& cv) {
   if constexpr (KS < kKS) {
     bf16x8 xn;
     if constexpr (KS + WS_LA < kKS) xn = afrag<KS + WS_LA>(tile, aoff);
@@ -343,15 +402,24 @@ __device__ __forceinline__ void ws_mfma_from(const char* tile, const int (&aoff)
       if (agpr) mfma1<true, KS == 0>(acc[t], x0, wf[t][KS]);
       else mfma1<false, KS == 0>(acc[t], x0, wf[t][KS]);
     }
-    if constexpr (WS_LA == 1) ws_mfma_from<S, KS + 1>(tile, aoff, wf, acc, xn, xn);
-    else ws_mfma_from<S, KS + 1>(tile, aoff, wf, acc, x1, xn);
+    if constexpr (CV::kUnits > 0) {
+      constexpr int U = (KS + 1) * CV::kUnits / kKS;        // units due after this k-step
+      constexpr int U0 = KS * CV::kUnits / kKS;
+      if constexpr (U > U0) {
+        __builtin_amdgcn_sched_barrier(0);
+        cv.template unit<U - 1>();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    if constexpr (WS_LA == 1) ws_mfma_from<S, KS + 1>(tile, aoff, wf, acc, xn, xn, cv);
+    else ws_mfma_from<S, KS + 1>(tile, aoff, wf, acc, x1, xn, cv);
   }
 }
-template <class S>
+template <class S, class CV = WsNoConv>
 __device__ __forceinline__ void ws_mfma(const char* tile, const int (&aoff)[4], const bf16x8 (&wf)[S::NT][kKS],
-                                        f32x4 (&acc)[S::NT]) {
-  if constexpr (WS_LA == 1) ws_mfma_from<S, 0>(tile, aoff, wf, acc, afrag<0>(tile, aoff), afrag<0>(tile, aoff));
-  else ws_mfma_from<S, 0>(tile, aoff, wf, acc, afrag<0>(tile, aoff), afrag<1>(tile, aoff));
+                                        f32x4 (&acc)[S::NT], const CV& cv = CV{}) {
+  if constexpr (WS_LA == 1) ws_mfma_from<S, 0>(tile, aoff, wf, acc, afrag<0>(tile, aoff), afrag<0>(tile, aoff), cv);
+  else ws_mfma_from<S, 0>(tile, aoff, wf, acc, afrag<0>(tile, aoff), afrag<1>(tile, aoff), cv);
   // MFMA D -> VALU readers of the epilogue (hipcc pads nothing after an asm MFMA)
   if constexpr (S::NT == 4) asm volatile("s_nop 7\n\ts_nop 7" ::"v"(acc[0]), "v"(acc[1]), "v"(acc[2]), "v"(acc[3]));
   else asm volatile("s_nop 7\n\ts_nop 7" ::"v"(acc[0]), "v"(acc[1]));
@@ -457,9 +525,11 @@ __device__ __forceinline__ void wait_vm_sw(int n) {
 
 template <int WAVES, int NOISE, bool TEACHER>
 __device__ __forceinline__ void ws_loop(const Ctx& C, const int j0, const int Q, const int w, const int lane,
-                                        char* smem, const uint32_t sbase, const bf16x8 (&wf)[16 / WAVES][kKS],
-                                        const float (&bh)[16 / WAVES], const float* fk, const uint32_t* vb) {
+                                        char* smem, const uint32_t sbase, const bf16x8* W, const float* bias,
+                                        const float* fk, const uint32_t* vb) {
   using S = Shape<WAVES>;
+  bf16x8 wf[S::NT][kKS];
+  float bh[S::NT];
   float ssum[S::NT], scnt[S::NT];
   uint32_t bw[S::NT];
   const float* raw0 = reinterpret_cast<const float*>(smem + kOffRaw);
@@ -467,6 +537,15 @@ __device__ __forceinline__ void ws_loop(const Ctx& C, const int j0, const int Q,
   char* tile0 = smem + kOffTile;
   char* tile1 = smem + kOffTile + kTile;
   auto jobq = [&](int q) { return job_of(C, TEACHER, j0 + (q >> 1)); };
+  // valid-row mask of sub-slab q (uniform): an empty one (frames past every utterance's end,
+  // e.g. rows 304..319 of a 300-frame utterance) is neither converted nor multiplied -- the
+  // epilogue's valid mask zeroes it anyway
+  auto vmask_of = [&](int q) -> uint32_t {
+    return __builtin_amdgcn_readfirstlane((vb[q >> 1] >> (16 * (q & 1))) & 0xffffu);
+  };
+  // xs stores convert(q) issued (the counted vmcnt waits depend on them; for an empty sub-slab
+  // 0 even where it zeroes padded rows' copies: under-counting younger stores only waits longer)
+  auto xs_of = [&](int q) -> int { return vmask_of(q) ? n_xs<S>(jobq(q).kind) : 0; };
   auto dma = [&](int q) {
     if (q < Q) {
       const Job J = jobq(q);
@@ -474,8 +553,14 @@ __device__ __forceinline__ void ws_loop(const Ctx& C, const int j0, const int Q,
     }
   };
   // convert sub-slab q (its half HN is a template parameter: raw stage and tile HN)
-  auto convert = [&](auto hn_tag, const Job& J) {
+  auto convert = [&](auto hn_tag, const Job& J, uint32_t vm) {
     constexpr int HN = decltype(hn_tag)::value;
+    if (vm == 0) {
+      // nothing to multiply; the student's bf16 copies of padded frames inside the utterance
+      // still get finite bytes (the weight gradient multiplies them by a zero mask)
+      if constexpr (!TEACHER) ws_zero_xs<S, HN>(C, J, w, lane);
+      return;
+    }
     const float* rawp = HN ? raw1 : raw0;
     char* tl = HN ? tile1 : tile0;
     if constexpr (TEACHER) ws_convert<S, NOISE, KIND_WEAK, HN>(C, J, w, lane, rawp, tl, fk);
@@ -493,30 +578,52 @@ __device__ __forceinline__ void ws_loop(const Ctx& C, const int j0, const int Q,
       for (int m = 0; m < 4; ++m) aoff[m] = (ln & 15) * kTileRow + 16 * ((4 * m + (ln >> 4)) ^ (ln & 15));
     }
     unsigned long long c0 = WS_CLK(), c1 = c0, c2 = c0;
-    if (q + 1 < Q) {
-      const Job Jn = jobq(q + 1);
-      // this wave's DMA of sub-slab q+1 (issued at the end of iteration q-2) has landed once at
-      // most these younger VMEM ops remain: xs stores of convert(q), epilogue(q-1), DMA(q+2)
-      wait_vm_sw<S::kDma>(n_xs<S>(jobq(q).kind) + (q > 0 ? n_epi<TEACHER, 1 - H>() : 0) +
-                          (q + 2 < Q ? S::kDma : 0));
-      c1 = WS_CLK();
-      // The two waves sharing a SIMD (w and w + WAVES/2) run the two halves in opposite
-      // order, so one's MFMA chain overlaps the other's RNG/convert VALU work between barriers.
-      if (S::STAGGER && w >= WAVES / 2) {
-        convert(std::integral_constant<int, 1 - H>{}, Jn);
-        c2 = WS_CLK();
+    const uint32_t vmask = vmask_of(q);
+    auto mfma = [&]() {
+      if (vmask) {
         ws_mfma<S>(H ? tile1 : tile0, aoff, wf, acc);
       } else {
-        ws_mfma<S>(H ? tile1 : tile0, aoff, wf, acc);
+#pragma unroll
+        for (int t = 0; t < S::NT; ++t) acc[t] = f32x4{};
+      }
+    };
+    if (q + 1 < Q) {
+      const Job Jn = jobq(q + 1);
+      const uint32_t vmn = vmask_of(q + 1);
+      // this wave's DMA of sub-slab q+1 (issued at the end of iteration q-2) has landed once at
+      // most these younger VMEM ops remain: xs stores of convert(q), epilogue(q-1), DMA(q+2)
+      wait_vm_sw<S::kDma>(xs_of(q) + (q > 0 ? n_epi<TEACHER, 1 - H>() : 0) + (q + 2 < Q ? S::kDma : 0));
+      c1 = WS_CLK();
+      if (WS_INTERLEAVE && vmask && vmn) {
+        // MFMA(q) with convert(q+1)'s units riding along the chain
+        constexpr int HN = 1 - H;
+        const float* rawp = HN ? raw1 : raw0;
+        char* tl = HN ? tile1 : tile0;
+        const char* tm = H ? tile1 : tile0;
+        if constexpr (TEACHER) {
+          ws_mfma<S>(tm, aoff, wf, acc, WsConv<S, NOISE, KIND_WEAK, HN>(C, Jn, w, lane, rawp, tl, fk));
+        } else if (Jn.kind == KIND_CLEAN) {
+          ws_mfma<S>(tm, aoff, wf, acc, WsConv<S, NOISE, KIND_CLEAN, HN>(C, Jn, w, lane, rawp, tl, fk));
+        } else {
+          ws_mfma<S>(tm, aoff, wf, acc, WsConv<S, NOISE, KIND_STRONG, HN>(C, Jn, w, lane, rawp, tl, fk));
+        }
+        c2 = WS_CLK();
+      } else if (S::STAGGER && w >= WAVES / 2) {
+        // The two waves sharing a SIMD (w and w + WAVES/2) run the two halves in opposite
+        // order, so one's MFMA chain overlaps the other's RNG/convert VALU work between barriers.
+        convert(std::integral_constant<int, 1 - H>{}, Jn, vmn);
+        c2 = WS_CLK();
+        mfma();
+      } else {
+        mfma();
         DAD_PROBE_FENCE2(acc[0], acc[S::NT - 1]);
         c2 = WS_CLK();
-        convert(std::integral_constant<int, 1 - H>{}, Jn);
+        convert(std::integral_constant<int, 1 - H>{}, Jn, vmn);
       }
     } else {
-      ws_mfma<S>(H ? tile1 : tile0, aoff, wf, acc);
+      mfma();
     }
     const unsigned long long c3 = WS_CLK();
-    const uint32_t vmask = (vb[q >> 1] >> (16 * H)) & 0xffffu;
     ws_epilogue<S, TEACHER, H>(C, jobq(q), w, lane, vmask, bh, acc, ssum, scnt, bw);
     const unsigned long long c4 = WS_CLK();
     dma(q + 3);
@@ -529,10 +636,22 @@ __device__ __forceinline__ void ws_loop(const Ctx& C, const int j0, const int Q,
 #elif WS_PRIO == 2
   if (w < WAVES / 2) __builtin_amdgcn_s_setprio(1);
 #endif
+  // the first two sub-slabs' DMAs go out ahead of the resident W1 (48 KB per wave), so
+  // sub-slab 0 is converted while W1 streams in
   dma(0);
   dma(1);
-  wait_vm_sw<S::kDma>(Q > 1 ? S::kDma : 0);   // sub-slab 0 landed
-  convert(std::integral_constant<int, 0>{}, jobq(0));
+  const int hw = S::HW * w;
+#pragma unroll
+  for (int t = 0; t < S::NT; ++t)   // fragment-major shadow (dad_w1frag_index): 1 KB coalesced loads
+#pragma unroll
+    for (int ks = 0; ks < kKS; ++ks) wf[t][ks] = W[(size_t)(((hw >> 4) + t) * kKS + ks) * 64 + lane];
+#pragma unroll
+  for (int t = 0; t < S::NT; ++t) bh[t] = bias[hw + 16 * t + (lane & 15)];
+  constexpr int kW1 = S::NT * kKS + S::NT;   // VMEM loads of the resident W1 and the bias
+  static_assert(S::kDma + kW1 <= 63, "vmcnt range");
+  if (Q > 1) wait_vm<S::kDma + kW1>();        // sub-slab 0 landed (DMA 1 and W1 still in flight)
+  else wait_vm<kW1>();
+  convert(std::integral_constant<int, 0>{}, jobq(0), vmask_of(0));
   dma(2);
   lds_barrier();
   for (int q = 0; q < Q; q += 2) {   // Q is even: a job is two sub-slabs
@@ -573,23 +692,13 @@ __device__ __forceinline__ void encode_ws_body(const DadEncodeArgs& a, char* sme
     const uint64_t bal = __ballot(v);
     if ((lane & 31) == 0) vb[p / DAD_SLAB] = (uint32_t)(bal >> (lane & 32));
   }
-  asm volatile("" ::: "memory");   // the pad/u loads above retire before W1 is requested
+  __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): the pad / u loads retired (no DMA in flight yet)
+  lds_barrier();                        // fk / vb visible
+  WS_STAMP(1, DAD_PROBE_WALL());
   const bf16x8* W = reinterpret_cast<const bf16x8*>(teacher ? a.w1bf_teacher : a.w1bf_student);
   const float* bias = teacher ? a.b1_teacher : a.b1_student;
-  const int hw = S::HW * w;
-  bf16x8 wf[S::NT][kKS];           // fragment-major shadow (dad_w1frag_index): 1 KB coalesced loads
-#pragma unroll
-  for (int t = 0; t < S::NT; ++t)
-#pragma unroll
-    for (int ks = 0; ks < kKS; ++ks) wf[t][ks] = W[(size_t)(((hw >> 4) + t) * kKS + ks) * 64 + lane];
-  float bh[S::NT];
-#pragma unroll
-  for (int t = 0; t < S::NT; ++t) bh[t] = bias[hw + 16 * t + (lane & 15)];
-  __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): W1 and bias resident (a wait the compiler sees)
-  lds_barrier();                        // fk / vb visible (no DMA in flight yet)
-  WS_STAMP(1, DAD_PROBE_WALL());
-  if (teacher) ws_loop<WAVES, NOISE, true>(C, j0, 2 * nj, w, lane, smem, sbase, wf, bh, fk, vb);
-  else ws_loop<WAVES, NOISE, false>(C, j0, 2 * nj, w, lane, smem, sbase, wf, bh, fk, vb);
+  if (teacher) ws_loop<WAVES, NOISE, true>(C, j0, 2 * nj, w, lane, smem, sbase, W, bias, fk, vb);
+  else ws_loop<WAVES, NOISE, false>(C, j0, 2 * nj, w, lane, smem, sbase, W, bias, fk, vb);
   WS_STAMP(2, DAD_PROBE_WALL());
   WS_STAMP(3, ((unsigned long long)teacher << 16) | (unsigned long long)(2 * nj));
 }
