@@ -161,6 +161,29 @@ def test_bf16_step_close_to_oracle():
         assert cos > 0.99, cos
 
 
+def test_modular_encoder_bf16_matches_torch_fp32():
+    """The modular encoder op in BF16 (set_precision): within bf16 rounding of the fp32 torch op,
+    with padded frames and a slab count that leaves a sub-slab past every utterance's end."""
+    import dadpkg
+    p = dadpkg.pkg()
+    torch.manual_seed(1)
+    m = p.SSRLModel().cuda()
+    m.set_precision(p._lib.PREC_BF16)
+    B, T = 5, 300
+    x = torch.randn(B, T, 768, device="cuda")
+    pad = torch.zeros(B, T, dtype=torch.bool, device="cuda")
+    pad[1, 140:] = True
+    pad[3, 17:] = True
+    enc = m.student_encoder
+    e = enc(x, pad)
+    torch.cuda.synchronize()
+    W, b = enc.pre_net.weight.detach(), enc.pre_net.bias.detach()
+    h = torch.relu(x @ W.T + b) * (~pad).unsqueeze(-1).float()
+    ref = h.sum(1) / (~pad).float().sum(1, keepdim=True).clamp(min=1.0)
+    assert torch.isfinite(e).all()
+    assert gh.rel(e.detach().cpu(), ref.cpu()) < 2e-2
+
+
 def test_modular_encoder_matches_torch_fp32():
     """Emotion2VecEncoder forward/backward (HIP) vs a plain PyTorch fp32 reference of the op."""
     import dadpkg
