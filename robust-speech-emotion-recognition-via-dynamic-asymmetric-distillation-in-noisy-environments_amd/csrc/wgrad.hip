@@ -173,12 +173,13 @@ __global__ __launch_bounds__(DAD_WGRAD_THREADS) void dad_wgrad_f32(DadWgradArgs 
 //     disjoint bank quarters), read as k-major B fragments with ds_read_b64_tr_b16;
 //   G is never staged: each lane loads the ReLU' row masks (one u32 per h) of its own two
 //     hidden units straight into registers, and its A fragment (8 rows of one h) is byte
-//     (16 ks + 8 (lane/32)) of that mask, expanded nibble by nibble through a 16-entry LDS
-//     table (conflict-free) into four 0xFFFF/0 dword masks and AND-ed with bf16(dL/de_u[h] /
-//     len_u) in both halves: two table reads and four ANDs per fragment.
-// Software pipeline, one barrier per round: round j computes slab j from one LDS buffer while
-// it stages slab j+1 into the other and issues the loads of slab j+1+WGD_DEPTH, all in one
-// basic block so the staging VALU fills the MFMA gaps.  dL/de_u[h] / len_u of the
+//     (16 ks + 8 (lane/32)) of that mask, expanded through a 256-entry LDS table into four
+//     0xFFFF/0 dword masks and AND-ed with bf16(dL/de_u[h] / len_u) in both halves: one
+//     bitfield extract, one table read and four ANDs per fragment.  (The loop is bound by
+//     vector issue, about ten VALU instructions per MFMA, so table reads replace arithmetic.)
+// Software pipeline, one barrier per TWO rounds: round j computes slab j from LDS buffer j&3
+// while it stages slab j+2 into buffer (j+2)&3 and issues the loads of slab j+2+WGD_DEPTH,
+// all in one basic block so the staging VALU fills the MFMA gaps.  dL/de_u[h] / len_u of the
 // workgroup's utterances is rebuilt in the prologue (fused_ge1) while the first loads are in
 // flight.  Output: one f32 partial slab per split, summed in fixed order by dad_reduce.
 static_assert(WGD_THREADS == 256 * WGD_GROUPS && DAD_H == 256, "dad_wgrad_direct: groups of 256 threads, thread = h");
@@ -263,22 +264,17 @@ __device__ __forceinline__ void wgd_load(const DadWgradArgs& a, const WgdTable& 
 __device__ __forceinline__ void wgd_stage(const WgdSlab& r, __bf16* Xt) {
   const int tid = threadIdx.x & 255;
   const int row = tid >> 3;
-  const bool ok = row < r.nvalid;
-  const uint4 raw = __builtin_bit_cast(uint4, r.x);
-  const uint4 v = ok ? raw : uint4{0u, 0u, 0u, 0u};   // rows past the utterance: zero
-  *reinterpret_cast<uint4*>(&Xt[row * WGD_XP + (tid & 7) * 8]) = v;
+  // rows past the utterance hold a copy of its last row (finite); their ReLU' mask bits are 0
+  *reinterpret_cast<uint4*>(&Xt[row * WGD_XP + (tid & 7) * 8]) = __builtin_bit_cast(uint4, r.x);
 }
 
 // A fragment of h tile ht, k rows 16 ks + 8 (lane/32) + 0..7: bit ? gb : 0 (bf16 bits).
-// lut[n] = the 0xFFFF/0 halfword masks of the 4 bits of nibble n (8 B): the 16-entry table
-// spans the 32 banks once, so a 32-lane half-wave's reads are conflict-free (equal entries
-// broadcast, different entries sit on different banks).
-__device__ __forceinline__ uint4 wgd_amask(uint32_t mask, const uint2* lut, int ks) {
+// lut[b] = the 0xFFFF/0 halfword masks of the 8 bits of byte b (16 B, 4 KB table): one
+// bitfield extract and one 16-B LDS read per fragment.
+__device__ __forceinline__ uint4 wgd_amask(uint32_t mask, const uint4* lut, int ks) {
   const int lane = threadIdx.x & 63;
-  const uint32_t byte = mask >> (16 * ks + 8 * (lane >> 5));
-  const uint2 lo = lut[byte & 15u];
-  const uint2 hi = lut[(byte >> 4) & 15u];
-  return uint4{lo.x, lo.y, hi.x, hi.y};
+  const uint32_t byte = __builtin_amdgcn_ubfe(mask, 16 * ks + 8 * (lane >> 5), 8);
+  return lut[byte];
 }
 
 // one slab's operands for one wave: A (G) fragments a[ks][m], B (x) fragments b[ks][n]
@@ -296,7 +292,7 @@ struct WgdRaw {
 };
 
 template <bool SU>
-__device__ __forceinline__ WgdRaw wgd_read(const __bf16* Xt, const uint32_t (&mk)[2], const uint2* lut,
+__device__ __forceinline__ WgdRaw wgd_read(const __bf16* Xt, const uint32_t (&mk)[2], const uint4* lut,
                                            const uint16_t* gs, int ul, int wv) {
   WgdRaw w;
   const int i = threadIdx.x & 31;
@@ -352,7 +348,7 @@ __device__ __forceinline__ int wgd_utt(const DadGeom& g, int s) {
 // one 256 h x WGD_DB d tile over slabs [s0, s1): fp32 partial (direct) or bf16 S_u (SU)
 template <bool SU>
 __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceArgs& ra, int s0, int s1, int dbase,
-                                         float* outf, __bf16* outb, __bf16* Xt, const uint2* lut, uint16_t* gs,
+                                         float* outf, __bf16* outb, __bf16* Xt, const uint4* lut, uint16_t* gs,
                                          float* red) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane((tid >> 6) & 3);
@@ -375,7 +371,7 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
     const int mine = (n - grp + WGD_GROUPS - 1) / WGD_GROUPS;   // group 1 may have one slab fewer
     const int cntmin = n / WGD_GROUPS;
     const int u0 = wgd_utt(g, s0), nu = wgd_utt(g, s1 - 1) - u0 + 1;
-    __bf16* Xg = Xt + grp * (2 * DAD_SLAB * WGD_XP);   // this group's two LDS buffers
+    __bf16* Xg = Xt + grp * (4 * DAD_SLAB * WGD_XP);   // this group's four LDS buffers
     // dL/de_u[h] / max(1, len_u) of this split's utterances (group 0, thread = h) as bf16; the
     // host bounds a split to WGD_MAXU slabs, hence utterances.  The first eight utterances'
     // vector loads go out before the slab prefetch, so their math never waits on it.
@@ -394,6 +390,7 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
     // loads make the compiler merge the paths' pending counts into a vmcnt(0) drain
 #pragma unroll
     for (int k = 0; k < WGD_DEPTH; ++k) wgd_load(a, tab, min(k, jlast), sfirst, dbase, wv, r[k]);
+    const unsigned long long ta = WGD_CLK();
     if (!SU && grp == 0) {
       for (int ul0 = 0; ul0 < nu; ul0 += 8) {
         float v[8];
@@ -408,50 +405,59 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
           if (ul0 + k < nu) gs[(ul0 + k) * DAD_H + tid] = __builtin_bit_cast(uint16_t, (__bf16)v[k]);
       }
     }
-    // slab 0 of each group into buffer 0; its ring slot reloads slab WGD_DEPTH
+    const unsigned long long tb = WGD_CLK();
+    // slabs 0 and 1 of each group into buffers 0 and 1; their ring slots reload slabs 4 and 5
+    static_assert(WGD_DEPTH == 4, "dad_wgrad_direct: four ring slots = four LDS buffers");
     if (mine > 0) wgd_stage(r[0], Xg);
-    int ul = r[0].ul;
-    uint32_t mw[2] = {r[0].mw[0], r[0].mw[1]};
-    wgd_load(a, tab, min(WGD_DEPTH, jlast), sfirst, dbase, wv, r[0]);
+    if (mine > 1) wgd_stage(r[1], Xg + DAD_SLAB * WGD_XP);
+    int ulq[2] = {r[0].ul, r[1].ul};   // utterance slot and row masks of slabs j, j+1 (by parity)
+    uint32_t mwq[2][2] = {{r[0].mw[0], r[0].mw[1]}, {r[1].mw[0], r[1].mw[1]}};
+    wgd_load(a, tab, min(4, jlast), sfirst, dbase, wv, r[0]);
+    wgd_load(a, tab, min(5, jlast), sfirst, dbase, wv, r[1]);
+    const unsigned long long tc = WGD_CLK();
     __syncthreads();
     t1 = WGD_CLK();
-    // round j: read slab j's operands from buffer j&1 into registers | MFMAs of slab j-1 from
-    // the registers read in round j-1 (so they never wait on LDS) | stage slab j+1 into
-    // buffer (j+1)&1 from ring slot (j+1)%DEPTH and reload that slot with slab j+1+DEPTH |
-    // barrier
+    WGD_ACC(3, ta - t0); WGD_ACC(6, tb - ta); WGD_ACC(7, tc - tb); (void)ta; (void)tb; (void)tc;
+    // round j: read slab j's operands from buffer j&3 into registers | MFMAs of slab j-1 from
+    // the registers read in round j-1 (so they never wait on LDS) | stage slab j+2 into
+    // buffer (j+2)&3 from ring slot (j+2)&3 and reload that slot with slab j+6.  A slab is
+    // staged two rounds before it is read, so one barrier per TWO rounds (after odd j) orders
+    // every staging before its reads and every read before its buffer is restaged.
     WgdFrag F;
-    auto round = [&](int jr, int k, bool prev, bool comp, bool stage) {
+    auto round = [&](int jr, int k, bool prev, bool comp, bool stage, bool bar) {
       const unsigned long long c0 = WGD_CLK();
-      const int nk = (k + 1) % WGD_DEPTH;
+      const int nk = (k + 2) % WGD_DEPTH;
       WgdRaw R;
-      if (comp) R = wgd_read<SU>(Xg + (k & 1) * (DAD_SLAB * WGD_XP), mw, lut, gs, ul, wv);
+      if (comp) R = wgd_read<SU>(Xg + (k & 3) * (DAD_SLAB * WGD_XP), mwq[k & 1], lut, gs, ulq[k & 1], wv);
       __builtin_amdgcn_sched_barrier(0);   // reads first, their latency under the MFMAs
       if (prev) wgd_mma(F, acc);
-      if (stage) wgd_stage(r[nk], Xg + ((k + 1) & 1) * (DAD_SLAB * WGD_XP));
-      ul = r[nk].ul;
-      mw[0] = r[nk].mw[0];
-      mw[1] = r[nk].mw[1];
-      wgd_load(a, tab, min(jr + 1 + WGD_DEPTH, jlast), sfirst, dbase, wv, r[nk]);
+      if (stage) wgd_stage(r[nk], Xg + ((k + 2) & 3) * (DAD_SLAB * WGD_XP));
+      ulq[k & 1] = r[nk].ul;
+      mwq[k & 1][0] = r[nk].mw[0];
+      mwq[k & 1][1] = r[nk].mw[1];
+      wgd_load(a, tab, min(jr + 2 + WGD_DEPTH, jlast), sfirst, dbase, wv, r[nk]);
       __builtin_amdgcn_sched_barrier(0);
       if (comp) F = wgd_finish(R);
       const unsigned long long c1 = WGD_CLK();
-      __syncthreads();
+      if (bar) __syncthreads();
       WGD_ACC(4, c1 - c0); WGD_ACC(5, WGD_CLK() - c1); WGD_ACC(8, 1);
       (void)c0; (void)c1;
     };
     // round 0, then blocks of WGD_DEPTH rounds in which both groups have every step (no early
     // exits: an exit inside the block would reach the loop header with a different load
     // order and force vmcnt(0) there; ring slots are compile-time: j = 1 mod WGD_DEPTH at a
-    // block start), then the last rounds with per-group flags and the final MFMAs
-    round(0, 0, false, mine > 0, 1 < mine);
+    // block start), then the last rounds with per-group flags and the final MFMAs.  Both groups
+    // run the same rounds, so the barriers (after odd rounds) match.
+    round(0, 0, false, mine > 0, 2 < mine, false);
     int j = 1;
-    for (; j + WGD_DEPTH <= cntmin - 1; j += WGD_DEPTH) {
+    for (; j + WGD_DEPTH + 1 < cntmin; j += WGD_DEPTH) {   // every round stages slab j + k + 2 < cntmin
 #pragma unroll
-      for (int k = 0; k < WGD_DEPTH; ++k) round(j + k, k + 1, true, true, true);
+      for (int k = 0; k < WGD_DEPTH; ++k) round(j + k, k + 1, true, true, true, (k & 1) == 0);
     }
 #pragma unroll
-    for (int k = 0; k < WGD_DEPTH + 2; ++k)   // nround - j <= WGD_DEPTH + 1
-      if (j + k < nround) round(j + k, k + 1, j + k - 1 < mine, j + k < mine, j + k + 1 < mine);
+    for (int k = 0; k < WGD_DEPTH + 3; ++k)   // nround - j <= WGD_DEPTH + 2
+      if (j + k < nround)
+        round(j + k, k + 1, j + k - 1 < mine, j + k < mine, j + k + 2 < mine, (k & 1) == 0);
     if (nround - 1 < mine) wgd_mma(F, acc);
     t2 = WGD_CLK();
   }
@@ -486,15 +492,15 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
   (void)t0; (void)t1; (void)t2;
 }
 
-// the 16-entry nibble table of the A-fragment masks (threads 0..15)
-__device__ __forceinline__ void wgd_lut(uint2* lut) {
+// the 256-entry byte table of the A-fragment masks (threads 0..255)
+__device__ __forceinline__ void wgd_lut(uint4* lut) {
   const int t = threadIdx.x;
-  if (t < 16) {
-    uint32_t e[2];
+  if (t < 256) {
+    uint32_t e[4];
 #pragma unroll
-    for (int p = 0; p < 2; ++p)
+    for (int p = 0; p < 4; ++p)
       e[p] = (((t >> (2 * p)) & 1) ? 0x0000ffffu : 0u) | (((t >> (2 * p + 1)) & 1) ? 0xffff0000u : 0u);
-    lut[t] = uint2{e[0], e[1]};
+    lut[t] = uint4{e[0], e[1], e[2], e[3]};
   }
 }
 
@@ -502,8 +508,8 @@ __device__ double extra_block(const DadReduceArgs& a, int e, int tid, float (*xs
 
 __global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct(DadWgradArgs a, DadReduceArgs ra) {
   DAD_GUARD_BLOCK(WGD_THREADS);
-  __shared__ __attribute__((aligned(16))) __bf16 Xt[WGD_GROUPS * 2 * DAD_SLAB * WGD_XP];
-  __shared__ __attribute__((aligned(16))) uint2 lut[16];
+  __shared__ __attribute__((aligned(16))) __bf16 Xt[WGD_GROUPS * 4 * DAD_SLAB * WGD_XP];
+  __shared__ __attribute__((aligned(16))) uint4 lut[256];
   __shared__ __attribute__((aligned(16))) uint16_t gs[WGD_MAXU * DAD_H];
   __shared__ __attribute__((aligned(16))) float red[WGD_GROUPS == 2 ? DAD_H * WGD_DB : 1];
   // XCD-aware tile order (grid is a multiple of 8; workgroups go round-robin over the 8
@@ -548,8 +554,8 @@ __global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct(DadWgradArgs 
 // Runs on a side stream concurrently with pool/tail/ECDA; dad_wsum applies dL/de_u / len_u.
 __global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_su(DadWgradArgs a) {
   DAD_GUARD_BLOCK(WGD_THREADS);
-  __shared__ __attribute__((aligned(16))) __bf16 Xt[WGD_GROUPS * 2 * DAD_SLAB * WGD_XP];
-  __shared__ __attribute__((aligned(16))) uint2 lut[16];
+  __shared__ __attribute__((aligned(16))) __bf16 Xt[WGD_GROUPS * 4 * DAD_SLAB * WGD_XP];
+  __shared__ __attribute__((aligned(16))) uint4 lut[256];
   __shared__ __attribute__((aligned(16))) float red[WGD_GROUPS == 2 ? DAD_H * WGD_DB : 1];
   DadReduceArgs unused;
   const DadGeom& g = a.g;

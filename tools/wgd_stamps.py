@@ -32,6 +32,7 @@ def main():
     e = e[e[:, 8] > 0]
     m = e.mean(0)
     print("workgroups %d; cycles: prologue %.0f loop %.0f epilogue %.0f" % (len(e), m[0], m[1], m[2]))
+    print("prologue: to slab loads %.0f, dL/de table %.0f, first staging %.0f, barrier %.0f" % (m[3], m[6], m[7], m[0] - m[3] - m[6] - m[7]))
     print("per round (n=%.1f): compute+stage+load %.0f barrier %.0f" % (m[8], m[4] / m[8], m[5] / m[8]))
 
 
