@@ -172,12 +172,19 @@ __device__ __forceinline__ float keep_value(const uint8_t* keep, uint32_t key, i
 
 
 // LDS-DMA: 16 B per lane of `src` into LDS at lds_dst + 16 * lane (M0 = wave-uniform LDS
-// byte address).  Inline asm: the compiler neither counts it in its vmcnt waits nor drains it
-// at barriers; the caller waits for it (s_waitcnt vmcnt) before reading the LDS bytes.
-__device__ __forceinline__ void dad_glds16(const void* src, uint32_t lds_dst) {
+// byte address), three consecutive 1-KB pieces (src, src + 1 KB, src + 2 KB -> lds_dst, +1 KB,
+// +2 KB) under ONE M0 write: the instruction offset advances the global address and the LDS
+// destination alike.  Inline asm: the compiler neither counts it in its vmcnt waits nor drains
+// it at barriers; the caller waits for it (s_waitcnt vmcnt) before reading the LDS bytes.
+__device__ __forceinline__ void dad_glds16x3(const void* src, uint32_t lds_dst) {
   uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(src), "s"(lds_dst) : "memory");
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "global_load_lds_dwordx4 %1, off offset:1024\n\t"
+      "global_load_lds_dwordx4 %1, off offset:2048\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep) : "v"(src), "s"(lds_dst) : "memory");
 }
 
 // ---------------------------------------------------------------------------------
