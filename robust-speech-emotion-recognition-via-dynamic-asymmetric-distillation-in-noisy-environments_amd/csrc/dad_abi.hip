@@ -509,10 +509,19 @@ int dad_rng_draws(const dad_config* cfg, int which, uint64_t first, size_t n, fl
 }
 
 // ----------------------------------------------------------------- modular encoder ops
+}  // extern "C"
+
+// The modular encoder ops' workspace: the FP32 layout plus the bf16 row-copy region, so the
+// BF16 encoder writes its copies to scratch instead of testing for a missing buffer in the
+// conversion units it interleaves with the MFMA k-steps (a branch there splits the schedule).
+static DadWs enc_layout(const DadGeom& G) {
+  return dad_ws_layout(G, dad_auto_splits(G, DAD_PREC_FP32, 1), DAD_PREC_BF16, false);
+}
+
+extern "C" {
 size_t dad_encoder_workspace_bytes(int B, int T) {
   if (B < 1 || T < 1) return 0;
-  const DadGeom g = dad_geom(B, T, 0, 0);
-  return dad_ws_layout(g, dad_auto_splits(g, DAD_PREC_FP32, 1), DAD_PREC_FP32, false).bytes;
+  return enc_layout(dad_geom(B, T, 0, 0)).bytes;
 }
 
 }  // extern "C"
@@ -558,6 +567,7 @@ int encoder_forward_impl(const float* x, const uint8_t* pad, int B, int T, const
   ea.part_sum = ws_ptr<float>(workspace, L.part_sum);
   ea.part_cnt = ws_ptr<float>(workspace, L.part_cnt);
   ea.bits = ws_ptr<uint32_t>(workspace, L.bits);
+  ea.xs_bf16 = ws_ptr<__bf16>(workspace, L.xs_bf16);
   const dim3 egrid((B * G.ncc + 3) / 4);
   if (precision == DAD_PREC_BF16) {
     int cus = 0;
@@ -603,7 +613,7 @@ int dad_encoder_forward(const float* x, const uint8_t* pad, int B, int T, const 
   if (B < 1 || B > DAD_MAX_BATCH || T < 1) return DAD_E_SHAPE;
   if (precision != DAD_PREC_FP32 && precision != DAD_PREC_BF16) return DAD_E_ARG;
   const DadGeom G = dad_geom(B, T, 0, 0);
-  const DadWs L = dad_ws_layout(G, dad_auto_splits(G, DAD_PREC_FP32, 1), DAD_PREC_FP32, false);
+  const DadWs L = enc_layout(G);
   return encoder_forward_impl(x, pad, B, T, w1, b1, precision, workspace, (hipStream_t)stream, L,
                               ws_ptr<float>(workspace, L.vlen), e_out);
 }
@@ -614,8 +624,8 @@ int dad_encoder_backward(const float* x, const uint8_t* pad, int B, int T, const
   if (B < 1 || B > DAD_MAX_BATCH || T < 1) return DAD_E_SHAPE;
   hipStream_t stream = (hipStream_t)stream_;
   const DadGeom G = dad_geom(B, T, 0, 0);
-  const int splits = dad_auto_splits(G, DAD_PREC_FP32, 1);
-  const DadWs L = dad_ws_layout(G, splits, DAD_PREC_FP32, false);
+  const DadWs L = enc_layout(G);
+  const int splits = L.splits;
   float* vlen = ws_ptr<float>(workspace, L.vlen);
   // recompute the ReLU'/valid bits and per-slab active counts (FP32 forward)
   int rc = encoder_forward_impl(x, pad, B, T, w1, b1, DAD_PREC_FP32, workspace, stream, L, nullptr, nullptr);

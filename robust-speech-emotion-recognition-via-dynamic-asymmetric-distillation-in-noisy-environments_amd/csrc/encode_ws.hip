@@ -303,7 +303,7 @@ struct WsConv {
                     __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{v[2], v[3]}, bf16x2))};
     if constexpr (strong) o = tzero ? uint2{0u, 0u} : o;
     *reinterpret_cast<uint2*>(trow + 512 * k) = o;             // chunk 32k + (lane>>1), swizzled by row
-    if (KIND != KIND_WEAK && C.xs) {   // (the modular encoder op keeps no copy: xs null)
+    if constexpr (KIND != KIND_WEAK) {
       // 32-bit byte offset from the uniform base (saddr store, no 64-bit address math)
       const uint32_t boff = ((uint32_t)grow * (uint32_t)DAD_D + (uint32_t)d) * 2u;
       *reinterpret_cast<uint2*>(reinterpret_cast<char*>(strong ? C.xsn : C.xs) + boff) = o;
@@ -544,7 +544,7 @@ __device__ __forceinline__ void ws_loop(const Ctx& C, const int j0, const int Q,
   };
   // xs stores convert(q) issued (the counted vmcnt waits depend on them; for an empty sub-slab
   // 0 even where it zeroes padded rows' copies: under-counting younger stores only waits longer)
-  auto xs_of = [&](int q) -> int { return (vmask_of(q) && C.xs) ? n_xs<S>(jobq(q).kind) : 0; };
+  auto xs_of = [&](int q) -> int { return vmask_of(q) ? n_xs<S>(jobq(q).kind) : 0; };
   auto dma = [&](int q) {
     if (q < Q) {
       const Job J = jobq(q);
@@ -557,7 +557,7 @@ __device__ __forceinline__ void ws_loop(const Ctx& C, const int j0, const int Q,
     if (vm == 0) {
       // nothing to multiply; the student's bf16 copies of padded frames inside the utterance
       // still get finite bytes (the weight gradient multiplies them by a zero mask)
-      if (!TEACHER && C.xs) ws_zero_xs<S, HN>(C, J, w, lane);
+      if constexpr (!TEACHER) ws_zero_xs<S, HN>(C, J, w, lane);
       return;
     }
     const float* rawp = HN ? raw1 : raw0;
