@@ -169,6 +169,16 @@ __device__ __forceinline__ float keep_value(const uint8_t* keep, uint32_t key, i
   else k = dad_uniform_at(key, (uint32_t)(b * DAD_H + h)) >= p;
   return k ? scale : 0.0f;
 }
+// The same with the explicit-or-counter choice made by the caller, once, outside its loops
+// (EXPLICIT = the mask pointers are set): no load sits inside a branch, so a batch of these
+// keeps its loads in flight instead of draining vmcnt at every call.
+template <bool EXPLICIT>
+__device__ __forceinline__ float keep_value_t(const uint8_t* keep, uint32_t key, int b, int h, float p, float scale) {
+  bool k;
+  if constexpr (EXPLICIT) k = keep[(size_t)b * DAD_H + h] != 0;
+  else k = dad_uniform_at(key, (uint32_t)(b * DAD_H + h)) >= p;
+  return p <= 0.0f ? 1.0f : (k ? scale : 0.0f);
+}
 
 
 // LDS-DMA: 16 B per lane of `src` into LDS at lds_dst + 16 * lane (M0 = wave-uniform LDS

@@ -15,6 +15,8 @@
 // so the GEMM runs as soon as the forward has produced the bits (on a second stream) and
 // dad_wsum applies the scale.  BF16 fused step: dad_wgrad_direct after the losses, with the
 // scale folded into the A operand (one GEMM, no S_u round trip through HBM).
+#include <type_traits>
+
 #include "dad_common.h"
 #include "dad_kernels.h"
 #include "dad_probe.h"
@@ -77,20 +79,29 @@ __device__ __forceinline__ void wg_range(const DadWgradArgs& a, int split, int& 
 // I/model.py:62-63) plus the ECDA part where ECDA wrote the row.
 // ec = ge_ecda[u][h] as loaded by the caller (read whatever the flag: unflagged rows hold
 // stale values and are selected away, so a caller can keep all its loads in flight)
-__device__ __forceinline__ float fused_ge1_ec(const DadReduceArgs& a, int Bc, int u, int h, const float (&w2)[4],
-                                              float ec, float* kv_out = nullptr) {
-  const f32x4 gz = *reinterpret_cast<const f32x4*>(a.gzb + (size_t)u * DAD_C);
+// EX: explicit dropout masks (a.keep1 set), chosen by the caller outside its loops
+// (gz = dL/dz[u], ef = eflag[u], ec as loaded by the caller)
+template <bool EX>
+__device__ __forceinline__ float fused_ge1_v(const DadReduceArgs& a, int Bc, int u, int h, const float (&w2)[4],
+                                             const f32x4& gz, uint32_t ef, float ec, float* kv_out = nullptr) {
   const bool strong = u >= Bc;
   const int b = strong ? u - Bc : u;
-  const float kv = strong ? keep_value(a.keep2, a.key_drop2, b, h, a.p_drop, a.drop_scale)
-                          : keep_value(a.keep1, a.key_drop1, b, h, a.p_drop, a.drop_scale);
+  const float kv = keep_value_t<EX>(strong ? a.keep2 : a.keep1, strong ? a.key_drop2 : a.key_drop1, b, h, a.p_drop,
+                                    a.drop_scale);
   if (kv_out) *kv_out = kv;
   const float z = ((w2[0] * gz[0] + w2[1] * gz[1]) + w2[2] * gz[2]) + w2[3] * gz[3];
-  return z * kv + (a.eflag[u] ? ec : 0.0f);
+  return z * kv + (ef ? ec : 0.0f);
 }
+template <bool EX>
+__device__ __forceinline__ float fused_ge1_ec(const DadReduceArgs& a, int Bc, int u, int h, const float (&w2)[4],
+                                              float ec, float* kv_out = nullptr) {
+  return fused_ge1_v<EX>(a, Bc, u, h, w2, *reinterpret_cast<const f32x4*>(a.gzb + (size_t)u * DAD_C), a.eflag[u], ec,
+                         kv_out);
+}
+template <bool EX>
 __device__ __forceinline__ float fused_ge1(const DadReduceArgs& a, int Bc, int u, int h, const float (&w2)[4],
                                            float* kv_out = nullptr) {
-  return fused_ge1_ec(a, Bc, u, h, w2, a.ge_ecda[(size_t)u * DAD_H + h], kv_out);
+  return fused_ge1_ec<EX>(a, Bc, u, h, w2, a.ge_ecda[(size_t)u * DAD_H + h], kv_out);
 }
 
 }  // namespace
@@ -375,12 +386,22 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
     // dL/de_u[h] / max(1, len_u) of this split's utterances (group 0, thread = h) as bf16; the
     // host bounds a split to WGD_MAXU slabs, hence utterances.  The first eight utterances'
     // vector loads go out before the slab prefetch, so their math never waits on it.
-    float w2[4] = {0.0f, 0.0f, 0.0f, 0.0f}, ec0[8];
+    // (the first eight utterances' dL/dz, ECDA flag and length too: all of the table's
+    // inputs for a split of <= 8 utterances are in flight before the first slab load)
+    float w2[4] = {0.0f, 0.0f, 0.0f, 0.0f}, ec0[8], vl0[8];
+    f32x4 gz0[8];
+    uint32_t ef0[8];
     if (!SU && grp == 0) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) w2[c] = ra.student[DAD_OFF_W2 + c * DAD_H + tid];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) ec0[k] = ra.ge_ecda[(size_t)(u0 + min(k, nu - 1)) * DAD_H + tid];
+      for (int k = 0; k < 8; ++k) {
+        const int u = u0 + min(k, nu - 1);
+        ec0[k] = ra.ge_ecda[(size_t)u * DAD_H + tid];
+        gz0[k] = *reinterpret_cast<const f32x4*>(ra.gzb + (size_t)u * DAD_C);
+        ef0[k] = ra.eflag[u];
+        vl0[k] = ra.vlen[u];
+      }
     }
     const int sfirst = s0 + grp;
     const WgdTable tab = wgd_table(g, min(sfirst + WGD_GROUPS * lane, s1 - 1), u0);
@@ -391,19 +412,24 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
 #pragma unroll
     for (int k = 0; k < WGD_DEPTH; ++k) wgd_load(a, tab, min(k, jlast), sfirst, dbase, wv, r[k]);
     const unsigned long long ta = WGD_CLK();
-    if (!SU && grp == 0) {
+    auto ge_table = [&](auto ex_tag) {
+      constexpr bool EX = decltype(ex_tag)::value;
       for (int ul0 = 0; ul0 < nu; ul0 += 8) {
         float v[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {   // eight utterances' loads in flight (index clamped)
           const int u = u0 + min(ul0 + k, nu - 1);
-          v[k] = (ul0 == 0 ? fused_ge1_ec(ra, g.Bc, u, tid, w2, ec0[k]) : fused_ge1(ra, g.Bc, u, tid, w2)) /
-                 fmaxf(ra.vlen[u], 1.0f);
+          v[k] = ul0 == 0 ? fused_ge1_v<EX>(ra, g.Bc, u, tid, w2, gz0[k], ef0[k], ec0[k]) / fmaxf(vl0[k], 1.0f)
+                          : fused_ge1<EX>(ra, g.Bc, u, tid, w2) / fmaxf(ra.vlen[u], 1.0f);
         }
 #pragma unroll
         for (int k = 0; k < 8; ++k)
           if (ul0 + k < nu) gs[(ul0 + k) * DAD_H + tid] = __builtin_bit_cast(uint16_t, (__bf16)v[k]);
       }
+    };
+    if (!SU && grp == 0) {
+      if (ra.keep1) ge_table(std::true_type{});
+      else ge_table(std::false_type{});
     }
     const unsigned long long tb = WGD_CLK();
     // slabs 0 and 1 of each group into buffers 0 and 1; their ring slots reload slabs 4 and 5
@@ -581,7 +607,8 @@ __global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_su(DadWgradArgs a) {
 static_assert(DAD_REDUCE_THREADS == 256 && DAD_H == 16 * DAD_REDUCE_XBLK, "extra blocks: 16 h x 16 row groups");
 
 // run by 256 threads (tid = 0..255 of a workgroup or of half of one), combining in xs
-__device__ double extra_block(const DadReduceArgs& a, int e, int tid, float (*xs)[16][6]) {
+template <bool EX>
+__device__ double extra_block_t(const DadReduceArgs& a, int e, int tid, float (*xs)[16][6]) {
   const int hl = tid & 15, rg = tid >> 4;
   const int h = 16 * e + hl;
   const DadGeom& g = a.g;
@@ -603,7 +630,7 @@ __device__ double extra_block(const DadReduceArgs& a, int e, int tid, float (*xs
       const int r = min(r0 + 16 * k, nb - 1);
       kv[k] = 1.0f;
       if (fused) {
-        gv[k] = fused_ge1(a, g.Bc, r, h, w2, &kv[k]);
+        gv[k] = fused_ge1<EX>(a, g.Bc, r, h, w2, &kv[k]);
         const int erow = r >= g.Bc ? g.Bn + r : r;   // strong row b lives at Bc + Bn + b
         em[k] = a.emb[(size_t)erow * DAD_H + h];
         gzv[k] = *reinterpret_cast<const f32x4*>(a.gzb + (size_t)r * DAD_C);
@@ -662,6 +689,9 @@ __device__ double extra_block(const DadReduceArgs& a, int e, int tid, float (*xs
     ex[15] = ecda_l;
   }
   return sq;
+}
+__device__ double extra_block(const DadReduceArgs& a, int e, int tid, float (*xs)[16][6]) {
+  return a.keep1 ? extra_block_t<true>(a, e, tid, xs) : extra_block_t<false>(a, e, tid, xs);
 }
 
 static_assert(DAD_REDUCE_THREADS == 4 * (DAD_REDUCE_COLS / 4), "dad_reduce: 4 split groups x float4 columns");
@@ -726,7 +756,8 @@ __global__ __launch_bounds__(DAD_REDUCE_THREADS) void dad_wsum(DadReduceArgs a) 
     const float w2h[4] = {a.student[DAD_OFF_W2 + h], a.student[DAD_OFF_W2 + DAD_H + h],
                           a.student[DAD_OFF_W2 + 2 * DAD_H + h], a.student[DAD_OFF_W2 + 3 * DAD_H + h]};
     for (int u = tid; u < nutt; u += DAD_REDUCE_THREADS)
-      gsh[u] = fused_ge1(a, g.Bc, u, h, w2h) / fmaxf(a.vlen[u], 1.0f);
+      gsh[u] = (a.keep1 ? fused_ge1<true>(a, g.Bc, u, h, w2h) : fused_ge1<false>(a, g.Bc, u, h, w2h)) /
+               fmaxf(a.vlen[u], 1.0f);
     __syncthreads();
     const int col = tid & (DAD_REDUCE_COLS / 4 - 1), ug = tid / (DAD_REDUCE_COLS / 4);
     const size_t off = (size_t)h * DAD_D + dcol0 + (size_t)col * 4;
