@@ -128,10 +128,22 @@ struct Job {
 
 // job j of the workgroup's role list: teacher -> weak slab j; student -> clean slab j, then
 // strong slab j - Jc.  Slab numbering matches dad_pool / the weight gradient.
+// WS_MIX: the student list alternates clean and strong slabs (clean s, strong s, clean s+1, ...;
+// the longer list's remainder last), so a student workgroup's DMA/store-heavy clean sub-slabs
+// and RNG-heavy strong sub-slabs overlap instead of running in separate workgroups.
+#ifndef WS_MIX
+#define WS_MIX 0
+#endif
 __device__ __forceinline__ Job job_of(const Ctx& C, bool teacher, int j) {
   Job J;
+#if WS_MIX
+  const int m = min(C.Jc, C.Js);
+  const bool noisy = teacher || (j < 2 * m ? (j & 1) : C.Js > C.Jc);
+  const int s = teacher ? j : (j < 2 * m ? j >> 1 : j - m);
+#else
   const bool noisy = teacher || j >= C.Jc;
   const int s = (teacher || j < C.Jc) ? j : j - C.Jc;
+#endif
   const int nc = noisy ? C.ncn : C.ncc;
   J.kind = teacher ? KIND_WEAK : (noisy ? KIND_STRONG : KIND_CLEAN);
   J.b = fast_div(s, noisy ? C.mcn : C.mcc);
@@ -162,7 +174,14 @@ __device__ __forceinline__ void job_range(const Ctx& C, int wg, int nt, int ns, 
   auto at = [&](int kk) -> int {
     if (kk >= ns) return C.Jc + C.Js;
     const float B = wtot * (float)kk / (float)ns;
+#if WS_MIX
+    // cost of the first j jobs: (j >> 1)(1 + wstrong) + (j & 1) in the alternating part
+    const int m = min(C.Jc, C.Js);
+    const float pm = (float)m * (1.0f + wstrong), wr = C.Js > C.Jc ? wstrong : 1.0f;
+    const int j = B <= pm ? (int)(2.0f * B / (1.0f + wstrong) + 0.5f) : 2 * m + (int)((B - pm) / wr + 0.5f);
+#else
     const int j = B <= (float)C.Jc ? (int)(B + 0.5f) : C.Jc + (int)((B - (float)C.Jc) / wstrong + 0.5f);
+#endif
     return j < 0 ? 0 : (j > C.Jc + C.Js ? C.Jc + C.Js : j);
   };
   j0 = at(k);
