@@ -122,7 +122,7 @@ int device_cus(int* out) {
 // CU, teacher : student in proportion to their work (32-row slab costs: clean 1, weak
 // kWsWeak, strong kWsStrong -- the augmentation RNG dominates a noisy slab), more
 // workgroups than CUs only when a range would exceed DAD_ENC_WS_MAXJ jobs.
-constexpr float kWsWeak = 1.03f, kWsStrong = 1.47f;   // measured (tools/ws_stamps.py fit)
+constexpr float kWsWeak = 1.03f, kWsStrong = 1.55f;   // sweeps of 300-step benches (tools/gpu_ws_sweep.sh)
 // DAD_WS_WEIGHTS="weak,strong" overrides the two costs (tuning runs; read once per process)
 struct WsWeights { float weak, strong; };
 WsWeights ws_weights() {
@@ -150,7 +150,8 @@ void ws_split(const DadGeom& G, int Bn, int cus, int& nt, int& ns) {
     nt = std::min(nt, Jt);
     ns = std::min(ns, Jc + Js);
   }
-  nt = std::max(nt, (Jt + DAD_ENC_WS_MAXJ - 1) / DAD_ENC_WS_MAXJ);
+  // ranges are priced by live sub-slabs (encode_ws.hip job_range): within two jobs of the even split
+  nt = std::max(nt, (Jt + DAD_ENC_WS_MAXJ - 3) / (DAD_ENC_WS_MAXJ - 2));
   const double wtot = Jc + Js * (double)kWsStrong;
   ns = std::max(ns, (int)(wtot / (DAD_ENC_WS_MAXJ - 2)) + 1);
 }

@@ -128,22 +128,10 @@ struct Job {
 
 // job j of the workgroup's role list: teacher -> weak slab j; student -> clean slab j, then
 // strong slab j - Jc.  Slab numbering matches dad_pool / the weight gradient.
-// WS_MIX: the student list alternates clean and strong slabs (clean s, strong s, clean s+1, ...;
-// the longer list's remainder last), so a student workgroup's DMA/store-heavy clean sub-slabs
-// and RNG-heavy strong sub-slabs overlap instead of running in separate workgroups.
-#ifndef WS_MIX
-#define WS_MIX 0
-#endif
 __device__ __forceinline__ Job job_of(const Ctx& C, bool teacher, int j) {
   Job J;
-#if WS_MIX
-  const int m = min(C.Jc, C.Js);
-  const bool noisy = teacher || (j < 2 * m ? (j & 1) : C.Js > C.Jc);
-  const int s = teacher ? j : (j < 2 * m ? j >> 1 : j - m);
-#else
   const bool noisy = teacher || j >= C.Jc;
   const int s = (teacher || j < C.Jc) ? j : j - C.Jc;
-#endif
   const int nc = noisy ? C.ncn : C.ncc;
   J.kind = teacher ? KIND_WEAK : (noisy ? KIND_STRONG : KIND_CLEAN);
   J.b = fast_div(s, noisy ? C.mcn : C.mcc);
@@ -158,31 +146,38 @@ __device__ __forceinline__ Job job_of(const Ctx& C, bool teacher, int j) {
   return J;
 }
 
-// Contiguous job range of workgroup wg.  Teacher workgroups split the weak slabs evenly;
-// student workgroups split clean (cost 1) + strong (cost wstrong) slabs by cost.
+// Contiguous job range of workgroup wg, split by cost in live 16-row sub-slabs: the last slab
+// of an utterance holds ceil(T/16) - 2(nc-1) of them (one at T = 300: rows 304..319 are
+// skipped), so a range of whole jobs is priced by the sub-slabs it runs, not by its job count.
+// Teacher workgroups split the weak sub-slabs; student workgroups the clean (cost 1) + strong
+// (cost wstrong) sub-slabs.
+// cumulative live sub-slabs of the first j jobs of one branch (nc slabs, L live sub-slabs per
+// utterance), and the job boundary nearest to x of them
+__device__ __forceinline__ int live_jobs_at(float x, int nc, int L, int J) {
+  if (x <= 0.0f) return 0;
+  const int b = (int)(x / (float)L);
+  const float r = x - (float)b * (float)L;
+  const int c = min((int)(0.5f * r + 0.5f), nc);
+  return min(b * nc + c, J);
+}
 __device__ __forceinline__ void job_range(const Ctx& C, int wg, int nt, int ns, float wstrong, bool& teacher,
                                           int& j0, int& j1) {
-  const int Jt = C.Js;
+  const int Lc = (C.Tc + kSub - 1) / kSub, Ln = (C.Tn + kSub - 1) / kSub;
   teacher = wg < nt;
   if (teacher) {
-    j0 = (int)((long)wg * Jt / nt);
-    j1 = (int)((long)(wg + 1) * Jt / nt);
+    const float tot = (float)C.Bn * (float)Ln;
+    auto at = [&](int k) { return k >= nt ? C.Js : live_jobs_at(tot * (float)k / (float)nt, C.ncn, Ln, C.Js); };
+    j0 = at(wg);
+    j1 = at(wg + 1);
     return;
   }
   const int k = wg - nt;
-  const float wtot = (float)C.Jc + (float)C.Js * wstrong;
+  const float cc = C.Jc ? (float)C.Bc * (float)Lc : 0.0f;      // clean cost
+  const float wtot = cc + (C.Js ? (float)C.Bn * (float)Ln * wstrong : 0.0f);
   auto at = [&](int kk) -> int {
     if (kk >= ns) return C.Jc + C.Js;
     const float B = wtot * (float)kk / (float)ns;
-#if WS_MIX
-    // cost of the first j jobs: (j >> 1)(1 + wstrong) + (j & 1) in the alternating part
-    const int m = min(C.Jc, C.Js);
-    const float pm = (float)m * (1.0f + wstrong), wr = C.Js > C.Jc ? wstrong : 1.0f;
-    const int j = B <= pm ? (int)(2.0f * B / (1.0f + wstrong) + 0.5f) : 2 * m + (int)((B - pm) / wr + 0.5f);
-#else
-    const int j = B <= (float)C.Jc ? (int)(B + 0.5f) : C.Jc + (int)((B - (float)C.Jc) / wstrong + 0.5f);
-#endif
-    return j < 0 ? 0 : (j > C.Jc + C.Js ? C.Jc + C.Js : j);
+    return B <= cc ? live_jobs_at(B, C.ncc, Lc, C.Jc) : C.Jc + live_jobs_at((B - cc) / wstrong, C.ncn, Ln, C.Js);
   };
   j0 = at(k);
   j1 = at(k + 1);
@@ -257,6 +252,9 @@ __device__ __forceinline__ int live_rows(const Job& J, int half, int w) {
 #ifndef WS_REGION
 #define WS_REGION 1
 #endif
+#ifndef WS_WT
+#define WS_WT 1        // bf16 copy stores write-through (sc1): no dirty L2 lines at the kernel end (A/B: -0.5 us)
+#endif
 #ifndef WS_PRIO
 #define WS_PRIO 0      // static s_setprio 1 for: 0 no wave, 1 waves WAVES/2.., 2 waves ..WAVES/2-1
 #endif
@@ -325,7 +323,10 @@ struct WsConv {
     if constexpr (KIND != KIND_WEAK) {
       // 32-bit byte offset from the uniform base (saddr store, no 64-bit address math)
       const uint32_t boff = ((uint32_t)grow * (uint32_t)DAD_D + (uint32_t)d) * 2u;
-      *reinterpret_cast<uint2*>(reinterpret_cast<char*>(strong ? C.xsn : C.xs) + boff) = o;
+      if constexpr (WS_WT)
+        __hip_atomic_store(reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(strong ? C.xsn : C.xs) + boff),
+                           __builtin_bit_cast(uint64_t, o), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else *reinterpret_cast<uint2*>(reinterpret_cast<char*>(strong ? C.xsn : C.xs) + boff) = o;
     }
   }
   template <int U = 0>

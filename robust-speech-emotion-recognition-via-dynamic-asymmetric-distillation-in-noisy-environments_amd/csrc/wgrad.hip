@@ -356,6 +356,10 @@ __device__ __forceinline__ int wgd_utt(const DadGeom& g, int s) {
 
 }  // namespace
 
+// WGD_WT: partial-slab stores write-through (sc1): no dirty L2 lines left for the kernel-end release
+#ifndef WGD_WT
+#define WGD_WT 0
+#endif
 // one 256 h x WGD_DB d tile over slabs [s0, s1): fp32 partial (direct) or bf16 S_u (SU)
 template <bool SU>
 __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceArgs& ra, int s0, int s1, int dbase,
@@ -511,6 +515,7 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
           const int d = 32 * nn + (lane & 31);
           const float v = acc[m][nn][rr] + (WGD_GROUPS == 2 ? red[h * WGD_DB + d] : 0.0f);
           if constexpr (SU) outb[(size_t)h * DAD_D + dbase + d] = (__bf16)v;
+          else if constexpr (WGD_WT) __hip_atomic_store(outf + (size_t)h * DAD_D + dbase + d, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           else outf[(size_t)h * DAD_D + dbase + d] = v;
         }
   if constexpr (WGD_GROUPS == 2) __syncthreads();   // red free for the next tile
