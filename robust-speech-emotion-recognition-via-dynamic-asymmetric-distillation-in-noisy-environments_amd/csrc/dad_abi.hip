@@ -324,6 +324,9 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   if (!cfg->warmup && DAD_FUSED_TAIL) {
     hipLaunchKernelGGL(dad_tail_ecda, dim3(1 + DAD_C), dim3(DAD_TAIL_THREADS), 0, stream, ta, ca);
     DAD_TRY(hipGetLastError());
+#ifdef DAD_PROBE_TAIL_TWICE   // diagnostic: a second (idempotent) launch runs with its code warm
+    hipLaunchKernelGGL(dad_tail_ecda, dim3(1 + DAD_C), dim3(DAD_TAIL_THREADS), 0, stream, ta, ca);
+#endif
   } else {
     hipLaunchKernelGGL(dad_tail, dim3(1), dim3(DAD_TAIL_THREADS), 0, stream, ta);
     DAD_TRY(hipGetLastError());

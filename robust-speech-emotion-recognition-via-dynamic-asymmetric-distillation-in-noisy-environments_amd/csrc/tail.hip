@@ -680,6 +680,7 @@ __device__ __forceinline__ float ecda_mmd_coef(EcdaSmem& S, const RW& R, int n, 
     const int sl = item & (ks - 1);
     int bi = 0, bj = 0;
     if (on) ecda_tri(item >> lks, nb, bi, bj);
+    ECDA_STAMP(20);
     // packed accumulators: (sum over even dims, sum over odd dims) of each pair, so the
     // squares accumulate by v_pk_fma_f32 (half the VALU issues of scalar FMAs)
     f32x2 acc2[4][4];
@@ -720,6 +721,8 @@ __device__ __forceinline__ float ecda_mmd_coef(EcdaSmem& S, const RW& R, int n, 
     for (int p = 0; p < 4; ++p)
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[4 * p + r] = acc2[p][r][0] + acc2[p][r][1];
+    DAD_PROBE_FENCE2(v[0], v[15]);
+    ECDA_STAMP(21);
     // combine the slices: lane sl ends with pairs [base, base + 16/ks) of the block
     int base = 0;
     switch (lks) {
@@ -729,6 +732,8 @@ __device__ __forceinline__ float ecda_mmd_coef(EcdaSmem& S, const RW& R, int n, 
       case 3: base = ecda_reduce_scatter<8>(v, sl); break;
       default: base = ecda_reduce_scatter<16>(v, sl); break;
     }
+    DAD_PROBE_FENCE2(v[0], v[1]);
+    ECDA_STAMP(22);
     if (on) {
       const int m = 16 >> lks;
 #pragma unroll

@@ -53,7 +53,8 @@ def main():
         o = c * S
         parts = ["%s %.2f" % (names[k], rel(o + k)) for k in range(9) if on(o + k)]
         sub = ["%s %.2f" % (nm, rel(o + k)) for k, nm in ((12, "dist"), (13, "sumD"), (14, "coef"), (15, "terms"),
-                                                          (16, "cnt"), (17, "cpart"), (18, "cbar"), (19, "stage0"))
+                                                          (16, "cnt"), (17, "cpart"), (18, "cbar"), (19, "stage0"),
+                                                          (20, "d-tri"), (21, "d-acc"), (22, "d-rs"))
                if on(o + k)]
         print("ecda class %d (n=%d ns=%d): %s | sub: %s" % (c, last[o + 10], last[o + 11], "  ".join(parts), "  ".join(sub)))
 
