@@ -255,6 +255,9 @@ __device__ __forceinline__ int live_rows(const Job& J, int half, int w) {
 #ifndef WS_WT
 #define WS_WT 1        // bf16 copy stores write-through (sc1): no dirty L2 lines at the kernel end (A/B: -0.5 us)
 #endif
+#ifndef WS_LDS_FIRST
+#define WS_LDS_FIRST 0
+#endif
 #ifndef WS_PRIO
 #define WS_PRIO 0      // static s_setprio 1 for: 0 no wave, 1 waves WAVES/2.., 2 waves ..WAVES/2-1
 #endif
@@ -292,6 +295,12 @@ struct WsConv {
     char* trow = tile + r * kTileRow + 16 * ((lane >> 1) ^ (r & 15)) + 8 * (lane & 1);
     const int d = 256 * k + 4 * lane;
     f32x4 v = *reinterpret_cast<const f32x4*>(rrow + 256 * k);
+    [[maybe_unused]] f32x4 kp;
+    if constexpr (strong) kp = *reinterpret_cast<const f32x4*>(fk + d);
+#if WS_LDS_FIRST
+    // the unit's LDS reads go out before its RNG chain, which then covers their latency
+    if constexpr (KIND != KIND_CLEAN) __builtin_amdgcn_sched_barrier(0);
+#endif
     if constexpr (KIND != KIND_CLEAN) {
       f32x4 n;
       if constexpr (NOISE) {
@@ -310,7 +319,6 @@ struct WsConv {
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = v[e] + n[e];
       if constexpr (strong) {
-        const f32x4 kp = *reinterpret_cast<const f32x4*>(fk + d);
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = v[e] * kp[e];
       }
