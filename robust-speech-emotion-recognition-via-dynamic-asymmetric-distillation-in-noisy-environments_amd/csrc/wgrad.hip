@@ -387,21 +387,23 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
     const int cntmin = n / WGD_GROUPS;
     const int u0 = wgd_utt(g, s0), nu = wgd_utt(g, s1 - 1) - u0 + 1;
     __bf16* Xg = Xt + grp * (4 * DAD_SLAB * WGD_XP);   // this group's four LDS buffers
-    // dL/de_u[h] / max(1, len_u) of this split's utterances (group 0, thread = h) as bf16; the
-    // host bounds a split to WGD_MAXU slabs, hence utterances.  The first eight utterances'
-    // vector loads go out before the slab prefetch, so their math never waits on it.
-    // (the first eight utterances' dL/dz, ECDA flag and length too: all of the table's
-    // inputs for a split of <= 8 utterances are in flight before the first slab load)
-    float w2[4] = {0.0f, 0.0f, 0.0f, 0.0f}, ec0[8], vl0[8];
-    f32x4 gz0[8];
-    uint32_t ef0[8];
-    if (!SU && grp == 0) {
+    // dL/de_u[h] / max(1, len_u) of this split's utterances (thread = h of each group) as bf16;
+    // the host bounds a split to WGD_MAXU slabs, hence utterances.  In each batch of eight
+    // utterances group g builds entries 4g .. 4g+3 (KG per group).  The first batch's vector
+    // loads (dL/dz, ECDA row and flag, length) go out before the slab prefetch, so their math
+    // never waits on it.
+    constexpr int KG = 8 / WGD_GROUPS;
+    const int hh = tid & (DAD_H - 1);
+    float w2[4] = {0.0f, 0.0f, 0.0f, 0.0f}, ec0[KG], vl0[KG];
+    f32x4 gz0[KG];
+    uint32_t ef0[KG];
+    if (!SU) {
 #pragma unroll
-      for (int c = 0; c < 4; ++c) w2[c] = ra.student[DAD_OFF_W2 + c * DAD_H + tid];
+      for (int c = 0; c < 4; ++c) w2[c] = ra.student[DAD_OFF_W2 + c * DAD_H + hh];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int u = u0 + min(k, nu - 1);
-        ec0[k] = ra.ge_ecda[(size_t)u * DAD_H + tid];
+      for (int k = 0; k < KG; ++k) {
+        const int u = u0 + min(grp * KG + k, nu - 1);
+        ec0[k] = ra.ge_ecda[(size_t)u * DAD_H + hh];
         gz0[k] = *reinterpret_cast<const f32x4*>(ra.gzb + (size_t)u * DAD_C);
         ef0[k] = ra.eflag[u];
         vl0[k] = ra.vlen[u];
@@ -419,19 +421,21 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
     auto ge_table = [&](auto ex_tag) {
       constexpr bool EX = decltype(ex_tag)::value;
       for (int ul0 = 0; ul0 < nu; ul0 += 8) {
-        float v[8];
+        float v[KG];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {   // eight utterances' loads in flight (index clamped)
-          const int u = u0 + min(ul0 + k, nu - 1);
-          v[k] = ul0 == 0 ? fused_ge1_v<EX>(ra, g.Bc, u, tid, w2, gz0[k], ef0[k], ec0[k]) / fmaxf(vl0[k], 1.0f)
-                          : fused_ge1<EX>(ra, g.Bc, u, tid, w2) / fmaxf(ra.vlen[u], 1.0f);
+        for (int k = 0; k < KG; ++k) {   // the group's utterances' loads in flight (index clamped)
+          const int u = u0 + min(ul0 + grp * KG + k, nu - 1);
+          v[k] = ul0 == 0 ? fused_ge1_v<EX>(ra, g.Bc, u, hh, w2, gz0[k], ef0[k], ec0[k]) / fmaxf(vl0[k], 1.0f)
+                          : fused_ge1<EX>(ra, g.Bc, u, hh, w2) / fmaxf(ra.vlen[u], 1.0f);
         }
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-          if (ul0 + k < nu) gs[(ul0 + k) * DAD_H + tid] = __builtin_bit_cast(uint16_t, (__bf16)v[k]);
+        for (int k = 0; k < KG; ++k) {
+          const int uk = ul0 + grp * KG + k;
+          if (uk < nu) gs[uk * DAD_H + hh] = __builtin_bit_cast(uint16_t, (__bf16)v[k]);
+        }
       }
     };
-    if (!SU && grp == 0) {
+    if (!SU) {
       if (ra.keep1) ge_table(std::true_type{});
       else ge_table(std::false_type{});
     }
