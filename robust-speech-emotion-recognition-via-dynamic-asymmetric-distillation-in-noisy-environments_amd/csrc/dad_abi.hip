@@ -136,6 +136,13 @@ WsWeights ws_weights() {
   }();
   return w;
 }
+// DAD_WS_TABLE=1 turns the student range table on (off by default: at B=64, T=300 it brings the
+// modelled slowest student range from 18.6 to 17.5 clean-sub-slab units, but the launch measured
+// unchanged (62.7 vs 63.0 us) in A/B runs; read once per process)
+bool ws_table_on() {
+  static const bool on = [] { const char* e = getenv("DAD_WS_TABLE"); return e && strcmp(e, "1") == 0; }();
+  return on;
+}
 void ws_split(const DadGeom& G, int Bn, int cus, int& nt, int& ns) {
   const float kWsWeak = ws_weights().weak, kWsStrong = ws_weights().strong;
   const int Jt = Bn * G.ncn, Jc = G.Bc * G.ncc, Js = Jt;
@@ -154,6 +161,58 @@ void ws_split(const DadGeom& G, int Bn, int cus, int& nt, int& ns) {
   nt = std::max(nt, (Jt + DAD_ENC_WS_MAXJ - 3) / (DAD_ENC_WS_MAXJ - 2));
   const double wtot = Jc + Js * (double)kWsStrong;
   ns = std::max(ns, (int)(wtot / (DAD_ENC_WS_MAXJ - 2)) + 1);
+}
+
+// Student ranges of the W-stationary encoder by a min-max assignment: every student workgroup
+// takes a contiguous run of strong jobs, then a contiguous run of clean jobs, filled up to a
+// common cost bound T (jobs priced by live 16-row sub-slabs: clean 1, strong wstrong); the
+// smallest T that places every job in ns workgroups (bisection).  The clean jobs (cost 2 or 1)
+// fill what the coarser strong jobs (2 wstrong) leave, so the slowest range sits about half a
+// clean job above the mean instead of up to a strong job (ws_split's contiguous ranges).
+// Cached per geometry: computed once, then copied into each launch's arguments.
+bool ws_student_table(const DadGeom& G, int Bn, int ns, float wstrong, DadEncodeArgs& ea) {
+  const int Jc = G.Bc * G.ncc, Js = Bn * G.ncn;
+  ea.ws_tab_n = 0;
+  if (ns <= 0 || ns > DAD_WS_TAB || Jc + Js == 0 || Jc > 65535 || Js > 65535) return false;
+  struct Key { int Bc, Tc, Bn, Tn, ns; float w; };
+  static thread_local Key key{-1, -1, -1, -1, -1, 0.0f};
+  static thread_local uint16_t tab[DAD_WS_TAB][4];
+  const Key k{G.Bc, G.Tc, Bn, G.Tn, ns, wstrong};
+  if (!(key.Bc == k.Bc && key.Tc == k.Tc && key.Bn == k.Bn && key.Tn == k.Tn && key.ns == k.ns && key.w == k.w)) {
+    auto live = [](int c, int T) { return (c * DAD_SLAB + 16 < T) ? 2 : 1; };   // live sub-slabs of slab c
+    auto cs = [&](int j) { return wstrong * (float)live(j % G.ncn, G.Tn); };
+    auto cc = [&](int j) { return (float)live(j % G.ncc, G.Tc); };
+    // greedy fill to T; returns the workgroups used (ns + 1 when T is too small)
+    auto fill = [&](float T, bool write) {
+      int sp = 0, cp = 0, k = 0;
+      for (; k < ns && (sp < Js || cp < Jc); ++k) {
+        float cost = 0.0f;
+        const int s0 = sp, c0 = cp;
+        while (sp < Js && sp - s0 < DAD_ENC_WS_MAXJ - 2 && cost + cs(sp) <= T) cost += cs(sp++);
+        while (cp < Jc && (sp - s0) + (cp - c0) < DAD_ENC_WS_MAXJ - 2 && cost + cc(cp) <= T) cost += cc(cp++);
+        if (sp == s0 && cp == c0) return ns + 1;   // a single job above T
+        if (write) { tab[k][0] = (uint16_t)s0; tab[k][1] = (uint16_t)sp; tab[k][2] = (uint16_t)c0; tab[k][3] = (uint16_t)cp; }
+      }
+      if (sp < Js || cp < Jc) return ns + 1;
+      if (write)
+        for (int r = k; r < ns; ++r) { tab[r][0] = tab[r][1] = (uint16_t)Js; tab[r][2] = tab[r][3] = (uint16_t)Jc; }
+      return k;
+    };
+    float tot = 0.0f, jmax = 0.0f;
+    for (int j = 0; j < Js; ++j) { tot += cs(j); jmax = std::max(jmax, cs(j)); }
+    for (int j = 0; j < Jc; ++j) { tot += cc(j); jmax = std::max(jmax, cc(j)); }
+    float lo = tot / (float)ns, hi = lo + 2.0f * jmax + 1.0f;
+    if (fill(hi, false) > ns) return false;
+    for (int it = 0; it < 24; ++it) {
+      const float mid = 0.5f * (lo + hi);
+      if (fill(mid, false) <= ns) hi = mid; else lo = mid;
+    }
+    fill(hi, true);
+    key = k;
+  }
+  memcpy(ea.ws_tab, tab, sizeof(uint16_t) * 4 * (size_t)ns);
+  ea.ws_tab_n = ns;
+  return true;
 }
 
 }  // namespace
@@ -243,6 +302,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
       if (rc) return rc;
       ws_split(G, Bn, cus, ea.ws_nt, ea.ws_ns);
       ea.ws_wstrong = ws_weights().strong;
+      if (ws_table_on()) ws_student_table(G, Bn, ea.ws_ns, ea.ws_wstrong, ea);
       if (ea.ws_nt + ea.ws_ns > 0) {
         if (explicit_rng) hipLaunchKernelGGL(dad_encode_ws_explicit, dim3(ea.ws_nt + ea.ws_ns), dim3(DAD_ENC_WS_THREADS), 0,
                                              stream, ea);

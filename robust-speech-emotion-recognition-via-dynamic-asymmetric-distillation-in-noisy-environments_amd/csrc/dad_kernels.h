@@ -7,6 +7,7 @@
 #define DAD_ENC_F32_THREADS 256
 #define DAD_ENC_WS_THREADS 512                               // W-stationary bf16 encoder (8 waves, two per SIMD)
 #define DAD_ENC_WS_MAXJ 256                                  // max 32-row jobs per encoder workgroup
+#define DAD_WS_TAB 256                                       // student workgroups of the host range table
 #define DAD_POOL_THREADS 256
 #define DAD_TAIL_THREADS 512
 #define DAD_ECDA_THREADS 512
@@ -57,6 +58,10 @@ struct DadEncodeArgs {
   __bf16* xs_bf16;          // BF16 mode: the student's MFMA input, clean rows then strong rows (for wgrad)
   int ws_nt, ws_ns;         // dad_encode_ws: teacher / student workgroups
   float ws_wstrong;         // dad_encode_ws: cost of a strong slab relative to a clean one
+  // dad_encode_ws student ranges from the host's min-max assignment (ws_tab_n = ws_ns, else 0 and
+  // the closed-form split): student k runs strong jobs [t[k][0], t[k][1]) then clean [t[k][2], t[k][3])
+  int ws_tab_n;
+  uint16_t ws_tab[DAD_WS_TAB][4];
 };
 
 struct DadPoolArgs {

@@ -183,6 +183,13 @@ __device__ __forceinline__ void job_range(const Ctx& C, int wg, int nt, int ns, 
   j1 = at(k + 1);
 }
 
+// a workgroup's jobs: local job l is job a0 + l for l < na, then b0 + (l - na) (student ranges
+// of the host table: strong jobs, then clean jobs; otherwise one contiguous range)
+struct JobMap {
+  int a0, na, b0;
+  __device__ __forceinline__ int operator()(int l) const { return l < na ? a0 + l : b0 + (l - na); }
+};
+
 template <int NOISE>
 __device__ __forceinline__ int tstart_of(const Ctx& C, int b) {
   if (NOISE && C.start) return (int)C.start[b];
@@ -551,7 +558,7 @@ __device__ __forceinline__ void wait_vm_sw(int n) {
 }  // namespace
 
 template <int WAVES, int NOISE, bool TEACHER>
-__device__ __forceinline__ void ws_loop(const Ctx& C, const int j0, const int Q, const int w, const int lane,
+__device__ __forceinline__ void ws_loop(const Ctx& C, const JobMap jm, const int Q, const int w, const int lane,
                                         char* smem, const uint32_t sbase, const bf16x8* W, const float* bias,
                                         const float* fk, const uint32_t* vb) {
   using S = Shape<WAVES>;
@@ -563,7 +570,7 @@ __device__ __forceinline__ void ws_loop(const Ctx& C, const int j0, const int Q,
   const float* raw1 = reinterpret_cast<const float*>(smem + kOffRaw + kRawStage);
   char* tile0 = smem + kOffTile;
   char* tile1 = smem + kOffTile + kTile;
-  auto jobq = [&](int q) { return job_of(C, TEACHER, j0 + (q >> 1)); };
+  auto jobq = [&](int q) { return job_of(C, TEACHER, jm(q >> 1)); };
   // valid-row mask of sub-slab q (uniform): an empty one (frames past every utterance's end,
   // e.g. rows 304..319 of a 300-frame utterance) is neither converted nor multiplied -- the
   // epilogue's valid mask zeroes it anyway
@@ -700,7 +707,14 @@ __device__ __forceinline__ void encode_ws_body(const DadEncodeArgs& a, char* sme
   bool teacher;
   int j0, j1;
   job_range(C, blockIdx.x, a.ws_nt, a.ws_ns, a.ws_wstrong, teacher, j0, j1);
-  const int nj = j1 - j0;
+  JobMap jm{j0, j1 - j0, 0};
+  int nj = j1 - j0;
+  if (!teacher && a.ws_tab_n > 0) {
+    const int k = (int)blockIdx.x - a.ws_nt;
+    const int s0 = a.ws_tab[k][0], s1 = a.ws_tab[k][1], c0 = a.ws_tab[k][2], c1 = a.ws_tab[k][3];
+    jm = JobMap{C.Jc + s0, s1 - s0, c0};
+    nj = (s1 - s0) + (c1 - c0);
+  }
   if (nj <= 0) return;
   const uint32_t sbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;   // LDS byte address
 
@@ -712,7 +726,7 @@ __device__ __forceinline__ void encode_ws_body(const DadEncodeArgs& a, char* sme
       fk[d] = dad_feat_keep(C.u, C.key_feat, d, C.feat_p);     // I/utils.py:343 (rand(D) > p)
     }
   for (int p = tid; p < nj * DAD_SLAB; p += S::kThreads) {
-    const Job J = job_of(C, teacher, j0 + p / DAD_SLAB);
+    const Job J = job_of(C, teacher, jm(p / DAD_SLAB));
     const int t = J.c * DAD_SLAB + (p & (DAD_SLAB - 1));
     const uint8_t* pad = J.kind == KIND_CLEAN ? C.mc : C.mn;
     const bool v = t < J.T && pad[J.row0 + t] == 0;
@@ -724,8 +738,8 @@ __device__ __forceinline__ void encode_ws_body(const DadEncodeArgs& a, char* sme
   WS_STAMP(1, DAD_PROBE_WALL());
   const bf16x8* W = reinterpret_cast<const bf16x8*>(teacher ? a.w1bf_teacher : a.w1bf_student);
   const float* bias = teacher ? a.b1_teacher : a.b1_student;
-  if (teacher) ws_loop<WAVES, NOISE, true>(C, j0, 2 * nj, w, lane, smem, sbase, W, bias, fk, vb);
-  else ws_loop<WAVES, NOISE, false>(C, j0, 2 * nj, w, lane, smem, sbase, W, bias, fk, vb);
+  if (teacher) ws_loop<WAVES, NOISE, true>(C, jm, 2 * nj, w, lane, smem, sbase, W, bias, fk, vb);
+  else ws_loop<WAVES, NOISE, false>(C, jm, 2 * nj, w, lane, smem, sbase, W, bias, fk, vb);
   WS_STAMP(2, DAD_PROBE_WALL());
   WS_STAMP(3, ((unsigned long long)teacher << 16) | (unsigned long long)(2 * nj));
 }
