@@ -44,6 +44,9 @@ FLAVOR_DEFAULTS = {
 _MODULE_FLAVOR = {"config": "iemocap", "config_casia": "casia", "config_emodb": "emodb"}
 
 
+_MISSING = object()
+
+
 class ConfigView:
     """Read-through view of a config source (module, dict or object) with dataset defaults.
 
@@ -62,20 +65,28 @@ class ConfigView:
         self.overrides = dict(overrides)
 
     def __getattr__(self, name):
-        if name.startswith("_") or name in ("flavor", "source", "overrides"):
+        # called for every config read of every step (dad_config_for reads ~40): one dict fetch
+        # per source, no hasattr + getattr pairs
+        if name[:1] == "_" or name in ("flavor", "source", "overrides"):
             raise AttributeError(name)
-        ov = self.__dict__.get("overrides", {})
-        if name in ov:
+        d = self.__dict__
+        ov = d.get("overrides")
+        if ov and name in ov:
             return ov[name]
-        src = self.__dict__.get("source")
-        if isinstance(src, dict):
-            if name in src:
-                return src[name]
-        elif src is not None and hasattr(src, name):
-            return getattr(src, name)
-        d = FLAVOR_DEFAULTS[self.__dict__["flavor"]]
-        if name in d:
-            return d[name]
+        src = d.get("source")
+        if src is not None:
+            if type(src) is dict or isinstance(src, dict):
+                if name in src:
+                    return src[name]
+            else:
+                v = getattr(src, name, _MISSING)
+                if v is not _MISSING:
+                    return v
+        fl = d.get("flavor")
+        if fl is not None:
+            dd = FLAVOR_DEFAULTS[fl]
+            if name in dd:
+                return dd[name]
         raise AttributeError(name)
 
     def effective_switches(self):
@@ -117,7 +128,9 @@ class ConfigView:
 
 def dad_config_for(view, Bc, Tc, Bn, Tn, epoch, adam_step, lr=None, precision=_lib.PREC_FP32,
                    rng_mode=_lib.RNG_COUNTER, seed=0, counter=0, dp_world=1, splits=0):
-    """Fill a `dad_config` for one step. `adam_step` is the Adam step count AFTER this step."""
+    """Fill a `dad_config` for one step. `adam_step` is the Adam step count AFTER this step.
+    (The c_float fields round each Python float to nearest, as np.float32 would; only drop_scale
+    is computed in float32 arithmetic, as nn.Dropout's 1/(1-p) is.)"""
     if view.INPUT_DIM != 768 or view.HIDDEN_DIM != 256 or view.NUM_CLASSES != 4:
         raise ValueError("the MI355X kernels are built for INPUT_DIM=768, HIDDEN_DIM=256, NUM_CLASSES=4")
     use_dacp, use_ecda, use_entropy, class_aware = view.effective_switches()
@@ -133,35 +146,35 @@ def dad_config_for(view, Bc, Tc, Bn, Tn, epoch, adam_step, lr=None, precision=_l
     c.use_dacp, c.use_entropy, c.class_aware = int(use_dacp), int(use_entropy), int(class_aware)
     c.ecda_on = int(use_ecda and w_ecda > 0)
     c.dp_world = int(dp_world)
-    c.w_kl, c.w_ecda = F32(w_kl), F32(w_ecda)
+    c.w_kl, c.w_ecda = w_kl, w_ecda
     gamma = view.DACP_QUANTILE_START + (view.DACP_QUANTILE_END - view.DACP_QUANTILE_START) * (epoch / view.EPOCHS)
-    c.dacp_gamma = F32(gamma)
+    c.dacp_gamma = gamma
     a = view.DACP_THRESHOLD_SMOOTHING_ALPHA
-    c.dacp_k, c.dacp_lambda = F32(view.DACP_SENSITIVITY_K), F32(view.DACP_CALIBRATION_STRENGTH_LAMBDA)
-    c.dacp_alpha, c.dacp_one_m_alpha = F32(a), F32(1 - a)
-    c.fixed_thr = F32(view.FIXED_CONFIDENCE_THRESHOLD)
-    c.ecda_att_lambda = F32(view.ECDA_CLASS_ATTENTION_LAMBDA)
-    c.ecda_gamma, c.ecda_delta = F32(view.ECDA_COMPACTNESS_WEIGHT_GAMMA), F32(view.ECDA_REPULSION_WEIGHT_DELTA)
-    c.ls_eps = F32(view.LABEL_SMOOTHING_FACTOR if view.USE_LABEL_SMOOTHING else 0.0)
+    c.dacp_k, c.dacp_lambda = view.DACP_SENSITIVITY_K, view.DACP_CALIBRATION_STRENGTH_LAMBDA
+    c.dacp_alpha, c.dacp_one_m_alpha = a, 1 - a
+    c.fixed_thr = view.FIXED_CONFIDENCE_THRESHOLD
+    c.ecda_att_lambda = view.ECDA_CLASS_ATTENTION_LAMBDA
+    c.ecda_gamma, c.ecda_delta = view.ECDA_COMPACTNESS_WEIGHT_GAMMA, view.ECDA_REPULSION_WEIGHT_DELTA
+    c.ls_eps = view.LABEL_SMOOTHING_FACTOR if view.USE_LABEL_SMOOTHING else 0.0
     p = view.DROPOUT_RATE
-    c.p_drop = F32(p)
+    c.p_drop = p
     c.drop_scale = F32(1.0) / F32(1 - p) if p < 1 else F32(0.0)
-    c.feat_p = F32(p)                                   # DataAugmentation.dropout_rate (I/utils.py:325)
-    c.weak_std, c.strong_std = F32(view.WEAK_NOISE_STD), F32(view.STRONG_NOISE_STD)
+    c.feat_p = p                                   # DataAugmentation.dropout_rate (I/utils.py:325)
+    c.weak_std, c.strong_std = view.WEAK_NOISE_STD, view.STRONG_NOISE_STD
     tn = c.Tn if c.Tn > 0 else 1
     mlen = int(tn * view.TEMPORAL_MASK_RATIO) if view.TEMPORAL_MASK_RATIO > 0 else 0
     c.mask_len = mlen
     c.start_hi = max(1, tn - mlen + 1)
     c.clip = int(bool(view.GRADIENT_CLIPPING))
-    c.max_norm = F32(view.MAX_GRAD_NORM)
+    c.max_norm = view.MAX_GRAD_NORM
     b1, b2 = 0.9, 0.999
-    c.lr_step_size = F32(lr / (1 - b1 ** adam_step))
-    c.bc2_sqrt = F32(math.sqrt(1 - b2 ** adam_step))
-    c.beta1, c.one_m_beta1, c.beta2, c.one_m_beta2 = F32(b1), F32(1 - b1), F32(b2), F32(1 - b2)
-    c.adam_eps, c.weight_decay = F32(1e-8), F32(view.WEIGHT_DECAY)
+    c.lr_step_size = lr / (1 - b1 ** adam_step)
+    c.bc2_sqrt = math.sqrt(1 - b2 ** adam_step)
+    c.beta1, c.one_m_beta1, c.beta2, c.one_m_beta2 = b1, 1 - b1, b2, 1 - b2
+    c.adam_eps, c.weight_decay = 1e-8, view.WEIGHT_DECAY
     m = view.EMA_MOMENTUM
-    c.ema_m, c.ema_one_m = F32(m), F32(1.0 - m)
+    c.ema_m, c.ema_one_m = m, 1.0 - m
     beta = view.DACP_QUALITY_SMOOTHING_BETA
-    c.dacp_beta, c.dacp_one_m_beta = F32(beta), F32(1 - beta)
+    c.dacp_beta, c.dacp_one_m_beta = beta, 1 - beta
     c.splits = int(splits)
     return c
