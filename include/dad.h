@@ -161,6 +161,10 @@ typedef struct dad_state {
 size_t dad_param_count(void);
 int dad_workspace_bytes(const dad_config* cfg, size_t* bytes);
 const char* dad_error_string(int code);
+/* Host-only planning of the BF16 encoder grid (no device call): teacher / student workgroups
+ * for a device of `cus` compute units and the most 32-row jobs any workgroup's range holds
+ * (always <= 256, the kernel's per-workgroup table).  Diagnostics and tests. */
+int dad_encoder_ws_plan(const dad_config* cfg, int cus, int* nt, int* ns, int* max_jobs);
 
 /* --- fused train step ---------------------------------------------------------------
  * Replaces the body of Trainer.train_epoch's loop (I/train.py:484-492):

@@ -143,7 +143,23 @@ bool ws_table_on() {
   static const bool on = [] { const char* e = getenv("DAD_WS_TABLE"); return e && strcmp(e, "1") == 0; }();
   return on;
 }
-void ws_split(const DadGeom& G, int Bn, int cus, int& nt, int& ns) {
+// the largest job range of the teacher (or student) workgroups of a split, by the kernel's own
+// range function (dad_ws_job_range)
+int ws_max_range(const DadGeom& G, int Bn, int nt, int ns, float wstrong, bool teacher_side) {
+  const int Js = Bn * G.ncn;
+  int worst = 0;
+  const int lo = teacher_side ? 0 : nt, hi = teacher_side ? nt : nt + ns;
+  for (int wg = lo; wg < hi; ++wg) {
+    bool t = false;
+    int j0 = 0, j1 = 0;
+    dad_ws_job_range(wg, nt, ns, wstrong, G.Bc, G.Tc, G.ncc, Bn, G.Tn, G.ncn, Js, t, j0, j1);
+    worst = std::max(worst, j1 - j0);
+  }
+  return worst;
+}
+// Returns DAD_E_SHAPE if no split keeps every range within DAD_ENC_WS_MAXJ jobs (cannot happen
+// for B <= DAD_MAX_BATCH: one job per workgroup always fits).
+int ws_split(const DadGeom& G, int Bn, int cus, int& nt, int& ns) {
   const float kWsWeak = ws_weights().weak, kWsStrong = ws_weights().strong;
   const int Jt = Bn * G.ncn, Jc = G.Bc * G.ncc, Js = Jt;
   if (Jt == 0) {
@@ -157,10 +173,18 @@ void ws_split(const DadGeom& G, int Bn, int cus, int& nt, int& ns) {
     nt = std::min(nt, Jt);
     ns = std::min(ns, Jc + Js);
   }
-  // ranges are priced by live sub-slabs (encode_ws.hip job_range): within two jobs of the even split
-  nt = std::max(nt, (Jt + DAD_ENC_WS_MAXJ - 3) / (DAD_ENC_WS_MAXJ - 2));
-  const double wtot = Jc + Js * (double)kWsStrong;
-  ns = std::max(ns, (int)(wtot / (DAD_ENC_WS_MAXJ - 2)) + 1);
+  // every range within DAD_ENC_WS_MAXJ jobs (the kernel's valid-bit table), checked with the
+  // kernel's range function: ranges are priced by live sub-slabs, so a job-count bound is not
+  // enough when clean and strong jobs hold different numbers of live sub-slabs (Tc != Tn)
+  nt = std::max(nt, (Jt + DAD_ENC_WS_MAXJ - 1) / DAD_ENC_WS_MAXJ);
+  ns = std::max(ns, (Jc + Js + DAD_ENC_WS_MAXJ - 1) / DAD_ENC_WS_MAXJ);
+  while (nt > 0 && ws_max_range(G, Bn, nt, ns, kWsStrong, true) > DAD_ENC_WS_MAXJ) {
+    if (++nt > Jt) return DAD_E_SHAPE;
+  }
+  while (ws_max_range(G, Bn, nt, ns, kWsStrong, false) > DAD_ENC_WS_MAXJ) {
+    if (++ns > Jc + Js) return DAD_E_SHAPE;
+  }
+  return DAD_OK;
 }
 
 // Student ranges of the W-stationary encoder by a min-max assignment: every student workgroup
@@ -232,6 +256,19 @@ const char* dad_error_string(int code) {
   }
 }
 
+int dad_encoder_ws_plan(const dad_config* cfg, int cus, int* nt, int* ns, int* max_jobs) {
+  int rc = check_cfg(cfg);
+  if (rc) return rc;
+  if (cus < 2 || !nt || !ns || !max_jobs) return DAD_E_ARG;
+  const DadGeom G = geom_of(cfg);
+  const int Bn = cfg->warmup ? 0 : G.Bn;
+  rc = ws_split(G, Bn, cus, *nt, *ns);
+  if (rc) return rc;
+  const float ws = ws_weights().strong;
+  *max_jobs = std::max(ws_max_range(G, Bn, *nt, *ns, ws, true), ws_max_range(G, Bn, *nt, *ns, ws, false));
+  return DAD_OK;
+}
+
 int dad_workspace_bytes(const dad_config* cfg, size_t* bytes) {
   int rc = check_cfg(cfg);
   if (rc) return rc;
@@ -300,7 +337,8 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
       int cus = 0;
       const int rc = device_cus(&cus);
       if (rc) return rc;
-      ws_split(G, Bn, cus, ea.ws_nt, ea.ws_ns);
+      const int rs = ws_split(G, Bn, cus, ea.ws_nt, ea.ws_ns);
+      if (rs) return rs;
       ea.ws_wstrong = ws_weights().strong;
       if (ws_table_on()) ws_student_table(G, Bn, ea.ws_ns, ea.ws_wstrong, ea);
       if (ea.ws_nt + ea.ws_ns > 0) {
@@ -384,9 +422,6 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   if (!cfg->warmup && DAD_FUSED_TAIL) {
     hipLaunchKernelGGL(dad_tail_ecda, dim3(1 + DAD_C), dim3(DAD_TAIL_THREADS), 0, stream, ta, ca);
     DAD_TRY(hipGetLastError());
-#ifdef DAD_PROBE_TAIL_TWICE   // diagnostic: a second (idempotent) launch runs with its code warm
-    hipLaunchKernelGGL(dad_tail_ecda, dim3(1 + DAD_C), dim3(DAD_TAIL_THREADS), 0, stream, ta, ca);
-#endif
   } else {
     hipLaunchKernelGGL(dad_tail, dim3(1), dim3(DAD_TAIL_THREADS), 0, stream, ta);
     DAD_TRY(hipGetLastError());
@@ -637,7 +672,8 @@ int encoder_forward_impl(const float* x, const uint8_t* pad, int B, int T, const
     int cus = 0;
     const int rc = device_cus(&cus);
     if (rc) return rc;
-    ws_split(G, 0, cus, ea.ws_nt, ea.ws_ns);
+    const int rs = ws_split(G, 0, cus, ea.ws_nt, ea.ws_ns);
+    if (rs) return rs;
     ea.ws_wstrong = ws_weights().strong;
     hipLaunchKernelGGL(dad_encode_ws, dim3(ea.ws_nt + ea.ws_ns), dim3(DAD_ENC_WS_THREADS), 0, stream, ea);
   } else {

@@ -261,6 +261,49 @@ static inline __host__ __device__ DadGeom dad_geom(int Bc, int Tc, int Bn, int T
   return g;
 }
 
+// Job ranges of the W-stationary BF16 encoder (encode_ws.hip), shared by the kernel and the
+// host (ws_split sizes the grid with it, so host and kernel count work in the same units).
+// Jobs are 32-row slabs; teacher workgroups [0, nt) split the weak slabs, student workgroups
+// [nt, nt + ns) the clean slabs (cost 1 per live 16-row sub-slab) then the strong slabs (cost
+// wstrong per live sub-slab).  The last slab of an utterance holds ceil(T/16) - 2(nc-1) live
+// sub-slabs (one at T = 300: rows 304..319 are skipped), so ranges are priced by the sub-slabs
+// they run, not by their job count.  Js = Bn * ncn, or 0 in warm-up.
+// live_jobs_at: the job boundary nearest to x cumulative live sub-slabs of one branch (nc slabs,
+// L live sub-slabs per utterance, J jobs).
+static inline __host__ __device__ int dad_live_jobs_at(float x, int nc, int L, int J) {
+  if (x <= 0.0f) return 0;
+  const int b = (int)(x / (float)L);
+  const float r = x - (float)b * (float)L;
+  const int c0 = (int)(0.5f * r + 0.5f);
+  const int c = c0 < nc ? c0 : nc;
+  const int j = b * nc + c;
+  return j < J ? j : J;
+}
+static inline __host__ __device__ void dad_ws_job_range(int wg, int nt, int ns, float wstrong, int Bc, int Tc, int ncc,
+                                                        int Bn, int Tn, int ncn, int Js, bool& teacher, int& j0,
+                                                        int& j1) {
+  const int Lc = (Tc + 15) / 16, Ln = (Tn + 15) / 16, Jc = Bc * ncc;
+  teacher = wg < nt;
+  if (teacher) {
+    const float tot = (float)Bn * (float)Ln;
+    j0 = wg >= nt ? Js : dad_live_jobs_at(tot * (float)wg / (float)nt, ncn, Ln, Js);
+    j1 = wg + 1 >= nt ? Js : dad_live_jobs_at(tot * (float)(wg + 1) / (float)nt, ncn, Ln, Js);
+    return;
+  }
+  const int k = wg - nt;
+  const float cc = Jc ? (float)Bc * (float)Lc : 0.0f;      // clean cost
+  const float wtot = cc + (Js ? (float)Bn * (float)Ln * wstrong : 0.0f);
+  int j[2];
+  for (int e = 0; e < 2; ++e) {
+    const int kk = k + e;
+    if (kk >= ns) { j[e] = Jc + Js; continue; }
+    const float B = wtot * (float)kk / (float)ns;
+    j[e] = B <= cc ? dad_live_jobs_at(B, ncc, Lc, Jc) : Jc + dad_live_jobs_at((B - cc) / wstrong, ncn, Ln, Js);
+  }
+  j0 = j[0];
+  j1 = j[1];
+}
+
 // Workspace layout (bytes), shared by host and device.  All offsets 256-B aligned.
 //   slab-indexed buffers: clean slabs [0, Bc*ncc), noisy slabs after them.
 struct DadWs {

@@ -146,41 +146,11 @@ __device__ __forceinline__ Job job_of(const Ctx& C, bool teacher, int j) {
   return J;
 }
 
-// Contiguous job range of workgroup wg, split by cost in live 16-row sub-slabs: the last slab
-// of an utterance holds ceil(T/16) - 2(nc-1) of them (one at T = 300: rows 304..319 are
-// skipped), so a range of whole jobs is priced by the sub-slabs it runs, not by its job count.
-// Teacher workgroups split the weak sub-slabs; student workgroups the clean (cost 1) + strong
-// (cost wstrong) sub-slabs.
-// cumulative live sub-slabs of the first j jobs of one branch (nc slabs, L live sub-slabs per
-// utterance), and the job boundary nearest to x of them
-__device__ __forceinline__ int live_jobs_at(float x, int nc, int L, int J) {
-  if (x <= 0.0f) return 0;
-  const int b = (int)(x / (float)L);
-  const float r = x - (float)b * (float)L;
-  const int c = min((int)(0.5f * r + 0.5f), nc);
-  return min(b * nc + c, J);
-}
+// Contiguous job range of workgroup wg: dad_ws_job_range (dad_common.h), the same function
+// the host runs to size the grid (ws_split, dad_abi.hip), so no range exceeds DAD_ENC_WS_MAXJ.
 __device__ __forceinline__ void job_range(const Ctx& C, int wg, int nt, int ns, float wstrong, bool& teacher,
                                           int& j0, int& j1) {
-  const int Lc = (C.Tc + kSub - 1) / kSub, Ln = (C.Tn + kSub - 1) / kSub;
-  teacher = wg < nt;
-  if (teacher) {
-    const float tot = (float)C.Bn * (float)Ln;
-    auto at = [&](int k) { return k >= nt ? C.Js : live_jobs_at(tot * (float)k / (float)nt, C.ncn, Ln, C.Js); };
-    j0 = at(wg);
-    j1 = at(wg + 1);
-    return;
-  }
-  const int k = wg - nt;
-  const float cc = C.Jc ? (float)C.Bc * (float)Lc : 0.0f;      // clean cost
-  const float wtot = cc + (C.Js ? (float)C.Bn * (float)Ln * wstrong : 0.0f);
-  auto at = [&](int kk) -> int {
-    if (kk >= ns) return C.Jc + C.Js;
-    const float B = wtot * (float)kk / (float)ns;
-    return B <= cc ? live_jobs_at(B, C.ncc, Lc, C.Jc) : C.Jc + live_jobs_at((B - cc) / wstrong, C.ncn, Ln, C.Js);
-  };
-  j0 = at(k);
-  j1 = at(k + 1);
+  dad_ws_job_range(wg, nt, ns, wstrong, C.Bc, C.Tc, C.ncc, C.Bn, C.Tn, C.ncn, C.Js, teacher, j0, j1);
 }
 
 // a workgroup's jobs: local job l is job a0 + l for l < na, then b0 + (l - na) (student ranges

@@ -1235,10 +1235,6 @@ __global__ __launch_bounds__(TAIL_THREADS) void dad_tail_ecda(DadTailArgs ta, Da
   } u;
   if (blockIdx.x == 0) tail_block(ta, u.t);
   else {
-#ifdef DAD_PROBE_ECDA_TWICE   // diagnostic: the class block again (idempotent), its code now in the I-cache
-    ecda_block<true>(ca, (int)blockIdx.x - 1, u.e.s, u.e.pdist, &ta, u.e.p);
-    __syncthreads();
-#endif
     ecda_block<true>(ca, (int)blockIdx.x - 1, u.e.s, u.e.pdist, &ta, u.e.p);
   }
 }

@@ -46,6 +46,28 @@ def test_host_only_queries():
     assert L.dad_encoder_workspace_bytes(8, 20) > 0
 
 
+@pytest.mark.parametrize("Bc,Tc,Bn,Tn,cus", [
+    (64, 300, 64, 300, 256),       # the bench geometry
+    (1024, 300, 1024, 1280, 256),  # long noisy batch: strong jobs hold 2.0 live sub-slabs, clean ones 1.9
+    (1024, 1280, 1024, 300, 256),
+    (1024, 2000, 1024, 30, 8),     # few CUs: many jobs per workgroup on both sides
+    (1000, 40, 3, 4000, 4),
+])
+def test_encoder_ws_plan_keeps_every_range_within_the_kernel_table(Bc, Tc, Bn, Tn, cus):
+    """The BF16 encoder's job table holds DAD_ENC_WS_MAXJ = 256 jobs per workgroup.  The host
+    plan (the kernel's own range function, priced in live sub-slabs) must never exceed it,
+    including geometries where clean and strong jobs hold different numbers of sub-slabs."""
+    p = dadpkg.pkg()
+    L = p.lib()
+    for epoch in (0, 60):
+        cfg = p.dad_config_for(p.ConfigView(flavor="iemocap"), Bc, Tc, Bn, Tn, epoch, 1,
+                               precision=p._lib.PREC_BF16)
+        nt, ns, mj = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
+        assert L.dad_encoder_ws_plan(cfg, cus, ctypes.byref(nt), ctypes.byref(ns), ctypes.byref(mj)) == 0
+        assert 0 < mj.value <= 256, (Bc, Tc, Bn, Tn, cus, epoch, nt.value, ns.value, mj.value)
+        assert ns.value >= 1 and (nt.value >= 1) == (epoch >= 30)
+
+
 def test_ctypes_structs_match_c_layout(tmp_path):
     """Compile a C probe against include/dad.h and compare sizeof/offsetof with ctypes."""
     p = dadpkg.pkg()
