@@ -35,11 +35,13 @@ METRIC = "utterances/sec (DAD train step) batch=64 at 1/2/4/8 MI355X; loss parit
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BF16_PEAK_TFLOPS = 2500.0      # dense bf16 MFMA
 FP32_PEAK_TFLOPS = 157.3       # f32 MFMA == f32 vector rate
-EVENT_EVERY = 4                # timed steps per encoder event pair
+EVENT_EVERY = 8                # every 8th timed step (every steps/4-th in short runs) records hip events
+                               # at its kernel boundaries (dad_timing_start): per-kernel durations, live
 CPU_BASELINE_SECONDS = 15.0    # bounded CPU sample (PyTorch-CPU steps until this much time)
 N_BATCHES = 8                  # distinct resident batches cycled by the timed steps: 8 x 118 MB of f32
                                # features, past the 256 MB infinity cache, so encoder reads come from HBM
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_latest.json")   # tools/profile_report.py --json
+MFMA_TARGET = 0.40             # north_star: >= 40 % MFMA utilisation on the encoder linears
 
 
 def init_model_weights(model, seed, margin=5.0):
@@ -63,18 +65,6 @@ def init_model_weights(model, seed, margin=5.0):
     return P.float()
 
 
-def event_pairs(steps):
-    """(start, end) timing events for the encoder launch of every EVENT_EVERY-th timed step,
-    created and recorded once outside the timed region (first-use costs stay out of it)."""
-    pairs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-             for _ in range((steps + EVENT_EVERY - 1) // EVENT_EVERY)]
-    for a, b in pairs:
-        a.record()
-        b.record()
-    torch.cuda.synchronize()
-    return pairs
-
-
 def make_batches(P, n, B, T, seed, device, snr_db=5.0):
     """n (clean, noisy) batch pairs, all frames valid (BASELINE.md §3 inputs)."""
     g = torch.Generator(device=device).manual_seed(seed)
@@ -92,15 +82,33 @@ def make_batches(P, n, B, T, seed, device, snr_db=5.0):
     return out
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the committed PMC summary (FETCH_SIZE x 2 + WRITE_SIZE,
-    MI355X_MICROARCH.md corrections), or None when no summary covers it."""
+def lib_sha16():
+    """sha256 (16 hex) of the loaded libdad_hip.so: ties PMC summaries to the code they measured."""
+    import hashlib
+    try:
+        return hashlib.sha256(open(PKG._build.lib_path(os.environ.get("DAD_LIB_VARIANT") or None), "rb").read()
+                              ).hexdigest()[:16]
+    except OSError:
+        return None
+
+
+def pmc_counters(kernel):
+    """Per-launch PMC values of `kernel` from the committed summary (tools/profile_report.py): HBM
+    bytes (2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md's gfx950 correction) and the matrix
+    pipe's busy cycles.  The summary records the library hash it was measured with; `stale` is
+    True when that is not the library loaded now (the counters then describe other code)."""
     try:
         d = json.load(open(PMC_SUMMARY))
-        k = d["kernels"][kernel]
-        return float(k["hbm_bytes_per_launch"]), d.get("source", PMC_SUMMARY)
     except Exception:
-        return None, None
+        return None
+    k = d.get("kernels", {}).get(kernel)
+    if k is None:
+        return None
+    out = dict(k)
+    out["source"] = d.get("source", PMC_SUMMARY)
+    out["lib_sha16"] = d.get("lib_sha16")
+    out["stale"] = d.get("lib_sha16") != lib_sha16()
+    return out
 
 
 def _cpu_model():
@@ -113,14 +121,12 @@ def _cpu_model():
     return None
 
 
-def cpu_baseline(B, T, steps, epoch, seconds=CPU_BASELINE_SECONDS):
-    """The PyTorch-CPU step (oracle/torch_cpu.py: the reference's step on the same ATen ops,
-    calibrated against the imported reference in profiles/r02_cpu_calibration.json) on this
-    host: torch's intra-op pool sized to the job's CPU share (OMP_NUM_THREADS, else every CPU
-    in the affinity mask); at least `steps` steps after 2 warm-ups, until `seconds` of steps."""
+def _cpu_leg(B, T, steps, epoch, threads, seconds):
+    """PyTorch-CPU steps (oracle/torch_cpu.py) with torch's intra-op pool at `threads`: 2 warm-ups,
+    then steps until `seconds` of timed steps, at least `steps` of them unless the leg's wall
+    time (warm-ups included) passes 2 x `seconds` (an oversubscribed pool: a 256-thread pool on a
+    16-CPU job share ran 17 s per step); median seconds per step."""
     from oracle import dad_oracle, synth, torch_cpu
-    host_cpus = len(os.sched_getaffinity(0))
-    threads = int(os.environ.get("OMP_NUM_THREADS") or host_cpus)
     prev = torch.get_num_threads()
     torch.set_num_threads(threads)
     try:
@@ -129,7 +135,7 @@ def cpu_baseline(B, T, steps, epoch, seconds=CPU_BASELINE_SECONDS):
         st = torch_cpu.TorchCPUStep(W1, b1, W2, b2, cfg)
         times = []
         k = 0
-        while k < steps + 2 or (sum(times[2:]) < seconds and k < 200):
+        while (k < steps + 2 and sum(times) < 2 * seconds) or (sum(times[2:]) < seconds and k < 200) or k < 3:
             inp = synth.make_step_inputs(0, k, B, T, ragged=False)
             t0 = time.perf_counter()
             st.step(inp, epoch)
@@ -137,19 +143,39 @@ def cpu_baseline(B, T, steps, epoch, seconds=CPU_BASELINE_SECONDS):
             k += 1
     finally:
         torch.set_num_threads(prev)
-    med = statistics.median(times[2:])
-    out = {"value": B / med, "unit": "utterances/s", "cores": threads, "kind": "port",
-           "host_cpus": host_cpus, "cpu_model": _cpu_model(),
-           "sample": "%d steps (after 2 warm-ups, %.1f s) of the PyTorch-CPU DAD step (oracle/torch_cpu.py), B=%d "
-                     "T=%d epoch %d, torch RNG; median %.3f s/step" % (len(times) - 2, sum(times[2:]), B, T, epoch, med)}
+    return statistics.median(times[2:]), len(times) - 2, sum(times[2:])
+
+
+def cpu_baseline(B, T, steps, epoch, seconds=CPU_BASELINE_SECONDS):
+    """The PyTorch-CPU step (oracle/torch_cpu.py: the reference's step on the same ATen ops,
+    calibrated against the imported reference in profiles/r02_cpu_calibration.json) on this
+    host, timed twice: with the job's CPU share (OMP_NUM_THREADS) and with every CPU of the
+    affinity mask (the node's own host cores).  `value` is the faster of the two."""
+    host_cpus = len(os.sched_getaffinity(0))
+    job = int(os.environ.get("OMP_NUM_THREADS") or host_cpus)
+    legs = []
+    for n in sorted({job, host_cpus}):
+        med, k, tot = _cpu_leg(B, T, steps, epoch, n, seconds / (2 if host_cpus != job else 1))
+        legs.append({"threads": n, "value": B / med, "median_s_per_step": med, "steps": k, "seconds": tot})
+    best = max(legs, key=lambda r: r["value"])
+    out = {"value": best["value"], "unit": "utterances/s", "cores": best["threads"], "kind": "port",
+           "host_cpus": host_cpus, "job_threads": job, "cpu_model": _cpu_model(), "legs": legs,
+           "sample": "PyTorch-CPU DAD step (oracle/torch_cpu.py), B=%d T=%d epoch %d, torch RNG, timed at %s threads "
+                     "(>= %d steps after 2 warm-ups, about %.0f s in all); value = the faster leg"
+                     % (B, T, epoch, " and ".join(str(r["threads"]) for r in legs), steps, seconds)}
+    # port/reference ratio measured in the container (profiles/r02_cpu_calibration.json) at the
+    # thread counts it has; applied only inside that range (never extrapolated to more threads)
     try:
         cal = json.load(open(os.path.join(ROOT, "profiles", "r02_cpu_calibration.json")))
-        rows = cal["by_threads"]
-        near = min(rows, key=lambda n: abs(int(n) - threads))
-        r = rows[near]["ratio_port_over_reference"]
-        out["calibration"] = {"ratio_port_over_reference": r, "at_threads": int(near),
-                              "container_cpu": cal.get("cpu_model"), "source": "profiles/r02_cpu_calibration.json",
-                              "reference_equivalent_value": out["value"] * r}
+        rows = {int(k): v["ratio_port_over_reference"] for k, v in cal["by_threads"].items()}
+        n = best["threads"]
+        inside = min(rows) <= n <= max(rows)
+        out["calibration"] = {"ratio_port_over_reference_by_threads": rows, "container_cpu": cal.get("cpu_model"),
+                              "source": "profiles/r02_cpu_calibration.json", "applies": inside,
+                              "reference_equivalent_value": out["value"] * rows[min(rows, key=lambda k: abs(k - n))]
+                              if inside else None,
+                              "note": None if inside else "measured at %s threads only; %d threads is outside that "
+                              "range, so no reference-equivalent value is derived" % (sorted(rows), n)}
     except Exception:
         out["calibration"] = None
     return out
@@ -298,7 +324,7 @@ def run_mixed(args, model, dev, rank, world, dist, comm):
             yield from PKG.data.DeviceLoader(store, batch_size=B, shuffle=True, generator=g, fused=True,
                                              with_labels=labeled)
 
-    folds, events = [], []
+    folds, ktimes = [], []
     n = 0
     for k in range(args.folds):
         tr = mixed_fold_train(starts, meta, k)
@@ -313,19 +339,16 @@ def run_mixed(args, model, dev, rank, world, dist, comm):
                 c, nb = next(ci), next(ni)
                 step.view = views[n % 3]
                 n += 1
-                step.kernel_events = fold_events[i // EVENT_EVERY] if (timed and i % EVENT_EVERY == 0) else None
                 if timed:
                     for b in (c, nb):
                         f = b["net_input"]["feats"]
                         rows += int(f.store.sizes[f.index].sum())
                     utts += c["net_input"]["feats"].shape[0]
                 step.step(c, nb, args.epoch)
-            step.kernel_events = None
             return rows, utts
-        fold_events = event_pairs(args.steps)
-        events.extend(fold_events)
         run(args.warmup if k == 0 else 3, False)
         torch.cuda.synchronize()
+        timer = PKG._lib.KernelTimer(event_every(args.steps), args.steps + 1)
         if dist:
             dist.barrier()
         t0 = time.perf_counter()
@@ -334,6 +357,7 @@ def run_mixed(args, model, dev, rank, world, dist, comm):
         if dist:
             dist.barrier()
         el = time.perf_counter() - t0
+        ktimes.append(timer.stop())
         if dist:
             t = torch.tensor([el], dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -343,7 +367,151 @@ def run_mixed(args, model, dev, rank, world, dist, comm):
             utts = int(u.item())
         folds.append({"fold": k, "train_utterances": int(len(tr)), "seconds": el, "utterances": utts,
                       "value": utts / el, "avg_valid_frames_per_step": rows / args.steps})
-    return step, folds, events
+    return step, folds, merge_ktimes(ktimes)
+
+
+def event_every(steps):
+    return max(1, min(EVENT_EVERY, steps // 4))
+
+
+def merge_ktimes(parts):
+    """Weighted mean of several KernelTimer.stop() results."""
+    acc = {}
+    for p in parts:
+        for k, (m, n) in p.items():
+            t, c = acc.get(k, (0.0, 0))
+            acc[k] = (t + m * n, c + n)
+    return {k: (t / c, c) for k, (t, c) in acc.items() if c}
+
+
+ENC_KERNEL = {"bf16": "dad_encode_ws", "fp32": "dad_encode_f32"}
+WGRAD_KERNEL = {"bf16": ("wgrad", "dad_wgrad_direct"), "fp32": ("side", "dad_wgrad_f32")}
+KNAMES = {"bf16": {"encode": "dad_encode_ws", "pool": "dad_pool", "tail": "dad_tail_ecda", "wgrad": "dad_wgrad_direct",
+                   "reduce": "dad_reduce", "optim": "dad_optim"},
+          "fp32": {"encode": "dad_encode_f32", "pool": "dad_pool", "tail": "dad_tail_ecda", "side": "dad_wgrad_f32",
+                   "wgrad": "dad_wsum (after the side-stream join)", "optim": "dad_optim"}}
+
+
+def rooflines(ktimes, rows_c, rows_n, ms_step, precision):
+    """`roofline` of the dominant kernel (the encoder), `step_roofline` of the whole step and the
+    per-kernel table (live HIP-event durations of dad_timing_start) with MFMA utilisation of the
+    encoder linears.  Algorithmic work:
+      encoder:  bytes = (rows_c + rows_n) x 768 x 4 (both fp32 feature tensors, read once),
+                flops = 2 x 768 x 256 x (rows_c + 2 rows_n)  (student-clean, teacher-weak, student-strong)
+      dW1:      flops = 2 x 768 x 256 x (rows_c + rows_n)
+      step:     t_roof = max(F / P_mfma, Q / BW) with F = 2 x 768 x 256 x (2 rows_c + 3 rows_n).
+    bound: the encoder's arithmetic intensity against the ridge point P_mfma / BW."""
+    peak_tf = BF16_PEAK_TFLOPS if precision == "bf16" else FP32_PEAK_TFLOPS
+    enc_bytes = int((rows_c + rows_n) * 768 * 4)
+    enc_flops = 2 * 768 * 256 * (rows_c + 2 * rows_n)
+    wg_flops = 2 * 768 * 256 * (rows_c + rows_n)
+    step_flops = 2 * 768 * 256 * (2 * rows_c + 3 * rows_n)
+    names = KNAMES[precision]
+    kern = {}
+    for k, (m, n) in sorted(ktimes.items()):
+        kern[names.get(k, k)] = {"avg_ms": m, "timed_launches": n}
+    if "encode" not in ktimes:
+        return None, None, kern
+    enc = ktimes["encode"][0]
+    wkey, wname = WGRAD_KERNEL[precision]
+    wg = ktimes.get(wkey, (float("nan"), 0))[0]
+    ridge = peak_tf * 1e12 / (HBM_PEAK_GBS * 1e9)
+    intensity = enc_flops / enc_bytes
+    bound = "mfma" if intensity > ridge else "hbm"
+    ekn = ENC_KERNEL[precision]
+    pmc = pmc_counters(ekn)
+    traffic = pmc["hbm_bytes_per_launch"] if pmc and "hbm_bytes_per_launch" in pmc else None
+    if bound == "hbm":
+        achieved, peak, unit, work = enc_bytes / (enc * 1e-3) / 1e9, HBM_PEAK_GBS, "GB/s", enc_bytes
+    else:
+        achieved, peak, unit, work = enc_flops / (enc * 1e-3) / 1e12, peak_tf, "TFLOP/s", enc_flops
+    rf = {"bound": bound, "kernel": ekn, "achieved": achieved, "peak": peak, "unit": unit, "frac": achieved / peak,
+          "traffic": traffic, "avg_launch_ms": enc, "timed_launches": ktimes.get("encode", (0, 0))[1],
+          "algorithmic_bytes_per_launch": enc_bytes, "algorithmic_flops_per_launch": enc_flops,
+          "arithmetic_intensity_flop_per_byte": intensity, "ridge_flop_per_byte": ridge,
+          "traffic_source": None if pmc is None else pmc["source"],
+          "traffic_stale": None if pmc is None else pmc["stale"]}
+    t_roof = max(step_flops / (peak_tf * 1e12), enc_bytes / (HBM_PEAK_GBS * 1e9))
+    srf = {"t_roof_us": t_roof * 1e6, "t_step_us": ms_step * 1e3, "frac": t_roof / (ms_step * 1e-3),
+           "flops_per_step": step_flops, "bytes_per_step": enc_bytes, "mfma_peak_tflops": peak_tf}
+    # MFMA utilisation of the encoder linears (north_star: >= 40 %): algorithmic FLOPs / time / peak
+    enc_tf = enc_flops / (enc * 1e-3) / 1e12
+    wg_tf = wg_flops / (wg * 1e-3) / 1e12
+    mf = {ekn: {"flops": enc_flops, "avg_ms": enc, "tflops": enc_tf, "util": enc_tf / peak_tf},
+          wname: {"flops": wg_flops, "avg_ms": wg, "tflops": wg_tf, "util": wg_tf / peak_tf},
+          "encoder_linears": {"flops": enc_flops + wg_flops, "ms": enc + wg,
+                              "util": (enc_flops + wg_flops) / ((enc + wg) * 1e-3) / 1e12 / peak_tf,
+                              "target": MFMA_TARGET},
+          "peak_tflops": peak_tf, "peak_source": "MI355X_MICROARCH.md dense MFMA peak (%s)" % precision}
+    for kn in (ekn, wname):   # matrix-pipe busy share from the committed PMC pass, when it covers this library
+        pk = pmc_counters(kn)
+        if pk and pk.get("mfma_busy_frac") is not None:
+            mf[kn]["pmc_matrix_busy_frac"] = pk["mfma_busy_frac"]
+            mf[kn]["pmc_stale"] = pk["stale"]
+    kern["mfma_util"] = mf
+    return rf, srf, kern
+
+
+def snapshot(model, step):
+    """Model parameters + step state (Adam moments, DACP state, step counters)."""
+    return model.student_flat.clone(), model.teacher_flat.clone(), step.state_dict()
+
+
+def restore(model, step, snap):
+    with torch.no_grad():
+        model.student_flat.copy_(snap[0])
+        model.teacher_flat.copy_(snap[1])
+    step.load_state_dict(snap[2])
+    step.refresh_shadow()
+
+
+def parity_block(model, step, view, snap, batch, epoch):
+    """bf16 (the timed mode) vs fp32 (the reference's arithmetic, exact-f32 MFMA) on the first timed
+    batch from the state the timed region started in, with the same counter-RNG draws (same seed
+    and global step): the four loss terms, the student logits and the DACP mask.  The golden
+    replays of tests/test_gpu_bf16_parity.py pin the same comparison against the reference."""
+    c, nb = batch
+    out = {}
+    for prec in ("bf16", "fp32"):
+        restore(model, step, snap)
+        s = PKG.DADStep(model, view, precision=prec, rng="counter", seed=step.seed)
+        s.load_state_dict(snap[2])
+        l = s.step(c, nb, epoch)
+        torch.cuda.synchronize()
+        Bc, Bn = s._last_shape
+        o = s.outputs(Bc, Bn)
+        out[prec] = {"losses": {k: float(v) for k, v in l.items()},
+                     "z_clean": o["z_clean"].detach().cpu().double(), "z_strong": o["z_strong"].detach().cpu().double(),
+                     "mask": o["mask"].detach().cpu()}
+    restore(model, step, snap)
+    b, f = out["bf16"], out["fp32"]
+    rel = lambda a, r: float((a - r).abs().max() / max(1e-6, float(r.abs().max())))
+    return {"batch": "first timed batch", "reference_mode": "fp32 (exact-f32 MFMA), same counter-RNG draws",
+            "losses_bf16": b["losses"], "losses_fp32": f["losses"],
+            "loss_err": {k: abs(b["losses"][k] - f["losses"][k]) / max(1.0, abs(f["losses"][k])) for k in f["losses"]},
+            "z_clean_err": rel(b["z_clean"], f["z_clean"]), "z_strong_err": rel(b["z_strong"], f["z_strong"]),
+            "mask_equal": bool(torch.equal(b["mask"], f["mask"])), "mask_sum": float(f["mask"].sum()),
+            "err_definition": "losses |bf16 - fp32| / max(1, |fp32|); logits max|bf16 - fp32| / max|fp32|"}
+
+
+def fp32_mode(model, view, data, B, T, args):
+    """The reference's arithmetic (fp32 operands, exact-f32 MFMA) timed over args.fp32_steps steps,
+    with its own per-kernel timing and rooflines (fp32 MFMA peak)."""
+    s32 = PKG.DADStep(model, view, precision="fp32", rng="counter", seed=5)
+    for i in range(3):
+        s32.step(data[i % 4][0], data[i % 4][1], args.epoch)
+    torch.cuda.synchronize()
+    n = args.fp32_steps
+    timer = PKG._lib.KernelTimer(4, n // 4 + 1)
+    t1 = time.perf_counter()
+    for i in range(n):
+        s32.step(data[i % 4][0], data[i % 4][1], args.epoch)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t1) / n
+    kt = timer.stop()
+    rf, srf, kern = rooflines(kt, B * T, B * T, dt * 1e3, "fp32")
+    return {"value": B / dt, "ms_per_step": dt * 1e3, "steps": n, "dtype": "f32", "roofline": rf,
+            "step_roofline": srf, "kernels": kern}
 
 
 def _free_port():
@@ -411,8 +579,9 @@ def main():
                     help="gradient all-reduce transport for N > 1 (gloo lets ranks share one GPU)")
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--fp32-steps", type=int, default=10, help="also time the FP32 parity mode (N=1)")
+    ap.add_argument("--fp32-steps", type=int, default=24, help="also time the FP32 parity mode (N=1)")
     ap.add_argument("--no-data-path", action="store_true", help="skip the device collate measurement (N=1)")
+    ap.add_argument("--no-parity", action="store_true", help="skip the bf16-vs-fp32 parity block (N=1)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -450,10 +619,9 @@ def main():
         print("bench.py: the %s transport connected %d ranks, expected %d" % (args.comm, ranks_seen, args.gpus),
               file=sys.stderr)
         sys.exit(3)
-    events = []
     folds = None
     if args.mixed:
-        step, folds, events = run_mixed(args, model, dev, rank, world, dist, comm)
+        step, folds, ktimes = run_mixed(args, model, dev, rank, world, dist, comm)
         elapsed = sum(f["seconds"] for f in folds)
         total_utts = sum(f["utterances"] for f in folds)
         timed_steps = args.steps * args.folds
@@ -465,28 +633,26 @@ def main():
         data = make_batches(P, N_BATCHES, B, T, seed=17 + rank, device=dev, snr_db=args.snr)
         torch.cuda.synchronize()
 
-        def run(n, events=None):
-            # encoder-launch events on every EVENT_EVERY-th step of the timed region only: a
-            # timing event pair costs a few microseconds of stream time, which would otherwise
-            # be charged to every step.  The pairs are created (and first recorded) before the
-            # timed region, so it contains only their records.
+        def run(n):
             for i in range(n):
-                step.kernel_events = events[i // EVENT_EVERY] if (events is not None and i % EVENT_EVERY == 0) else None
                 c, nb = data[i % len(data)]
                 step.step(c, nb, args.epoch)
-            step.kernel_events = None
 
-        events = event_pairs(args.steps)
         run(args.warmup)
         torch.cuda.synchronize()
+        snap = snapshot(model, step)          # the state the first timed step starts from
+        # every EVENT_EVERY-th timed step records hip events at its kernel boundaries (created
+        # here, outside the timed region; the region only records them)
+        timer = PKG._lib.KernelTimer(event_every(args.steps), args.steps + 1)
         if dist:
             dist.barrier()
         t0 = time.perf_counter()
-        run(args.steps, events)
+        run(args.steps)
         torch.cuda.synchronize()
         if dist:
             dist.barrier()
         elapsed = time.perf_counter() - t0
+        ktimes = timer.stop()
         if dist:
             t = torch.tensor([elapsed], dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -498,20 +664,13 @@ def main():
     nbc = step._last_shape
     msum = float(step.outputs(*nbc)["msum"])
     ecda_on = float(step.outputs(*nbc)["ecda_on"])
-    enc_ms = statistics.mean(a.elapsed_time(b) for a, b in events)
 
-    fp32 = None
-    if rank == 0 and world == 1 and args.fp32_steps > 0 and args.precision == "bf16" and not args.mixed:
-        s32 = PKG.DADStep(model, view, precision="fp32", rng="counter", seed=5)
-        for i in range(3):
-            s32.step(data[i % 4][0], data[i % 4][1], args.epoch)
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        for i in range(args.fp32_steps):
-            s32.step(data[i % 4][0], data[i % 4][1], args.epoch)
-        torch.cuda.synchronize()
-        dt = (time.perf_counter() - t1) / args.fp32_steps
-        fp32 = {"value": B / dt, "ms_per_step": dt * 1e3, "dtype": "f32"}
+    parity = fp32 = None
+    if rank == 0 and world == 1 and args.precision == "bf16" and not args.mixed:
+        if not args.no_parity:
+            parity = parity_block(model, step, view, snap, data[0], args.epoch)
+        if args.fp32_steps > 0:
+            fp32 = fp32_mode(model, view, data, B, T, args)
     data_path = None
     if rank == 0 and world == 1 and not args.no_data_path and not args.mixed:
         data_path = data_path_bench(step, B, T, args.epoch, dev)
@@ -525,13 +684,6 @@ def main():
     ms = elapsed / timed_steps * 1e3
     value = total_utts / elapsed
     rows = rows_per_step / 2                            # valid frames per batch (clean = noisy count here)
-    enc_bytes = int(rows_per_step * 768 * 4)            # clean + noisy fp32 features, read once
-    enc_gbs = enc_bytes / (enc_ms * 1e-3) / 1e9
-    flops = 2 * 768 * 256 * (2 * rows + 3 * rows)       # 5 encoder-sized contractions / step
-    peak_tf = BF16_PEAK_TFLOPS if args.precision == "bf16" else FP32_PEAK_TFLOPS
-    t_roof = max(flops / (peak_tf * 1e12), enc_bytes / (HBM_PEAK_GBS * 1e9))
-    enc_kernel = "dad_encode_ws" if args.precision == "bf16" else "dad_encode_f32"
-    traffic, traffic_src = pmc_traffic(enc_kernel)
     if args.mixed:
         workload = ("IEMOCAP+CASIA+EMODB mixed-batch DAD step (configs[4]): batch=%d/GPU of utterances from all three "
                     "corpora (synthetic stores with each corpus's utterance count and fold structure, %d-%d frames), "
@@ -546,6 +698,7 @@ def main():
                     "post-warm-up epoch %d, counter-RNG augmentation in-kernel"
                     % (args.flavor.upper(), " (configs[3]: DACP+ECDA forced on; SCL is 0 in the reference)"
                        if args.force_ecda else "", B, T, args.snr, args.epoch))
+    rf, srf, kern = rooflines(ktimes, rows, rows, ms, args.precision)
     line = {
         "metric": METRIC, "value": value, "unit": "utterances/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
@@ -554,13 +707,11 @@ def main():
                    "global_batch": B * world, "per_gpu_batch": B, "seq_len": T, "feature_dim": 768,
                    "parallelism": "dp%d" % world},
         "comm": {"transport": args.comm if world > 1 else None, "ranks_seen": ranks_seen},
-        "roofline": {"bound": "hbm", "kernel": enc_kernel, "achieved": enc_gbs,
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": enc_gbs / HBM_PEAK_GBS, "traffic": traffic,
-                     "traffic_source": traffic_src, "avg_launch_ms": enc_ms, "algorithmic_bytes_per_launch": enc_bytes},
-        "step_roofline": {"t_roof_us": t_roof * 1e6, "t_step_us": ms * 1e3, "frac": t_roof / (ms * 1e-3),
-                          "flops_per_step": flops, "bytes_per_step": enc_bytes, "mfma_peak_tflops": peak_tf},
+        "roofline": rf, "step_roofline": srf, "kernels": kern,
         "losses_last_step": losses, "mask_sum_last_step": msum, "ecda_on_last_step": ecda_on,
     }
+    if parity is not None:
+        line["parity"] = parity
     if folds is not None:
         line["folds"] = folds
     if fp32 is not None:

@@ -314,6 +314,25 @@ int dad_ecda_loss(const dad_config* cfg, const float* clean, int B, const float*
 #define DAD_DRAW_KEEP2 6
 int dad_rng_draws(const dad_config* cfg, int which, uint64_t first, size_t n, float* out, void* stream);
 
+/* --- per-kernel timing of the fused step (diagnostics; not inside graph capture) ------
+ * dad_timing_start(every, max_steps): from now on every `every`-th step (counted at its
+ * dad_step_encode / dad_step_compute call) records hip events at the boundaries of its kernels
+ * on the caller's stream, up to max_steps timed steps; all events are created here, so a timed
+ * region only records them.  dad_timing_stop: waits for the recorded events and returns, per
+ * kernel k < n (DAD_TK_*), the summed milliseconds ms_sum[k] over count[k] timed steps, then
+ * frees the events and turns timing off.  The FP32 step's dW1 GEMM runs on a side stream
+ * (DAD_TK_SIDE); its DAD_TK_WGRAD interval is the join + dad_wsum. */
+#define DAD_TK_ENCODE 0       /* dad_encode_ws / dad_encode_f32 */
+#define DAD_TK_POOL 1         /* dad_pool */
+#define DAD_TK_TAIL 2         /* dad_tail_ecda (or dad_tail + dad_ecda) */
+#define DAD_TK_WGRAD 3        /* dad_wgrad_direct (BF16) / join + dad_wsum (FP32) */
+#define DAD_TK_REDUCE 4       /* dad_reduce (BF16) */
+#define DAD_TK_OPTIM 5        /* dad_optim */
+#define DAD_TK_SIDE 6         /* dad_wgrad_f32 on the side stream (FP32) */
+#define DAD_TK_KERNELS 7
+int dad_timing_start(int every, int max_steps);
+int dad_timing_stop(double* ms_sum, int* count, int n);
+
 /* --- data-parallel gradient exchange (RCCL over xGMI) ------------------------------ */
 int dad_comm_unique_id_bytes(void);
 int dad_comm_get_unique_id(void* id_out);

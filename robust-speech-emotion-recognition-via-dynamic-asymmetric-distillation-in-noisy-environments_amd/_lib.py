@@ -119,6 +119,8 @@ EXPORTS = {
                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "dad_rng_draws": (ctypes.c_int, [ctypes.POINTER(DadConfig), ctypes.c_int, ctypes.c_uint64, ctypes.c_size_t,
                                      ctypes.c_void_p, ctypes.c_void_p]),
+    "dad_timing_start": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    "dad_timing_stop": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
     "dad_comm_unique_id_bytes": (ctypes.c_int, []),
     "dad_comm_get_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
     "dad_comm_init": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_void_p, ctypes.c_int]),
@@ -127,6 +129,9 @@ EXPORTS = {
     "dad_comm_allreduce_f32": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
     "dad_comm_destroy": (ctypes.c_int, [ctypes.c_void_p]),
 }
+
+# per-kernel timing slots (dad.h DAD_TK_*)
+TK_NAMES = ["encode", "pool", "tail", "wgrad", "reduce", "optim", "side"]
 
 _LIB = None
 
@@ -162,3 +167,20 @@ def check(rc, what=""):
 def ptr(t):
     """Device pointer of a tensor (or None)."""
     return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+class KernelTimer:
+    """dad_timing_start / dad_timing_stop: mean duration (ms) per kernel of the fused step over
+    every `every`-th step while active.  `stop()` returns {name: (mean_ms, n_steps)}."""
+
+    def __init__(self, every=4, max_steps=256):
+        check(lib().dad_timing_start(int(every), int(max_steps)), "dad_timing_start")
+        self.active = True
+
+    def stop(self):
+        n = len(TK_NAMES)
+        ms = (ctypes.c_double * n)()
+        cnt = (ctypes.c_int * n)()
+        self.active = False
+        check(lib().dad_timing_stop(ms, cnt, n), "dad_timing_stop")
+        return {TK_NAMES[k]: (ms[k] / cnt[k], cnt[k]) for k in range(n) if cnt[k] > 0}

@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <mutex>
+#include <vector>
 
 #include "dad_common.h"
 #include "dad_kernels.h"
@@ -239,9 +240,80 @@ bool ws_student_table(const DadGeom& G, int Bn, int ns, float wstrong, DadEncode
   return true;
 }
 
+// Per-kernel timing of the fused step (dad_timing_start / dad_timing_stop): every `every`-th
+// step (counted at its encoder call) records hip events at the kernel boundaries of the
+// caller's stream (and around the side-stream GEMM of the FP32 step).  Events are created up
+// front by dad_timing_start, so a timed region only records them.  Not for graph capture.
+enum { TK_E0, TK_E1, TK_POOL, TK_TAIL, TK_WGRAD, TK_RED, TK_OPT0, TK_OPT1, TK_S0, TK_S1, TK_N };
+struct Timing {
+  int every = 0;
+  long calls = 0;
+  int cur = -1;                        // event set of the step being timed, -1: none
+  std::vector<hipEvent_t> ev;          // nset * TK_N
+  std::vector<uint8_t> rec;            // recorded flags
+  int nset = 0, used = 0;
+};
+Timing g_tk;
+std::mutex g_tk_mu;
+
+void tk_begin() {
+  std::lock_guard<std::mutex> lk(g_tk_mu);
+  g_tk.cur = -1;
+  if (g_tk.every <= 0) return;
+  if (g_tk.calls++ % g_tk.every == g_tk.every - 1 && g_tk.used < g_tk.nset) g_tk.cur = g_tk.used++;
+}
+void tk_mark(int point, hipStream_t s) {
+  std::lock_guard<std::mutex> lk(g_tk_mu);
+  if (g_tk.cur < 0) return;
+  const size_t i = (size_t)g_tk.cur * TK_N + point;
+  if (hipEventRecord(g_tk.ev[i], s) == hipSuccess) g_tk.rec[i] = 1;
+}
+void tk_end() {
+  std::lock_guard<std::mutex> lk(g_tk_mu);
+  g_tk.cur = -1;
+}
+
 }  // namespace
 
 extern "C" {
+
+int dad_timing_start(int every, int max_steps) {
+  std::lock_guard<std::mutex> lk(g_tk_mu);
+  if (every < 1 || max_steps < 1) return DAD_E_ARG;
+  for (hipEvent_t e : g_tk.ev) (void)hipEventDestroy(e);
+  g_tk = Timing();
+  g_tk.ev.assign((size_t)max_steps * TK_N, nullptr);
+  g_tk.rec.assign((size_t)max_steps * TK_N, 0);
+  for (auto& e : g_tk.ev) DAD_TRY(hipEventCreate(&e));
+  g_tk.every = every;
+  g_tk.nset = max_steps;
+  return DAD_OK;
+}
+
+int dad_timing_stop(double* ms_sum, int* count, int n) {
+  std::lock_guard<std::mutex> lk(g_tk_mu);
+  static const int pairs[DAD_TK_KERNELS][2] = {{TK_E0, TK_E1}, {TK_E1, TK_POOL}, {TK_POOL, TK_TAIL}, {TK_TAIL, TK_WGRAD},
+                                               {TK_WGRAD, TK_RED}, {TK_OPT0, TK_OPT1}, {TK_S0, TK_S1}};
+  if (n < 0 || (n > 0 && (!ms_sum || !count))) return DAD_E_ARG;
+  for (int k = 0; k < n; ++k) { ms_sum[k] = 0.0; count[k] = 0; }
+  int rc = DAD_OK;
+  for (int s = 0; s < g_tk.used && rc == DAD_OK; ++s) {
+    const size_t b = (size_t)s * TK_N;
+    for (int k = 0; k < n && k < DAD_TK_KERNELS; ++k) {
+      const int a = pairs[k][0], z = pairs[k][1];
+      if (!g_tk.rec[b + a] || !g_tk.rec[b + z]) continue;
+      float ms = 0.0f;
+      hipError_t e = hipEventSynchronize(g_tk.ev[b + z]);
+      if (e == hipSuccess) e = hipEventElapsedTime(&ms, g_tk.ev[b + a], g_tk.ev[b + z]);
+      if (e != hipSuccess) { rc = (int)e; break; }
+      ms_sum[k] += ms;
+      count[k] += 1;
+    }
+  }
+  for (hipEvent_t e : g_tk.ev) (void)hipEventDestroy(e);
+  g_tk = Timing();
+  return rc;
+}
 
 size_t dad_param_count(void) { return DAD_NPARAM; }
 
@@ -333,6 +405,8 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   const int nwaves = G.Bc * G.ncc + Bn * G.ncn;
   const dim3 egrid((nwaves + 3) / 4);
   if (do_encode) {
+    tk_begin();
+    tk_mark(TK_E0, stream);
     if (bf16) {
       int cus = 0;
       const int rc = device_cus(&cus);
@@ -350,6 +424,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
       hipLaunchKernelGGL(dad_encode_f32, egrid, dim3(DAD_ENC_F32_THREADS), 0, stream, ea);
     }
     DAD_TRY(hipGetLastError());
+    tk_mark(TK_E1, stream);
   }
   if (!do_backward) return DAD_OK;
 
@@ -376,6 +451,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
     wa.splits = nutt; wa.per_utt = 1; wa.wpart = sbuf;
     DAD_TRY(hipEventRecord(side->fork, stream));
     DAD_TRY(hipStreamWaitEvent(side->s, side->fork, 0));
+    tk_mark(TK_S0, side->s);
     if (bf16) {
       wa.su = reinterpret_cast<__bf16*>(sbuf);
       wa.ntiles = WGD_NDB * nutt;
@@ -387,6 +463,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
       hipLaunchKernelGGL(dad_wgrad_f32, dim3(sgrid), dim3(DAD_WGRAD_THREADS), 0, side->s, wa);
     }
     DAD_TRY(hipGetLastError());
+    tk_mark(TK_S1, side->s);
     DAD_TRY(hipEventRecord(side->join, side->s));
   }
 
@@ -404,6 +481,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   pa.eflag = eflag; pa.tail_terms = st->tail + DAD_T_ECDA_TERM;
   hipLaunchKernelGGL(dad_pool, dim3(G.Bc + Bn), dim3(DAD_POOL_THREADS), 0, stream, pa);
   DAD_TRY(hipGetLastError());
+  tk_mark(TK_POOL, stream);
 
   // 4. losses, DACP mask, analytic backward to dL/de and the classifier grads
   DadTailArgs ta;
@@ -431,6 +509,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
     }
   }
 
+  tk_mark(TK_TAIL, stream);
   // 6. dW1 (join, then sum_u (dL/de_u / len_u) * S_u; or the direct split-K GEMM), db1,
   //    dW2, loss totals, squared-norm partials
   DadReduceArgs ra;
@@ -452,15 +531,19 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
     const int grid = (wa.ntiles + WGD_XWG + 7) / 8 * 8;
     hipLaunchKernelGGL(dad_wgrad_direct, dim3(grid), dim3(WGD_THREADS), 0, stream, wa, ra);
     DAD_TRY(hipGetLastError());
+    tk_mark(TK_WGRAD, stream);
     ra.splits = splits; ra.wpart = wa.wpart;
     hipLaunchKernelGGL(dad_reduce, dim3(DAD_REDUCE_BLOCKS - DAD_REDUCE_XBLK), dim3(DAD_REDUCE_THREADS), 0, stream, ra);
+    DAD_TRY(hipGetLastError());
+    tk_mark(TK_RED, stream);
   } else {
     DAD_TRY(hipStreamWaitEvent(stream, side->join, 0));
     ra.splits = nutt; ra.wpart = sbuf;
     if (bf16) ra.su = wa.su;
     hipLaunchKernelGGL(dad_wsum, dim3(DAD_REDUCE_BLOCKS), dim3(DAD_REDUCE_THREADS), 0, stream, ra);
+    DAD_TRY(hipGetLastError());
+    tk_mark(TK_WGRAD, stream);
   }
-  DAD_TRY(hipGetLastError());
   return DAD_OK;
 }
 
@@ -504,8 +587,11 @@ int dad_step_apply(const dad_config* cfg, const dad_state* st, void* workspace, 
   oa.w1bf_teacher = reinterpret_cast<__bf16*>(st->w1bf_teacher);
   oa.dacp = st->dacp; oa.tailf = st->tail; oa.normpart = normpart; oa.nnorm = nnorm;
   oa.losses_out = st->losses;
+  tk_mark(TK_OPT0, stream);
   hipLaunchKernelGGL(dad_optim, dim3(nblk), dim3(DAD_OPTIM_THREADS), 0, stream, oa);
   DAD_TRY(hipGetLastError());
+  tk_mark(TK_OPT1, stream);
+  tk_end();
   return DAD_OK;
 }
 

@@ -119,7 +119,6 @@ class DADStep:
         self.global_step = 0
         self._ws = None
         self._bufs = {}
-        self.kernel_events = None     # (start, end) events, or a list to append them to, around the encoder launch
         self._shadow_dirty = False
         self.refresh_shadow()
 
@@ -273,18 +272,7 @@ class DADStep:
         ws = self._workspace(cfg)
         stream = self._stream()
         L = _lib.lib()
-        ev = self.kernel_events
-        if ev is not None:
-            # a (start, end) pair created by the caller ahead of a timed region, or a list to
-            # which a fresh pair is appended
-            e0, e1 = ev if isinstance(ev, tuple) else (torch.cuda.Event(enable_timing=True),
-                                                        torch.cuda.Event(enable_timing=True))
-            e0.record()
         _lib.check(L.dad_step_encode(cfg, bt, st, _lib.ptr(ws), stream), "dad_step_encode")
-        if ev is not None:
-            e1.record()
-            if not isinstance(ev, tuple):
-                ev.append((e0, e1))
         _lib.check(L.dad_step_backward(cfg, bt, st, _lib.ptr(ws), stream), "dad_step_backward")
         if self.comm is not None and self.comm.world > 1:
             self.comm.allreduce_grad(st, stream, grad=self.grad)

@@ -66,10 +66,17 @@ def test_bf16_counter_rng_matches_fp32_counter_rng(B, T):
     f, b = outs
     for k in ("e_clean", "e_teacher", "e_strong", "z_clean", "z_teacher", "z_strong"):
         gh.close(b[k], f[k], BF16_TOL, "counter %s B%d T%d" % (k, B, T))
-    if np.array_equal(b["mask"], f["mask"]):
-        assert _grad_cos(b["grads"], f["grads"]) > 0.99
+    # the discrete DACP decisions agree at this geometry (a flip would move KL / ECDA by a
+    # finite step, which no precision bound covers); then every loss term is within the bf16
+    # loss bound of test_gpu_bf16_parity (the golden replays of the same mode)
+    from test_gpu_bf16_parity import BF16_LOSS_TOL
+    assert np.array_equal(b["mask"], f["mask"]), "bf16 and fp32 DACP masks differ (B%d T%d)" % (B, T)
+    assert _grad_cos(b["grads"], f["grads"]) > 0.99
     for k in ("total_loss", "supervised_ce_loss", "consistency_loss", "ecda_loss"):
-        assert np.isfinite(b[k])
+        err = abs(b[k] - f[k]) / max(1.0, abs(f[k]))
+        print("counter B%d T%d %s: bf16 %.7g fp32 %.7g rel %.3g" % (B, T, k, b[k], f[k], err))
+        assert err <= BF16_LOSS_TOL, (k, b[k], f[k], err)
+    assert f["ecda_loss"] != 0.0 and f["consistency_loss"] != 0.0
 
 
 def test_bf16_counter_steps_stay_finite():

@@ -58,16 +58,40 @@ def pmc_agg(pmc_dir):
     return agg
 
 
+N_SIMDS = 1024   # MI355X: 256 CUs x 4 SIMDs
+
+
+def lib_sha16():
+    import hashlib
+    p = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                     "robust-speech-emotion-recognition-via-dynamic-asymmetric-distillation-in-noisy-environments_amd",
+                     "lib", "libdad_hip.so")
+    try:
+        return hashlib.sha256(open(p, "rb").read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
 def pmc_json(pmc_dir, title):
     agg = pmc_agg(pmc_dir)
+    mean = lambda k, c: (sum(agg[(k, c)]) / len(agg[(k, c)])) if agg.get((k, c)) else None
     out = {}
     for k in sorted({k for k, _ in agg}):
-        f, w = agg.get((k, "FETCH_SIZE")), agg.get((k, "WRITE_SIZE"))
-        if f and w:
-            kb = 2 * sum(f) / len(f) + sum(w) / len(w)
-            out[k] = {"hbm_bytes_per_launch": kb * 1024.0, "fetch_kb_x2": 2 * sum(f) / len(f),
-                      "write_kb": sum(w) / len(w), "launches": len(f)}
-    return {"source": title, "units": "bytes per launch = (2 x FETCH_SIZE + WRITE_SIZE) KB x 1024", "kernels": out}
+        f, w = mean(k, "FETCH_SIZE"), mean(k, "WRITE_SIZE")
+        e = {}
+        if f is not None and w is not None:
+            e.update({"hbm_bytes_per_launch": (2 * f + w) * 1024.0, "fetch_kb_x2": 2 * f, "write_kb": w,
+                      "launches": len(agg[(k, "FETCH_SIZE")])})
+        mb, ga = mean(k, "SQ_VALU_MFMA_BUSY_CYCLES"), mean(k, "GRBM_GUI_ACTIVE")
+        if mb is not None and ga:
+            # busy cycles summed over SIMDs / (SIMDs x kernel cycles); GRBM_GUI_ACTIVE sums 8 XCDs
+            e["mfma_busy_frac"] = mb / (N_SIMDS * ga / 8.0)
+            e["mfma_busy_cycles"] = mb
+        if e:
+            out[k] = e
+    return {"source": title, "lib_sha16": lib_sha16(),
+            "units": "bytes per launch = (2 x FETCH_SIZE + WRITE_SIZE) KB x 1024; mfma_busy_frac = "
+                     "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)", "kernels": out}
 
 
 def pmc(pmc_dir):
