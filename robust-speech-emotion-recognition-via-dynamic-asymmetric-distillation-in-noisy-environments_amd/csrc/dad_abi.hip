@@ -109,6 +109,12 @@ bool wgrad_direct() {
   return !(e && strcmp(e, "su") == 0);
 }
 
+// DAD_TAIL_W=0 selects the general tail + ECDA launch for every batch (A/B runs; read once)
+bool tail_w_on() {
+  static const bool on = [] { const char* e = getenv("DAD_TAIL_W"); return !(e && strcmp(e, "0") == 0); }();
+  return on;
+}
+
 int device_cus(int* out) {
   static int cache[kMaxDevices];
   int dev = 0;
@@ -497,8 +503,13 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   memset(&ca, 0, sizeof(ca));
   ca.cfg = *cfg; ca.yc = bt->yc; ca.emb = st->emb; ca.tailf = st->tail;
   ca.tail_terms = st->tail + DAD_T_ECDA_TERM; ca.ge = ge_ecda; ca.scratch = ecda_scratch; ca.eflag = eflag;
+  ca.sink = ws_ptr<float>(workspace, L.gflat);
   if (!cfg->warmup && DAD_FUSED_TAIL) {
-    hipLaunchKernelGGL(dad_tail_ecda, dim3(1 + DAD_C), dim3(DAD_TAIL_THREADS), 0, stream, ta, ca);
+    // batches of at most 64 utterances per side, class-aware MMD: the wave-centric launch
+    if (G.Bc <= 64 && Bn <= 64 && cfg->class_aware && tail_w_on())
+      hipLaunchKernelGGL(dad_tail_ecda_w, dim3(1 + DAD_C), dim3(DAD_TAIL_THREADS), 0, stream, ta, ca);
+    else
+      hipLaunchKernelGGL(dad_tail_ecda, dim3(1 + DAD_C), dim3(DAD_TAIL_THREADS), 0, stream, ta, ca);
     DAD_TRY(hipGetLastError());
   } else {
     hipLaunchKernelGGL(dad_tail, dim3(1), dim3(DAD_TAIL_THREADS), 0, stream, ta);

@@ -104,6 +104,7 @@ struct DadEcdaArgs {
   float* ge;              // ECDA part of dL/de: member rows written (and flagged in eflag)
   uint32_t* eflag;
   float* scratch;         // global fallback for large member sets
+  float* sink;            // dad_tail_ecda_w: [DAD_H] floats its unselected lanes store to
 };
 
 struct DadWgradArgs {
@@ -166,6 +167,7 @@ __global__ void dad_pool(DadPoolArgs a);
 __global__ void dad_tail(DadTailArgs a);
 __global__ void dad_ecda(DadEcdaArgs a);
 __global__ void dad_tail_ecda(DadTailArgs ta, DadEcdaArgs ca);
+__global__ void dad_tail_ecda_w(DadTailArgs ta, DadEcdaArgs ca);   // B, Bn <= 64, class-aware
 __global__ void dad_wgrad_f32(DadWgradArgs a);
 __global__ void dad_wgrad_direct(DadWgradArgs a, DadReduceArgs r);
 __global__ void dad_wgrad_su(DadWgradArgs a);

@@ -34,6 +34,10 @@ DAD_PROBE_BUFFER(ecda_stamps, DAD_C * ECDA_SLOTS + 16)
 #define TAIL_CYCLES(k) \
   if (threadIdx.x == 0) DAD_PROBE_SET(ecda_stamps, DAD_C * ECDA_SLOTS + (k), DAD_PROBE_CLK())
 
+// stamp from wave 1's first lane (the tail block's DACP / KL wave)
+#define TAIL_STAMP_W1(k) \
+  if (threadIdx.x == 64 && blockIdx.x == 0) DAD_PROBE_SET(ecda_stamps, DAD_C * ECDA_SLOTS + (k), DAD_PROBE_WALL())
+
 #define TAIL_THREADS DAD_TAIL_THREADS
 
 __device__ __forceinline__ float block_sum_f(float v, float* red) {
@@ -1237,6 +1241,831 @@ __global__ __launch_bounds__(TAIL_THREADS) void dad_tail_ecda(DadTailArgs ta, Da
   else {
     ecda_block<true>(ca, (int)blockIdx.x - 1, u.e.s, u.e.pdist, &ta, u.e.p);
   }
+}
+
+// =====================================================================================
+// Wave-centric tail + ECDA for batches of at most 64 utterances per side (the bench
+// geometry): dad_tail_ecda_w.  Same outputs as dad_tail_ecda, far fewer barrier-separated
+// phases:
+//  * DACP (I/utils.py:449-507) inside ONE wave: lane i = noisy row i; ranks by an LDS
+//    broadcast sweep, the per-class quantile by lanes 0..3, thresholds broadcast by readlane
+//    (dacp_wave; the arithmetic of dacp_thresholds, so the masks are bit-identical).  Every
+//    wave of an ECDA block derives the mask itself: no barrier before the class work.
+//  * the tail block: CE in wave 0 (lane = clean row), teacher certainty + DACP + KL in wave 1
+//    (lane = noisy row), wave reductions by DPP, one barrier to combine.
+//  * an ECDA class block stages its CANDIDATE rows (clean label c, noisy pseudo-label c: known
+//    before the mask) from the registers they were prefetched into; the pairwise distances
+//    come from a Gram matrix on the fp32 matrix cores (v_mfma_f32_32x32x2_f32, K split over
+//    the 8 waves), D_ij = |z_i|^2 + |z_j|^2 - 2 z_i.z_j; the member gradients
+//    2 sum_j C_ij (z_i - z_j) = 2 (rowsum(C)_i z_i - (C Z)_i) are a second MFMA GEMM.
+//    Four workgroup barriers in all.  A class with more than 64 candidates falls back to
+//    ecda_block (the general path) inside the same launch.
+// =====================================================================================
+#define TW_MAXB 64
+#define EW_ZP 260          // staged row pitch (floats): 16-B aligned rows, <= 2-way bank conflicts
+#define EW_CP 66           // D / C matrix pitch (narrow)
+#define EW_CPW 130         // D / C matrix pitch (wide, 128 candidates)
+
+// DACP scratch of a workgroup: per-wave partial ranks and per-wave sorted-score tables
+struct DacpBlockScratch {
+  int rk[TW_MAXB][ECDA_THREADS / 64];
+  float srt[ECDA_THREADS / 64][DAD_C][TW_MAXB];
+};
+
+// The DACP state a wave reads (uniform): tau, Q and the calibrated anchors.  Loaded by ONE
+// unconditional load per lane (lane k < 20 holds dacp[k]) issued with the kernel's other entry
+// loads, then broadcast by readlane: a load under a lane condition would be waited for on the
+// spot (the compiler drains vmcnt where the paths merge), one memory round trip per value.
+__device__ __forceinline__ float sel4(const float (&v)[DAD_C], int k) {
+  return k == 0 ? v[0] : (k == 1 ? v[1] : (k == 2 ? v[2] : v[3]));
+}
+__device__ __forceinline__ int sel4i(const int (&v)[DAD_C], int k) {
+  return k == 0 ? v[0] : (k == 1 ? v[1] : (k == 2 ? v[2] : v[3]));
+}
+
+struct DacpState {
+  float tau[DAD_C], Q[DAD_C], anc[DAD_C];
+};
+
+// segmented sums by DPP (no LDS-routed shuffles): the sum of each aligned group of N lanes lands
+// in the group's LAST lane (N = 4, 8, 16 inside a 16-lane row; 32 adds row_bcast:15)
+template <int N>
+__device__ __forceinline__ float dpp_seg_sum(float v) {
+  static_assert(N == 4 || N == 8 || N == 16 || N == 32, "segment");
+  v += dad_dpp_f<0x111>(v);
+  v += dad_dpp_f<0x112>(v);
+  if constexpr (N >= 8) v += dad_dpp_f<0x114>(v);
+  if constexpr (N >= 16) v += dad_dpp_f<0x118>(v);
+  if constexpr (N == 32) v += dad_dpp_f<0x142, 0xa>(v);
+  return v;
+}
+__device__ __forceinline__ DacpState dacp_state_of(float dv) {
+  DacpState d;
+#pragma unroll
+  for (int k = 0; k < DAD_C; ++k) {
+    d.tau[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dv), k));
+    d.Q[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dv), 4 + k));
+    d.anc[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dv), 16 + k));
+  }
+  return d;
+}
+
+// DACP thresholds (I/utils.py:449-507) by all 8 waves of a workgroup, every wave holding the
+// scores s and pseudo-labels p of every noisy row (lane i = row i < Bn; p = -1 past Bn).  Wave g
+// counts, for every row, the rows j in [8g, 8g + 8) of its class below it (ties by index:
+// readlane sweep, bitwise so nothing branches); one barrier; the rank is the sum of the 8
+// partials.  Then every wave sorts into its own table and lanes 0..3 take torch.quantile(linear)
+// of their class; outputs uniform.  The arithmetic is dacp_thresholds', so the thresholds and
+// masks are bit-identical to the general path's.
+__device__ __forceinline__ void dacp_block8(const dad_config& cfg, int Bn, float s, int p, const DacpState& D,
+                                            DacpBlockScratch& W, float (&tau)[DAD_C], float (&wc)[DAD_C],
+                                            float (&that)[DAD_C], float (&fl)[DAD_C]) {
+  const int lane = threadIdx.x & 63;
+  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  TAIL_STAMP_W1(7);
+  int part = 0;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int j = 8 * g + u;
+    const float sj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s), j));
+    const int pj = __builtin_amdgcn_readlane(p, j);
+    part += (int)((pj == p) & ((sj < s) | ((sj == s) & (j < lane))));
+  }
+  W.rk[lane][g] = part;
+  __syncthreads();
+  const u32x4 r0 = *reinterpret_cast<const u32x4*>(&W.rk[lane][0]);
+  const u32x4 r1 = *reinterpret_cast<const u32x4*>(&W.rk[lane][4]);
+  const int cnt = (int)(((r0[0] + r0[1]) + (r0[2] + r0[3])) + ((r1[0] + r1[1]) + (r1[2] + r1[3])));
+  TAIL_STAMP_W1(8);
+  int ncls[DAD_C];
+#pragma unroll
+  for (int c = 0; c < DAD_C; ++c) ncls[c] = (int)__popcll(__ballot(lane < Bn && p == c));
+  float (*srt)[TW_MAXB] = W.srt[g];
+  if (lane < Bn) srt[p][cnt] = s;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  float tn = 0.0f, w = 0.0f, th = 0.0f, f = 0.0f;
+  if (lane < DAD_C) {
+    const int c = lane;
+    const float q0 = D.Q[0], q1 = D.Q[1], q2 = D.Q[2], q3 = D.Q[3];
+    const float qc = sel4(D.Q, c), tc = sel4(D.tau, c), ac = sel4(D.anc, c);
+    const float qmean = (((q0 + q1) + q2) + q3) / 4.0f;
+    w = 1.0f / (1.0f + expf(-(cfg.dacp_k * (qc - qmean))));
+    const int n = sel4i(ncls, c);
+    // torch.quantile(linear): rank = q*(n-1) in f32, lerp(below, above, rank-floor)
+    const float rank = cfg.dacp_gamma * (float)(n - 1);
+    const int lo = (int)rank;
+    const int hi = (int)ceilf(rank);
+    const float wgt = rank - (float)lo;
+    const float vlo = srt[c][lo < 0 ? 0 : lo], vhi = srt[c][hi < 0 ? 0 : hi];
+    const float q = wgt < 0.5f ? vlo + wgt * (vhi - vlo) : vhi - (vhi - vlo) * (1.0f - wgt);
+    th = n > 0 ? q : tc;
+    const float adj = cfg.dacp_lambda * (w - 0.5f);
+    f = fmaxf(th + adj, ac);
+    tn = cfg.dacp_alpha * tc + cfg.dacp_one_m_alpha * f;
+  }
+  DAD_PROBE_FENCE2(tn, f);
+  TAIL_STAMP_W1(9);
+#pragma unroll
+  for (int c = 0; c < DAD_C; ++c) {
+    tau[c] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tn), c));
+    wc[c] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), c));
+    that[c] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(th), c));
+    fl[c] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(f), c));
+  }
+  DAD_PROBE_FENCE2(tau[3], fl[3]);
+  TAIL_STAMP_W1(10);
+}
+
+// the DACP / fixed-threshold mask of noisy row `lane` (I/train.py:413-420), score s, pseudo-label
+// p; called by all 8 waves of a workgroup (one barrier inside when DACP is on)
+struct WaveMask {
+  float s, q[DAD_C];
+  int p;                 // pseudo-label, -1 on lanes >= Bn
+  bool m;                // masked in (confident)
+  float tau[DAD_C], wc[DAD_C], that[DAD_C], fl[DAD_C];
+};
+__device__ __forceinline__ void block_mask(const dad_config& cfg, int Bn, const f32x4& zt, const DacpState& D,
+                                           DacpBlockScratch& W, WaveMask& M) {
+  const int lane = threadIdx.x & 63;
+  {
+    const float z[4] = {zt[0], zt[1], zt[2], zt[3]};
+    teacher_certainty(z, cfg, M.q, M.s, M.p);   // every lane (rows past Bn are clamped copies)
+  }
+  if (lane >= Bn) {
+    M.s = 0.0f;
+    M.p = -1;
+  }
+  if (cfg.use_dacp) {
+    dacp_block8(cfg, Bn, M.s, M.p, D, W, M.tau, M.wc, M.that, M.fl);
+    M.m = (lane < Bn) & (M.s >= sel4(M.tau, M.p < 0 ? 0 : M.p));
+  } else {
+#pragma unroll
+    for (int c = 0; c < DAD_C; ++c) { M.tau[c] = 0.0f; M.wc[c] = 1.0f; M.that[c] = 0.0f; M.fl[c] = 0.0f; }
+    M.m = (lane < Bn) & (M.s >= cfg.fixed_thr);
+  }
+}
+
+struct TailW {
+  DacpBlockScratch dw;
+  double d[2][8];
+  float f[2][4];
+};
+
+// The tail (block 0) for B, Bn <= 64: see tail_block for the reference lines of each step.
+// Every wave: entry loads, teacher certainty and the DACP mask (block_mask: one barrier);
+// wave 0: CE on the clean logits (lane = clean row); wave 1: DACP outputs, epoch statistics and
+// the masked KL (lane = noisy row); one barrier to combine.
+__device__ __forceinline__ void tail_block_w(const DadTailArgs& a, TailW& T) {
+  const dad_config& cfg = a.cfg;
+  const int B = cfg.B, Bn = cfg.Bn;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  float* tf = a.tailf;
+  float* extras = a.grad + DAD_NPARAM;
+  const float eps = cfg.ls_eps;
+  TAIL_STAMP(0);
+  TAIL_CYCLES(12);
+  // entry loads, unconditional (rows clamped): clean logits + labels, teacher and strong logits,
+  // the DACP state
+  const int rc = lane < B ? lane : B - 1, rn = lane < Bn ? lane : Bn - 1;
+  const f32x4 zv = reinterpret_cast<const f32x4*>(a.logits)[rc];
+  const int yv = (int)a.yc[rc];
+  const f32x4 zt = reinterpret_cast<const f32x4*>(a.logits + (size_t)B * DAD_C)[rn];
+  const f32x4 zs = reinterpret_cast<const f32x4*>(a.logits + (size_t)(B + Bn) * DAD_C)[rn];
+  const float dv = a.dacp[lane < DAD_DACP_FLOATS ? lane : 0];
+  // teacher probs + certainty + DACP mask (I/train.py:408-420, I/utils.py:400-507), lane = noisy row
+  const DacpState D = dacp_state_of(dv);
+  WaveMask M;
+  block_mask(cfg, Bn, zt, D, T.dw, M);
+  TAIL_STAMP_W1(4);
+  if (w == 0) {
+    // supervised CE with label smoothing on the clean logits (I/train.py:364,400), lane = row
+    double ce_part = 0.0, b2p[4] = {0.0, 0.0, 0.0, 0.0};
+    {
+      const int y = yv;
+      const float z[4] = {zv[0], zv[1], zv[2], zv[3]};
+      float m = -INFINITY;
+      for (int c = 0; c < 4; ++c) m = fmaxf(m, z[c]);
+      float se = 0.0f;
+      for (int c = 0; c < 4; ++c) se += expf(z[c] - m);
+      const float lse = m + logf(se);
+      float lsum = 0.0f, g[4];
+      for (int c = 0; c < 4; ++c) {
+        const float ls = z[c] - lse;
+        lsum += ls;
+        const float pr = expf(ls);
+        g[c] = (pr - (c == y ? 1.0f - eps : 0.0f) - eps * 0.25f) / (float)B;
+        b2p[c] = lane < B ? (double)g[c] : 0.0;
+      }
+      const float zy = y == 0 ? z[0] : (y == 1 ? z[1] : (y == 2 ? z[2] : z[3]));
+      ce_part = lane < B ? -(1.0 - (double)eps) * (double)(zy - lse) - (double)eps * 0.25 * (double)lsum : 0.0;
+      if (lane < B) *reinterpret_cast<f32x4*>(a.gzb + (size_t)lane * DAD_C) = f32x4{g[0], g[1], g[2], g[3]};
+    }
+    const double ce = dad_wave_sum_d(ce_part) / (double)B;
+    double b2[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) b2[c] = dad_wave_sum_d(b2p[c]);
+    TAIL_STAMP(2);
+    if (lane == 0) {
+      T.d[0][0] = ce;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) T.d[0][1 + c] = b2[c];
+    }
+  } else if (w == 1) {
+    if (cfg.use_dacp) {
+      if (lane < DAD_C) {
+        const int c = lane;
+        tf[DAD_T_W + c] = sel4(M.wc, c);
+        tf[DAD_T_TAU_BEFORE + c] = sel4(D.tau, c);
+        tf[DAD_T_TAU_AFTER + c] = sel4(M.tau, c);
+        tf[DAD_T_FLOORED + c] = sel4(M.fl, c);
+        tf[DAD_T_TAU_HAT + c] = sel4(M.that, c);
+        extras[c] = sel4(M.fl, c);
+      }
+      // epoch statistics of update_class_quality_scores_epoch (I/utils.py:503-505)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const double st = dad_wave_sum_d(M.p == c ? (double)M.s : 0.0);
+        const double ct = dad_wave_sum_d(M.p == c ? 1.0 : 0.0);
+        if (lane == 0) {
+          extras[4 + c] = (float)st;
+          extras[8 + c] = (float)ct;
+        }
+      }
+    } else if (lane < DAD_C) {
+      tf[DAD_T_W + lane] = 1.0f;
+      extras[0 + lane] = 0.0f;
+      extras[4 + lane] = 0.0f;
+      extras[8 + lane] = 0.0f;
+    }
+    const float mk = M.m ? 1.0f : 0.0f;
+    const float msum = (float)__popcll(__ballot(M.m));   // the mask sum (an exact count)
+    const bool kl_on = msum > 1.0f;                      // I/train.py:444
+    // masked consistency KL(q || p_student) (I/train.py:445-447) and its logit grad
+    const float denom = msum + 1e-8f;
+    double kl_part = 0.0, b2p[4] = {0.0, 0.0, 0.0, 0.0};
+    {
+      const float z[4] = {zs[0], zs[1], zs[2], zs[3]};
+      float m = -INFINITY;
+      for (int c = 0; c < 4; ++c) m = fmaxf(m, z[c]);
+      float se = 0.0f;
+      for (int c = 0; c < 4; ++c) se += expf(z[c] - m);
+      const float lse = m + logf(se);
+      float klb = 0.0f, g[4];
+      for (int c = 0; c < 4; ++c) {
+        const float q = M.q[c];
+        const float ls = z[c] - lse;
+        const float t = q * (logf(q) - ls);
+        klb += q > 0.0f ? t : 0.0f;
+        g[c] = kl_on ? cfg.w_kl * mk * (expf(ls) - q) / denom : 0.0f;
+        b2p[c] = lane < Bn ? (double)g[c] : 0.0;
+      }
+      kl_part = lane < Bn ? (double)(klb * mk) : 0.0;
+      if (lane < Bn) {
+        *reinterpret_cast<f32x4*>(a.gzb + (size_t)(B + lane) * DAD_C) = f32x4{g[0], g[1], g[2], g[3]};
+        // per-sample outputs (noisy batch) for inspection / ECDA
+        tf[DAD_TAIL_HDR + lane] = M.s;
+        tf[DAD_TAIL_HDR + Bn + lane] = (float)M.p;
+        tf[DAD_TAIL_HDR + 2 * Bn + lane] = mk;
+        *reinterpret_cast<f32x4*>(tf + DAD_TAIL_HDR + 3 * Bn + lane * 4) = f32x4{M.q[0], M.q[1], M.q[2], M.q[3]};
+      }
+    }
+    TAIL_STAMP_W1(5);
+    const double kls = dad_wave_sum_d(kl_part);
+    double b2[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) b2[c] = dad_wave_sum_d(b2p[c]);
+    if (lane == 0) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) T.d[1][1 + c] = b2[c];
+      T.f[1][0] = kl_on ? (float)(kls / (double)denom) : 0.0f;
+      T.f[1][1] = msum;
+      T.f[1][2] = kl_on ? 1.0f : 0.0f;
+    }
+    TAIL_STAMP_W1(6);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const float kl_on = T.f[1][2];
+    tf[DAD_T_CE] = (float)T.d[0][0];
+    tf[DAD_T_KL] = T.f[1][0];
+    tf[DAD_T_SCL] = 0.0f;
+    tf[DAD_T_MSUM] = T.f[1][1];
+    tf[DAD_T_KL_ON] = kl_on;
+    tf[DAD_T_ECDA_ON] = (kl_on != 0.0f && cfg.ecda_on) ? 1.0f : 0.0f;
+  }
+  if (tid < 4) a.grad[DAD_OFF_B2 + tid] = (float)(T.d[0][1 + tid] + T.d[1][1 + tid]);
+  TAIL_CYCLES(13);
+  TAIL_STAMP(1);
+}
+
+struct __attribute__((aligned(16))) EcdaW {
+  union {
+    float zc[(TW_MAXB + 1) * EW_ZP];    // narrow (<= 64 candidates): staged candidate rows + a spare row
+    float dbw[2 * TW_MAXB * EW_CPW];    // wide (65..128): D, then the MMD coefficients
+  } a;
+  union {
+    DacpBlockScratch dw;                     // DACP scratch (before barrier 1)
+    float gp[10][32 * 32];                   // Gram partial tiles (after barrier 1)
+  } b;
+  union {
+    float cp[ECDA_THREADS / 64][DAD_C][DAD_H];   // per-wave centroid partial sums (until barrier 2)
+    float dbn[TW_MAXB * EW_CP];                  // narrow: D, then the MMD coefficients (after barrier 2)
+  } c;
+  float cent[DAD_C][DAD_H];
+  float nz[2 * TW_MAXB], wz[2 * TW_MAXB], rs[2 * TW_MAXB];
+  int rowz[2 * TW_MAXB], mem[2 * TW_MAXB];
+  int cnt[DAD_C];                       // masked noisy rows per class (pseudo-label)
+  float repg[DAD_H];
+  float pd[DAD_C][DAD_C];
+  double bwp[ECDA_THREADS / 64];
+  double t3p[ECDA_THREADS / 64][3];
+  float cmp[ECDA_THREADS / 64];
+};
+
+// upper-triangle tile pair index of (ti <= tj) among nt tiles, and its inverse
+__device__ __forceinline__ int ew_pair(int ti, int tj, int nt) { return ti * nt - ti * (ti - 1) / 2 + (tj - ti); }
+__device__ __forceinline__ void ew_pair_inv(int pr, int nt, int& ti, int& tj) {
+  ti = 0;
+  while (pr >= nt - ti) { pr -= nt - ti; ++ti; }
+  tj = ti + pr;
+}
+
+// The class work after the candidates are known.  WIDE = more than 64 candidates: rows are read
+// from the embedding buffer (global, through the candidate -> row table) instead of LDS.
+template <bool WIDE>
+__device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, EcdaW& S, const WaveMask& M,
+                                             const f32x4 (&ps)[ECDA_PRE_U], const int prd,
+                                             const int ncls, const int nvalid, const int npairs, const bool gc,
+                                             const bool rep_on, const float rep_coef, const float att_c, const int ncs,
+                                             const int ncand_all, const double wsum_t) {
+  const dad_config& cfg = a.cfg;
+  const int B = cfg.B, Bn = cfg.Bn;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int g = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kh = lane >> 5, l32 = lane & 31;
+  const float* emb_c = a.emb;
+  const float* emb_s = a.emb + (size_t)(B + Bn) * DAD_H;
+  const int npad = ncand_all <= 32 ? 32 : (ncand_all <= 64 ? 64 : 128);
+  const int nt = npad / 32;                       // 32-row tiles
+  const int npt = nt * (nt + 1) / 2;              // upper-triangle tile pairs: 1, 3 or 10
+  const int ks = npt == 1 ? 8 : (npt == 3 ? 2 : 1);   // K splits per pair
+  float* db = WIDE ? S.a.dbw : S.c.dbn;
+  const int dp = WIDE ? EW_CPW : EW_CP;
+  const int cnc = S.cnt[c];
+  const int nmem = ncs + cnc;   // members: clean candidates + masked noisy candidates
+  // candidate row i: LDS (narrow) or the embedding buffer (wide; rows past the candidates: zero)
+  auto rowp = [&](int i) -> const float* {
+    if constexpr (WIDE) return (i < ncs ? emb_c : emb_s) + (size_t)S.rowz[i < ncand_all ? i : 0] * DAD_H;
+    else return &S.a.zc[i * EW_ZP];
+  };
+  auto rowv = [&](int i, int col) -> float {
+    if constexpr (WIDE) return i < ncand_all ? rowp(i)[col] : 0.0f;
+    else return S.a.zc[i * EW_ZP + col];
+  };
+  if (gc) {
+    // Gram partials: tile pair (ti, tj) over a K slice, fp32 matrix cores
+    for (int item = g; item < npt * ks; item += ECDA_NG) {
+      const int pr = item / ks, sl = item - pr * ks;
+      int ti, tj;
+      ew_pair_inv(pr, nt, ti, tj);
+      const int kw = DAD_H / ks, k0 = sl * kw;
+      const int ia = 32 * ti + l32, ib = 32 * tj + l32;
+      const float* ra = rowp(ia) + kh;
+      const float* rb = rowp(ib) + kh;
+      const bool za = WIDE && ia >= ncand_all, zb = WIDE && ib >= ncand_all;
+      f32x16 acc = f32x16{};
+      for (int k = k0; k < k0 + kw; k += 8) {
+        float av[4], bv[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          av[e] = za ? 0.0f : ra[k + 2 * e];
+          bv[e] = zb ? 0.0f : rb[k + 2 * e];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[e], bv[e], acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) S.b.gp[item][dad_acc_row(r, kh) * 32 + l32] = acc[r];
+    }
+  }
+  // centroids of every class over its masked noisy rows, partials combined in wave order
+  for (int e = tid; e < DAD_C * DAD_H; e += ECDA_THREADS) {
+    const int k = e >> 8, hh = e & (DAD_H - 1);
+    float sk = 0.0f;
+#pragma unroll
+    for (int gg = 0; gg < ECDA_NG; ++gg) sk += S.c.cp[gg][k][hh];
+    const int nk = S.cnt[k];
+    S.cent[k][hh] = nk > 0 ? sk / (float)nk : 0.0f;
+  }
+  ECDA_STAMP(4);
+  __syncthreads();   // ---------------------------------------------------------------- 2
+  ECDA_STAMP(5);
+  // element ownership of the [npad x npad] matrices: row ei, columns ej0 .. ej0 + ept - 1
+  const int ept = npad * npad / ECDA_THREADS;     // 2, 8 or 32
+  const int tpr = npad / ept;                     // threads per row: 16, 8 or 4
+  const int ei = tid / tpr, ej0 = (tid - ei * tpr) * ept;
+  double bwpart = 0.0;
+  if (gc) {
+    // branch-free: every element computed, invalid ones selected to 0
+    const int mi = S.mem[ei < ncand_all ? ei : 0] & (ei < ncand_all ? 1 : 0);
+    for (int e = 0; e < ept; ++e) {
+      const int i = ei, j = ej0 + e;
+      // G_ij read at (min, max) in the upper-triangle tiles: D is symmetric bit for bit
+      const int lo = i < j ? i : j, hi = i < j ? j : i;
+      const int pr = ew_pair(lo >> 5, hi >> 5, nt);
+      float gsum = 0.0f;
+      for (int s2 = 0; s2 < ks; ++s2) gsum += S.b.gp[pr * ks + s2][(lo & 31) * 32 + (hi & 31)];
+      const bool ok = (i < ncand_all) & (j < ncand_all) & (i != j);
+      const float d = ok ? fmaxf((S.nz[lo] + S.nz[hi]) - 2.0f * gsum, 0.0f) : 0.0f;
+      const int mj = S.mem[j < ncand_all ? j : 0];
+      bwpart += (ok & (mi != 0) & (mj != 0)) ? (double)d : 0.0;
+      db[i * dp + j] = d;
+    }
+  }
+  // centroid distances (I/utils.py:582-595): 32 threads per (p, q) pair, pair-symmetric order
+  {
+    const int pair = tid / 32, t32 = tid & 31;
+    float d = 0.0f;
+    if (pair < DAD_C * DAD_C) {
+      const int p = pair / DAD_C, q = pair % DAD_C;
+      const int lo = p < q ? p : q, hi = p < q ? q : p;
+      const int np = S.cnt[p];
+      const int nq = S.cnt[q];
+      if (p < ncls && q < ncls && np > 0 && nq > 0 && p != q) {
+        const f32x4* a0 = reinterpret_cast<const f32x4*>(&S.cent[lo][t32 * (DAD_H / 32)]);
+        const f32x4* a1 = reinterpret_cast<const f32x4*>(&S.cent[hi][t32 * (DAD_H / 32)]);
+        const f32x4 x0 = a0[0], x1 = a0[1], y0 = a1[0], y1 = a1[1];
+        const float v[8] = {x0[0] - y0[0], x0[1] - y0[1], x0[2] - y0[2], x0[3] - y0[3],
+                            x1[0] - y1[0], x1[1] - y1[1], x1[2] - y1[2], x1[3] - y1[3]};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) d += v[k] * v[k];
+      }
+    }
+    d = dpp_seg_sum<32>(d);
+    if (pair < DAD_C * DAD_C && t32 == 31) S.pd[pair / DAD_C][pair % DAD_C] = sqrtf(d);
+  }
+  // compactness partial (I/utils.py:614-616): this wave's masked noisy rows of class c
+  if (gc) {
+    float cpart = 0.0f;
+    const f32x4 mu = *reinterpret_cast<const f32x4*>(&S.cent[c][4 * lane]);
+#pragma unroll
+    for (int u = 0; u < ECDA_PRE_U; ++u) {
+      const int b = g + ECDA_NG * u;
+      const int pk = __builtin_amdgcn_readlane(prd, b < 64 ? b : 0);
+      if (b < Bn && pk == c) {
+        const f32x4 df = ps[u] - mu;
+        cpart += ((df[0] * df[0] + df[1] * df[1]) + df[2] * df[2]) + df[3] * df[3];
+      }
+    }
+    cpart = dad_wave_sum(cpart);
+    bwpart = dad_wave_sum_d(bwpart);
+    if (lane == 0) { S.cmp[g] = cpart; S.bwp[g] = bwpart; }
+  }
+  __syncthreads();   // ---------------------------------------------------------------- 3
+  ECDA_STAMP(6);
+  const float wscale = cfg.w_ecda;
+  float pd[DAD_C][DAD_C];
+#pragma unroll
+  for (int p = 0; p < DAD_C; ++p)
+#pragma unroll
+    for (int q = 0; q < DAD_C; ++q) pd[p][q] = S.pd[p][q];
+  float rep = 0.0f;
+  if (nvalid > 1) {
+    float sp = 0.0f;
+#pragma unroll
+    for (int p = 0; p < DAD_C; ++p)
+#pragma unroll
+      for (int q = p + 1; q < DAD_C; ++q) {
+        const int np = S.cnt[p];
+        const int nq = S.cnt[q];
+        if (q < ncls && np > 0 && nq > 0) sp += pd[p][q];
+      }
+    rep = -sp / (float)npairs;
+  }
+  // repulsion grad of the class's noisy members, per hidden unit (d rep / d mu_c / n_c)
+  if (tid < DAD_H) {
+    float rep_g = 0.0f;
+    if (rep_on) {
+      float ce[DAD_C];
+#pragma unroll
+      for (int q = 0; q < DAD_C; ++q) ce[q] = S.cent[q][tid];
+      float gsum = 0.0f;
+#pragma unroll
+      for (int q = 0; q < DAD_C; ++q) {
+        const int nq = S.cnt[q];
+        if (q == c || q >= ncls || nq == 0) continue;
+        const float nd = S.pd[c][q];
+        if (nd > 0.0f) gsum += (sel4(ce, c) - ce[q]) / nd;
+      }
+      rep_g = wscale * rep_coef * (-gsum / (float)npairs / (float)cnc);
+    }
+    S.repg[tid] = rep_g;
+  }
+  const float Wss = (float)ncs * (float)ncs + 1e-8f;
+  const float Wtt = (float)(wsum_t * wsum_t) + 1e-8f;
+  const float Wst = (float)((double)ncs * wsum_t) + 1e-8f;
+  if (gc) {
+    // detached bandwidth (I/utils.py:540-544) and the weighted kernel terms (I/utils.py:546-563):
+    // every ordered member pair (i, j); the symmetric coefficients Csym_ij = dmmd/dD_ij + dmmd/dD_ji
+    double bws = 0.0;
+#pragma unroll
+    for (int gg = 0; gg < ECDA_NG; ++gg) bws += S.bwp[gg];
+    float bw = nmem > 1 ? (float)(bws / (double)(nmem * nmem - nmem)) : 1.0f;
+    bw = bw / 4.0f;
+    float ibw[5];
+#pragma unroll
+    for (int m = 0; m < 5; ++m) ibw[m] = 1.0f / (bw * (float)(1 << m) + 1e-8f);
+    double t3[3] = {0.0, 0.0, 0.0};
+    float rsp = 0.0f;
+    // branch-free: every element's K and coefficient computed, selected by pair type
+    const int ic = ei < ncand_all ? ei : 0;
+    const bool mi = (ei < ncand_all) & (S.mem[ic] != 0);
+    const float wi = S.wz[ic];
+    const bool si = ei < ncs;
+    const float css = 2.0f / Wss, ctt = 2.0f / Wtt, cst = -2.0f / Wst;
+    for (int e = 0; e < ept; ++e) {
+      const int j = ej0 + e;
+      const int jc = j < ncand_all ? j : 0;
+      const bool on = mi & (j < ncand_all) & (S.mem[jc] != 0);
+      const float wj = S.wz[jc];
+      const float d = db[ei * dp + j];
+      float K = 0.0f, dK = 0.0f;
+#pragma unroll
+      for (int m = 0; m < 5; ++m) {
+        const float ex = __expf(-d * ibw[m]);
+        K += ex;
+        dK -= ex * ibw[m];
+      }
+      const bool sj = j < ncs;
+      const bool ss = on & si & sj, tt = on & !si & !sj, st = on & si & !sj, ts = on & !si & sj;
+      const float ww = wi * wj;
+      t3[0] += ss ? (double)K : 0.0;
+      t3[1] += tt ? (double)K * ww : 0.0;
+      t3[2] += st ? (double)K * wj : 0.0;
+      // Csym: SS 2/Wss dK, TT 2 w_i w_j/Wtt dK, ST -2 w_j/Wst dK, TS -2 w_i/Wst dK
+      const float vss = css * dK, vtt = (ctt * ww) * dK, vst = (cst * wj) * dK, vts = (cst * wi) * dK;
+      float v = ss ? vss : (tt ? vtt : (st ? vst : (ts ? vts : 0.0f)));
+      v = ei == j ? 0.0f : v;
+      db[ei * dp + j] = v;
+      rsp += v;
+    }
+
+    // row sums of the coefficients: the tpr threads of a row are adjacent lanes
+    rsp = tpr == 16 ? dpp_seg_sum<16>(rsp) : (tpr == 8 ? dpp_seg_sum<8>(rsp) : dpp_seg_sum<4>(rsp));
+    if ((tid & (tpr - 1)) == tpr - 1) S.rs[ei] = rsp;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) t3[k] = dad_wave_sum_d(t3[k]);
+    if (lane == 0) { S.t3p[g][0] = t3[0]; S.t3p[g][1] = t3[1]; S.t3p[g][2] = t3[2]; }
+  }
+  __syncthreads();   // ---------------------------------------------------------------- 4
+  ECDA_STAMP(7);
+  float* ge_c = a.ge;
+  float* ge_s = a.ge + (size_t)B * DAD_H;
+  if (gc) {
+    double t3[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+    for (int gg = 0; gg < ECDA_NG; ++gg) {
+      t3[0] += S.t3p[gg][0];
+      t3[1] += S.t3p[gg][1];
+      t3[2] += S.t3p[gg][2];
+    }
+    // t_ss, t_tt, t_st as the reference forms them in float32 (I/utils.py:558-563)
+    const float mmd = (float)t3[0] / Wss + (float)t3[1] / Wtt - 2.0f * ((float)t3[2] / Wst);
+    float csum = 0.0f;
+#pragma unroll
+    for (int gg = 0; gg < ECDA_NG; ++gg) csum += S.cmp[gg];
+    const float comp = csum / (float)cnc;
+    if (tid == 0) {
+      a.tail_terms[c] = att_c * (mmd + cfg.ecda_gamma * comp + cfg.ecda_delta * rep);
+      a.tail_terms[DAD_T_ECDA_GATE - DAD_T_ECDA_TERM + c] = 1.0f;
+    }
+    const float mmd_scale = wscale * att_c;
+    const float comp_scale = wscale * att_c * cfg.ecda_gamma * (2.0f / (float)cnc);
+    // member grads 2 sum_j Csym_ij (z_i - z_j) = 2 (rs_i z_i - (Csym Z)_i): (Csym Z) on the
+    // matrix cores, 32 candidates x 32 hidden units per item
+    for (int item = g; item < nt * (DAD_H / 32); item += ECDA_NG) {
+      const int ti = item >> 3, tc = item & 7;
+      const int d = 32 * tc + l32;
+      f32x16 acc = f32x16{};
+      const float* ra = &db[(32 * ti + l32) * dp + kh];
+      for (int k = 0; k < npad; k += 8) {
+        float av[4], bv[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          av[e] = ra[k + 2 * e];
+          bv[e] = rowv(k + kh + 2 * e, d);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[e], bv[e], acc, 0, 0, 0);
+      }
+      const float mu = S.cent[c][d], rg = S.repg[d];
+      // every accumulator row stored: members to their ge row, the rest to the sink (no branch)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = 32 * ti + dad_acc_row(r, kh);
+        const int ic = i < ncand_all ? i : 0;
+        const bool ok = (i < ncand_all) & (S.mem[ic] != 0);
+        const float zi = rowv(i, d);
+        const bool noisy = i >= ncs;
+        const float gv = mmd_scale * (2.0f * (S.rs[ic] * zi - acc[r])) + (noisy ? comp_scale * (zi - mu) + rg : 0.0f);
+        float* dst = ok ? (noisy ? ge_s : ge_c) + (size_t)S.rowz[ic] * DAD_H + d : a.sink + d;
+        *dst = gv;
+      }
+    }
+  } else {
+    // a class below the gate only feeds the repulsion: its noisy members get repg
+    const int nct = ncand_all - ncs;
+    for (int e = tid; e < nct * (DAD_H / 4); e += ECDA_THREADS) {
+      const int i = ncs + e / (DAD_H / 4), q = e % (DAD_H / 4);
+      if (S.mem[i])
+        reinterpret_cast<f32x4*>(ge_s + (size_t)S.rowz[i] * DAD_H)[q] = reinterpret_cast<const f32x4*>(S.repg)[q];
+    }
+  }
+  for (int i = tid; i < ncand_all; i += ECDA_THREADS)
+    if (S.mem[i]) a.eflag[i < ncs ? S.rowz[i] : B + S.rowz[i]] = 1u;
+  ECDA_STAMP(8);
+  if (tid == 0) ECDA_STAMP_SIZES(c, ncand_all, ncs);
+}
+
+// One ECDA class (I/utils.py:565-632, class-aware) for B, Bn <= 64.
+__device__ __forceinline__ void ecda_block_w(const DadEcdaArgs& a, const DadTailArgs& ta, const int c, EcdaW& S) {
+  const dad_config& cfg = a.cfg;
+  const int B = cfg.B, Bn = cfg.Bn;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int g = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const float* emb_c = a.emb;
+  const float* emb_s = a.emb + (size_t)(B + Bn) * DAD_H;
+  ECDA_STAMP(0);
+  // ---- entry: teacher logits (lane = noisy row), labels (lane = clean row), and the embedding
+  // rows this wave handles (rows g, g + 8, ...; lane = 16-B column chunk), all in flight
+  // every load unconditional (rows clamped; the clamped duplicates are never used): a load
+  // under a condition is waited for where the paths merge, one round trip each
+  const int rc = lane < B ? lane : B - 1, rn = lane < Bn ? lane : Bn - 1;
+  const f32x4 zt = reinterpret_cast<const f32x4*>(ta.logits + (size_t)B * DAD_C)[rn];
+  const int yv = (int)a.yc[rc];
+  const float dv = ta.dacp[lane < DAD_DACP_FLOATS ? lane : 0];
+  // the rows are issued after the DACP inputs, so the DACP waits for those alone (counted
+  // vmcnt) while the rows are still in flight
+  __builtin_amdgcn_sched_barrier(0);
+  // strong rows: all (the centroids of every class need the masked ones)
+  f32x4 pc[ECDA_PRE_U], ps[ECDA_PRE_U];
+#pragma unroll
+  for (int u = 0; u < ECDA_PRE_U; ++u) {
+    const int b = g + ECDA_NG * u;
+    ps[u] = reinterpret_cast<const f32x4*>(emb_s + (size_t)(b < Bn ? b : Bn - 1) * DAD_H)[lane];
+  }
+  const int y = lane < B ? yv : -1;
+  // clean rows: only this class's candidates (label c), compacted; wave g loads candidates
+  // g, g + 8, ... (row 0 past the last), in flight during the DACP.  Per-CU load bandwidth from
+  // another XCD's writes is the limit here, so rows nobody stages are not fetched.
+  const uint64_t bcl = __ballot(y == c);
+  const int ncl = (int)__popcll(bcl);
+  const int posl = (int)__popcll(bcl & ((1ull << lane) - 1ull));
+#pragma unroll
+  for (int u = 0; u < ECDA_PRE_U; ++u) {
+    const int j = g + ECDA_NG * u;
+    const uint64_t hit = __ballot((y == c) & (posl == j));
+    const int row = hit ? (int)__builtin_ctzll(hit) : 0;
+    pc[u] = reinterpret_cast<const f32x4*>(emb_c + (size_t)row * DAD_H)[lane];
+  }
+  // ---- the DACP mask, in this wave (every wave computes the same one)
+  WaveMask M;
+  block_mask(cfg, Bn, zt, dacp_state_of(dv), S.b.dw, M);
+  ECDA_STAMP(1);
+  const int prd = M.m ? M.p : -1;                                // I/utils.py:573-576
+  const float msum = (float)__popcll(__ballot(M.m));
+  if (!(msum > 1.0f && cfg.ecda_on)) return;                     // I/train.py:444,450
+  const int ncls = cfg.use_dacp ? DAD_C : (Bn < DAD_C ? Bn : DAD_C);
+  if (c >= ncls) return;
+  // per-class counts, attention, gates, repulsion coefficient (uniform; I/utils.py:582-610)
+  int cc[DAD_C], cn[DAD_C];
+#pragma unroll
+  for (int k = 0; k < DAD_C; ++k) {
+    cc[k] = k < ncls ? (int)__popcll(__ballot(y == k)) : 0;
+    cn[k] = k < ncls ? (int)__popcll(__ballot(prd == k)) : 0;
+  }
+  float att[DAD_C];
+  if (cfg.use_dacp) {
+    const float wmean = (((M.wc[0] + M.wc[1]) + M.wc[2]) + M.wc[3]) / 4.0f;
+#pragma unroll
+    for (int k = 0; k < DAD_C; ++k) att[k] = expf(cfg.ecda_att_lambda * (wmean - M.wc[k]));
+  } else {
+#pragma unroll
+    for (int k = 0; k < DAD_C; ++k) att[k] = 1.0f;
+  }
+  int nvalid = 0;
+#pragma unroll
+  for (int k = 0; k < DAD_C; ++k) nvalid += (k < ncls && cn[k] > 0) ? 1 : 0;
+  const int npairs = nvalid * (nvalid - 1) / 2;
+#if DAD_PROBE_ON
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // stamps build: when the prefetched rows have landed
+  ECDA_STAMP(9);
+#endif
+  bool gated[DAD_C];
+  float rep_coef = 0.0f;
+#pragma unroll
+  for (int k = 0; k < DAD_C; ++k) {
+    gated[k] = k < ncls && cc[k] >= 2 && cn[k] >= 2;   // I/utils.py:609-610
+    if (gated[k]) rep_coef += att[k] * cfg.ecda_delta;
+  }
+  const int cnc = c == 0 ? cn[0] : (c == 1 ? cn[1] : (c == 2 ? cn[2] : cn[3]));
+  const int ccc = c == 0 ? cc[0] : (c == 1 ? cc[1] : (c == 2 ? cc[2] : cc[3]));
+  const bool gc = c == 0 ? gated[0] : (c == 1 ? gated[1] : (c == 2 ? gated[2] : gated[3]));
+  const float att_c = sel4(att, c);
+  const bool rep_on = nvalid > 1 && cnc > 0 && rep_coef != 0.0f;
+  if (!gc && !rep_on) return;
+  // candidates: clean rows of label c (members when gated), then noisy rows of pseudo-label c
+  // (members when masked in); positions by ballot prefix counts, every wave alike
+  const bool ccand = gc && y == c;
+  const bool ncand = lane < Bn && M.p == c;
+  const uint64_t bc = __ballot(ccand), bn = __ballot(ncand);
+  const int ncs = gc ? ccc : 0;
+  const int ncand_all = ncs + (int)__popcll(bn);
+  const bool wide = ncand_all > TW_MAXB;
+  const uint64_t below = (1ull << lane) - 1ull;
+  const int posc = (int)__popcll(bc & below);
+  const int posn = ncs + (int)__popcll(bn & below);
+  // ---- stage: candidate norms (and, narrow, rows), weights, rows and member flags; the
+  // per-wave centroid partial sums of every class
+  // a wave's candidate rows: their candidate positions (uniform), the others go to the spare
+  // row TW_MAXB (narrow) -- unconditional stores, no branches; norms by one batched butterfly
+  float nrm[2 * ECDA_PRE_U];
+  int npos[2 * ECDA_PRE_U];
+#pragma unroll
+  for (int u = 0; u < ECDA_PRE_U; ++u) {
+    const int b = g + ECDA_NG * u;                 // noisy row b; clean candidate b (compacted)
+    const bool okc = gc & (b < ncl);
+    const bool okn = (b < Bn) & (((bn >> b) & 1ull) != 0);
+    npos[2 * u] = okc ? b : -1;
+    npos[2 * u + 1] = okn ? __builtin_amdgcn_readlane(posn, b) : -1;
+    if (!wide) {
+      *reinterpret_cast<f32x4*>(&S.a.zc[(okc ? npos[2 * u] : TW_MAXB) * EW_ZP + 4 * lane]) = pc[u];
+      *reinterpret_cast<f32x4*>(&S.a.zc[(okn ? npos[2 * u + 1] : TW_MAXB) * EW_ZP + 4 * lane]) = ps[u];
+    }
+    nrm[2 * u] = ((pc[u][0] * pc[u][0] + pc[u][1] * pc[u][1]) + pc[u][2] * pc[u][2]) + pc[u][3] * pc[u][3];
+    nrm[2 * u + 1] = ((ps[u][0] * ps[u][0] + ps[u][1] * ps[u][1]) + ps[u][2] * ps[u][2]) + ps[u][3] * ps[u][3];
+  }
+#pragma unroll
+  for (int q = 0; q < 2 * ECDA_PRE_U; ++q) {   // candidate rows only (about 4 per wave): uniform branches
+    if (npos[q] >= 0) {
+      const float r = dad_wave_sum(nrm[q]);
+      if (lane == 0) S.nz[npos[q]] = r;
+    }
+  }
+  ECDA_STAMP(12);
+  if (!wide) {
+    const int npad = ncand_all <= 32 ? 32 : 64;
+    for (int r = ncand_all + g; r < npad; r += ECDA_NG) *reinterpret_cast<f32x4*>(&S.a.zc[r * EW_ZP + 4 * lane]) = f32x4{};
+  }
+  if (g == 0) {
+    if (lane < DAD_C) S.cnt[lane] = sel4i(cn, lane);
+    if (ccand) { S.rowz[posc] = lane; S.wz[posc] = 1.0f; S.mem[posc] = 1; }
+    if (ncand) { S.rowz[posn] = lane; S.wz[posn] = M.s; S.mem[posn] = M.m ? 1 : 0; }
+  }
+  {
+    // the class of each row is wave-uniform: one add per row into its class's sum (a uniform
+    // branch), not a select per class
+    f32x4 cs0 = f32x4{}, cs1 = f32x4{}, cs2 = f32x4{}, cs3 = f32x4{};
+#pragma unroll
+    for (int u = 0; u < ECDA_PRE_U; ++u) {
+      const int b = g + ECDA_NG * u;
+      const int pk = b < Bn ? __builtin_amdgcn_readlane(prd, b) : -1;
+      switch (pk) {
+        case 0: cs0 += ps[u]; break;
+        case 1: cs1 += ps[u]; break;
+        case 2: cs2 += ps[u]; break;
+        case 3: cs3 += ps[u]; break;
+        default: break;
+      }
+    }
+    *reinterpret_cast<f32x4*>(&S.c.cp[g][0][4 * lane]) = cs0;
+    *reinterpret_cast<f32x4*>(&S.c.cp[g][1][4 * lane]) = cs1;
+    *reinterpret_cast<f32x4*>(&S.c.cp[g][2][4 * lane]) = cs2;
+    *reinterpret_cast<f32x4*>(&S.c.cp[g][3][4 * lane]) = cs3;
+  }
+  // weight sum of the noisy members (I/utils.py:552-557), in every wave
+  const double wsum_t = dad_wave_sum_d((ncand && M.m) ? (double)M.s : 0.0);
+  (void)cc;
+  ECDA_STAMP(2);
+  __syncthreads();   // ---------------------------------------------------------------- 1
+  ECDA_STAMP(3);
+  if (wide)
+    ecda_class_w<true>(a, c, S, M, ps, prd, ncls, nvalid, npairs, gc, rep_on, rep_coef, att_c, ncs, ncand_all, wsum_t);
+  else
+    ecda_class_w<false>(a, c, S, M, ps, prd, ncls, nvalid, npairs, gc, rep_on, rep_coef, att_c, ncs, ncand_all, wsum_t);
+}
+
+// block 0: the wave-centric tail; blocks 1..C: ECDA class blockIdx.x - 1.  Host contract:
+// B <= 64, Bn <= 64, class-aware MMD (dad_tail_ecda otherwise).
+__global__ __launch_bounds__(TAIL_THREADS) void dad_tail_ecda_w(DadTailArgs ta, DadEcdaArgs ca) {
+  DAD_GUARD_BLOCK(TAIL_THREADS);
+  __shared__ union UW {
+    TailW t;
+    EcdaW e;
+  } u;
+  if (ta.cfg.B > TW_MAXB || ta.cfg.Bn > TW_MAXB) return;
+  if (blockIdx.x == 0) tail_block_w(ta, u.t);
+  else ecda_block_w(ca, ta, (int)blockIdx.x - 1, u.e);
 }
 
 // ------------------------------------------------------------- helper-type drop-ins

@@ -1,0 +1,56 @@
+"""Diagnostic: dad_tail_ecda_w phase timeline (build variant 'stamps', -DDAD_PROBE_STAMPS; never the
+product library).  Runs bench-shaped steps and prints the median phase ends (us after the tail
+block's start) of the tail block and the four ECDA class blocks."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ.setdefault("DAD_LIB_VARIANT", "stamps")
+import bench  # noqa: E402
+
+PKG = bench.PKG
+
+
+def main():
+    B, T = 64, 300
+    model = PKG.SSRLModel().cuda()
+    P = bench.init_model_weights(model, seed=0)
+    step = PKG.DADStep(model, flavor="iemocap", precision="bf16", rng="counter", seed=1)
+    data = bench.make_batches(P, 2, B, T, seed=17, device=torch.device("cuda"))
+    S = 24  # slots per ECDA class (tail.hip ECDA_SLOTS)
+    L = PKG.lib()
+    reps = int(os.environ.get("STAMP_REPS", "15"))
+    raw = []
+    for r in range(reps):   # the last step of a 4-step burst, reps times
+        for i in range(4):
+            step.step(data[i % 2][0], data[i % 2][1], 60)
+        torch.cuda.synchronize()
+        ebuf = (ctypes.c_ulonglong * (4 * S + 16))()
+        assert L.dad_probe_read_ecda_stamps(ebuf, len(ebuf)) == 0
+        raw.append(np.frombuffer(ebuf, dtype=np.uint64).astype(np.int64))
+    raw = np.stack(raw[2:] if reps > 4 else raw)
+    T0 = 4 * S
+    t0 = raw[:, T0:T0 + 1]
+    rel = np.median((raw - t0) / 100.0, axis=0)
+    on = np.all(raw > 0, axis=0)
+    print("median of %d steps; us after the tail block's start" % raw.shape[0])
+    print("tail: " + "  ".join("%s %.2f" % (n, rel[T0 + k]) for k, n in ((4, "mask"), (2, "ce-wave"), (7, "certainty"), (8, "ranks"), (9, "quantile"),
+                                                                          (10, "bcast"), (4, "dacp-wave"), (5, "kl"),
+                                                                          (6, "w1-done"), (1, "end")) if on[T0 + k]))
+    if on[T0 + 13] and on[T0 + 12]:
+        ghz = np.median((raw[:, T0 + 13] - raw[:, T0 + 12]) / ((raw[:, T0 + 1] - raw[:, T0]) * 10.0))
+        print("  tail block clock: %.2f GHz" % ghz)
+    names = ["start", "dacp", "staged", "b1", "gram+cent", "b2", "b3", "b4", "end", "rows-landed", "", "", "norms"]
+    for c in range(4):
+        o = c * S
+        print("ecda class %d (cand %d, clean %d): %s" % (c, raw[-1, o + 10], raw[-1, o + 11], "  ".join(
+            "%s %.2f" % (names[k], rel[o + k]) for k in (0, 1, 9, 12, 2, 3, 4, 5, 6, 7, 8) if on[o + k])))
+
+
+if __name__ == "__main__":
+    main()
