@@ -385,11 +385,13 @@ def merge_ktimes(parts):
 
 
 ENC_KERNEL = {"bf16": "dad_encode_ws", "fp32": "dad_encode_f32"}
-WGRAD_KERNEL = {"bf16": ("wgrad", "dad_wgrad_direct"), "fp32": ("side", "dad_wgrad_f32")}
+WGRAD_KERNEL = {"bf16": ("wgrad", "dad_wgrad_direct"), "fp32": ("wgrad", "dad_wgrad_f32")}
+# (the labels of the default direct weight gradient; DAD_WGRAD[_F32]=su runs S_u on a side stream,
+# timed as "side", and dad_wsum in the "wgrad" slot)
 KNAMES = {"bf16": {"encode": "dad_encode_ws", "pool": "dad_pool", "tail": "dad_tail_ecda", "wgrad": "dad_wgrad_direct",
                    "reduce": "dad_reduce", "optim": "dad_optim"},
-          "fp32": {"encode": "dad_encode_f32", "pool": "dad_pool", "tail": "dad_tail_ecda", "side": "dad_wgrad_f32",
-                   "wgrad": "dad_wsum (after the side-stream join)", "optim": "dad_optim"}}
+          "fp32": {"encode": "dad_encode_f32", "pool": "dad_pool", "tail": "dad_tail_ecda", "wgrad": "dad_wgrad_f32",
+                   "reduce": "dad_reduce", "side": "dad_wgrad_f32 (S_u, side stream)", "optim": "dad_optim"}}
 
 
 def rooflines(ktimes, rows_c, rows_n, ms_step, precision):

@@ -108,6 +108,14 @@ bool wgrad_direct() {
   const char* e = getenv("DAD_WGRAD");
   return !(e && strcmp(e, "su") == 0);
 }
+// FP32: likewise the direct split-K GEMM after the losses (default), or S_u per utterance on
+// the side stream (DAD_WGRAD_F32=su).  S_u costs 98 MB written and read again and its 768
+// per-utterance tiles do not divide evenly over the CUs: measured 254 + 15 us against ~130 +
+// 8 us for the direct form, which only loses the ~40 us of pool/tail overlap.
+bool wgrad_f32_direct() {
+  const char* e = getenv("DAD_WGRAD_F32");
+  return !(e && strcmp(e, "su") == 0);
+}
 
 // DAD_TAIL_W=0 selects the general tail + ECDA launch for every batch (A/B runs; read once)
 bool tail_w_on() {
@@ -450,7 +458,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   wa.strong_std = cfg->strong_std; wa.feat_p = cfg->feat_p;
   wa.bits = bits; wa.ge = ge; wa.vlen = vlen; wa.xs_bf16 = xs_bf16;
   SideStream* side = nullptr;
-  const bool factorised = !bf16 || !wgrad_direct();
+  const bool factorised = bf16 ? !wgrad_direct() : !wgrad_f32_direct();
   if (factorised) {
     const int rc = side_stream(&side);
     if (rc) return rc;
@@ -466,7 +474,9 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
     } else {
       wa.ntiles = 6 * nutt;
       const int sgrid = std::max(1, std::min(wa.ntiles, side->cus - kReservedCUs));
-      hipLaunchKernelGGL(dad_wgrad_f32, dim3(sgrid), dim3(DAD_WGRAD_THREADS), 0, side->s, wa);
+      DadReduceArgs none;
+      memset(&none, 0, sizeof(none));
+      hipLaunchKernelGGL(dad_wgrad_f32, dim3(sgrid), dim3(DAD_WGRAD_THREADS), 0, side->s, wa, none);
     }
     DAD_TRY(hipGetLastError());
     tk_mark(TK_S1, side->s);
@@ -534,7 +544,21 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   ra.key_drop1 = k.drop1; ra.key_drop2 = k.drop2; ra.p_drop = cfg->p_drop; ra.drop_scale = cfg->drop_scale;
   ra.ge = ge; ra.vlen = vlen; ra.cnt_tot = cnt_tot; ra.tailf = st->tail;
   ra.grad = st->grad; ra.normpart = normpart;
-  if (!factorised) {
+  if (!factorised && !bf16) {
+    // FP32 direct: G = ReLU' * dL/de / len rebuilt per slab from the tail's dL/dz and the
+    // ECDA rows; one tile = (split, 128 columns); then every reduce block (dW1 sums and the
+    // db1 / dW2 / totals blocks)
+    wa.splits = splits; wa.per_utt = 0;
+    wa.wpart = ws_ptr<float>(workspace, L.wpart);
+    wa.ntiles = 6 * splits;
+    hipLaunchKernelGGL(dad_wgrad_f32, dim3(wa.ntiles), dim3(DAD_WGRAD_THREADS), 0, stream, wa, ra);
+    DAD_TRY(hipGetLastError());
+    tk_mark(TK_WGRAD, stream);
+    ra.splits = splits; ra.wpart = wa.wpart;
+    hipLaunchKernelGGL(dad_reduce, dim3(DAD_REDUCE_BLOCKS), dim3(DAD_REDUCE_THREADS), 0, stream, ra);
+    DAD_TRY(hipGetLastError());
+    tk_mark(TK_RED, stream);
+  } else if (!factorised) {
     wa.splits = splits; wa.per_utt = 0;
     wa.wpart = ws_ptr<float>(workspace, L.wpart);
     wa.ntiles = WGD_NDB * splits;
@@ -836,7 +860,9 @@ int dad_encoder_backward(const float* x, const uint8_t* pad, int B, int T, const
   wa.g = G; wa.warmup = 1; wa.splits = splits; wa.ntiles = 6 * splits;
   wa.xc = x; wa.bits = ws_ptr<uint32_t>(workspace, L.bits); wa.ge = de; wa.vlen = vlen;
   wa.wpart = ws_ptr<float>(workspace, L.wpart);
-  hipLaunchKernelGGL(dad_wgrad_f32, dim3(6 * splits), dim3(DAD_WGRAD_THREADS), 0, stream, wa);
+  DadReduceArgs none;
+  memset(&none, 0, sizeof(none));
+  hipLaunchKernelGGL(dad_wgrad_f32, dim3(6 * splits), dim3(DAD_WGRAD_THREADS), 0, stream, wa, none);
   DAD_TRY(hipGetLastError());
   float* gflat = ws_ptr<float>(workspace, L.gflat);
   DadReduceArgs ra;

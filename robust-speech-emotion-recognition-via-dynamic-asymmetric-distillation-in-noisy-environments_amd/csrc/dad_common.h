@@ -329,8 +329,8 @@ struct DadWs {
 
 static inline size_t dad_align(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// weight-gradient split-K factor.  FP32 (dad_wgrad_f32, 6 column blocks per split): 64
-// splits.  BF16 (dad_wgrad_direct, 12 column blocks per split): 21 splits -> 252 workgroups,
+// weight-gradient split-K factor.  FP32 (dad_wgrad_f32, 6 column blocks per split): 42
+// splits -> 252 tiles.  BF16 (dad_wgrad_direct, 12 column blocks per split): 21 splits -> 252 workgroups,
 // one per CU, and never more than WGD_MAXU = 64 slabs per split (its dL/de table in LDS).
 // Both are bounded by the number of 32-row slabs.
 #ifndef WGD_SPLITS
@@ -339,7 +339,8 @@ static inline size_t dad_align(size_t x) { return (x + 255) & ~(size_t)255; }
 static inline int dad_wgd_min_splits(int total) { return (total + 63) / 64; }
 static inline int dad_auto_splits(const DadGeom& g, int precision, int warmup) {
   const int total = g.Bc * g.ncc + (warmup ? 0 : g.Bn * g.ncn);
-  const int target = precision == DAD_PREC_BF16 ? WGD_SPLITS : 64;
+  // FP32: 42 splits x 6 column blocks = 252 tiles, one per CU
+  const int target = precision == DAD_PREC_BF16 ? WGD_SPLITS : 42;
   int s = total < target ? total : target;
   if (precision == DAD_PREC_BF16 && s < dad_wgd_min_splits(total)) s = dad_wgd_min_splits(total);
   return s;

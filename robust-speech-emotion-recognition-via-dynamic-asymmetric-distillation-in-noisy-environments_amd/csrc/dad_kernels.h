@@ -168,7 +168,7 @@ __global__ void dad_tail(DadTailArgs a);
 __global__ void dad_ecda(DadEcdaArgs a);
 __global__ void dad_tail_ecda(DadTailArgs ta, DadEcdaArgs ca);
 __global__ void dad_tail_ecda_w(DadTailArgs ta, DadEcdaArgs ca);   // B, Bn <= 64, class-aware
-__global__ void dad_wgrad_f32(DadWgradArgs a);
+__global__ void dad_wgrad_f32(DadWgradArgs a, DadReduceArgs r);   // r: the fused step's dL/de sources (gzb) or zeroed
 __global__ void dad_wgrad_direct(DadWgradArgs a, DadReduceArgs r);
 __global__ void dad_wgrad_su(DadWgradArgs a);
 __global__ void dad_wsum(DadReduceArgs a);

@@ -136,8 +136,86 @@ __device__ __forceinline__ void encode_finish(const DadEncodeArgs& a, const Enco
 }  // namespace
 
 // ------------------------------------------------------------------- FP32 (parity mode)
+// Software-pipelined over the 96 k-steps: the W1 fragments (16 x 16 B per lane, both networks
+// on a noisy slab) and the x chunk of k-step n+1 are loaded while the MFMAs of k-step n run
+// (unconditional loads, the last step's prefetch clamped), so the L2 round trip of W1 is
+// not paid once per k-step.
+template <bool NOISY, bool EXPLICIT>
+__device__ __forceinline__ void encode_f32_slab(const DadEncodeArgs& a, const float* X, const float* Ws,
+                                                const float* Wt, int grow, int kh, bool tin, bool tzero, const float* fk,
+                                                f32x16 (&acc0)[DAD_HT], f32x16 (&acc1)[DAD_HT]) {
+  constexpr int NW = NOISY ? 2 : 1;
+  f32x4 xc = ld4(X + 4 * kh), wc[NW][DAD_HT];
+  f32x4 nwc, nsc;
+#pragma unroll
+  for (int ht = 0; ht < DAD_HT; ++ht) {
+    wc[0][ht] = ld4(Ws + (size_t)ht * 32 * DAD_D);
+    if constexpr (NOISY) wc[1][ht] = ld4(Wt + (size_t)ht * 32 * DAD_D);
+  }
+  if constexpr (NOISY && EXPLICIT) {
+    nwc = ld4(a.nw + (size_t)grow * DAD_D + 4 * kh);
+    nsc = ld4(a.ns + (size_t)grow * DAD_D + 4 * kh);
+  }
+  for (int d0 = 0; d0 < DAD_D; d0 += 8) {
+    const int dn = d0 + 8 < DAD_D ? d0 + 8 : d0;   // next k-step (the last one reloads itself)
+    f32x4 xn = ld4(X + dn + 4 * kh), wn[NW][DAD_HT];
+    f32x4 nwn, nsn;
+#pragma unroll
+    for (int ht = 0; ht < DAD_HT; ++ht) {
+      wn[0][ht] = ld4(Ws + (size_t)ht * 32 * DAD_D + dn);
+      if constexpr (NOISY) wn[1][ht] = ld4(Wt + (size_t)ht * 32 * DAD_D + dn);
+    }
+    if constexpr (NOISY && EXPLICIT) {
+      nwn = ld4(a.nw + (size_t)grow * DAD_D + dn + 4 * kh);
+      nsn = ld4(a.ns + (size_t)grow * DAD_D + dn + 4 * kh);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const f32x4 x = tin ? xc : f32x4{};
+    if constexpr (!NOISY) {
+#pragma unroll
+      for (int ht = 0; ht < DAD_HT; ++ht)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc0[ht] = __builtin_amdgcn_mfma_f32_32x32x2f32(x[e], wc[0][ht][e], acc0[ht], 0, 0, 0);
+    } else {
+      const int d = d0 + 4 * kh;
+      f32x4 nw, ns;
+      if constexpr (EXPLICIT) { nw = nwc; ns = nsc; }
+      else {
+        nw = dad_normal4(a.key_weak, (uint32_t)grow, (uint32_t)d);
+        ns = dad_normal4(a.key_strong, (uint32_t)grow, (uint32_t)d);
+      }
+      // op order of the reference: noise * std then add; * feature mask; temporal zero
+      const f32x4 kp = *reinterpret_cast<const f32x4*>(fk + d);
+      f32x4 xw, xs;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        xw[e] = x[e] + nw[e] * a.weak_std;
+        const float v = (x[e] + ns[e] * a.strong_std) * kp[e];
+        xs[e] = tzero ? 0.0f : v;
+      }
+#pragma unroll
+      for (int ht = 0; ht < DAD_HT; ++ht)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          acc0[ht] = __builtin_amdgcn_mfma_f32_32x32x2f32(xw[e], wc[1][ht][e], acc0[ht], 0, 0, 0);
+          acc1[ht] = __builtin_amdgcn_mfma_f32_32x32x2f32(xs[e], wc[0][ht][e], acc1[ht], 0, 0, 0);
+        }
+    }
+    xc = xn;
+#pragma unroll
+    for (int k = 0; k < NW; ++k)
+#pragma unroll
+      for (int ht = 0; ht < DAD_HT; ++ht) wc[k][ht] = wn[k][ht];
+    if constexpr (NOISY && EXPLICIT) { nwc = nwn; nsc = nsn; }
+  }
+}
+
 __global__ __launch_bounds__(DAD_ENC_F32_THREADS) void dad_encode_f32(DadEncodeArgs a) {
   DAD_GUARD_BLOCK(DAD_ENC_F32_THREADS);
+  // the strong augmentation's feature keep flags (I/utils.py:343), once per workgroup
+  __shared__ __attribute__((aligned(16))) float fk[DAD_D];
+  for (int d = threadIdx.x; d < DAD_D; d += DAD_ENC_F32_THREADS) fk[d] = dad_feat_keep(a.u, a.key_feat, d, a.feat_p);
+  __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const int wid = blockIdx.x * 4 + wv;
@@ -167,33 +245,8 @@ __global__ __launch_bounds__(DAD_ENC_F32_THREADS) void dad_encode_f32(DadEncodeA
     acc1[ht] = f32x16{};
   }
   // k ordering: step (d0, e, kh) uses channel d0 + 4*kh + e for BOTH operands
-  if (!g.noisy) {
-    for (int d0 = 0; d0 < DAD_D; d0 += 8) {
-      const f32x4 x = tin ? ld4(X + d0 + 4 * kh) : f32x4{};
-#pragma unroll
-      for (int ht = 0; ht < DAD_HT; ++ht) {
-        const f32x4 w = ld4(Ws + (size_t)ht * 32 * DAD_D + d0);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc0[ht] = __builtin_amdgcn_mfma_f32_32x32x2f32(x[e], w[e], acc0[ht], 0, 0, 0);
-      }
-    }
-  } else {
-    for (int d0 = 0; d0 < DAD_D; d0 += 8) {
-      const int d = d0 + 4 * kh;
-      const f32x4 x = tin ? ld4(X + d) : f32x4{};
-      f32x4 xw, xs;
-      augment4(a, x, grow, d, tzero, xw, xs);
-#pragma unroll
-      for (int ht = 0; ht < DAD_HT; ++ht) {
-        const f32x4 wt = ld4(Wt + (size_t)ht * 32 * DAD_D + d0);
-        const f32x4 ws = ld4(Ws + (size_t)ht * 32 * DAD_D + d0);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          acc0[ht] = __builtin_amdgcn_mfma_f32_32x32x2f32(xw[e], wt[e], acc0[ht], 0, 0, 0);
-          acc1[ht] = __builtin_amdgcn_mfma_f32_32x32x2f32(xs[e], ws[e], acc1[ht], 0, 0, 0);
-        }
-      }
-    }
-  }
+  if (!g.noisy) encode_f32_slab<false, false>(a, X, Ws, Wt, grow, kh, tin, tzero, fk, acc0, acc1);
+  else if (a.nw) encode_f32_slab<true, true>(a, X, Ws, Wt, grow, kh, tin, tzero, fk, acc0, acc1);
+  else encode_f32_slab<true, false>(a, X, Ws, Wt, grow, kh, tin, tzero, fk, acc0, acc1);
   encode_finish(a, g, acc0, acc1, vbits);
 }

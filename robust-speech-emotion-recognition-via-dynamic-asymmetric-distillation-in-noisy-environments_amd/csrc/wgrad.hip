@@ -109,66 +109,208 @@ __device__ __forceinline__ float fused_ge1(const DadReduceArgs& a, int Bc, int u
 // ------------------------------------------------------------------- FP32 (parity mode)
 // grid = 6 column blocks x splits; wave = 32 columns x 256 rows of dW1.
 // v_mfma_f32_32x32x2_f32: A[i=h][k] = G[row k][h], B[k][j=d] = x[row k][d] (k = 2 rows).
-__global__ __launch_bounds__(DAD_WGRAD_THREADS) void dad_wgrad_f32(DadWgradArgs a) {
-  DAD_GUARD_BLOCK(DAD_WGRAD_THREADS);
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int i = lane & 31, kh = lane >> 5;
-  for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
-  const int dblk = tile % 6, split = tile / 6;
-  const int d0 = (dblk * 4 + wv) * 32;
-  int s0, s1;
-  wg_range(a, split, s0, s1);
-  f32x16 acc[DAD_HT];
+//
+// An f32 MFMA holds the SIMD's vector issue for its whole 64 cycles (PMC: zero VALU/MFMA
+// co-execution cycles), so every VALU instruction of the loop adds its 4+ cycles to the
+// MFMA time: the loop is built to issue as few as possible per MFMA.
+//   * G (256 h x 32 rows of the slab, = ReLU' bit ? dL/de_u[h] / len_u : 0) is built ONCE per
+//     workgroup into LDS (thread = h, double-buffered, one barrier per slab) and read as MFMA
+//     A operands with ds_read_b128 (4 row pairs per read), instead of every wave rebuilding
+//     all of it per MFMA (select + scale: 2-3 VALU per MFMA, and the fused dL/de per h).
+//   * x (rows 2j + kh at column d) is loaded one slab ahead through a buffer descriptor of the
+//     slab's valid rows (rows past the utterance read 0; one add per load for the address).
+// The strong branch's augmentation is regenerated per element (counter RNG or explicit noise).
+constexpr int F32_GP = 36;   // G tile pitch per h: [kh][16 pairs] + 4 floats (conflict-free b128 reads)
+
+// the scale of G: 1 (S_u mode), dL/de / len from a dL/de buffer, or rebuilt from the tail's
+// dL/dz and the ECDA rows (fused step, fused_ge1)
+enum { F32_SU = 0, F32_GE = 1, F32_FUSED = 2 };
+
+struct F32X {
+  float x[16], n[16];
+};
+
+// this lane's x (and explicit noise) of slab s: rows 2j + kh, column d
+template <bool EXPLICIT, bool STORE>
+__device__ __forceinline__ void f32_xload(const DadWgradArgs& a, int s, int d, int kh, F32X& r) {
+  const SlabIdx q = wg_slab(a, s);
+  const int nval = min(DAD_SLAB, q.T - q.c * DAD_SLAB);   // rows of the slab inside the utterance
+#ifndef F32_BUFLOAD
+#define F32_BUFLOAD 1
+#endif
+  if constexpr (!STORE && F32_BUFLOAD) {
+    const float* X = (q.br ? a.xn : a.xc) + (q.row0 + (size_t)q.c * DAD_SLAB) * DAD_D;
+    const auto rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(X), 0, nval * DAD_D * 4, 0x00020000);
+    // The row offset goes in voffset, not soffset: the range check compares voffset (+ the
+    // instruction offset) with num_records, so rows past the utterance read 0 and nothing is
+    // read past the slab.  (The builtin returns the raw bits: __uint_as_float, not a value
+    // conversion.)
+    const int vo = (kh * DAD_D + d) * 4;
 #pragma unroll
-  for (int ht = 0; ht < DAD_HT; ++ht) acc[ht] = f32x16{};
-  const int d = d0 + i;
-  for (int s = s0; s < s1; ++s) {
-    const SlabIdx q = wg_slab(a, s);
+    for (int j = 0; j < 16; ++j)
+      r.x[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, vo + j * 2 * DAD_D * 4, 0, 0));
+    if constexpr (EXPLICIT) {
+      const float* N = a.ns + (q.row0 + (size_t)q.c * DAD_SLAB) * DAD_D;
+      const auto rn = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(N), 0, nval * DAD_D * 4, 0x00020000);
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        r.n[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rn, vo + j * 2 * DAD_D * 4, 0, 0));
+    }
+  } else {
     const float* X = q.br ? a.xn : a.xc;
-    float scale[DAD_HT];
-    if (a.per_utt) {
 #pragma unroll
-      for (int ht = 0; ht < DAD_HT; ++ht) scale[ht] = 1.0f;
-    } else {
-      const float len = fmaxf(a.vlen[q.erow], 1.0f);
-#pragma unroll
-      for (int ht = 0; ht < DAD_HT; ++ht) scale[ht] = a.ge[(size_t)q.erow * DAD_H + ht * 32 + i] / len;
+    for (int j = 0; j < 16; ++j) {
+      const int t = min(q.c * DAD_SLAB + 2 * j + kh, q.T - 1);
+      r.x[j] = X[dad_src_row(a.src, q.br, q.b, q.T, t) * DAD_D + d];
+      if constexpr (EXPLICIT) r.n[j] = a.ns[(q.row0 + t) * DAD_D + d];
     }
-    int st = 0;
-    float fkeep = 1.0f;
-    if (q.br) {
-      st = a.mask_len > 0 ? wg_tstart(a, q.b) : 0;
-      fkeep = wg_featkeep(a, d);
-    }
-    // row masks of this lane's hidden units h = 32 ht + i (bit r = row r of the slab)
-    uint32_t mw[DAD_HT];
+  }
+}
+
+// G inputs of thread h for slab s: the ReLU' row mask and the ECDA row / dL/de value
+struct F32GIn {
+  uint32_t mw;
+  float ec;
+};
+template <int MODE>
+__device__ __forceinline__ void f32_gload(const DadWgradArgs& a, const DadReduceArgs& ra, int s, int h, F32GIn& r) {
+  const SlabIdx q = wg_slab(a, s);
+  r.mw = a.bits[q.bits_slab * DAD_H + h];
+  r.ec = 0.0f;
+  if constexpr (MODE == F32_GE) r.ec = a.ge[(size_t)q.erow * DAD_H + h];
+  if constexpr (MODE == F32_FUSED) r.ec = ra.ge_ecda[(size_t)q.erow * DAD_H + h];
+}
+
+// G^T of slab s into LDS: thread h writes G[h][kh][j] = bit (2j + kh) of its mask ? scale : 0
+template <int MODE, bool KEEPX>
+__device__ __forceinline__ void f32_gbuild(const DadWgradArgs& a, const DadReduceArgs& ra, int s, int h,
+                                           const float (&w2h)[4], const F32GIn& gi, float* G) {
+  const SlabIdx q = wg_slab(a, s);
+  float scale = 1.0f;
+  if constexpr (MODE == F32_GE) scale = gi.ec / fmaxf(a.vlen[q.erow], 1.0f);
+  if constexpr (MODE == F32_FUSED) {
+    // dL/de_u[h] / max(1, len_u), as dad_wgrad_direct builds it (bf16 there, f32 here)
+    const int u = q.erow;
+    const f32x4 gz = *reinterpret_cast<const f32x4*>(ra.gzb + (size_t)u * DAD_C);
+    scale = fused_ge1_v<KEEPX>(ra, a.g.Bc, u, h, w2h, gz, ra.eflag[u], gi.ec) / fmaxf(ra.vlen[u], 1.0f);
+  }
+  const uint32_t sb = __float_as_uint(scale);
 #pragma unroll
-    for (int ht = 0; ht < DAD_HT; ++ht) mw[ht] = a.bits[q.bits_slab * DAD_H + ht * 32 + i];
-    for (int rr = 0; rr < DAD_SLAB; rr += 2) {
-      if (q.c * DAD_SLAB + rr >= q.T) break;
-      const int t = q.c * DAD_SLAB + rr + kh;
-      const bool tin = t < q.T;
-      const size_t grow = q.row0 + (tin ? t : 0);
-      float x = tin ? X[dad_src_row(a.src, q.br, q.b, q.T, t) * DAD_D + d] : 0.0f;
-      if (q.br && tin) {
-        const float n = a.ns ? a.ns[grow * DAD_D + d] : dad_normal1(a.key_strong, (uint32_t)(grow * DAD_D + d));
+  for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) {
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        v[e] = __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)gi.mw, 2 * (4 * q4 + e) + kh, 1) & sb);
+      *reinterpret_cast<f32x4*>(G + h * F32_GP + kh * 16 + 4 * q4) = v;
+    }
+}
+
+// one slab's 128 MFMAs of this wave: A from the LDS G tile, B = x (strong: augmented here)
+template <bool EXPLICIT, bool STRONG>
+__device__ __forceinline__ void f32_mma(const DadWgradArgs& a, const SlabIdx& q, int d, int kh, float fkeep, int st,
+                                        const float* G, const F32X& r, f32x16 (&acc)[DAD_HT]) {
+  const int lane = threadIdx.x & 63;
+  const float* gl = G + (lane & 31) * F32_GP + kh * 16;
+#pragma unroll
+  for (int q4 = 0; q4 < 4; ++q4) {
+    f32x4 gv[DAD_HT];
+#pragma unroll
+    for (int ht = 0; ht < DAD_HT; ++ht) gv[ht] = *reinterpret_cast<const f32x4*>(gl + ht * 32 * F32_GP + 4 * q4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int j = 4 * q4 + e;
+      float x = r.x[j];
+      if constexpr (STRONG) {
+        const int t = q.c * DAD_SLAB + 2 * j + kh;
+        const bool tin = t < q.T;
+        const size_t grow = q.row0 + (tin ? t : 0);
+        const float n = EXPLICIT ? r.n[j] : dad_normal1(a.key_strong, (uint32_t)(grow * DAD_D + d));
         const float sn = n * a.strong_std;
         x = (x + sn) * fkeep;
-        if (a.mask_len > 0 && t >= st && t < st + a.mask_len) x = 0.0f;
+        x = (t >= st && t < st + a.mask_len) ? 0.0f : x;   // (st + mask_len <= st when mask_len = 0)
+        x = tin ? x : 0.0f;
       }
 #pragma unroll
-      for (int ht = 0; ht < DAD_HT; ++ht) {
-        const float g = ((mw[ht] >> (rr + kh)) & 1u) ? scale[ht] : 0.0f;
-        acc[ht] = __builtin_amdgcn_mfma_f32_32x32x2f32(g, x, acc[ht], 0, 0, 0);
-      }
+      for (int ht = 0; ht < DAD_HT; ++ht) acc[ht] = __builtin_amdgcn_mfma_f32_32x32x2f32(gv[ht][e], x, acc[ht], 0, 0, 0);
     }
   }
-  float* out = a.wpart + (size_t)split * DAD_H * DAD_D;
+}
+
+template <bool EXPLICIT, int MODE, bool STORE, bool KEEPX>
+__device__ __forceinline__ void wgrad_f32_body(const DadWgradArgs& a, const DadReduceArgs& ra, float* Gs) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int i = lane & 31, kh = lane >> 5;
+  const int h = tid;   // (256 threads = the 256 hidden units, for the G tile)
+  float w2h[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  if constexpr (MODE == F32_FUSED)
 #pragma unroll
-  for (int ht = 0; ht < DAD_HT; ++ht)
+    for (int c = 0; c < 4; ++c) w2h[c] = ra.student[DAD_OFF_W2 + c * DAD_H + h];
+  for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+    const int dblk = tile % 6, split = tile / 6;
+    const int d = (dblk * 4 + wv) * 32 + i;
+    int s0, s1;
+    wg_range(a, split, s0, s1);
+    f32x16 acc[DAD_HT];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) out[(size_t)(ht * 32 + dad_acc_row(r, kh)) * DAD_D + d] = acc[ht][r];
+    for (int ht = 0; ht < DAD_HT; ++ht) acc[ht] = f32x16{};
+    const float fkeep = wg_featkeep(a, d);   // (the strong branch's feature mask; clean rows ignore it)
+    if (s0 < s1) {
+      F32GIn gi, gn;
+      F32X cur, nxt;
+      f32_gload<MODE>(a, ra, s0, h, gi);
+      f32_xload<EXPLICIT, STORE>(a, s0, d, kh, cur);
+      f32_gload<MODE>(a, ra, min(s0 + 1, s1 - 1), h, gn);
+      f32_gbuild<MODE, KEEPX>(a, ra, s0, h, w2h, gi, Gs);
+      f32_xload<EXPLICIT, STORE>(a, min(s0 + 1, s1 - 1), d, kh, nxt);
+      __syncthreads();
+      for (int s = s0; s < s1; ++s) {
+        const int buf = (s - s0) & 1;
+        const SlabIdx q = wg_slab(a, s);
+        const float* G = Gs + buf * (DAD_H * F32_GP);
+        if (q.br) {
+          const int st = a.mask_len > 0 ? (EXPLICIT ? (int)a.start[q.b] : dad_tstart_at(a.key_tstart, q.b, a.start_hi)) : 0;
+          f32_mma<EXPLICIT, true>(a, q, d, kh, fkeep, st, G, cur, acc);
+        } else {
+          f32_mma<EXPLICIT, false>(a, q, d, kh, fkeep, 0, G, cur, acc);
+        }
+        // the next slab's G (its inputs loaded a slab ago), then the loads of slab s + 2
+        if (s + 1 < s1) f32_gbuild<MODE, KEEPX>(a, ra, s + 1, h, w2h, gn, Gs + (buf ^ 1) * (DAD_H * F32_GP));
+        cur = nxt;
+        f32_gload<MODE>(a, ra, min(s + 2, s1 - 1), h, gn);
+        f32_xload<EXPLICIT, STORE>(a, min(s + 2, s1 - 1), d, kh, nxt);
+        __syncthreads();
+      }
+    }
+    float* out = a.wpart + (size_t)split * DAD_H * DAD_D;
+#pragma unroll
+    for (int ht = 0; ht < DAD_HT; ++ht)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) out[(size_t)(ht * 32 + dad_acc_row(r, kh)) * DAD_D + d] = acc[ht][r];
   }
+}
+
+// KEEPX: explicit classifier-dropout masks (fused mode only)
+template <bool EXPLICIT, int MODE, bool KEEPX>
+__device__ __forceinline__ void wgrad_f32_store(const DadWgradArgs& a, const DadReduceArgs& ra, float* Gs) {
+  if (a.src.rowc != nullptr) wgrad_f32_body<EXPLICIT, MODE, true, KEEPX>(a, ra, Gs);
+  else wgrad_f32_body<EXPLICIT, MODE, false, KEEPX>(a, ra, Gs);
+}
+template <bool EXPLICIT>
+__device__ __forceinline__ void wgrad_f32_mode(const DadWgradArgs& a, const DadReduceArgs& ra, float* Gs) {
+  if (a.per_utt) wgrad_f32_store<EXPLICIT, F32_SU, false>(a, ra, Gs);
+  else if (ra.gzb == nullptr) wgrad_f32_store<EXPLICIT, F32_GE, false>(a, ra, Gs);
+  else if (ra.keep1) wgrad_f32_store<EXPLICIT, F32_FUSED, true>(a, ra, Gs);
+  else wgrad_f32_store<EXPLICIT, F32_FUSED, false>(a, ra, Gs);
+}
+
+__global__ __launch_bounds__(DAD_WGRAD_THREADS) void dad_wgrad_f32(DadWgradArgs a, DadReduceArgs ra) {
+  DAD_GUARD_BLOCK(DAD_WGRAD_THREADS);
+  static_assert(DAD_WGRAD_THREADS == DAD_H, "dad_wgrad_f32: thread = hidden unit for the G tile");
+  __shared__ __attribute__((aligned(16))) float Gs[2 * DAD_H * F32_GP];
+  if (a.ns) wgrad_f32_mode<true>(a, ra, Gs);
+  else wgrad_f32_mode<false>(a, ra, Gs);
 }
 
 // ------------------------------------------------------------ BF16 (throughput mode)
@@ -280,12 +422,19 @@ __device__ __forceinline__ void wgd_stage(const WgdSlab& r, __bf16* Xt) {
 }
 
 // A fragment of h tile ht, k rows 16 ks + 8 (lane/32) + 0..7: bit ? gb : 0 (bf16 bits).
-// lut[b] = the 0xFFFF/0 halfword masks of the 8 bits of byte b (16 B, 4 KB table): one
-// bitfield extract and one 16-B LDS read per fragment.
+// lut[b][s] = the 0xFFFF/0 halfword masks of the 8 bits of byte b (16 B), once per 16-B bank
+// slot s (64 KB): lane l reads slot l & 15, which is a different slot for every lane of each
+// ds_read_b128 lane group ({0-3,12-15,20-27}, {4-11,16-19,28-31}, and +32), so the
+// data-dependent bytes never meet on a bank (one table with one copy: 27 % of the kernel's
+// LDS cycles were bank conflicts).  One bitfield extract and one 16-B LDS read per fragment.
+#ifndef WGD_LUT_SLOTS
+#define WGD_LUT_SLOTS 16   // 1: one 4 KB table (27 % of the LDS cycles bank conflicts)
+#endif
+constexpr int WGD_LUT = 256 * WGD_LUT_SLOTS;
 __device__ __forceinline__ uint4 wgd_amask(uint32_t mask, const uint4* lut, int ks) {
   const int lane = threadIdx.x & 63;
   const uint32_t byte = __builtin_amdgcn_ubfe(mask, 16 * ks + 8 * (lane >> 5), 8);
-  return lut[byte];
+  return lut[byte * WGD_LUT_SLOTS + (lane & (WGD_LUT_SLOTS - 1))];
 }
 
 // one slab's operands for one wave: A (G) fragments a[ks][m], B (x) fragments b[ks][n]
@@ -497,6 +646,7 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
   }
   const int kh = lane >> 5;
   if constexpr (WGD_GROUPS == 2) {
+    __syncthreads();   // red aliases the x tiles: every group's last reads are done
     // exchange halves: group 0 finishes h tile 2w (+ group 1's partial), group 1 tile 2w+1
 #pragma unroll
     for (int m = 0; m < 2; ++m)
@@ -527,26 +677,44 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
   (void)t0; (void)t1; (void)t2;
 }
 
-// the 256-entry byte table of the A-fragment masks (threads 0..255)
+// the byte table of the A-fragment masks, 16 slot copies per byte (wgd_amask)
 __device__ __forceinline__ void wgd_lut(uint4* lut) {
-  const int t = threadIdx.x;
-  if (t < 256) {
+  // consecutive threads store consecutive 16-B slots (conflict-free stores); entry i is byte
+  // i / 16, the byte's four dwords by sign-extended bit fields
+#pragma unroll
+  for (int k = 0; k < (WGD_LUT + WGD_THREADS - 1) / WGD_THREADS; ++k) {
+    const int i = k * WGD_THREADS + threadIdx.x;
+    if (WGD_LUT < WGD_THREADS && i >= WGD_LUT) break;
+    const int t = i / WGD_LUT_SLOTS;
     uint32_t e[4];
 #pragma unroll
     for (int p = 0; p < 4; ++p)
-      e[p] = (((t >> (2 * p)) & 1) ? 0x0000ffffu : 0u) | (((t >> (2 * p + 1)) & 1) ? 0xffff0000u : 0u);
-    lut[t] = uint4{e[0], e[1], e[2], e[3]};
+      e[p] = ((uint32_t)__builtin_amdgcn_sbfe(t, 2 * p, 1) & 0x0000ffffu) |
+             ((uint32_t)__builtin_amdgcn_sbfe(t, 2 * p + 1, 1) & 0xffff0000u);
+    lut[i] = uint4{e[0], e[1], e[2], e[3]};
   }
 }
+
+// LDS of the weight-gradient workgroups (160 KB with the dL/de table): the x tiles, then the
+// mask table; the end-of-tile exchange (red, 64 KB) reuses the x tiles and the spare space
+// after them (the table stays intact for the next tile)
+constexpr int WGD_XT = WGD_GROUPS * 4 * DAD_SLAB * WGD_XP;   // bf16 elements
+constexpr int WGD_RED = WGD_GROUPS == 2 ? DAD_H * WGD_DB : 1;
+struct __attribute__((aligned(16))) WgdSmem {
+  union {
+    __bf16 xt[WGD_XT];
+    float red[WGD_RED];
+  } a;
+  uint4 lut[WGD_LUT];
+};
 
 __device__ double extra_block(const DadReduceArgs& a, int e, int tid, float (*xs)[16][6]);
 
 __global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct(DadWgradArgs a, DadReduceArgs ra) {
   DAD_GUARD_BLOCK(WGD_THREADS);
-  __shared__ __attribute__((aligned(16))) __bf16 Xt[WGD_GROUPS * 4 * DAD_SLAB * WGD_XP];
-  __shared__ __attribute__((aligned(16))) uint4 lut[256];
+  __shared__ WgdSmem S;
   __shared__ __attribute__((aligned(16))) uint16_t gs[WGD_MAXU * DAD_H];
-  __shared__ __attribute__((aligned(16))) float red[WGD_GROUPS == 2 ? DAD_H * WGD_DB : 1];
+  __bf16* Xt = S.a.xt;
   // XCD-aware tile order (grid is a multiple of 8; workgroups go round-robin over the 8
   // XCDs): each XCD takes a consecutive run of tiles, so the column blocks of one split,
   // which read the same ReLU' row masks, share an L2
@@ -559,8 +727,8 @@ __global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct(DadWgradArgs 
     // in the (otherwise unused) x-tile LDS.
     const int xi = tile - a.ntiles;
     if (xi >= WGD_XWG) return;
-    static_assert(sizeof(Xt) >= 2 * 16 * 16 * 6 * sizeof(float), "extra-block scratch fits the x tile");
-    __shared__ double wred[WGD_THREADS / 64];
+    static_assert(sizeof(S.a) >= 2 * 16 * 16 * 6 * sizeof(float), "extra-block scratch fits the x tile");
+    double* wred = reinterpret_cast<double*>(S.lut);   // (the mask table is not used here)
     const int half = threadIdx.x >> 8, htid = threadIdx.x & 255;
     float (*xs)[16][6] = reinterpret_cast<float (*)[16][6]>(Xt) + 16 * half;
     constexpr int per_wg = DAD_REDUCE_XBLK / WGD_XWG;
@@ -580,8 +748,9 @@ __global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct(DadWgradArgs 
   const int total = wg_total(a);
   const int per = (total + a.splits - 1) / a.splits;
   const int s0 = split * per, s1 = min(total, s0 + per);
-  wgd_lut(lut);   // (the tile's first barrier orders it before the first read)
-  wgd_tile<false>(a, ra, s0, s1, dblk * WGD_DB, a.wpart + (size_t)split * DAD_H * DAD_D, nullptr, Xt, lut, gs, red);
+  wgd_lut(S.lut);   // (the tile's first barrier orders it before the first read)
+  wgd_tile<false>(a, ra, s0, s1, dblk * WGD_DB, a.wpart + (size_t)split * DAD_H * DAD_D, nullptr, Xt, S.lut, gs,
+                  S.a.red);
 }
 
 // FP32-free loss-independent factor for the BF16 step: S_u = bits_u^T X_u (G = 0/1 exactly,
@@ -589,19 +758,17 @@ __global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct(DadWgradArgs 
 // Runs on a side stream concurrently with pool/tail/ECDA; dad_wsum applies dL/de_u / len_u.
 __global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_su(DadWgradArgs a) {
   DAD_GUARD_BLOCK(WGD_THREADS);
-  __shared__ __attribute__((aligned(16))) __bf16 Xt[WGD_GROUPS * 4 * DAD_SLAB * WGD_XP];
-  __shared__ __attribute__((aligned(16))) uint4 lut[256];
-  __shared__ __attribute__((aligned(16))) float red[WGD_GROUPS == 2 ? DAD_H * WGD_DB : 1];
+  __shared__ WgdSmem S;
   DadReduceArgs unused;
   const DadGeom& g = a.g;
   const int nsc = g.Bc * g.ncc;
-  wgd_lut(lut);
+  wgd_lut(S.lut);
   for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
     const int u = tile / WGD_NDB, dblk = tile - u * WGD_NDB;
     const int s0 = u < g.Bc ? u * g.ncc : nsc + (u - g.Bc) * g.ncn;
     const int s1 = s0 + (u < g.Bc ? g.ncc : g.ncn);
-    wgd_tile<true>(a, unused, s0, s1, dblk * WGD_DB, nullptr, a.su + (size_t)u * DAD_H * DAD_D, Xt, lut, nullptr,
-                   red);
+    wgd_tile<true>(a, unused, s0, s1, dblk * WGD_DB, nullptr, a.su + (size_t)u * DAD_H * DAD_D, S.a.xt, S.lut,
+                   nullptr, S.a.red);
   }
 }
 

@@ -14,4 +14,10 @@ timeout -k 10 200 python bench.py --no-cpu-baseline --no-parity --fp32-steps 0 -
 python -c "
 import json; d=json.loads([l for l in open('gpurun_out/bq.log') if l.startswith('{')][-1])
 print('value %.0f ms %.4f' % (d['value'], d['ms_per_step']), {k: round(v['avg_ms'] * 1e3, 1) for k, v in d['kernels'].items() if 'avg_ms' in v})"
+if [ -n "${PMC:-}" ]; then
+  R="$GRAFT_REPO_ROOT"
+  (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $PMC --kernel-trace --kernel-include-regex "${PMC_REGEX:-dad_}" --output-format csv \
+    -d "$R/gpurun_out/qpmc" -o run -- python "$R/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --no-parity --fp32-steps 0 \
+    --no-data-path > "$R/gpurun_out/qpmc.log" 2>&1) && python tools/pmc_brief.py gpurun_out/qpmc/run_counter_collection.csv || exit 1
+fi
 exit $rc
