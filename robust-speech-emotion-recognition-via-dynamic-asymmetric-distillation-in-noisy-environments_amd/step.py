@@ -141,17 +141,25 @@ class DADStep:
         self.dacp[16:20].copy_(a)
 
     def _param_key(self):
-        """Identity + write count of the model's flat parameter vectors.  Writes through the
-        parameter views (load_state_dict, optimizer steps, copy_) bump the shared version
-        counter; kernel writes made outside this step (SSRLModel.update_teacher_ema) bump
-        `model.param_writes`; `.to()` rebinds the storage."""
+        """Identity + write count of the model's flat parameter vectors.  In-place writes to
+        the parameters themselves (load_state_dict, optimizer steps, `p.copy_`) bump the shared
+        version counter; kernel writes made outside this step (SSRLModel.update_teacher_ema)
+        bump `model.param_writes`; `.to()` rebinds the storage.
+
+        NOT detected: writes through `p.data` (`p.data.copy_(...)`, the style of the
+        reference's model.py:204-223).  `.data` is a detached alias with a version counter of
+        its own, so such a write leaves this key unchanged and the next BF16 step would run on
+        the old bf16 W1 shadows.  Call `refresh_shadow()` after writing through `.data`
+        (tests/test_gpu_shadow.py).  A per-step content check would cost a read of both W1
+        copies (1.5 MB) on every step."""
         m = self.model
         s, t = m.student_flat, m.teacher_flat
         return (s.data_ptr(), t.data_ptr(), s._version, t._version, getattr(m, "param_writes", 0))
 
     def refresh_shadow(self):
         """Re-derive the bf16 W1 shadows after the caller changed the model's parameters
-        (step() also does this by itself whenever `_param_key` changed)."""
+        (step() also does this by itself whenever `_param_key` changed; required after writes
+        through `.data`, which `_param_key` cannot see)."""
         st = self._state_struct(0)
         _lib.check(_lib.lib().dad_refresh_shadow(st, self._stream()), "dad_refresh_shadow")
         self._shadow_dirty = False
