@@ -238,6 +238,23 @@ __device__ __forceinline__ int live_rows(const Job& J, int half, int w) {
 #ifndef WS_PRIO
 #define WS_PRIO 0      // static s_setprio 1 for: 0 no wave, 1 waves WAVES/2.., 2 waves ..WAVES/2-1
 #endif
+// Floor knockouts (diagnostic builds only, tools/gpu_ws_floor.sh; results are wrong by design):
+// WS_FLOOR_NO_RNG  constant noise instead of the counter RNG (the add and the masks stay)
+// WS_FLOOR_NO_XS   no bf16 copy stores
+// WS_FLOOR_NO_MFMA no MFMAs (accumulators stay zero)
+// WS_FLOOR_NO_DMA  no row DMA after the first two sub-slabs (stale LDS rows)
+#ifndef WS_FLOOR_NO_RNG
+#define WS_FLOOR_NO_RNG 0
+#endif
+#ifndef WS_FLOOR_NO_XS
+#define WS_FLOOR_NO_XS 0
+#endif
+#ifndef WS_FLOOR_NO_MFMA
+#define WS_FLOOR_NO_MFMA 0
+#endif
+#ifndef WS_FLOOR_NO_DMA
+#define WS_FLOOR_NO_DMA 0
+#endif
 template <class S, int NOISE, int KIND, int HALF>
 struct WsConv {
   static constexpr bool strong = KIND == KIND_STRONG;
@@ -284,6 +301,8 @@ struct WsConv {
         n = *reinterpret_cast<const f32x4*>(nsrc + (size_t)grow * DAD_D + d);
 #pragma unroll
         for (int e = 0; e < 4; ++e) n[e] *= sd;
+      } else if constexpr (WS_FLOOR_NO_RNG) {
+        n = f32x4{sd, sd, sd, sd};
       } else {
         const uint32_t p = ((uint32_t)grow * (uint32_t)DAD_D + (uint32_t)d) >> 1;
         float z0, z1, z2, z3;
@@ -305,7 +324,7 @@ struct WsConv {
                     __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{v[2], v[3]}, bf16x2))};
     if constexpr (strong) o = tzero ? uint2{0u, 0u} : o;
     *reinterpret_cast<uint2*>(trow + 512 * k) = o;             // chunk 32k + (lane>>1), swizzled by row
-    if constexpr (KIND != KIND_WEAK) {
+    if constexpr (KIND != KIND_WEAK && !WS_FLOOR_NO_XS) {
       // 32-bit byte offset from the uniform base (saddr store, no 64-bit address math)
       const uint32_t boff = ((uint32_t)grow * (uint32_t)DAD_D + (uint32_t)d) * 2u;
       if constexpr (WS_WT)
@@ -364,6 +383,10 @@ __device__ __forceinline__ void ws_zero_xs(const Ctx& C, const Job& J, int w, in
 // k-step takes C = 0; a chain on one accumulator needs no wait states.
 template <bool AGPR, bool FIRST>
 __device__ __forceinline__ void mfma1(f32x4& acc, const bf16x8& xa, const bf16x8& wfr) {
+  if constexpr (WS_FLOOR_NO_MFMA) {
+    if constexpr (FIRST) acc = f32x4{};
+    return;
+  }
   if constexpr (AGPR) {
     if constexpr (FIRST) asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(acc) : "v"(xa), "a"(wfr));
     else asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(xa), "a"(wfr));
@@ -509,7 +532,9 @@ __device__ __forceinline__ void ws_epilogue(const Ctx& C, const Job& J, int w, i
 
 // VMEM instructions one wave issues per sub-slab (the counted vmcnt waits depend on them)
 template <class S>
-__device__ __forceinline__ constexpr int n_xs(int kind) { return kind != KIND_WEAK ? S::kXsRow * S::RPW : 0; }
+__device__ __forceinline__ constexpr int n_xs(int kind) {
+  return (kind != KIND_WEAK && !WS_FLOOR_NO_XS) ? S::kXsRow * S::RPW : 0;
+}
 template <bool TEACHER, int HALF>
 __device__ __forceinline__ constexpr int n_epi() { return TEACHER ? HALF : 3 * HALF; }
 
@@ -551,7 +576,7 @@ __device__ __forceinline__ void ws_loop(const Ctx& C, const JobMap jm, const int
   // 0 even where it zeroes padded rows' copies: under-counting younger stores only waits longer)
   auto xs_of = [&](int q) -> int { return vmask_of(q) ? n_xs<S>(jobq(q).kind) : 0; };
   auto dma = [&](int q) {
-    if (q < Q) {
+    if (q < Q && !(WS_FLOOR_NO_DMA && q >= 2)) {
       const Job J = jobq(q);
       dma_rows<S>(J.kind == KIND_CLEAN ? C.xc : C.xn, J, q & 1, w, sbase + kOffRaw + (q & 1) * kRawStage, lane);
     }

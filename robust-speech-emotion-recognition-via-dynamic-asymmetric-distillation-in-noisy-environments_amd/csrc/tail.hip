@@ -25,6 +25,14 @@
 DAD_PROBE_BUFFER(ecda_stamps, DAD_C * ECDA_SLOTS + 16)
 #define ECDA_STAMP(k) \
   if (threadIdx.x == 0) DAD_PROBE_SET(ecda_stamps, (gridDim.x > DAD_C ? blockIdx.x - 1 : blockIdx.x) * ECDA_SLOTS + (k), DAD_PROBE_WALL())
+// shader-clock stamp of wave 0 (cycle-level sub-phases of the stamps build), pinned in place
+#define ECDA_CYC(k)                                                                          \
+  do {                                                                                       \
+    __builtin_amdgcn_sched_barrier(0);                                                       \
+    if (threadIdx.x == 0)                                                                    \
+      DAD_PROBE_SET(ecda_stamps, (gridDim.x > DAD_C ? blockIdx.x - 1 : blockIdx.x) * ECDA_SLOTS + (k), DAD_PROBE_CLK()); \
+    __builtin_amdgcn_sched_barrier(0);                                                       \
+  } while (0)
 #define ECDA_STAMP_SIZES(c, n, ns) \
   do { DAD_PROBE_SET(ecda_stamps, (c) * ECDA_SLOTS + 10, (n)); DAD_PROBE_SET(ecda_stamps, (c) * ECDA_SLOTS + 11, (ns)); } while (0)
 #define TAIL_STAMP(k) \
@@ -1623,6 +1631,12 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
     else return S.a.zc[i * EW_ZP + col];
   };
   if (gc) {
+    // squared norms of the candidate rows (a runtime loop: only the candidates are summed)
+    for (int r = g; r < ncand_all; r += ECDA_NG) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(rowp(r) + 4 * lane);
+      const float nr = dad_wave_sum(((v[0] * v[0] + v[1] * v[1]) + v[2] * v[2]) + v[3] * v[3]);
+      if (lane == 0) S.nz[r] = nr;
+    }
     // Gram partials: tile pair (ti, tj) over a K slice, fp32 matrix cores
     for (int item = g; item < npt * ks; item += ECDA_NG) {
       const int pr = item / ks, sl = item - pr * ks;
@@ -1960,6 +1974,7 @@ __device__ __forceinline__ void ecda_block_w(const DadEcdaArgs& a, const DadTail
 #if DAD_PROBE_ON
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // stamps build: when the prefetched rows have landed
   ECDA_STAMP(9);
+  ECDA_CYC(19);
 #endif
   bool gated[DAD_C];
   float rep_coef = 0.0f;
@@ -1973,6 +1988,7 @@ __device__ __forceinline__ void ecda_block_w(const DadEcdaArgs& a, const DadTail
   const bool gc = c == 0 ? gated[0] : (c == 1 ? gated[1] : (c == 2 ? gated[2] : gated[3]));
   const float att_c = sel4(att, c);
   const bool rep_on = nvalid > 1 && cnc > 0 && rep_coef != 0.0f;
+  ECDA_CYC(13);
   if (!gc && !rep_on) return;
   // candidates: clean rows of label c (members when gated), then noisy rows of pseudo-label c
   // (members when masked in); positions by ballot prefix counts, every wave alike
@@ -1989,30 +2005,24 @@ __device__ __forceinline__ void ecda_block_w(const DadEcdaArgs& a, const DadTail
   // per-wave centroid partial sums of every class
   // a wave's candidate rows: their candidate positions (uniform), the others go to the spare
   // row TW_MAXB (narrow) -- unconditional stores, no branches; norms by one batched butterfly
-  float nrm[2 * ECDA_PRE_U];
   int npos[2 * ECDA_PRE_U];
 #pragma unroll
   for (int u = 0; u < ECDA_PRE_U; ++u) {
     const int b = g + ECDA_NG * u;                 // noisy row b; clean candidate b (compacted)
     const bool okc = gc & (b < ncl);
     const bool okn = (b < Bn) & (((bn >> b) & 1ull) != 0);
-    npos[2 * u] = okc ? b : -1;
-    npos[2 * u + 1] = okn ? __builtin_amdgcn_readlane(posn, b) : -1;
-    if (!wide) {
-      *reinterpret_cast<f32x4*>(&S.a.zc[(okc ? npos[2 * u] : TW_MAXB) * EW_ZP + 4 * lane]) = pc[u];
-      *reinterpret_cast<f32x4*>(&S.a.zc[(okn ? npos[2 * u + 1] : TW_MAXB) * EW_ZP + 4 * lane]) = ps[u];
-    }
-    nrm[2 * u] = ((pc[u][0] * pc[u][0] + pc[u][1] * pc[u][1]) + pc[u][2] * pc[u][2]) + pc[u][3] * pc[u][3];
-    nrm[2 * u + 1] = ((ps[u][0] * ps[u][0] + ps[u][1] * ps[u][1]) + ps[u][2] * ps[u][2]) + ps[u][3] * ps[u][3];
+    npos[2 * u] = __builtin_amdgcn_readfirstlane(okc ? b : -1);
+    npos[2 * u + 1] = __builtin_amdgcn_readfirstlane(okn ? __builtin_amdgcn_readlane(posn, b) : -1);
+    // candidate rows only, under uniform (scalar) branches: storing every row (the others to a
+    // spare row) had all 8 waves queue 128 KB of LDS writes at once (~2500 cycles per wave)
+    if (!wide & okc) *reinterpret_cast<f32x4*>(&S.a.zc[npos[2 * u] * EW_ZP + 4 * lane]) = pc[u];
+    if (!wide & okn) *reinterpret_cast<f32x4*>(&S.a.zc[npos[2 * u + 1] * EW_ZP + 4 * lane]) = ps[u];
   }
-#pragma unroll
-  for (int q = 0; q < 2 * ECDA_PRE_U; ++q) {   // candidate rows only (about 4 per wave): uniform branches
-    if (npos[q] >= 0) {
-      const float r = dad_wave_sum(nrm[q]);
-      if (lane == 0) S.nz[npos[q]] = r;
-    }
-  }
+  ECDA_CYC(14);
+  // (the candidates' squared norms are taken from the staged rows after barrier 1: here the
+  // compiler computed the wave sums of all 16 rows, candidate or not, ~2000 cycles)
   ECDA_STAMP(12);
+  ECDA_CYC(15);
   if (!wide) {
     const int npad = ncand_all <= 32 ? 32 : 64;
     for (int r = ncand_all + g; r < npad; r += ECDA_NG) *reinterpret_cast<f32x4*>(&S.a.zc[r * EW_ZP + 4 * lane]) = f32x4{};
@@ -2022,30 +2032,33 @@ __device__ __forceinline__ void ecda_block_w(const DadEcdaArgs& a, const DadTail
     if (ccand) { S.rowz[posc] = lane; S.wz[posc] = 1.0f; S.mem[posc] = 1; }
     if (ncand) { S.rowz[posn] = lane; S.wz[posn] = M.s; S.mem[posn] = M.m ? 1 : 0; }
   }
+  ECDA_CYC(16);
   {
     // the class of each row is wave-uniform: one add per row into its class's sum (a uniform
     // branch), not a select per class
+    // branch-free: each row added to every class sum times a uniform 0/1 factor (adding
+    // zeros leaves each sum bit-identical); a switch on the class made a branch per row and
+    // register copies at every join (~2000 cycles)
     f32x4 cs0 = f32x4{}, cs1 = f32x4{}, cs2 = f32x4{}, cs3 = f32x4{};
 #pragma unroll
     for (int u = 0; u < ECDA_PRE_U; ++u) {
       const int b = g + ECDA_NG * u;
-      const int pk = b < Bn ? __builtin_amdgcn_readlane(prd, b) : -1;
-      switch (pk) {
-        case 0: cs0 += ps[u]; break;
-        case 1: cs1 += ps[u]; break;
-        case 2: cs2 += ps[u]; break;
-        case 3: cs3 += ps[u]; break;
-        default: break;
-      }
+      const int pk = __builtin_amdgcn_readfirstlane(b < Bn ? __builtin_amdgcn_readlane(prd, b < 64 ? b : 0) : -1);
+      cs0 += ps[u] * (pk == 0 ? 1.0f : 0.0f);
+      cs1 += ps[u] * (pk == 1 ? 1.0f : 0.0f);
+      cs2 += ps[u] * (pk == 2 ? 1.0f : 0.0f);
+      cs3 += ps[u] * (pk == 3 ? 1.0f : 0.0f);
     }
     *reinterpret_cast<f32x4*>(&S.c.cp[g][0][4 * lane]) = cs0;
     *reinterpret_cast<f32x4*>(&S.c.cp[g][1][4 * lane]) = cs1;
     *reinterpret_cast<f32x4*>(&S.c.cp[g][2][4 * lane]) = cs2;
     *reinterpret_cast<f32x4*>(&S.c.cp[g][3][4 * lane]) = cs3;
   }
+  ECDA_CYC(17);
   // weight sum of the noisy members (I/utils.py:552-557), in every wave
   const double wsum_t = dad_wave_sum_d((ncand && M.m) ? (double)M.s : 0.0);
   (void)cc;
+  ECDA_CYC(18);
   ECDA_STAMP(2);
   __syncthreads();   // ---------------------------------------------------------------- 1
   ECDA_STAMP(3);

@@ -45,6 +45,13 @@ def main():
     if on[T0 + 13] and on[T0 + 12]:
         ghz = np.median((raw[:, T0 + 13] - raw[:, T0 + 12]) / ((raw[:, T0 + 1] - raw[:, T0]) * 10.0))
         print("  tail block clock: %.2f GHz" % ghz)
+    cyc = [(19, 13, "gates"), (13, 14, "stores+norm-math"), (14, 15, "norm-sums"), (15, 16, "zero+tables"),
+           (16, 17, "centroid-partials"), (17, 18, "wsum")]
+    for c in range(4):
+        o = c * S
+        if all(on[o + a] and on[o + b] for a, b, _ in cyc):
+            print("ecda class %d staging cycles: %s" % (c, "  ".join(
+                "%s %d" % (n, int(np.median(raw[:, o + b] - raw[:, o + a]))) for a, b, n in cyc)))
     names = ["start", "dacp", "staged", "b1", "gram+cent", "b2", "b3", "b4", "end", "rows-landed", "", "", "norms"]
     for c in range(4):
         o = c * S
