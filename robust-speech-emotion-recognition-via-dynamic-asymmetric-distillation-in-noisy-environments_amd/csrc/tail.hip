@@ -1270,13 +1270,18 @@ __global__ __launch_bounds__(TAIL_THREADS) void dad_tail_ecda(DadTailArgs ta, Da
 //    ecda_block (the general path) inside the same launch.
 // =====================================================================================
 #define TW_MAXB 64
-#define EW_ZP 260          // staged row pitch (floats): 16-B aligned rows, <= 2-way bank conflicts
-#define EW_CP 66           // D / C matrix pitch (narrow)
-#define EW_CPW 130         // D / C matrix pitch (wide, 128 candidates)
+// Pitches (floats) of the staged rows and the coefficient matrix: multiples of 4 (16-B rows) with
+// pitch/4 odd, so the MFMA operand reads -- one ds_read_b128 of 4 consecutive k per lane, the
+// 32 lanes of a half on 32 different rows -- fall on 16 different 16-B bank slots per lane group
+// (conflict-free; scalar reads of one column over rows at pitch 260 were 4-way conflicts)
+#define EW_ZP 260          // staged row pitch
+#define EW_CP 68           // coefficient matrix pitch (narrow)
+#define EW_CPW 132         // coefficient matrix pitch (wide, 128 candidates)
+#define EW_GP 33           // Gram tile row pitch: the distance pass reads tiles transposed too
 
 // DACP scratch of a workgroup: per-wave partial ranks and per-wave sorted-score tables
 struct DacpBlockScratch {
-  int rk[TW_MAXB][ECDA_THREADS / 64];
+  int rk[ECDA_THREADS / 64][TW_MAXB];   // [wave][row]: each wave's store is 64 consecutive ints
   float srt[ECDA_THREADS / 64][DAD_C][TW_MAXB];
 };
 
@@ -1339,11 +1344,12 @@ __device__ __forceinline__ void dacp_block8(const dad_config& cfg, int Bn, float
     const int pj = __builtin_amdgcn_readlane(p, j);
     part += (int)((pj == p) & ((sj < s) | ((sj == s) & (j < lane))));
   }
-  W.rk[lane][g] = part;
+  W.rk[g][lane] = part;   // ([row][wave] put 8 rows of a store on one bank: 8-way conflicts)
   __syncthreads();
-  const u32x4 r0 = *reinterpret_cast<const u32x4*>(&W.rk[lane][0]);
-  const u32x4 r1 = *reinterpret_cast<const u32x4*>(&W.rk[lane][4]);
-  const int cnt = (int)(((r0[0] + r0[1]) + (r0[2] + r0[3])) + ((r1[0] + r1[1]) + (r1[2] + r1[3])));
+  int r[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) r[k] = W.rk[k][lane];
+  const int cnt = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
   TAIL_STAMP_W1(8);
   int ncls[DAD_C];
 #pragma unroll
@@ -1573,7 +1579,7 @@ struct __attribute__((aligned(16))) EcdaW {
   } a;
   union {
     DacpBlockScratch dw;                     // DACP scratch (before barrier 1)
-    float gp[10][32 * 32];                   // Gram partial tiles (after barrier 1)
+    float gp[10][32 * EW_GP];                // Gram partial tiles (after barrier 1)
   } b;
   union {
     float cp[ECDA_THREADS / 64][DAD_C][DAD_H];   // per-wave centroid partial sums (until barrier 2)
@@ -1644,22 +1650,21 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
       ew_pair_inv(pr, nt, ti, tj);
       const int kw = DAD_H / ks, k0 = sl * kw;
       const int ia = 32 * ti + l32, ib = 32 * tj + l32;
-      const float* ra = rowp(ia) + kh;
-      const float* rb = rowp(ib) + kh;
+      // MFMA step e of a k-block of 8 takes k-index k + 4 kh + e on both operands (any k order
+      // sums the same dot products): each lane reads 4 consecutive floats per operand
+      const float* ra = rowp(ia) + 4 * kh;
+      const float* rb = rowp(ib) + 4 * kh;
       const bool za = WIDE && ia >= ncand_all, zb = WIDE && ib >= ncand_all;
       f32x16 acc = f32x16{};
       for (int k = k0; k < k0 + kw; k += 8) {
-        float av[4], bv[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          av[e] = za ? 0.0f : ra[k + 2 * e];
-          bv[e] = zb ? 0.0f : rb[k + 2 * e];
-        }
+        f32x4 av = *reinterpret_cast<const f32x4*>(ra + k), bv = *reinterpret_cast<const f32x4*>(rb + k);
+        if (za) av = f32x4{};
+        if (zb) bv = f32x4{};
 #pragma unroll
         for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[e], bv[e], acc, 0, 0, 0);
       }
 #pragma unroll
-      for (int r = 0; r < 16; ++r) S.b.gp[item][dad_acc_row(r, kh) * 32 + l32] = acc[r];
+      for (int r = 0; r < 16; ++r) S.b.gp[item][dad_acc_row(r, kh) * EW_GP + l32] = acc[r];
     }
   }
   // centroids of every class over its masked noisy rows, partials combined in wave order
@@ -1688,7 +1693,7 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
       const int lo = i < j ? i : j, hi = i < j ? j : i;
       const int pr = ew_pair(lo >> 5, hi >> 5, nt);
       float gsum = 0.0f;
-      for (int s2 = 0; s2 < ks; ++s2) gsum += S.b.gp[pr * ks + s2][(lo & 31) * 32 + (hi & 31)];
+      for (int s2 = 0; s2 < ks; ++s2) gsum += S.b.gp[pr * ks + s2][(lo & 31) * EW_GP + (hi & 31)];
       const bool ok = (i < ncand_all) & (j < ncand_all) & (i != j);
       const float d = ok ? fmaxf((S.nz[lo] + S.nz[hi]) - 2.0f * gsum, 0.0f) : 0.0f;
       const int mj = S.mem[j < ncand_all ? j : 0];
@@ -1861,14 +1866,13 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
       const int ti = item >> 3, tc = item & 7;
       const int d = 32 * tc + l32;
       f32x16 acc = f32x16{};
-      const float* ra = &db[(32 * ti + l32) * dp + kh];
+      const float* ra = &db[(32 * ti + l32) * dp + 4 * kh];
       for (int k = 0; k < npad; k += 8) {
-        float av[4], bv[4];
+        // step e: candidate k + 4 kh + e (one b128 read of the coefficient row per lane)
+        const f32x4 av = *reinterpret_cast<const f32x4*>(ra + k);
+        float bv[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          av[e] = ra[k + 2 * e];
-          bv[e] = rowv(k + kh + 2 * e, d);
-        }
+        for (int e = 0; e < 4; ++e) bv[e] = rowv(k + 4 * kh + e, d);
 #pragma unroll
         for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[e], bv[e], acc, 0, 0, 0);
       }
