@@ -159,6 +159,9 @@ typedef struct dad_state {
 
 /* --- sizing ------------------------------------------------------------------------ */
 size_t dad_param_count(void);
+/* The step workspace must be zero-filled when it is first allocated: it holds the BF16 encoder's
+   in-launch pooling arrival counters, which every completed step returns to zero (reuse across
+   steps and geometries needs no clearing). */
 int dad_workspace_bytes(const dad_config* cfg, size_t* bytes);
 const char* dad_error_string(int code);
 /* Host-only planning of the BF16 encoder grid (no device call): teacher / student workgroups

@@ -117,6 +117,14 @@ bool wgrad_f32_direct() {
   return !(e && strcmp(e, "su") == 0);
 }
 
+// DAD_POOL_FUSE=1: the BF16 encoder pools the slab partials in its own launch (last arriver per
+// utterance) instead of a dad_pool launch.  Off by default: measured 2.7 us per step slower
+// (encode_ws.hip, ws_pool_arrive).  Read once.
+bool pool_fuse_on() {
+  static const bool on = [] { const char* e = getenv("DAD_POOL_FUSE"); return e && strcmp(e, "1") == 0; }();
+  return on;
+}
+
 // DAD_TAIL_W=0 selects the general tail + ECDA launch for every batch (A/B runs; read once)
 bool tail_w_on() {
   static const bool on = [] { const char* e = getenv("DAD_TAIL_W"); return !(e && strcmp(e, "0") == 0); }();
@@ -402,6 +410,21 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   __bf16* xs_bf16 = ws_ptr<__bf16>(workspace, L.xs_bf16);
   const bool bf16 = cfg->precision == DAD_PREC_BF16;
 
+  // pooling arguments (dad_pool, or the BF16 encoder's in-launch pooling)
+  DadPoolArgs pa;
+  memset(&pa, 0, sizeof(pa));
+  pa.g = G; pa.warmup = cfg->warmup;
+  pa.mc = bt->mc; pa.mn = bt->mn; pa.part_sum = part_sum;
+  pa.student = st->student; pa.teacher = st->teacher;
+  if (explicit_rng) { pa.keep1 = bt->keep1; pa.keep2 = bt->keep2; }
+  pa.key_drop1 = k.drop1; pa.key_drop2 = k.drop2;
+  pa.p_drop = cfg->p_drop; pa.drop_scale = cfg->drop_scale;
+  pa.emb = st->emb; pa.vlen = vlen; pa.logits = st->logits;
+  pa.part_cnt = part_cnt; pa.cnt_tot = cnt_tot;
+  pa.eflag = eflag; pa.tail_terms = st->tail + DAD_T_ECDA_TERM;
+  // (split calls: the encode call pooled, so the backward call launches no dad_pool)
+  const bool pool_fused = bf16 && pool_fuse_on();
+
   // 1. fused augmentation + encoder GEMMs + pooling partials
   DadEncodeArgs ea;
   memset(&ea, 0, sizeof(ea));
@@ -416,6 +439,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   ea.key_weak = k.weak; ea.key_strong = k.strong; ea.key_feat = k.feat; ea.key_tstart = k.tstart;
   ea.weak_std = cfg->weak_std; ea.strong_std = cfg->strong_std; ea.feat_p = cfg->feat_p;
   ea.part_sum = part_sum; ea.part_cnt = part_cnt; ea.bits = bits; ea.xs_bf16 = xs_bf16;
+  if (pool_fused) { ea.pool = pa; ea.pool_cnt = ws_ptr<uint32_t>(workspace, L.pool_cnt); }
   const int nwaves = G.Bc * G.ncc + Bn * G.ncn;
   const dim3 egrid((nwaves + 3) / 4);
   if (do_encode) {
@@ -483,20 +507,11 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
     DAD_TRY(hipEventRecord(side->join, side->s));
   }
 
-  // 3. pooled embeddings + classifier logits
-  DadPoolArgs pa;
-  memset(&pa, 0, sizeof(pa));
-  pa.g = G; pa.warmup = cfg->warmup;
-  pa.mc = bt->mc; pa.mn = bt->mn; pa.part_sum = part_sum;
-  pa.student = st->student; pa.teacher = st->teacher;
-  if (explicit_rng) { pa.keep1 = bt->keep1; pa.keep2 = bt->keep2; }
-  pa.key_drop1 = k.drop1; pa.key_drop2 = k.drop2;
-  pa.p_drop = cfg->p_drop; pa.drop_scale = cfg->drop_scale;
-  pa.emb = st->emb; pa.vlen = vlen; pa.logits = st->logits;
-  pa.part_cnt = part_cnt; pa.cnt_tot = cnt_tot;
-  pa.eflag = eflag; pa.tail_terms = st->tail + DAD_T_ECDA_TERM;
-  hipLaunchKernelGGL(dad_pool, dim3(G.Bc + Bn), dim3(DAD_POOL_THREADS), 0, stream, pa);
-  DAD_TRY(hipGetLastError());
+  // 3. pooled embeddings + classifier logits (BF16: pooled inside the encoder launch)
+  if (!pool_fused) {
+    hipLaunchKernelGGL(dad_pool, dim3(G.Bc + Bn), dim3(DAD_POOL_THREADS), 0, stream, pa);
+    DAD_TRY(hipGetLastError());
+  }
   tk_mark(TK_POOL, stream);
 
   // 4. losses, DACP mask, analytic backward to dL/de and the classifier grads

@@ -323,6 +323,7 @@ struct DadWs {
   size_t w1bf;       // bf16 [H][D]                 modular encoder ops: bf16 copy of W1
   size_t gflat;      // f32 [DAD_GRAD_FLOATS]       modular encoder backward: scratch grad vector
   size_t sbuf;       // [Bc + Bn][H][D]             S_u = bits_u^T X_u, the loss-independent factor of dW1 (f32; bf16 in BF16 mode)
+  size_t pool_cnt;   // [3][DAD_MAX_BATCH] u32      in-launch pooling arrival counters (dad_encode_ws); zero at allocation
   size_t bytes;
   int splits;
 };
@@ -369,6 +370,7 @@ static inline DadWs dad_ws_layout(const DadGeom& g, int splits, int precision, b
   w.w1bf = off;     off = dad_align(off + 2 * (size_t)DAD_H * DAD_D);
   w.gflat = off;    off = dad_align(off + sizeof(float) * DAD_GRAD_FLOATS);
   w.sbuf = off;     off = dad_align(off + (fused ? (precision == DAD_PREC_BF16 ? 2 : sizeof(float)) * nb * DAD_H * DAD_D : 0));
+  w.pool_cnt = off; off = dad_align(off + sizeof(uint32_t) * 3 * DAD_MAX_BATCH);
   w.bytes = off;
   return w;
 }

@@ -41,6 +41,21 @@
 #define DAD_GUARD_BLOCK(n) \
   if (blockDim.x != (n) || blockDim.y != 1 || blockDim.z != 1) return
 
+struct DadPoolArgs {
+  DadGeom g;
+  int warmup;
+  const uint8_t* mc; const uint8_t* mn;
+  const float* part_sum;
+  const float* student; const float* teacher;     // flat params (W2/b2 used)
+  const uint8_t* keep1; const uint8_t* keep2;     // explicit dropout masks or NULL
+  uint32_t key_drop1, key_drop2;
+  float p_drop, drop_scale;
+  float* emb; float* vlen; float* logits;
+  const float* part_cnt; float* cnt_tot;
+  uint32_t* eflag;        // [Bc+Bn] ECDA row flags, zeroed here (ECDA flags the rows it writes)
+  float* tail_terms;      // per-class ECDA terms + gates, zeroed here (block 0)
+};
+
 struct DadEncodeArgs {
   DadGeom g;
   int warmup, mask_len, start_hi;
@@ -62,22 +77,13 @@ struct DadEncodeArgs {
   // the closed-form split): student k runs strong jobs [t[k][0], t[k][1]) then clean [t[k][2], t[k][3])
   int ws_tab_n;
   uint16_t ws_tab[DAD_WS_TAB][4];
+  // dad_encode_ws with pool_cnt set: the slab partials are pooled in the same launch (the last
+  // workgroup to finish an utterance's slabs of one kind pools them: dad_pool's outputs), so the
+  // step has no dad_pool launch.  pool_cnt: [3][DAD_MAX_BATCH] arrival counters, zero between steps.
+  DadPoolArgs pool;
+  uint32_t* pool_cnt;
 };
 
-struct DadPoolArgs {
-  DadGeom g;
-  int warmup;
-  const uint8_t* mc; const uint8_t* mn;
-  const float* part_sum;
-  const float* student; const float* teacher;     // flat params (W2/b2 used)
-  const uint8_t* keep1; const uint8_t* keep2;     // explicit dropout masks or NULL
-  uint32_t key_drop1, key_drop2;
-  float p_drop, drop_scale;
-  float* emb; float* vlen; float* logits;
-  const float* part_cnt; float* cnt_tot;
-  uint32_t* eflag;        // [Bc+Bn] ECDA row flags, zeroed here (ECDA flags the rows it writes)
-  float* tail_terms;      // per-class ECDA terms + gates, zeroed here (block 0)
-};
 
 struct DadTailArgs {
   dad_config cfg;

@@ -690,6 +690,131 @@ __device__ __forceinline__ void ws_loop(const Ctx& C, const JobMap jm, const int
   wait_vm<0>();
 }
 
+// ---------------------------------------------------------------- in-launch pooling
+// dad_pool's work for one (kind, utterance), by the workgroup whose slab partials completed it
+// (I/model.py:35-36 masked mean pool, I/model.py:54-64 classifier with dropout): the same
+// arithmetic and summation orders as dad_pool (tail.hip), so the outputs are identical.
+// Threads 0..255: the pooled sums (hidden unit h), the embedding and the logit partial dots;
+// threads 256..511: the active-count sums (student kinds).  scratch: 24 floats of LDS.
+__device__ __forceinline__ void ws_pool_one(const DadEncodeArgs& a, const Ctx& C, int key, float* scratch) {
+  const DadPoolArgs& p = a.pool;
+  const int kind = key / DAD_MAX_BATCH, b = key - kind * DAD_MAX_BATCH;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = tid & (DAD_H - 1), half = tid >> 8;
+  const bool noisy = kind != KIND_CLEAN, tch = kind == KIND_WEAK;
+  const int T = noisy ? C.Tn : C.Tc, nc = noisy ? C.ncn : C.ncc;
+  const uint8_t* pad = noisy ? C.mn : C.mc;
+  const size_t slab0 = kind == KIND_CLEAN ? (size_t)b * C.ncc
+                                          : (tch ? (size_t)C.nsc + (size_t)b * C.ncn : (size_t)C.nsc + C.nsn + (size_t)b * C.ncn);
+  const size_t cslab0 = noisy ? (size_t)C.nsc + (size_t)b * C.ncn : (size_t)b * C.ncc;
+  const int erow = kind == KIND_CLEAN ? b : (tch ? C.Bc + b : C.Bc + C.Bn + b);
+  const int vrow = noisy ? C.Bc + b : b;
+  float* red = scratch;            // [8] length partials
+  float* zred = scratch + 8;       // [4 classes][4 waves]
+  // every load first: length flags, slab partials (slab order), W2 columns
+  float len = 0.0f;
+  for (int t = tid; t < T; t += DAD_ENC_WS_THREADS) len += pad[(size_t)b * T + t] == 0 ? 1.0f : 0.0f;
+  const float* src = half == 0 ? p.part_sum + slab0 * DAD_H : p.part_cnt + cslab0 * DAD_H;
+  float sv = 0.0f;
+  if (half == 0 || !tch)
+    for (int c = 0; c < nc; ++c) sv += src[(size_t)c * DAD_H + h];
+  const float* pw = tch ? p.teacher : p.student;
+  float w2[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) w2[c] = pw[DAD_OFF_W2 + c * DAD_H + h];
+  const float kv = tch ? 1.0f
+                       : (kind == KIND_CLEAN ? keep_value(p.keep1, p.key_drop1, b, h, p.p_drop, p.drop_scale)
+                                             : keep_value(p.keep2, p.key_drop2, b, h, p.p_drop, p.drop_scale));
+  len = dad_wave_sum(len);   // an integer count: exact in any order
+  if (lane == 0) red[w] = len;
+  __syncthreads();
+  len = 0.0f;
+#pragma unroll
+  for (int k = 0; k < DAD_ENC_WS_THREADS / 64; ++k) len += red[k];
+  if (half == 0) {
+    const float e = sv / fmaxf(len, 1.0f);
+    p.emb[(size_t)erow * DAD_H + h] = e;
+    const float d = tch ? e : e * kv;   // teacher classifier: dropout p = 0 (I/model.py:121)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float z = dad_wave_sum(w2[c] * d);
+      if (lane == 0) zred[c * 4 + w] = z;
+    }
+  } else if (!tch) {
+    p.cnt_tot[(size_t)vrow * DAD_H + h] = sv;
+  }
+  if (tid == 0) p.vlen[vrow] = len;
+  __syncthreads();
+  if (tid < 4) {
+    const float dot = ((zred[tid * 4] + zred[tid * 4 + 1]) + zred[tid * 4 + 2]) + zred[tid * 4 + 3];
+    const float bias = (tch ? p.teacher : p.student)[DAD_OFF_B2 + tid];
+    p.logits[(size_t)erow * DAD_C + tid] = dot + bias;
+  }
+  __syncthreads();   // scratch free for the next task
+}
+
+// Arrival: each run of this workgroup's jobs on one (kind, utterance) adds its slab count to
+// that counter; the arrival that completes the utterance (count = its slabs) resets the counter
+// and pools.  Release: every wave has drained its stores (vmcnt(0) at the end of ws_loop), then
+// one agent-scope release fence before the counters; acquire: one agent fence before the reads
+// (MI355X guide, Guideline 16, counter form).
+// Measured (A/B, 400-step benches, same box): the encoder launch 62.5 -> 74.8 us with it (71.0
+// with write-through partial stores and no release fence instead, which cost the default path
+// ~0.5 us), the pool launch gone; the step 120.6 -> 128.4 us (123.9): the workgroups that finish
+// last are the ones that pool, each after a cross-XCD hand-off of its utterances' partials.  Off
+// by default (DAD_POOL_FUSE=1 enables it; parity tests pass either way).
+template <int WAVES>
+__device__ __forceinline__ void ws_pool_arrive(const DadEncodeArgs& a, const Ctx& C, bool teacher, const JobMap& jm,
+                                               int nj, char* smem) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  int* tasks = reinterpret_cast<int*>(smem + kOffVB);              // the valid-bit table is free now
+  float* scratch = reinterpret_cast<float*>(smem + kOffFK);        // so is the feature-flag table
+  __syncthreads();
+  if (tid < 64) {
+    if (lane == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (keep: the fence's own wait can be dropped)
+    }
+    int ntask = 0;
+    for (int l0 = 0; l0 < nj; l0 += 64) {
+      const int l = l0 + lane;
+      int key = -1, nck = 1;
+      if (l < nj) {
+        const Job J = job_of(C, teacher, jm(l));
+        key = J.kind * DAD_MAX_BATCH + J.b;
+        nck = J.kind == KIND_CLEAN ? C.ncc : C.ncn;
+      }
+      const int prev = __shfl_up(key, 1, 64);
+      const bool head = (l < nj) && (lane == 0 || prev != key);
+      const uint64_t heads = __ballot(head);
+      const int nv = min(64, nj - l0);
+      int n = 0;
+      if (head) {
+        const uint64_t after = heads & ~((2ull << lane) - 1ull);   // heads above this lane
+        const int next = after ? (int)__builtin_ctzll(after) : nv;
+        n = next - lane;
+      }
+      bool last = false;
+      if (head) {
+        const uint32_t old = __hip_atomic_fetch_add(&a.pool_cnt[key], (uint32_t)n, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+        last = old + (uint32_t)n == (uint32_t)nck;
+        if (last) __hip_atomic_store(&a.pool_cnt[key], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      const uint64_t lasts = __ballot(last);
+      if (last) tasks[1 + ntask + (int)__popcll(lasts & ((1ull << lane) - 1ull))] = key;
+      ntask += (int)__popcll(lasts);
+    }
+    if (lane == 0) {
+      tasks[0] = ntask;
+      if (ntask) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  const int ntask = tasks[0];
+  for (int t = 0; t < ntask; ++t) ws_pool_one(a, C, tasks[1 + t], scratch);
+}
+
 // NOISE: 0 = counter RNG, 1 = explicit noise tensors (parity mode)
 template <int WAVES, int NOISE>
 __device__ __forceinline__ void encode_ws_body(const DadEncodeArgs& a, char* smem) {
@@ -699,6 +824,12 @@ __device__ __forceinline__ void encode_ws_body(const DadEncodeArgs& a, char* sme
   const Ctx C = ctx_of(a);
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (a.pool_cnt && blockIdx.x == 0) {
+    // dad_pool's zeroing: the ECDA row flags and per-class terms that the ECDA blocks then set
+    // (their readers, the previous step's wgrad and reduce, have finished: stream order)
+    for (int i = tid; i < C.Bc + C.Bn; i += S::kThreads) a.pool.eflag[i] = 0u;
+    if (tid < 2 * DAD_C) a.pool.tail_terms[tid] = 0.0f;
+  }
   bool teacher;
   int j0, j1;
   job_range(C, blockIdx.x, a.ws_nt, a.ws_ns, a.ws_wstrong, teacher, j0, j1);
@@ -735,6 +866,7 @@ __device__ __forceinline__ void encode_ws_body(const DadEncodeArgs& a, char* sme
   const float* bias = teacher ? a.b1_teacher : a.b1_student;
   if (teacher) ws_loop<WAVES, NOISE, true>(C, jm, 2 * nj, w, lane, smem, sbase, W, bias, fk, vb);
   else ws_loop<WAVES, NOISE, false>(C, jm, 2 * nj, w, lane, smem, sbase, W, bias, fk, vb);
+  if (a.pool_cnt) ws_pool_arrive<WAVES>(a, C, teacher, jm, nj, smem);
   WS_STAMP(2, DAD_PROBE_WALL());
   WS_STAMP(3, ((unsigned long long)teacher << 16) | (unsigned long long)(2 * nj));
 }
