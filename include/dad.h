@@ -334,6 +334,10 @@ int dad_rng_draws(const dad_config* cfg, int which, uint64_t first, size_t n, fl
 #define DAD_TK_SIDE 6         /* dad_wgrad_f32 on the side stream (FP32) */
 #define DAD_TK_KERNELS 7
 int dad_timing_start(int every, int max_steps);
+/* dad_timing_kernels(mask): after dad_timing_start, record only the boundaries of the kernels
+ * whose bit (1 << DAD_TK_*) is set (default: all).  Each recorded event costs the stream a few
+ * microseconds, so a timed region that needs one kernel's duration records only its two. */
+int dad_timing_kernels(unsigned mask);
 int dad_timing_stop(double* ms_sum, int* count, int n);
 
 /* --- data-parallel gradient exchange (RCCL over xGMI) ------------------------------ */

@@ -120,6 +120,7 @@ EXPORTS = {
     "dad_rng_draws": (ctypes.c_int, [ctypes.POINTER(DadConfig), ctypes.c_int, ctypes.c_uint64, ctypes.c_size_t,
                                      ctypes.c_void_p, ctypes.c_void_p]),
     "dad_timing_start": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    "dad_timing_kernels": (ctypes.c_int, [ctypes.c_uint]),
     "dad_timing_stop": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
     "dad_comm_unique_id_bytes": (ctypes.c_int, []),
     "dad_comm_get_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
@@ -173,8 +174,14 @@ class KernelTimer:
     """dad_timing_start / dad_timing_stop: mean duration (ms) per kernel of the fused step over
     every `every`-th step while active.  `stop()` returns {name: (mean_ms, n_steps)}."""
 
-    def __init__(self, every=4, max_steps=256):
+    def __init__(self, every=4, max_steps=256, kernels=None):
+        """kernels: names (TK_NAMES) to time, default all; each recorded event costs stream time."""
         check(lib().dad_timing_start(int(every), int(max_steps)), "dad_timing_start")
+        if kernels is not None:
+            mask = 0
+            for k in kernels:
+                mask |= 1 << TK_NAMES.index(k)
+            check(lib().dad_timing_kernels(mask), "dad_timing_kernels")
         self.active = True
 
     def stop(self):

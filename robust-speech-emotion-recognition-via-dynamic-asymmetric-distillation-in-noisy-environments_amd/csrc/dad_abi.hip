@@ -267,7 +267,11 @@ bool ws_student_table(const DadGeom& G, int Bn, int ns, float wstrong, DadEncode
 // caller's stream (and around the side-stream GEMM of the FP32 step).  Events are created up
 // front by dad_timing_start, so a timed region only records them.  Not for graph capture.
 enum { TK_E0, TK_E1, TK_POOL, TK_TAIL, TK_WGRAD, TK_RED, TK_OPT0, TK_OPT1, TK_S0, TK_S1, TK_N };
+// (event-pair points of each DAD_TK_* kernel: dad_timing_stop's pairs)
+const int kTkPairs[DAD_TK_KERNELS][2] = {{TK_E0, TK_E1}, {TK_E1, TK_POOL}, {TK_POOL, TK_TAIL}, {TK_TAIL, TK_WGRAD},
+                                         {TK_WGRAD, TK_RED}, {TK_OPT0, TK_OPT1}, {TK_S0, TK_S1}};
 struct Timing {
+  unsigned points = ~0u;               // TK points recorded (dad_timing_kernels)
   int every = 0;
   long calls = 0;
   int cur = -1;                        // event set of the step being timed, -1: none
@@ -286,7 +290,7 @@ void tk_begin() {
 }
 void tk_mark(int point, hipStream_t s) {
   std::lock_guard<std::mutex> lk(g_tk_mu);
-  if (g_tk.cur < 0) return;
+  if (g_tk.cur < 0 || !((g_tk.points >> point) & 1u)) return;
   const size_t i = (size_t)g_tk.cur * TK_N + point;
   if (hipEventRecord(g_tk.ev[i], s) == hipSuccess) g_tk.rec[i] = 1;
 }
@@ -312,10 +316,18 @@ int dad_timing_start(int every, int max_steps) {
   return DAD_OK;
 }
 
+int dad_timing_kernels(unsigned mask) {
+  std::lock_guard<std::mutex> lk(g_tk_mu);
+  unsigned pts = 0;
+  for (int k = 0; k < DAD_TK_KERNELS; ++k)
+    if ((mask >> k) & 1u) pts |= (1u << kTkPairs[k][0]) | (1u << kTkPairs[k][1]);
+  g_tk.points = pts;
+  return DAD_OK;
+}
+
 int dad_timing_stop(double* ms_sum, int* count, int n) {
   std::lock_guard<std::mutex> lk(g_tk_mu);
-  static const int pairs[DAD_TK_KERNELS][2] = {{TK_E0, TK_E1}, {TK_E1, TK_POOL}, {TK_POOL, TK_TAIL}, {TK_TAIL, TK_WGRAD},
-                                               {TK_WGRAD, TK_RED}, {TK_OPT0, TK_OPT1}, {TK_S0, TK_S1}};
+  const auto& pairs = kTkPairs;
   if (n < 0 || (n > 0 && (!ms_sum || !count))) return DAD_E_ARG;
   for (int k = 0; k < n; ++k) { ms_sum[k] = 0.0; count[k] = 0; }
   int rc = DAD_OK;
