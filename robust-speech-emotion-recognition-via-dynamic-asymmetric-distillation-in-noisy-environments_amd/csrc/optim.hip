@@ -92,6 +92,69 @@ __device__ __forceinline__ void adam_ema_apply(const dad_config& cfg, float coef
   }
 }
 
+// The same update with 4 CONSECUTIVE parameters per thread (i = n0 + 4 tid .. +3; DAD_NPARAM and
+// the W1 size are multiples of 4): one 16-B load per stream and one 16-B store per written stream,
+// and the 4 bf16 shadow values of a thread are 4 consecutive k of one h, i.e. 8 contiguous bytes
+// of the fragment-major shadow (dad_w1frag_index: k & 7 is the innermost index).  The scalar
+// form issued 20 loads and 24 stores per thread, 8 of them 2-byte stores to scattered shadow
+// slots; the kernel's length was set by issuing them.  Used when every stream is 16-B aligned.
+static_assert(DAD_OPTIM_THREADS * 4 == 1024 && DAD_NPARAM % 4 == 0 && (DAD_H * DAD_D) % 4 == 0,
+              "dad_optim: 1024 parameters per block, 4 per thread, the W1 boundary on a 4-aligned index");
+struct AdamOperands4 {
+  f32x4 g, p, m, v, t;
+};
+
+__device__ __forceinline__ void adam_load4(size_t i0, const float* __restrict__ grad, const float* __restrict__ student,
+                                           const float* __restrict__ teacher, const float* __restrict__ exp_avg,
+                                           const float* __restrict__ exp_avg_sq, AdamOperands4& o) {
+  const size_t i = i0 < DAD_NPARAM ? i0 : 0;   // (clamped: the tail block's spare threads load a valid row)
+  o.g = *reinterpret_cast<const f32x4*>(grad + i);
+  o.p = *reinterpret_cast<const f32x4*>(student + i);
+  o.m = *reinterpret_cast<const f32x4*>(exp_avg + i);
+  o.v = *reinterpret_cast<const f32x4*>(exp_avg_sq + i);
+  o.t = *reinterpret_cast<const f32x4*>(teacher + i);
+}
+
+__device__ __forceinline__ void adam_ema_apply4(const dad_config& cfg, float coef, size_t i0, const AdamOperands4& o,
+                                                float* __restrict__ student, float* __restrict__ teacher,
+                                                float* __restrict__ exp_avg, float* __restrict__ exp_avg_sq,
+                                                __bf16* __restrict__ w1bf_s, __bf16* __restrict__ w1bf_t) {
+  if (i0 >= DAD_NPARAM) return;
+  f32x4 mo, vo, po, to;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {   // adam_ema_apply's arithmetic, element by element
+    float g = o.g[e] * coef;
+    float p = o.p[e];
+    g = g + cfg.weight_decay * p;
+    float m = o.m[e];
+    m = m + cfg.one_m_beta1 * (g - m);
+    float v = o.v[e];
+    v = v * cfg.beta2 + cfg.one_m_beta2 * g * g;
+    const float denom = sqrtf(v) / cfg.bc2_sqrt + cfg.adam_eps;
+    p = p + (-cfg.lr_step_size) * (m / denom);
+    mo[e] = m;
+    vo[e] = v;
+    po[e] = p;
+    to[e] = o.t[e] * cfg.ema_m + p * cfg.ema_one_m;
+  }
+  *reinterpret_cast<f32x4*>(exp_avg + i0) = mo;
+  *reinterpret_cast<f32x4*>(exp_avg_sq + i0) = vo;
+  *reinterpret_cast<f32x4*>(student + i0) = po;
+  if (!cfg.warmup) *reinterpret_cast<f32x4*>(teacher + i0) = to;
+  const f32x4 tt = cfg.warmup ? o.t : to;
+  if (i0 < (size_t)DAD_H * DAD_D) {
+    const uint32_t f = dad_w1frag_index((uint32_t)(i0 / DAD_D), (uint32_t)(i0 % DAD_D));
+    bf16x4 bs, bt;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      bs[e] = (__bf16)po[e];
+      bt[e] = (__bf16)tt[e];
+    }
+    *reinterpret_cast<bf16x4*>(w1bf_s + f) = bs;
+    *reinterpret_cast<bf16x4*>(w1bf_t + f) = bt;
+  }
+}
+
 __global__ __launch_bounds__(DAD_OPTIM_THREADS) void dad_optim(DadOptimArgs a) {
   DAD_GUARD_BLOCK(DAD_OPTIM_THREADS);
   __shared__ float coef_s;
@@ -99,8 +162,14 @@ __global__ __launch_bounds__(DAD_OPTIM_THREADS) void dad_optim(DadOptimArgs a) {
   const dad_config& cfg = a.cfg;
   const int tid = threadIdx.x;
   const size_t n0 = (size_t)blockIdx.x * 1024;
+  // 16-B aligned streams (the step's flat buffers): 4 consecutive parameters per thread
+  const bool vec = ((reinterpret_cast<uintptr_t>(a.grad) | reinterpret_cast<uintptr_t>(a.student) |
+                     reinterpret_cast<uintptr_t>(a.teacher) | reinterpret_cast<uintptr_t>(a.exp_avg) |
+                     reinterpret_cast<uintptr_t>(a.exp_avg_sq)) & 15u) == 0;
   AdamOperands o;
-  adam_load(n0, a.grad, a.student, a.teacher, a.exp_avg, a.exp_avg_sq, o);
+  AdamOperands4 o4;
+  if (vec) adam_load4(n0 + 4 * (size_t)tid, a.grad, a.student, a.teacher, a.exp_avg, a.exp_avg_sq, o4);
+  else adam_load(n0, a.grad, a.student, a.teacher, a.exp_avg, a.exp_avg_sq, o);
   // global norm from the squared-norm partials: all threads load, fixed-order combine
   double s = 0.0;
   for (int k = tid; k < a.nnorm; k += DAD_OPTIM_THREADS) s += (double)a.normpart[k];
@@ -127,7 +196,11 @@ __global__ __launch_bounds__(DAD_OPTIM_THREADS) void dad_optim(DadOptimArgs a) {
   }
   if (blockIdx.x == 0) dacp_commit(cfg, a.grad, a.dacp, tid);
   __syncthreads();
-  adam_ema_apply(cfg, coef_s, n0, o, a.student, a.teacher, a.exp_avg, a.exp_avg_sq, a.w1bf_student, a.w1bf_teacher);
+  if (vec)
+    adam_ema_apply4(cfg, coef_s, n0 + 4 * (size_t)tid, o4, a.student, a.teacher, a.exp_avg, a.exp_avg_sq,
+                    a.w1bf_student, a.w1bf_teacher);
+  else
+    adam_ema_apply(cfg, coef_s, n0, o, a.student, a.teacher, a.exp_avg, a.exp_avg_sq, a.w1bf_student, a.w1bf_teacher);
 }
 
 // DACPManager.update_class_quality_scores_epoch (I/utils.py:430-447)

@@ -1604,6 +1604,74 @@ __device__ __forceinline__ void ew_pair_inv(int pr, int nt, int& ti, int& tj) {
   tj = ti + pr;
 }
 
+// Member gradients of a narrow class (NP = 32 or 64 padded candidates, rows and coefficients in
+// LDS): 2 (rs_i z_i - (Csym Z)_i) scaled, plus the compactness and repulsion parts of the noisy
+// members, per item of 32 candidates x 32 hidden units.  Every LDS operand of an item -- the
+// NP/8 coefficient reads and 4 NP/8 row reads of the MFMA chain and the 16 rows' epilogue values
+// -- is issued before its first MFMA.  The 32 x 32 result goes out through the wave's own LDS
+// tile (the dead Gram partials, pitch EW_TP: the two lane halves' rows 32 banks apart), read back
+// as 4 consecutive hidden units per lane: 4 dwordx4 stores per lane instead of 16 dword stores
+// (the phase was bound by issuing the 32 KB of stores, not by the MFMA chain).
+#define EW_TP 40
+static_assert(ECDA_NG * 32 * EW_TP <= sizeof(EcdaW::b) / sizeof(float), "ew_member_grads: a 32 x EW_TP tile per wave in S.b");
+template <int NP>
+__device__ __forceinline__ void ew_member_grads(EcdaW& S, const float* db, int dp, int c, int ncs, int ncand_all,
+                                                float mmd_scale, float comp_scale, float* ge_c, float* ge_s,
+                                                float* sink) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int g = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kh = lane >> 5, l32 = lane & 31;
+  constexpr int NK = NP / 8;
+  for (int item = g; item < (NP / 32) * (DAD_H / 32); item += ECDA_NG) {
+    const int ti = item >> 3, tc = item & 7;
+    const int d = 32 * tc + l32;
+    const float* ra = &db[(32 * ti + l32) * dp + 4 * kh];
+    f32x4 av[NK];
+    float bv[NK][4];
+#pragma unroll
+    for (int q = 0; q < NK; ++q) {
+      av[q] = *reinterpret_cast<const f32x4*>(ra + 8 * q);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bv[q][e] = S.a.zc[(8 * q + 4 * kh + e) * EW_ZP + d];
+    }
+    float zi[16], rsv[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = 32 * ti + dad_acc_row(r, kh);   // (< NP <= TW_MAXB: staged or zero row)
+      const int ic = i < ncand_all ? i : 0;
+      zi[r] = S.a.zc[i * EW_ZP + d];
+      rsv[r] = S.rs[ic];
+    }
+    const float mu = S.cent[c][d], rg = S.repg[d];
+    f32x16 acc = f32x16{};
+#pragma unroll
+    for (int q = 0; q < NK; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[q][e], bv[q][e], acc, 0, 0, 0);
+    float* stg = &S.b.gp[0][0] + g * (32 * EW_TP);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = 32 * ti + dad_acc_row(r, kh);
+      const bool noisy = i >= ncs;
+      stg[dad_acc_row(r, kh) * EW_TP + l32] =
+          mmd_scale * (2.0f * (rsv[r] * zi[r] - acc[r])) + (noisy ? comp_scale * (zi[r] - mu) + rg : 0.0f);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // (the wave's own tile: LDS ops are in order)
+    // every row stored: members to their ge row, the rest to the sink (no branch)
+    const int rl = lane >> 3, c4 = 4 * (lane & 7);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int row = rl + 8 * k, i = 32 * ti + row;
+      const int ic = i < ncand_all ? i : 0;
+      const bool mem = (i < ncand_all) & (S.mem[ic] != 0);
+      const f32x4 v = *reinterpret_cast<const f32x4*>(stg + row * EW_TP + c4);
+      float* dst = mem ? (i >= ncs ? ge_s : ge_c) + (size_t)S.rowz[ic] * DAD_H + 32 * tc + c4 : sink + 32 * tc + c4;
+      *reinterpret_cast<f32x4*>(dst) = v;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // tile reads done before the next item's writes
+  }
+}
+
 // The class work after the candidates are known.  WIDE = more than 64 candidates: rows are read
 // from the embedding buffer (global, through the candidate -> row table) instead of LDS.
 template <bool WIDE>
@@ -1862,7 +1930,11 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
     const float comp_scale = wscale * att_c * cfg.ecda_gamma * (2.0f / (float)cnc);
     // member grads 2 sum_j Csym_ij (z_i - z_j) = 2 (rs_i z_i - (Csym Z)_i): (Csym Z) on the
     // matrix cores, 32 candidates x 32 hidden units per item
-    for (int item = g; item < nt * (DAD_H / 32); item += ECDA_NG) {
+    if constexpr (!WIDE) {
+      if (npad == 32) ew_member_grads<32>(S, db, dp, c, ncs, ncand_all, mmd_scale, comp_scale, ge_c, ge_s, a.sink);
+      else ew_member_grads<64>(S, db, dp, c, ncs, ncand_all, mmd_scale, comp_scale, ge_c, ge_s, a.sink);
+    }
+    for (int item = g; WIDE && item < nt * (DAD_H / 32); item += ECDA_NG) {
       const int ti = item >> 3, tc = item & 7;
       const int d = 32 * tc + l32;
       f32x16 acc = f32x16{};
