@@ -521,7 +521,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
 
   // 3. pooled embeddings + classifier logits (BF16: pooled inside the encoder launch)
   if (!pool_fused) {
-    hipLaunchKernelGGL(dad_pool, dim3(G.Bc + Bn), dim3(DAD_POOL_THREADS), 0, stream, pa);
+    hipLaunchKernelGGL(dad_pool, dim3(G.Bc + 2 * Bn), dim3(DAD_POOL_THREADS), 0, stream, pa);
     DAD_TRY(hipGetLastError());
   }
   tk_mark(TK_POOL, stream);
@@ -595,7 +595,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
     DAD_TRY(hipGetLastError());
     tk_mark(TK_WGRAD, stream);
     ra.splits = splits; ra.wpart = wa.wpart;
-    hipLaunchKernelGGL(dad_reduce, dim3(DAD_REDUCE_BLOCKS - DAD_REDUCE_XBLK), dim3(DAD_REDUCE_THREADS), 0, stream, ra);
+    hipLaunchKernelGGL(dad_reduce_w, dim3(DAD_REDUCE_BLOCKS - DAD_REDUCE_XBLK), dim3(64), 0, stream, ra);
     DAD_TRY(hipGetLastError());
     tk_mark(TK_RED, stream);
   } else {

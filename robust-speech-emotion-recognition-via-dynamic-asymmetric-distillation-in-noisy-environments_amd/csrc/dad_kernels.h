@@ -8,7 +8,7 @@
 #define DAD_ENC_WS_THREADS 512                               // W-stationary bf16 encoder (8 waves, two per SIMD)
 #define DAD_ENC_WS_MAXJ 256                                  // max 32-row jobs per encoder workgroup
 #define DAD_WS_TAB 256                                       // student workgroups of the host range table
-#define DAD_POOL_THREADS 256
+#define DAD_POOL_THREADS 64
 #define DAD_TAIL_THREADS 512
 #define DAD_ECDA_THREADS 512
 // 1: the tail and ECDA run as one launch (dad_tail_ecda): block 0 is the tail, blocks 1..C
@@ -179,6 +179,7 @@ __global__ void dad_wgrad_direct(DadWgradArgs a, DadReduceArgs r);
 __global__ void dad_wgrad_su(DadWgradArgs a);
 __global__ void dad_wsum(DadReduceArgs a);
 __global__ void dad_reduce(DadReduceArgs a);
+__global__ void dad_reduce_w(DadReduceArgs a);
 __global__ void dad_norm(float* grad, float* normpart, float inv_world);
 __global__ void dad_optim(DadOptimArgs a);
 __global__ void dad_commit_kernel(dad_config cfg, const float* grad, float* dacp, float* tailf, float* losses_out);

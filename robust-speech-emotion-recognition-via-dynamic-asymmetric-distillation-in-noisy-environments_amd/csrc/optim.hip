@@ -157,8 +157,6 @@ __device__ __forceinline__ void adam_ema_apply4(const dad_config& cfg, float coe
 
 __global__ __launch_bounds__(DAD_OPTIM_THREADS) void dad_optim(DadOptimArgs a) {
   DAD_GUARD_BLOCK(DAD_OPTIM_THREADS);
-  __shared__ float coef_s;
-  __shared__ double nred[DAD_OPTIM_THREADS / 64];
   const dad_config& cfg = a.cfg;
   const int tid = threadIdx.x;
   const size_t n0 = (size_t)blockIdx.x * 1024;
@@ -170,37 +168,36 @@ __global__ __launch_bounds__(DAD_OPTIM_THREADS) void dad_optim(DadOptimArgs a) {
   AdamOperands4 o4;
   if (vec) adam_load4(n0 + 4 * (size_t)tid, a.grad, a.student, a.teacher, a.exp_avg, a.exp_avg_sq, o4);
   else adam_load(n0, a.grad, a.student, a.teacher, a.exp_avg, a.exp_avg_sq, o);
-  // global norm from the squared-norm partials: all threads load, fixed-order combine
+  // global norm from the squared-norm partials: EVERY wave sums all of them in the same fixed
+  // order (lane-strided, then the wave reduction), so every wave of every block derives the
+  // same clip coefficient with no LDS round trip or barrier
+  const int lane = tid & 63;
+  constexpr int NJ = (DAD_REDUCE_BLOCKS + 63) / 64;   // (nnorm <= DAD_REDUCE_BLOCKS: one batch of loads)
+  float pv[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) pv[j] = a.normpart[min(lane + 64 * j, a.nnorm - 1)];
   double s = 0.0;
-  for (int k = tid; k < a.nnorm; k += DAD_OPTIM_THREADS) s += (double)a.normpart[k];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) s += lane + 64 * j < a.nnorm ? (double)pv[j] : 0.0;
+  for (int k = lane + 64 * NJ; k < a.nnorm; k += 64) s += (double)a.normpart[k];
   s = dad_wave_sum_d(s);
-  if ((tid & 63) == 0) nred[tid >> 6] = s;
-  __syncthreads();
-  if (tid < 64) {
-    s = 0.0;
-    for (int k = 0; k < DAD_OPTIM_THREADS / 64; ++k) s += nred[k];
-    if (tid == 0) {
-      const float norm = (float)sqrt(s);
-      float coef = 1.0f;
-      if (cfg.clip) coef = fminf(cfg.max_norm / (norm + 1e-6f), 1.0f);
-      coef_s = coef;
-      if (blockIdx.x == 0) {
-        a.tailf[DAD_T_CLIPNORM] = norm;
-        a.tailf[DAD_T_CLIPCOEF] = coef;
-        const float* ex = a.grad + DAD_NPARAM;
-        a.tailf[DAD_T_TOTAL] = ex[12];
-        if (a.losses_out)
-          for (int k = 0; k < 4; ++k) a.losses_out[k] = ex[12 + k];
-      }
-    }
+  const float norm = (float)sqrt(s);
+  float coef = 1.0f;
+  if (cfg.clip) coef = fminf(cfg.max_norm / (norm + 1e-6f), 1.0f);
+  if (blockIdx.x == 0 && tid == 0) {
+    a.tailf[DAD_T_CLIPNORM] = norm;
+    a.tailf[DAD_T_CLIPCOEF] = coef;
+    const float* ex = a.grad + DAD_NPARAM;
+    a.tailf[DAD_T_TOTAL] = ex[12];
+    if (a.losses_out)
+      for (int k = 0; k < 4; ++k) a.losses_out[k] = ex[12 + k];
   }
   if (blockIdx.x == 0) dacp_commit(cfg, a.grad, a.dacp, tid);
-  __syncthreads();
   if (vec)
-    adam_ema_apply4(cfg, coef_s, n0 + 4 * (size_t)tid, o4, a.student, a.teacher, a.exp_avg, a.exp_avg_sq,
+    adam_ema_apply4(cfg, coef, n0 + 4 * (size_t)tid, o4, a.student, a.teacher, a.exp_avg, a.exp_avg_sq,
                     a.w1bf_student, a.w1bf_teacher);
   else
-    adam_ema_apply(cfg, coef_s, n0, o, a.student, a.teacher, a.exp_avg, a.exp_avg_sq, a.w1bf_student, a.w1bf_teacher);
+    adam_ema_apply(cfg, coef, n0, o, a.student, a.teacher, a.exp_avg, a.exp_avg_sq, a.w1bf_student, a.w1bf_teacher);
 }
 
 // DACPManager.update_class_quality_scores_epoch (I/utils.py:430-447)

@@ -74,100 +74,87 @@ __device__ __forceinline__ double block_sum_d(double v, double* red) {
 
 
 // ------------------------------------------------------------------------------ pool
-// blocks [0, Bc): clean utterances; blocks [Bc, Bc+Bn): noisy utterances (teacher + strong)
+// One wave per (utterance, branch): blocks [0, Bc) clean, [Bc, Bc+Bn) teacher (weak),
+// [Bc+Bn, Bc+2Bn) student (strong).  Lane l owns hidden units 4l..4l+3, so a slab partial is
+// one 16-B load per lane, every load of the block (pad bytes, all slab partials in batches of
+// POOL_BATCH, active counts, W2 columns) is issued before the first sum, and the length and
+// the four logit dot products are wave reductions: no LDS, no barrier (the 256-thread form
+// issued 48 dword loads per thread and joined its 4 waves through LDS twice).  Embeddings sum
+// the slab partials in slab order (I/model.py:35-36 masked mean pooling); logits
+// W2 . dropout(e) + b2 (I/model.py:54-64; the teacher classifier's dropout is off).
+static_assert(DAD_POOL_THREADS == 64 && DAD_H == 4 * 64, "dad_pool: one wave, 4 hidden units per lane");
 __global__ __launch_bounds__(DAD_POOL_THREADS) void dad_pool(DadPoolArgs a) {
   DAD_GUARD_BLOCK(DAD_POOL_THREADS);
-  __shared__ float red[8];
-  __shared__ float zred[8][4];
   const DadGeom& g = a.g;
-  const int blk = blockIdx.x, h = threadIdx.x;
-  const int w = h >> 6, l = h & 63;
-  const bool noisy = blk >= g.Bc;
-  const int b = noisy ? blk - g.Bc : blk;
+  const int blk = blockIdx.x, lane = threadIdx.x;
+  const int kind = blk < g.Bc ? 0 : (blk < g.Bc + g.Bn ? 1 : 2);   // clean, teacher (weak), student (strong)
+  const int b = kind == 0 ? blk : (kind == 1 ? blk - g.Bc : blk - g.Bc - g.Bn);
+  const bool noisy = kind != 0, teacher = kind == 1;
   const int T = noisy ? g.Tn : g.Tc;
-  const uint8_t* pad = noisy ? a.mn : a.mc;
-  // valid length (I/model.py:35: (1-mask).sum(dim=1)); reduced below, after every other
-  // load of the block has been issued
-  float len = 0.0f;
-  for (int t = h; t < T; t += 256) len += pad[(size_t)b * T + t] == 0 ? 1.0f : 0.0f;
-  const float* W2s = a.student + DAD_OFF_W2;
-  const float* b2s = a.student + DAD_OFF_B2;
-  const float* W2t = a.teacher + DAD_OFF_W2;
-  const float* b2t = a.teacher + DAD_OFF_B2;
+  const uint8_t* pad = (noisy ? a.mn : a.mc) + (size_t)b * T;
   const size_t nsc = (size_t)g.Bc * g.ncc, nsn = (size_t)g.Bn * g.ncn;
-  const int nbr = noisy ? 2 : 1;
   const int nc = noisy ? g.ncn : g.ncc;
-  // every load first (slab partials of both branches, active counts, W2 columns, keep
-  // flag), then the stores: a store between loads would serialise them on possible aliasing
-  size_t slab0[2];
-  int erow[2];
-  if (!noisy) { slab0[0] = (size_t)b * g.ncc; erow[0] = b; slab0[1] = slab0[0]; erow[1] = b; }
-  else {
-    slab0[0] = nsc + (size_t)b * g.ncn;        erow[0] = g.Bc + b;          // teacher (weak)
-    slab0[1] = nsc + nsn + (size_t)b * g.ncn;  erow[1] = g.Bc + g.Bn + b;   // student (strong)
-  }
-  const size_t cslab0 = noisy ? nsc + (size_t)b * g.ncn : (size_t)b * g.ncc;
-  float ssum[2] = {0.0f, 0.0f};
-  float cnt = 0.0f;
-  // slab partials in batches of POOL_BATCH slabs, every load of a batch issued before the
-  // sums (index clamped, contribution masked; summed in slab order).  16 slabs of 32 rows
-  // cover T <= 512 frames in one round trip.
+  const size_t slab0 = kind == 0 ? (size_t)b * g.ncc : (kind == 1 ? nsc + (size_t)b * g.ncn : nsc + nsn + (size_t)b * g.ncn);
+  const size_t cslab0 = noisy ? nsc + (size_t)b * g.ncn : (size_t)b * g.ncc;   // active counts (clean / strong)
+  const int erow = kind == 0 ? b : (kind == 1 ? g.Bc + b : g.Bc + g.Bn + b);
+  const int h0 = 4 * lane;
+  // valid length (I/model.py:35: (1-mask).sum(dim=1))
+  float len = 0.0f;
+  for (int t = lane; t < T; t += 64) len += pad[t] == 0 ? 1.0f : 0.0f;
+  // slab partials and active counts, every load of a batch before its sums (index clamped,
+  // contribution masked; summed in slab order).  The teacher also loads the strong counts it
+  // does not use: no load under a branch.
   constexpr int POOL_BATCH = 16;
+  f32x4 ssum = f32x4{}, cnt = f32x4{};
   for (int c0 = 0; c0 < nc; c0 += POOL_BATCH) {
-    float p0[POOL_BATCH], p1[POOL_BATCH], pc[POOL_BATCH];
+    f32x4 ps[POOL_BATCH], pc[POOL_BATCH];
 #pragma unroll
     for (int k = 0; k < POOL_BATCH; ++k) {
       const int c = min(c0 + k, nc - 1);
-      p0[k] = a.part_sum[(slab0[0] + c) * DAD_H + h];
-      p1[k] = noisy ? a.part_sum[(slab0[1] + c) * DAD_H + h] : 0.0f;
-      pc[k] = a.part_cnt[(cslab0 + c) * DAD_H + h];
+      ps[k] = *reinterpret_cast<const f32x4*>(a.part_sum + (slab0 + c) * DAD_H + h0);
+      pc[k] = *reinterpret_cast<const f32x4*>(a.part_cnt + (cslab0 + c) * DAD_H + h0);
     }
 #pragma unroll
-    for (int k = 0; k < POOL_BATCH; ++k) {
-      if (c0 + k >= nc) break;
-      ssum[0] += p0[k];
-      ssum[1] += p1[k];
-      cnt += pc[k];
+    for (int k = 0; k < POOL_BATCH; ++k) {   // (+0 past the utterance's slabs: the sums are unchanged)
+      const bool in = c0 + k < nc;
+      ssum += in ? ps[k] : f32x4{};
+      cnt += in ? pc[k] : f32x4{};
     }
   }
-  float w2s[4], w2t[4];
+  const float* par = teacher ? a.teacher : a.student;
+  f32x4 w2[DAD_C];
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    w2s[c] = W2s[c * DAD_H + h];
-    w2t[c] = noisy ? W2t[c * DAD_H + h] : 0.0f;
-  }
-  const float kv = !noisy ? keep_value(a.keep1, a.key_drop1, b, h, a.p_drop, a.drop_scale)
-                          : keep_value(a.keep2, a.key_drop2, b, h, a.p_drop, a.drop_scale);
-  len = block_sum_f(len, red);
-  float zp[2][4];
-  for (int k = 0; k < nbr; ++k) {
-    const float e = ssum[k] / fmaxf(len, 1.0f);
-    a.emb[(size_t)erow[k] * DAD_H + h] = e;
-    const bool teacher = noisy && k == 0;
-    // teacher classifier: dropout p = 0 (I/model.py:121); students: dropout masks #1 / #2
-    const float d = teacher ? e : e * kv;
+  for (int c = 0; c < DAD_C; ++c) w2[c] = *reinterpret_cast<const f32x4*>(par + DAD_OFF_W2 + c * DAD_H + h0);
+  const float bias = par[DAD_OFF_B2 + (lane & (DAD_C - 1))];
+  f32x4 kv;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) zp[k][c] = dad_wave_sum((teacher ? w2t[c] : w2s[c]) * d);
+  for (int e = 0; e < 4; ++e)   // teacher classifier: dropout p = 0 (I/model.py:121); students: masks #1 / #2
+    kv[e] = teacher ? 1.0f
+                    : (kind == 0 ? keep_value(a.keep1, a.key_drop1, b, h0 + e, a.p_drop, a.drop_scale)
+                                 : keep_value(a.keep2, a.key_drop2, b, h0 + e, a.p_drop, a.drop_scale));
+  len = dad_wave_sum(len);
+  f32x4 e;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) e[k] = ssum[k] / fmaxf(len, 1.0f);
+  *reinterpret_cast<f32x4*>(a.emb + (size_t)erow * DAD_H + h0) = e;
+  const f32x4 d = teacher ? e : e * kv;
+  float zp[DAD_C];
+#pragma unroll
+  for (int c = 0; c < DAD_C; ++c)
+    zp[c] = dad_wave_sum(((w2[c][0] * d[0] + w2[c][1] * d[1]) + w2[c][2] * d[2]) + w2[c][3] * d[3]);
+  if (lane < DAD_C) a.logits[(size_t)erow * DAD_C + lane] = (lane == 0 ? zp[0] : (lane == 1 ? zp[1] : (lane == 2 ? zp[2] : zp[3]))) + bias;
+  if (!teacher) {
+    // active-row count per (utterance, h) of the branch that gets a gradient (clean / strong);
+    // the length, and the ECDA row flag (clean b / noisy Bc + b) starts at zero: the ECDA
+    // workgroups write only what they own
+    const int urow = noisy ? g.Bc + b : b;
+    *reinterpret_cast<f32x4*>(a.cnt_tot + (size_t)urow * DAD_H + h0) = cnt;
+    if (lane == 0) {
+      a.vlen[urow] = len;
+      a.eflag[urow] = 0u;
+    }
   }
-  // active-row count per (utterance, h) of the branch that gets a gradient (clean / strong)
-  a.cnt_tot[(size_t)(noisy ? g.Bc + b : b) * DAD_H + h] = cnt;
-  if (h == 0) a.vlen[blk] = len;
-  // ECDA row flag of this utterance (clean b / noisy Bc + b = blk) and the per-class ECDA
-  // terms and gates start at zero: the ECDA workgroups write only what they own
-  if (h == 0) a.eflag[blk] = 0u;
-  if (blk == 0 && h < 2 * DAD_C) a.tail_terms[h] = 0.0f;
-  if (l == 0)
-    for (int k = 0; k < nbr; ++k)
-      for (int c = 0; c < 4; ++c) zred[k * 4 + c][w] = zp[k][c];
-  __syncthreads();
-  if (h < nbr * 4) {
-    const int k = h >> 2, c = h & 3;
-    const bool teacher = noisy && k == 0;
-    const float dot = ((zred[h][0] + zred[h][1]) + zred[h][2]) + zred[h][3];
-    const float bias = teacher ? b2t[c] : b2s[c];
-    const int erow = !noisy ? b : (k == 0 ? g.Bc + b : g.Bc + g.Bn + b);
-    a.logits[(size_t)erow * DAD_C + c] = dot + bias;
-  }
+  if (blk == 0 && lane < 2 * DAD_C) a.tail_terms[lane] = 0.0f;   // per-class ECDA terms and gates
 }
 
 // ------------------------------------------------------------------------------ tail

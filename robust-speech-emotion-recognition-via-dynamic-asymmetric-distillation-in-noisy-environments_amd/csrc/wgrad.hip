@@ -915,6 +915,35 @@ __global__ __launch_bounds__(DAD_REDUCE_THREADS) void dad_reduce(DadReduceArgs a
 // loads in flight, the four groups combined in fixed order (deterministic).  Blocks NB + e:
 // db1, dW2, norm shares, loss totals (extra_block).  Every block: its squared-norm partial.
 static_assert(DAD_D % DAD_REDUCE_COLS == 0, "dad_wsum: whole blocks per dW1 row");
+// BF16 step (the extra blocks ran on spare dad_wgrad_direct workgroups): one wave per
+// DAD_REDUCE_COLS columns, 4 per lane, the splits summed in split order with every partial's
+// load issued first (batches of 8, index clamped, +0 past the last split), the squared-norm
+// partial a wave reduction: no LDS, no barrier (dad_reduce's 4 row groups met through LDS
+// twice).
+static_assert(DAD_REDUCE_COLS == 4 * 64, "dad_reduce_w: one wave, 4 columns per lane");
+__global__ __launch_bounds__(64) void dad_reduce_w(DadReduceArgs a) {
+  DAD_GUARD_BLOCK(64);
+  const int lane = threadIdx.x;
+  const size_t e0 = (size_t)blockIdx.x * DAD_REDUCE_COLS + 4 * (size_t)lane;
+  constexpr int KB = 8;
+  f32x4 t = f32x4{};
+  for (int k0 = 0; k0 < a.splits; k0 += KB) {
+    f32x4 v[KB];
+#pragma unroll
+    for (int k = 0; k < KB; ++k)
+      v[k] = *reinterpret_cast<const f32x4*>(a.wpart + (size_t)min(k0 + k, a.splits - 1) * DAD_H * DAD_D + e0);
+#pragma unroll
+    for (int k = 0; k < KB; ++k) t += k0 + k < a.splits ? v[k] : f32x4{};
+  }
+  *reinterpret_cast<f32x4*>(a.grad + DAD_OFF_W1 + e0) = t;
+  if (!a.want_norm) return;
+  double sq = 0.0;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) sq += (double)t[e] * t[e];
+  sq = dad_wave_sum_d(sq);
+  if (lane == 0) a.normpart[blockIdx.x] = (float)sq;
+}
+
 __global__ __launch_bounds__(DAD_REDUCE_THREADS) void dad_wsum(DadReduceArgs a) {
   DAD_GUARD_BLOCK(DAD_REDUCE_THREADS);
   __shared__ double red[DAD_REDUCE_THREADS / 64];
