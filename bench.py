@@ -410,7 +410,7 @@ WGRAD_KERNEL = {"bf16": ("wgrad", "dad_wgrad_direct"), "fp32": ("wgrad", "dad_wg
 # (the labels of the default direct weight gradient; DAD_WGRAD[_F32]=su runs S_u on a side stream,
 # timed as "side", and dad_wsum in the "wgrad" slot)
 KNAMES = {"bf16": {"encode": "dad_encode_ws", "pool": "dad_pool", "tail": "dad_tail_ecda", "wgrad": "dad_wgrad_direct",
-                   "reduce": "dad_reduce", "optim": "dad_optim"},
+                   "reduce": "dad_reduce_w", "optim": "dad_optim"},
           "fp32": {"encode": "dad_encode_f32", "pool": "dad_pool", "tail": "dad_tail_ecda", "wgrad": "dad_wgrad_f32",
                    "reduce": "dad_reduce", "side": "dad_wgrad_f32 (S_u, side stream)", "optim": "dad_optim"}}
 
