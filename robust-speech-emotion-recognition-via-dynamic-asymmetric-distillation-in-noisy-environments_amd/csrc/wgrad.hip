@@ -505,6 +505,9 @@ __device__ __forceinline__ int wgd_utt(const DadGeom& g, int s) {
 
 }  // namespace
 
+#ifndef WGD_PRIO
+#define WGD_PRIO 0   // 1 / 2: s_setprio 1 for slab group 0 / 1 in the loop (A/B option)
+#endif
 // WGD_WT: partial-slab stores write-through (sc1): no dirty L2 lines left for the kernel-end release
 #ifndef WGD_WT
 #define WGD_WT 0
@@ -599,6 +602,11 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
     wgd_load(a, tab, min(5, jlast), sfirst, dbase, wv, r[1]);
     const unsigned long long tc = WGD_CLK();
     __syncthreads();
+#if WGD_PRIO
+    // static priority for one slab group: the two waves sharing a SIMD (one per group) leave each
+    // barrier in step; the favoured one issues its MFMAs first and the other fills the gaps
+    if (grp == WGD_PRIO - 1) __builtin_amdgcn_s_setprio(1);
+#endif
     t1 = WGD_CLK();
     WGD_ACC(3, ta - t0); WGD_ACC(6, tb - ta); WGD_ACC(7, tc - tb); (void)ta; (void)tb; (void)tc;
     // round j: read slab j's operands from buffer j&3 into registers | MFMAs of slab j-1 from
