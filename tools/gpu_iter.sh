@@ -1,6 +1,10 @@
 # Iteration loop of a kernel change: the parity tests of the step, the tail/ECDA phase stamps
 # (lib variant 'stamps'), an A/B of the product library against variant 'old' (AB_ROUNDS
 # alternating 400-step benches), the host-overhead breakdown.  Stops at a crash or time limit.
+# Variants are built here, before the call (the box only runs what the snapshot carries), e.g.
+#   python -c "import sys; sys.path.insert(0, '<pkg>'); import _build; \
+#              _build.build(variant='stamps', extra=['-DDAD_PROBE_STAMPS'])"
+# and 'old' from the previous commit's sources (git stash; _build.build(variant='old'); git stash pop).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
