@@ -508,6 +508,9 @@ __device__ __forceinline__ int wgd_utt(const DadGeom& g, int s) {
 #ifndef WGD_PRIO
 #define WGD_PRIO 0   // 1 / 2: s_setprio 1 for slab group 0 / 1 in the loop (A/B option)
 #endif
+#ifndef WGD_NBUF
+#define WGD_NBUF 4   // x-tile LDS buffers per slab group (8: staging 4 rounds ahead, a barrier every 4 rounds)
+#endif
 // WGD_WT: partial-slab stores write-through (sc1): no dirty L2 lines left for the kernel-end release
 #ifndef WGD_WT
 #define WGD_WT 0
@@ -538,7 +541,7 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
     const int mine = (n - grp + WGD_GROUPS - 1) / WGD_GROUPS;   // group 1 may have one slab fewer
     const int cntmin = n / WGD_GROUPS;
     const int u0 = wgd_utt(g, s0), nu = wgd_utt(g, s1 - 1) - u0 + 1;
-    __bf16* Xg = Xt + grp * (4 * DAD_SLAB * WGD_XP);   // this group's four LDS buffers
+    __bf16* Xg = Xt + grp * (WGD_NBUF * DAD_SLAB * WGD_XP);   // this group's WGD_NBUF LDS buffers
     // dL/de_u[h] / max(1, len_u) of this split's utterances (thread = h of each group) as bf16;
     // the host bounds a split to WGD_MAXU slabs, hence utterances.  In each batch of eight
     // utterances group g builds entries 4g .. 4g+3 (KG per group).  The first batch's vector
@@ -592,14 +595,21 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
       else ge_table(std::false_type{});
     }
     const unsigned long long tb = WGD_CLK();
-    // slabs 0 and 1 of each group into buffers 0 and 1; their ring slots reload slabs 4 and 5
-    static_assert(WGD_DEPTH == 4, "dad_wgrad_direct: four ring slots = four LDS buffers");
-    if (mine > 0) wgd_stage(r[0], Xg);
-    if (mine > 1) wgd_stage(r[1], Xg + DAD_SLAB * WGD_XP);
-    int ulq[2] = {r[0].ul, r[1].ul};   // utterance slot and row masks of slabs j, j+1 (by parity)
-    uint32_t mwq[2][2] = {{r[0].mw[0], r[0].mw[1]}, {r[1].mw[0], r[1].mw[1]}};
-    wgd_load(a, tab, min(4, jlast), sfirst, dbase, wv, r[0]);
-    wgd_load(a, tab, min(5, jlast), sfirst, dbase, wv, r[1]);
+    // slabs 0 .. SD-1 of each group into buffers 0 .. SD-1; their ring slots reload slabs
+    // WGD_DEPTH .. WGD_DEPTH + SD - 1
+    constexpr int NB = WGD_NBUF, SD = WGD_NBUF / 2;   // LDS buffers, staging distance (rounds)
+    static_assert(WGD_DEPTH == 4 && (NB == 4 || NB == 8), "dad_wgrad_direct: four ring slots, 4 or 8 LDS buffers");
+    int ulq[SD];   // utterance slot and row masks of slabs j .. j+SD-1 (by j mod SD)
+    uint32_t mwq[SD][2];
+#pragma unroll
+    for (int q = 0; q < SD; ++q) {
+      if (mine > q) wgd_stage(r[q], Xg + q * (DAD_SLAB * WGD_XP));
+      ulq[q] = r[q].ul;
+      mwq[q][0] = r[q].mw[0];
+      mwq[q][1] = r[q].mw[1];
+    }
+#pragma unroll
+    for (int q = 0; q < SD; ++q) wgd_load(a, tab, min(WGD_DEPTH + q, jlast), sfirst, dbase, wv, r[q]);
     const unsigned long long tc = WGD_CLK();
     __syncthreads();
 #if WGD_PRIO
@@ -609,24 +619,25 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
 #endif
     t1 = WGD_CLK();
     WGD_ACC(3, ta - t0); WGD_ACC(6, tb - ta); WGD_ACC(7, tc - tb); (void)ta; (void)tb; (void)tc;
-    // round j: read slab j's operands from buffer j&3 into registers | MFMAs of slab j-1 from
-    // the registers read in round j-1 (so they never wait on LDS) | stage slab j+2 into
-    // buffer (j+2)&3 from ring slot (j+2)&3 and reload that slot with slab j+6.  A slab is
-    // staged two rounds before it is read, so one barrier per TWO rounds (after odd j) orders
-    // every staging before its reads and every read before its buffer is restaged.
+    // round j: read slab j's operands from buffer j % NB into registers | MFMAs of slab j-1 from
+    // the registers read in round j-1 (so they never wait on LDS) | stage slab j+SD into
+    // buffer (j+SD) % NB from ring slot (j+SD) % 4 and reload that slot with slab j+SD+4.  A slab
+    // is staged SD = NB/2 rounds before it is read, so one barrier per SD rounds (after rounds
+    // j = SD-1 mod SD) orders every staging before its reads and every read before its buffer is
+    // restaged (NB = 4: a barrier every two rounds; NB = 8: every four).
     WgdFrag F;
     auto round = [&](int jr, int k, bool prev, bool comp, bool stage, bool bar) {
       const unsigned long long c0 = WGD_CLK();
-      const int nk = (k + 2) % WGD_DEPTH;
+      const int nk = (k + SD) % WGD_DEPTH;
       WgdRaw R;
-      if (comp) R = wgd_read<SU>(Xg + (k & 3) * (DAD_SLAB * WGD_XP), mwq[k & 1], lut, gs, ulq[k & 1], wv);
+      if (comp) R = wgd_read<SU>(Xg + (k % NB) * (DAD_SLAB * WGD_XP), mwq[k % SD], lut, gs, ulq[k % SD], wv);
       __builtin_amdgcn_sched_barrier(0);   // reads first, their latency under the MFMAs
       if (prev) wgd_mma(F, acc);
-      if (stage) wgd_stage(r[nk], Xg + ((k + 2) & 3) * (DAD_SLAB * WGD_XP));
-      ulq[k & 1] = r[nk].ul;
-      mwq[k & 1][0] = r[nk].mw[0];
-      mwq[k & 1][1] = r[nk].mw[1];
-      wgd_load(a, tab, min(jr + 2 + WGD_DEPTH, jlast), sfirst, dbase, wv, r[nk]);
+      if (stage) wgd_stage(r[nk], Xg + ((k + SD) % NB) * (DAD_SLAB * WGD_XP));
+      ulq[k % SD] = r[nk].ul;
+      mwq[k % SD][0] = r[nk].mw[0];
+      mwq[k % SD][1] = r[nk].mw[1];
+      wgd_load(a, tab, min(jr + SD + WGD_DEPTH, jlast), sfirst, dbase, wv, r[nk]);
       __builtin_amdgcn_sched_barrier(0);
       if (comp) F = wgd_finish(R);
       const unsigned long long c1 = WGD_CLK();
@@ -634,21 +645,21 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
       WGD_ACC(4, c1 - c0); WGD_ACC(5, WGD_CLK() - c1); WGD_ACC(8, 1);
       (void)c0; (void)c1;
     };
-    // round 0, then blocks of WGD_DEPTH rounds in which both groups have every step (no early
-    // exits: an exit inside the block would reach the loop header with a different load
-    // order and force vmcnt(0) there; ring slots are compile-time: j = 1 mod WGD_DEPTH at a
-    // block start), then the last rounds with per-group flags and the final MFMAs.  Both groups
-    // run the same rounds, so the barriers (after odd rounds) match.
-    round(0, 0, false, mine > 0, 2 < mine, false);
+    // round 0, then blocks of NB rounds (NB is a multiple of the 4 ring slots) in which both
+    // groups have every step (no early exits: an exit inside the block would reach the loop
+    // header with a different load order and force vmcnt(0) there; buffers and ring slots are
+    // compile-time: j = 1 mod NB at a block start), then the last rounds with per-group flags and
+    // the final MFMAs.  Both groups run the same rounds, so the barriers match.
+    round(0, 0, false, mine > 0, SD < mine, false);
     int j = 1;
-    for (; j + WGD_DEPTH + 1 < cntmin; j += WGD_DEPTH) {   // every round stages slab j + k + 2 < cntmin
+    for (; j + NB - 1 + SD < cntmin; j += NB) {   // every round stages slab j + k + SD < cntmin
 #pragma unroll
-      for (int k = 0; k < WGD_DEPTH; ++k) round(j + k, k + 1, true, true, true, (k & 1) == 0);
+      for (int k = 0; k < NB; ++k) round(j + k, (k + 1) % NB, true, true, true, (k + 1) % SD == SD - 1);
     }
 #pragma unroll
-    for (int k = 0; k < WGD_DEPTH + 3; ++k)   // nround - j <= WGD_DEPTH + 2
+    for (int k = 0; k < NB + SD + 1; ++k)   // nround - j <= NB + SD
       if (j + k < nround)
-        round(j + k, k + 1, j + k - 1 < mine, j + k < mine, j + k + 2 < mine, (k & 1) == 0);
+        round(j + k, (k + 1) % NB, j + k - 1 < mine, j + k < mine, j + k + SD < mine, (k + 1) % SD == SD - 1);
     if (nround - 1 < mine) wgd_mma(F, acc);
     t2 = WGD_CLK();
   }
@@ -706,7 +717,7 @@ __device__ __forceinline__ void wgd_lut(uint4* lut) {
 // LDS of the weight-gradient workgroups (160 KB with the dL/de table): the x tiles, then the
 // mask table; the end-of-tile exchange (red, 64 KB) reuses the x tiles and the spare space
 // after them (the table stays intact for the next tile)
-constexpr int WGD_XT = WGD_GROUPS * 4 * DAD_SLAB * WGD_XP;   // bf16 elements
+constexpr int WGD_XT = WGD_GROUPS * WGD_NBUF * DAD_SLAB * WGD_XP;   // bf16 elements
 constexpr int WGD_RED = WGD_GROUPS == 2 ? DAD_H * WGD_DB : 1;
 struct __attribute__((aligned(16))) WgdSmem {
   union {
