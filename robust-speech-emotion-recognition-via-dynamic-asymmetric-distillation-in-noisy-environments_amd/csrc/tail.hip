@@ -98,16 +98,35 @@ __global__ __launch_bounds__(DAD_POOL_THREADS) void dad_pool(DadPoolArgs a) {
   const size_t cslab0 = noisy ? nsc + (size_t)b * g.ncn : (size_t)b * g.ncc;   // active counts (clean / strong)
   const int erow = kind == 0 ? b : (kind == 1 ? g.Bc + b : g.Bc + g.Bn + b);
   const int h0 = 4 * lane;
-  // valid length (I/model.py:35: (1-mask).sum(dim=1))
+  // First batch, every load issued before any sum: the pad bytes of frames lane + 64k (k <
+  // POOL_PADB: T <= 512), the slab partials and active counts of slabs 0 .. POOL_BATCH-1 (index
+  // clamped, contribution masked; summed in slab order).  (A pad loop with the sum inside waited
+  // on each byte before the next load: one memory round trip per 64 frames, ahead of the slab
+  // loads.)  The teacher also loads the strong counts it does not use: no load under a branch.
+  constexpr int POOL_PADB = 8, POOL_BATCH = 16;
+  uint8_t pv[POOL_PADB];
+#pragma unroll
+  for (int k = 0; k < POOL_PADB; ++k) pv[k] = pad[min(lane + 64 * k, T - 1)];
+  f32x4 ps[POOL_BATCH], pc[POOL_BATCH];
+#pragma unroll
+  for (int k = 0; k < POOL_BATCH; ++k) {
+    const int c = min(k, nc - 1);
+    ps[k] = *reinterpret_cast<const f32x4*>(a.part_sum + (slab0 + c) * DAD_H + h0);
+    pc[k] = *reinterpret_cast<const f32x4*>(a.part_cnt + (cslab0 + c) * DAD_H + h0);
+  }
+  // valid length (I/model.py:35: (1-mask).sum(dim=1)); frames past the first batch in a loop
   float len = 0.0f;
-  for (int t = lane; t < T; t += 64) len += pad[t] == 0 ? 1.0f : 0.0f;
-  // slab partials and active counts, every load of a batch before its sums (index clamped,
-  // contribution masked; summed in slab order).  The teacher also loads the strong counts it
-  // does not use: no load under a branch.
-  constexpr int POOL_BATCH = 16;
+#pragma unroll
+  for (int k = 0; k < POOL_PADB; ++k) len += ((lane + 64 * k < T) & (pv[k] == 0)) ? 1.0f : 0.0f;
+  for (int t = lane + 64 * POOL_PADB; t < T; t += 64) len += pad[t] == 0 ? 1.0f : 0.0f;
   f32x4 ssum = f32x4{}, cnt = f32x4{};
-  for (int c0 = 0; c0 < nc; c0 += POOL_BATCH) {
-    f32x4 ps[POOL_BATCH], pc[POOL_BATCH];
+#pragma unroll
+  for (int k = 0; k < POOL_BATCH; ++k) {   // (+0 past the utterance's slabs: the sums are unchanged)
+    const bool in = k < nc;
+    ssum += in ? ps[k] : f32x4{};
+    cnt += in ? pc[k] : f32x4{};
+  }
+  for (int c0 = POOL_BATCH; c0 < nc; c0 += POOL_BATCH) {   // utterances past 512 frames
 #pragma unroll
     for (int k = 0; k < POOL_BATCH; ++k) {
       const int c = min(c0 + k, nc - 1);
@@ -115,7 +134,7 @@ __global__ __launch_bounds__(DAD_POOL_THREADS) void dad_pool(DadPoolArgs a) {
       pc[k] = *reinterpret_cast<const f32x4*>(a.part_cnt + (cslab0 + c) * DAD_H + h0);
     }
 #pragma unroll
-    for (int k = 0; k < POOL_BATCH; ++k) {   // (+0 past the utterance's slabs: the sums are unchanged)
+    for (int k = 0; k < POOL_BATCH; ++k) {
       const bool in = c0 + k < nc;
       ssum += in ? ps[k] : f32x4{};
       cnt += in ? pc[k] : f32x4{};
