@@ -8,7 +8,7 @@ global-norm clip + Adam + teacher EMA (+ one RCCL all-reduce of the grads for N 
 Post-warm-up epoch 60 (full loss weights) with a confident synthetic teacher, so the KL and
 ECDA terms are active.  Inputs are resident in HBM before timing.
 
-    python bench.py [--gpus N --steps K --warmup W --precision bf16|fp32]
+    python bench.py [--gpus N --steps K --warmup W --precision fp16|bf16|fp32]
     torchrun --nproc-per-node N bench.py --gpus N ...          (one process per GPU)
 
 Prints ONE JSON line (rank 0).
@@ -33,7 +33,8 @@ PKG = importlib.import_module(
 
 METRIC = "utterances/sec (DAD train step) batch=64 at 1/2/4/8 MI355X; loss parity"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
-BF16_PEAK_TFLOPS = 2500.0      # dense bf16 MFMA
+BF16_PEAK_TFLOPS = 2500.0      # dense bf16 / fp16 MFMA (the same rate for both)
+PEAK_TFLOPS = {"fp16": BF16_PEAK_TFLOPS, "bf16": BF16_PEAK_TFLOPS}
 FP32_PEAK_TFLOPS = 157.3       # f32 MFMA == f32 vector rate
 # every 8th timed step (every steps/4-th in short runs) records hip events (DAD_BENCH_EVENT_EVERY
 # overrides, for measuring what the events themselves cost)
@@ -148,20 +149,47 @@ def _cpu_leg(B, T, steps, epoch, threads, seconds):
     return statistics.median(times[2:]), len(times) - 2, sum(times[2:])
 
 
+def job_cpus():
+    """CPUs this job may use: the affinity mask, capped by the cgroup CPU quota (cgroup v2
+    cpu.max / v1 cfs_quota_us).  On the GPU box the affinity mask lists all of the host's CPUs
+    while the job's share is a fraction of them (a 256-thread pool on a 16-CPU share ran one
+    step in 17 s, round 3)."""
+    n = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(p)
+    except (OSError, ValueError):
+        try:
+            q = float(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            p = float(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / p
+        except (OSError, ValueError):
+            pass
+    if quota is not None:
+        n = max(1, min(n, int(quota)))
+    return n
+
+
 def cpu_baseline(B, T, steps, epoch, seconds=CPU_BASELINE_SECONDS):
     """The PyTorch-CPU step (oracle/torch_cpu.py: the reference's step on the same ATen ops,
     calibrated against the imported reference in profiles/r02_cpu_calibration.json) on this
-    host, timed twice: with the job's CPU share (OMP_NUM_THREADS) and with every CPU of the
-    affinity mask (the node's own host cores).  `value` is the faster of the two."""
-    host_cpus = len(os.sched_getaffinity(0))
-    job = int(os.environ.get("OMP_NUM_THREADS") or host_cpus)
+    host with the job's CPU share: OMP_NUM_THREADS (16 on the GPU box) and, when it differs, the
+    CPUs the job may use (affinity mask capped by the cgroup quota, job_cpus()).  Each leg runs
+    2 warm-ups then at least `steps` timed steps; `value` is the faster leg."""
+    usable = job_cpus()
+    job = min(int(os.environ.get("OMP_NUM_THREADS") or usable), usable)
     legs = []
-    for n in sorted({job, host_cpus}):
-        med, k, tot = _cpu_leg(B, T, steps, epoch, n, seconds / (2 if host_cpus != job else 1))
+    threads = sorted({job, usable})
+    for n in threads:
+        med, k, tot = _cpu_leg(B, T, steps, epoch, n, seconds / len(threads))
         legs.append({"threads": n, "value": B / med, "median_s_per_step": med, "steps": k, "seconds": tot})
     best = max(legs, key=lambda r: r["value"])
     out = {"value": best["value"], "unit": "utterances/s", "cores": best["threads"], "kind": "port",
-           "host_cpus": host_cpus, "job_threads": job, "cpu_model": _cpu_model(), "legs": legs,
+           "host_cpus": os.cpu_count(), "usable_cpus": usable, "job_threads": job, "cpu_model": _cpu_model(),
+           "legs": legs,
            "sample": "PyTorch-CPU DAD step (oracle/torch_cpu.py), B=%d T=%d epoch %d, torch RNG, timed at %s threads "
                      "(>= %d steps after 2 warm-ups, about %.0f s in all); value = the faster leg"
                      % (B, T, epoch, " and ".join(str(r["threads"]) for r in legs), steps, seconds)}
@@ -405,17 +433,27 @@ def merge_ktimes(parts):
     return {k: (t / c, c) for k, (t, c) in acc.items() if c}
 
 
-ENC_KERNEL = {"bf16": "dad_encode_ws", "fp32": "dad_encode_f32"}
-WGRAD_KERNEL = {"bf16": ("wgrad", "dad_wgrad_direct"), "fp32": ("wgrad", "dad_wgrad_f32")}
-# (the labels of the default direct weight gradient; DAD_WGRAD[_F32]=su runs S_u on a side stream,
-# timed as "side", and dad_wsum in the "wgrad" slot)
-KNAMES = {"bf16": {"encode": "dad_encode_ws", "pool": "dad_pool", "tail": "dad_tail_ecda", "wgrad": "dad_wgrad_direct",
-                   "reduce": "dad_reduce_w", "optim": "dad_optim"},
-          "fp32": {"encode": "dad_encode_f32", "pool": "dad_pool", "tail": "dad_tail_ecda", "wgrad": "dad_wgrad_f32",
-                   "reduce": "dad_reduce", "side": "dad_wgrad_f32 (S_u, side stream)", "optim": "dad_optim"}}
+ENC_KERNEL = {"fp16": "dad_encode_ws_f16", "bf16": "dad_encode_ws", "fp32": "dad_encode_f32"}
+WGRAD_KERNEL = {"fp16": ("wgrad", "dad_wgrad_direct_f16"), "bf16": ("wgrad", "dad_wgrad_direct"),
+                "fp32": ("wgrad", "dad_wgrad_f32")}
+KNAMES = {p: {"encode": ENC_KERNEL[p], "pool": "dad_pool", "wgrad": WGRAD_KERNEL[p][1],
+              "reduce": "dad_reduce" if p == "fp32" else "dad_reduce_w", "optim": "dad_optim"}
+          for p in ("fp16", "bf16", "fp32")}
 
 
-def rooflines(ktimes, rows_c, rows_n, ms_step, precision):
+def class_aware(view):
+    """config.py's class_aware switch: USE_CLASS_AWARE_MMD on IEMOCAP, always on for CASIA / EMODB."""
+    return view.flavor != "iemocap" or bool(getattr(view, "USE_CLASS_AWARE_MMD", True))
+
+
+def tail_kernel(B, Bn, class_aware=True):
+    """The launch in the "tail" slot (dad_abi.hip): the wave-centric dad_tail_ecda_w for batches of
+    at most 64 per side with class-aware MMD (unless DAD_TAIL_W=0), else dad_tail_ecda."""
+    w = B <= 64 and Bn <= 64 and class_aware and os.environ.get("DAD_TAIL_W", "1") != "0"
+    return "dad_tail_ecda_w" if w else "dad_tail_ecda"
+
+
+def rooflines(ktimes, rows_c, rows_n, ms_step, precision, tail_name="dad_tail_ecda_w"):
     """`roofline` of the dominant kernel (the encoder), `step_roofline` of the whole step and the
     per-kernel table (live HIP-event durations of dad_timing_start) with MFMA utilisation of the
     encoder linears.  Algorithmic work:
@@ -424,12 +462,12 @@ def rooflines(ktimes, rows_c, rows_n, ms_step, precision):
       dW1:      flops = 2 x 768 x 256 x (rows_c + rows_n)
       step:     t_roof = max(F / P_mfma, Q / BW) with F = 2 x 768 x 256 x (2 rows_c + 3 rows_n).
     bound: the encoder's arithmetic intensity against the ridge point P_mfma / BW."""
-    peak_tf = BF16_PEAK_TFLOPS if precision == "bf16" else FP32_PEAK_TFLOPS
+    peak_tf = PEAK_TFLOPS.get(precision, FP32_PEAK_TFLOPS)
     enc_bytes = int((rows_c + rows_n) * 768 * 4)
     enc_flops = 2 * 768 * 256 * (rows_c + 2 * rows_n)
     wg_flops = 2 * 768 * 256 * (rows_c + rows_n)
     step_flops = 2 * 768 * 256 * (2 * rows_c + 3 * rows_n)
-    names = KNAMES[precision]
+    names = dict(KNAMES[precision], tail=tail_name)
     kern = {}
     for k, (m, n) in sorted(ktimes.items()):
         kern[names.get(k, k)] = {"avg_ms": m, "timed_launches": n}
@@ -488,14 +526,15 @@ def restore(model, step, snap):
     step.refresh_shadow()
 
 
-def parity_block(model, step, view, snap, batch, epoch):
-    """bf16 (the timed mode) vs fp32 (the reference's arithmetic, exact-f32 MFMA) on the first timed
-    batch from the state the timed region started in, with the same counter-RNG draws (same seed
-    and global step): the four loss terms, the student logits and the DACP mask.  The golden
-    replays of tests/test_gpu_bf16_parity.py pin the same comparison against the reference."""
+def parity_block(model, step, view, snap, batch, epoch, precision):
+    """The timed mode (fp16 or bf16 operands) vs fp32 (the reference's arithmetic, exact-f32 MFMA) on
+    the first timed batch from the state the timed region started in, with the same counter-RNG
+    draws (same seed and global step): the four loss terms, the student logits and the DACP mask.
+    The golden replays of tests/test_gpu_throughput_parity.py pin the same comparison against the
+    reference."""
     c, nb = batch
     out = {}
-    for prec in ("bf16", "fp32"):
+    for prec in (precision, "fp32"):
         restore(model, step, snap)
         s = PKG.DADStep(model, view, precision=prec, rng="counter", seed=step.seed)
         s.load_state_dict(snap[2])
@@ -507,35 +546,38 @@ def parity_block(model, step, view, snap, batch, epoch):
                      "z_clean": o["z_clean"].detach().cpu().double(), "z_strong": o["z_strong"].detach().cpu().double(),
                      "mask": o["mask"].detach().cpu()}
     restore(model, step, snap)
-    b, f = out["bf16"], out["fp32"]
+    b, f = out[precision], out["fp32"]
     rel = lambda a, r: float((a - r).abs().max() / max(1e-6, float(r.abs().max())))
-    return {"batch": "first timed batch", "reference_mode": "fp32 (exact-f32 MFMA), same counter-RNG draws",
-            "losses_bf16": b["losses"], "losses_fp32": f["losses"],
+    return {"batch": "first timed batch", "mode": precision,
+            "reference_mode": "fp32 (exact-f32 MFMA), same counter-RNG draws",
+            "losses_" + precision: b["losses"], "losses_fp32": f["losses"],
             "loss_err": {k: abs(b["losses"][k] - f["losses"][k]) / max(1.0, abs(f["losses"][k])) for k in f["losses"]},
             "z_clean_err": rel(b["z_clean"], f["z_clean"]), "z_strong_err": rel(b["z_strong"], f["z_strong"]),
             "mask_equal": bool(torch.equal(b["mask"], f["mask"])), "mask_sum": float(f["mask"].sum()),
-            "err_definition": "losses |bf16 - fp32| / max(1, |fp32|); logits max|bf16 - fp32| / max|fp32|"}
+            "bound": 1e-4 if precision == "fp16" else None,
+            "err_definition": "losses |x - fp32| / max(1, |fp32|); logits max|x - fp32| / max|fp32|"}
 
 
-def fp32_mode(model, view, data, B, T, args):
-    """The reference's arithmetic (fp32 operands, exact-f32 MFMA) timed over args.fp32_steps steps,
-    with its own per-kernel timing and rooflines (fp32 MFMA peak)."""
-    s32 = PKG.DADStep(model, view, precision="fp32", rng="counter", seed=5)
+def side_mode(model, view, data, B, T, args, precision, n):
+    """Another precision of the same step timed over n steps on the resident batches (eager
+    launches), with its own per-kernel timing and rooflines: fp32 (the reference's arithmetic,
+    exact-f32 MFMA, f32 peak) or bf16 (BASELINE configs[1]'s named dtype, bf16 peak)."""
+    s32 = PKG.DADStep(model, view, precision=precision, rng="counter", seed=5)
     for i in range(3):
         s32.step(data[i % 4][0], data[i % 4][1], args.epoch)
     torch.cuda.synchronize()
-    n = args.fp32_steps
     timer = PKG._lib.KernelTimer(4, n // 4 + 1, kernels=TIMED_KERNELS)
     t1 = time.perf_counter()
     for i in range(n):
         s32.step(data[i % 4][0], data[i % 4][1], args.epoch)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t1) / n
+    enc = timer.stop()          # (one timer at a time: dad_timing_start refuses a second)
     kt = kernel_pass(lambda: s32.step(data[0][0], data[0][1], args.epoch), max(8, n // 2))
-    kt.update(timer.stop())
-    rf, srf, kern = rooflines(kt, B * T, B * T, dt * 1e3, "fp32")
-    return {"value": B / dt, "ms_per_step": dt * 1e3, "steps": n, "dtype": "f32", "roofline": rf,
-            "step_roofline": srf, "kernels": kern}
+    kt.update(enc)
+    rf, srf, kern = rooflines(kt, B * T, B * T, dt * 1e3, precision, tail_kernel(B, B, class_aware(view)))
+    return {"value": B / dt, "ms_per_step": dt * 1e3, "steps": n, "dtype": "f32" if precision == "fp32" else precision,
+            "launch": "eager", "roofline": rf, "step_roofline": srf, "kernels": kern}
 
 
 def _free_port():
@@ -589,7 +631,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--precision", default="fp16", choices=["fp16", "bf16", "fp32"])
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--frames", type=int, default=300)
     ap.add_argument("--epoch", type=int, default=60)
@@ -601,13 +643,14 @@ def main():
     ap.add_argument("--folds", type=int, default=5)
     ap.add_argument("--comm", default="rccl", choices=["rccl", "gloo"],
                     help="gradient all-reduce transport for N > 1 (gloo lets ranks share one GPU)")
-    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--cpu-steps", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--fp32-steps", type=int, default=24, help="also time the FP32 parity mode (N=1)")
+    ap.add_argument("--bf16-steps", type=int, default=48, help="also time the BF16 mode (N=1, fp16 runs)")
     ap.add_argument("--kernel-steps", type=int, default=32,
                     help="steps of the per-kernel timing pass after the timed region (0: none)")
     ap.add_argument("--no-data-path", action="store_true", help="skip the device collate measurement (N=1)")
-    ap.add_argument("--no-parity", action="store_true", help="skip the bf16-vs-fp32 parity block (N=1)")
+    ap.add_argument("--no-parity", action="store_true", help="skip the 16-bit-vs-fp32 parity block (N=1)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -673,12 +716,14 @@ def main():
         # ~100 ms (steady clocks) instead of 5 warm-up steps after model setup.  (The driver's
         # --steps 20 --warmup 5 line had measured the clock ramp: 137 -> 130 -> 124 us per step
         # over consecutive 20-step segments, round 2.)
-        parity = fp32 = data_path = None
-        if rank == 0 and world == 1 and args.precision == "bf16":
+        parity = fp32 = bf16 = data_path = None
+        if rank == 0 and world == 1 and args.precision != "fp32":
             if not args.no_parity:
-                parity = parity_block(model, step, view, snap, data[0], args.epoch)
+                parity = parity_block(model, step, view, snap, data[0], args.epoch, args.precision)
             if args.fp32_steps > 0:
-                fp32 = fp32_mode(model, view, data, B, T, args)
+                fp32 = side_mode(model, view, data, B, T, args, "fp32", args.fp32_steps)
+            if args.precision == "fp16" and args.bf16_steps > 0:
+                bf16 = side_mode(model, view, data, B, T, args, "bf16", args.bf16_steps)
         if rank == 0 and world == 1 and not args.no_data_path:
             data_path = data_path_bench(step, B, T, args.epoch, dev)
         restore(model, step, snap)
@@ -708,7 +753,7 @@ def main():
         total_utts = B * world * args.steps
         rows_per_step = 2 * B * T
     if args.mixed:
-        parity = fp32 = data_path = None
+        parity = fp32 = bf16 = data_path = None
         losses = {k: float(v) for k, v in step.losses().items()}
         nbc = step._last_shape
         msum = float(step.outputs(*nbc)["msum"])
@@ -740,7 +785,8 @@ def main():
     # per-kernel table: the separate pass, with the timed region's encoder entry
     kt = dict(table)
     kt.update(ktimes)
-    rf, srf, kern = rooflines(kt, rows, rows, ms, args.precision)
+    rf, srf, kern = rooflines(kt, rows, rows, ms, args.precision,
+                              tail_kernel(B, B, True if args.mixed else class_aware(view)))
     kern["source"] = ("encoder: HIP events around it in the timed region (every %d-th step); the other "
                       "kernels: a separate pass of %d steps after it (events at every boundary of every "
                       "2nd step)" % (event_every(args.steps), args.kernel_steps))
@@ -748,6 +794,10 @@ def main():
         "metric": METRIC, "value": value, "unit": "utterances/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": args.precision, "data": "synthetic",
+        "dtype_note": {"fp16": "encoder and weight-gradient GEMMs on fp16 operands (11-bit significand), fp32 "
+                               "accumulation; everything else fp32 (the mode that meets north_star's 1e-4)",
+                       "bf16": "encoder and weight-gradient GEMMs on bf16 operands, fp32 accumulation",
+                       "fp32": "exact-f32 MFMA throughout"}[args.precision],
         "config": {"workload": workload, "flavor": "mixed" if args.mixed else args.flavor, "snr_db": args.snr,
                    "global_batch": B * world, "per_gpu_batch": B, "seq_len": T, "feature_dim": 768,
                    "parallelism": "dp%d" % world},
@@ -761,6 +811,8 @@ def main():
         line["folds"] = folds
     if fp32 is not None:
         line["fp32_mode"] = fp32
+    if bf16 is not None:
+        line["bf16_mode"] = bf16
     if data_path is not None:
         line["data_path"] = data_path
     if world == 1 and not args.no_cpu_baseline:

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define DAD_ABI_VERSION 2
+#define DAD_ABI_VERSION 3
 
 /* error codes (besides hipError_t values) */
 #define DAD_OK 0
@@ -70,11 +70,17 @@ extern "C" {
 #define DAD_T_ECDA_GATE 28    /* [4] */
 #define DAD_T_KL_ON 32
 #define DAD_T_ECDA_ON 33
+#define DAD_T_RANGE 34        /* u32 bits: nonzero once a step's pooled embedding or logit was not finite (FP16:
+                                 an encoder operand beyond +-65504; any mode: non-finite features); sticky: only
+                                 the caller clears it (the buffer starts zero-filled) */
 #define DAD_T_TAU_HAT 40      /* [4] batch quantile thresholds */
 /* after the header (noisy batch, Bn rows): score[Bn], pred[Bn] (as float), mask[Bn], q[Bn][4] */
 #define DAD_TAIL_FLOATS(Bn) (DAD_TAIL_HDR + (Bn) * (3 + DAD_NUM_CLASSES))
 
-enum dad_precision { DAD_PREC_FP32 = 0, DAD_PREC_BF16 = 1 };
+/* FP32: exact-f32 MFMA (the reference's arithmetic, parity mode).  FP16 / BF16: the encoder and
+ * weight-gradient GEMMs on 16-bit operands (fp16: 11-bit significand, the throughput mode that
+ * meets the 1e-4 loss/logit bound; bf16: 8-bit) with fp32 accumulation; everything else fp32. */
+enum dad_precision { DAD_PREC_FP32 = 0, DAD_PREC_BF16 = 1, DAD_PREC_FP16 = 2 };
 enum dad_rng_mode { DAD_RNG_EXPLICIT = 0, DAD_RNG_COUNTER = 1 };
 
 /* Every scalar the step reads from the reference's config module, resolved by the host
@@ -148,8 +154,8 @@ typedef struct dad_state {
   float* exp_avg;               /* [DAD_NPARAM] Adam m */
   float* exp_avg_sq;            /* [DAD_NPARAM] Adam v */
   float* grad;                  /* [DAD_GRAD_FLOATS] grads (+extras); the DP all-reduce buffer */
-  uint16_t* w1bf_student;       /* [256*768] bf16 shadow of student W1 */
-  uint16_t* w1bf_teacher;       /* [256*768] bf16 shadow of teacher W1 */
+  uint16_t* w1bf_student;       /* [256*768] 16-bit shadow of student W1 (fp16 in FP16 steps, else bf16) */
+  uint16_t* w1bf_teacher;       /* [256*768] 16-bit shadow of teacher W1 */
   float* dacp;                  /* [DAD_DACP_FLOATS] */
   float* tail;                  /* [DAD_TAIL_FLOATS(Bn)] per-step outputs */
   float* emb;                   /* [B+2*Bn][256] e_clean [B], e_teacher [Bn], e_strong [Bn] */
@@ -159,12 +165,10 @@ typedef struct dad_state {
 
 /* --- sizing ------------------------------------------------------------------------ */
 size_t dad_param_count(void);
-/* The step workspace must be zero-filled when it is first allocated: it holds the BF16 encoder's
-   in-launch pooling arrival counters, which every completed step returns to zero (reuse across
-   steps and geometries needs no clearing). */
+/* Step workspace bytes for cfg's geometry and precision (no initialisation needed). */
 int dad_workspace_bytes(const dad_config* cfg, size_t* bytes);
 const char* dad_error_string(int code);
-/* Host-only planning of the BF16 encoder grid (no device call): teacher / student workgroups
+/* Host-only planning of the 16-bit (FP16/BF16) encoder grid (no device call): teacher / student workgroups
  * for a device of `cus` compute units and the most 32-row jobs any workgroup's range holds
  * (always <= 256, the kernel's per-workgroup table).  Diagnostics and tests. */
 int dad_encoder_ws_plan(const dad_config* cfg, int cus, int* nt, int* ns, int* max_jobs);
@@ -174,7 +178,7 @@ int dad_encoder_ws_plan(const dad_config* cfg, int cus, int* nt, int* ns, int* m
  *   train_step (I/train.py:397-471) + backward + clip_grad_norm_ + Adam.step + update_teacher_ema.
  * dad_step_compute: encoder passes, losses, DACP mask, analytic backward -> state->grad.
  * dad_step_apply:   global-norm clip, Adam (L2 decay), teacher EMA, DACP state commit,
- *                   bf16 shadow refresh.  A DP caller all-reduces state->grad in between.
+ *                   16-bit W1 shadow refresh.  A DP caller all-reduces state->grad in between.
  * dad_step = compute + apply (single GPU). */
 int dad_step_compute(const dad_config* cfg, const dad_batch* batch, const dad_state* st,
                      void* workspace, void* stream);
@@ -197,9 +201,10 @@ int dad_step_commit(const dad_config* cfg, const dad_state* st, void* workspace,
 
 /* DACPManager.update_class_quality_scores_epoch (I/utils.py:430-447) */
 int dad_epoch_end(const dad_config* cfg, const dad_state* st, void* stream);
-/* refresh the bf16 shadows of W1 after the caller changed student/teacher params
- * (e.g. load_complete_pretrained_weights, I/model.py:143-198) */
-int dad_refresh_shadow(const dad_state* st, void* stream);
+/* refresh the 16-bit shadows of W1 after the caller changed student/teacher params
+ * (e.g. load_complete_pretrained_weights, I/model.py:143-198): fp16 for precision
+ * DAD_PREC_FP16, bf16 otherwise (the format the next step of that precision reads) */
+int dad_refresh_shadow(const dad_state* st, int precision, void* stream);
 
 /* SSRLModel.update_teacher_ema (I/model.py:211-223) over flat [W1|b1|W2|b2] vectors:
  * teacher = teacher*ema_m + student*ema_one_m (n floats) */
@@ -323,16 +328,15 @@ int dad_rng_draws(const dad_config* cfg, int which, uint64_t first, size_t n, fl
  * on the caller's stream, up to max_steps timed steps; all events are created here, so a timed
  * region only records them.  dad_timing_stop: waits for the recorded events and returns, per
  * kernel k < n (DAD_TK_*), the summed milliseconds ms_sum[k] over count[k] timed steps, then
- * frees the events and turns timing off.  The FP32 step's dW1 GEMM runs on a side stream
- * (DAD_TK_SIDE); its DAD_TK_WGRAD interval is the join + dad_wsum. */
-#define DAD_TK_ENCODE 0       /* dad_encode_ws / dad_encode_f32 */
+ * frees the events and turns timing off.  dad_timing_start fails (DAD_E_ARG) while a timing
+ * session is active: stop the first before starting another. */
+#define DAD_TK_ENCODE 0       /* dad_encode_ws[_f16] / dad_encode_f32 */
 #define DAD_TK_POOL 1         /* dad_pool */
-#define DAD_TK_TAIL 2         /* dad_tail_ecda (or dad_tail + dad_ecda) */
-#define DAD_TK_WGRAD 3        /* dad_wgrad_direct (BF16) / join + dad_wsum (FP32) */
-#define DAD_TK_REDUCE 4       /* dad_reduce (BF16) */
+#define DAD_TK_TAIL 2         /* dad_tail_ecda_w / dad_tail_ecda (or dad_tail + dad_ecda) */
+#define DAD_TK_WGRAD 3        /* dad_wgrad_direct (FP16/BF16) / dad_wgrad_f32 (FP32) */
+#define DAD_TK_REDUCE 4       /* dad_reduce_w (FP16/BF16) / dad_reduce (FP32) */
 #define DAD_TK_OPTIM 5        /* dad_optim */
-#define DAD_TK_SIDE 6         /* dad_wgrad_f32 on the side stream (FP32) */
-#define DAD_TK_KERNELS 7
+#define DAD_TK_KERNELS 6
 int dad_timing_start(int every, int max_steps);
 /* dad_timing_kernels(mask): after dad_timing_start, record only the boundaries of the kernels
  * whose bit (1 << DAD_TK_*) is set (default: all).  Each recorded event costs the stream a few

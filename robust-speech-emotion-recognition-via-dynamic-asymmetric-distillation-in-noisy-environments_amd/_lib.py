@@ -16,14 +16,14 @@ DAD_GRAD_FLOATS = DAD_NPARAM + DAD_GRAD_EXTRA
 DAD_DACP_FLOATS = 20
 DAD_TAIL_HDR = 64
 DAD_MAX_BATCH = 1024
-PREC_FP32, PREC_BF16 = 0, 1
+PREC_FP32, PREC_BF16, PREC_FP16 = 0, 1, 2
 DRAW_WEAK, DRAW_STRONG, DRAW_FEAT_KEEP, DRAW_TSTART, DRAW_KEEP1, DRAW_KEEP2 = range(1, 7)
 RNG_EXPLICIT, RNG_COUNTER = 0, 1
 
 # tail header slots (dad.h DAD_T_*)
 T_TOTAL, T_CE, T_KL, T_ECDA, T_SCL, T_MSUM, T_CLIPNORM, T_CLIPCOEF = range(8)
 T_W, T_TAU_BEFORE, T_TAU_AFTER, T_FLOORED, T_ECDA_TERM, T_ECDA_GATE = 8, 12, 16, 20, 24, 28
-T_KL_ON, T_ECDA_ON, T_TAU_HAT = 32, 33, 40
+T_KL_ON, T_ECDA_ON, T_RANGE, T_TAU_HAT = 32, 33, 34, 40
 
 
 def tail_floats(bn):
@@ -85,7 +85,7 @@ EXPORTS = {
     "dad_step_commit": (ctypes.c_int, [ctypes.POINTER(DadConfig), ctypes.POINTER(DadState),
                                        ctypes.c_void_p, ctypes.c_void_p]),
     "dad_epoch_end": (ctypes.c_int, [ctypes.POINTER(DadConfig), ctypes.POINTER(DadState), ctypes.c_void_p]),
-    "dad_refresh_shadow": (ctypes.c_int, [ctypes.POINTER(DadState), ctypes.c_void_p]),
+    "dad_refresh_shadow": (ctypes.c_int, [ctypes.POINTER(DadState), ctypes.c_int, ctypes.c_void_p]),
     "dad_teacher_ema": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_float,
                                        ctypes.c_float, ctypes.c_void_p]),
     "dad_encoder_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int, ctypes.c_int]),
@@ -132,7 +132,7 @@ EXPORTS = {
 }
 
 # per-kernel timing slots (dad.h DAD_TK_*)
-TK_NAMES = ["encode", "pool", "tail", "wgrad", "reduce", "optim", "side"]
+TK_NAMES = ["encode", "pool", "tail", "wgrad", "reduce", "optim"]
 
 _LIB = None
 
@@ -175,7 +175,8 @@ class KernelTimer:
     every `every`-th step while active.  `stop()` returns {name: (mean_ms, n_steps)}."""
 
     def __init__(self, every=4, max_steps=256, kernels=None):
-        """kernels: names (TK_NAMES) to time, default all; each recorded event costs stream time."""
+        """kernels: names (TK_NAMES) to time, default all; each recorded event costs stream time.
+        One timer at a time: dad_timing_start refuses (DadError) while another is active."""
         check(lib().dad_timing_start(int(every), int(max_steps)), "dad_timing_start")
         if kernels is not None:
             mask = 0

@@ -24,7 +24,7 @@ inline int check_cfg(const dad_config* c) {
   if (c->B < 1 || c->B > DAD_MAX_BATCH || c->T < 1) return DAD_E_SHAPE;
   if (c->Bn < 0 || c->Bn > DAD_MAX_BATCH || c->Tn < 0) return DAD_E_SHAPE;
   if (!c->warmup && (c->Bn < 1 || c->Tn < 1)) return DAD_E_SHAPE;
-  if (c->precision != DAD_PREC_FP32 && c->precision != DAD_PREC_BF16) return DAD_E_ARG;
+  if (c->precision != DAD_PREC_FP32 && !dad_prec16(c->precision)) return DAD_E_ARG;
   if (c->rng_mode != DAD_RNG_EXPLICIT && c->rng_mode != DAD_RNG_COUNTER) return DAD_E_ARG;
   if (c->dp_world < 1) return DAD_E_ARG;
   return DAD_OK;
@@ -35,7 +35,7 @@ inline DadGeom geom_of(const dad_config* c) { return dad_geom(c->B, c->T, c->Bn,
 inline int splits_of(const dad_config* c) {
   const DadGeom g = geom_of(c);
   if (c->splits <= 0) return dad_auto_splits(g, c->precision, c->warmup);
-  if (c->precision != DAD_PREC_BF16) return c->splits;
+  if (!dad_prec16(c->precision)) return c->splits;
   // dad_wgrad_direct holds at most WGD_MAXU slabs' utterances per split
   const int total = g.Bc * g.ncc + (c->warmup ? 0 : g.Bn * g.ncn);
   return std::max(c->splits, dad_wgd_min_splits(total));
@@ -68,68 +68,13 @@ inline Keys keys_of(const dad_config* c) {
   return k;
 }
 
-// Second stream per device for work that only depends on the forward: the
-// loss-independent factor S_u of the weight gradient runs there while pool/tail/ECDA
-// (a handful of workgroups) run on the caller's stream.  Fork/join by events, so the
-// step stays enqueue-only and graph-capturable.
-struct SideStream {
-  hipStream_t s = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-  int cus = 0;   // compute units of the device
-};
-// CUs the side-stream GEMM leaves free, so the caller-stream kernels that run meanwhile
-// (pool, the one-workgroup tail, ECDA's per-class workgroups) are dispatched at once
-// instead of waiting for a register file to drain
-constexpr int kReservedCUs = 32;   // 4 per XCD (workgroups are spread round-robin over the 8 XCDs)
-constexpr int kMaxDevices = 64;
-SideStream g_side[kMaxDevices];
-std::mutex g_side_mu;
-
-int side_stream(SideStream** out) {
-  int dev = 0;
-  DAD_TRY(hipGetDevice(&dev));
-  if (dev < 0 || dev >= kMaxDevices) return DAD_E_ARG;
-  std::lock_guard<std::mutex> lk(g_side_mu);
-  SideStream& ss = g_side[dev];
-  if (!ss.s) {
-    DAD_TRY(hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking));
-    DAD_TRY(hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming));
-    DAD_TRY(hipEventCreateWithFlags(&ss.join, hipEventDisableTiming));
-    DAD_TRY(hipDeviceGetAttribute(&ss.cus, hipDeviceAttributeMultiprocessorCount, dev));
-  }
-  *out = &ss;
-  return DAD_OK;
-}
-
-// BF16 weight-gradient strategy: the direct GEMM after the losses (default), or the factorised
-// S_u GEMM on the side stream (DAD_WGRAD=su, read per step).  Measured on MI355X the
-// side-stream fork/join latency (~7 + ~12 us) cancels the overlap, so direct is the default.
-bool wgrad_direct() {
-  const char* e = getenv("DAD_WGRAD");
-  return !(e && strcmp(e, "su") == 0);
-}
-// FP32: likewise the direct split-K GEMM after the losses (default), or S_u per utterance on
-// the side stream (DAD_WGRAD_F32=su).  S_u costs 98 MB written and read again and its 768
-// per-utterance tiles do not divide evenly over the CUs: measured 254 + 15 us against ~130 +
-// 8 us for the direct form, which only loses the ~40 us of pool/tail overlap.
-bool wgrad_f32_direct() {
-  const char* e = getenv("DAD_WGRAD_F32");
-  return !(e && strcmp(e, "su") == 0);
-}
-
-// DAD_POOL_FUSE=1: the BF16 encoder pools the slab partials in its own launch (last arriver per
-// utterance) instead of a dad_pool launch.  Off by default: measured 2.7 us per step slower
-// (encode_ws.hip, ws_pool_arrive).  Read once.
-bool pool_fuse_on() {
-  static const bool on = [] { const char* e = getenv("DAD_POOL_FUSE"); return e && strcmp(e, "1") == 0; }();
-  return on;
-}
-
 // DAD_TAIL_W=0 selects the general tail + ECDA launch for every batch (A/B runs; read once)
 bool tail_w_on() {
   static const bool on = [] { const char* e = getenv("DAD_TAIL_W"); return !(e && strcmp(e, "0") == 0); }();
   return on;
 }
+
+constexpr int kMaxDevices = 64;
 
 int device_cus(int* out) {
   static int cache[kMaxDevices];
@@ -159,13 +104,6 @@ WsWeights ws_weights() {
   }();
   return w;
 }
-// DAD_WS_TABLE=1 turns the student range table on (off by default: at B=64, T=300 it brings the
-// modelled slowest student range from 18.6 to 17.5 clean-sub-slab units, but the launch measured
-// unchanged (62.7 vs 63.0 us) in A/B runs; read once per process)
-bool ws_table_on() {
-  static const bool on = [] { const char* e = getenv("DAD_WS_TABLE"); return e && strcmp(e, "1") == 0; }();
-  return on;
-}
 // the largest job range of the teacher (or student) workgroups of a split, by the kernel's own
 // range function (dad_ws_job_range)
 int ws_max_range(const DadGeom& G, int Bn, int nt, int ns, float wstrong, bool teacher_side) {
@@ -182,7 +120,7 @@ int ws_max_range(const DadGeom& G, int Bn, int nt, int ns, float wstrong, bool t
 }
 // Returns DAD_E_SHAPE if no split keeps every range within DAD_ENC_WS_MAXJ jobs (cannot happen
 // for B <= DAD_MAX_BATCH: one job per workgroup always fits).
-int ws_split(const DadGeom& G, int Bn, int cus, int& nt, int& ns) {
+int ws_split_uncached(const DadGeom& G, int Bn, int cus, int& nt, int& ns) {
   const float kWsWeak = ws_weights().weak, kWsStrong = ws_weights().strong;
   const int Jt = Bn * G.ncn, Jc = G.Bc * G.ncc, Js = Jt;
   if (Jt == 0) {
@@ -209,67 +147,29 @@ int ws_split(const DadGeom& G, int Bn, int cus, int& nt, int& ns) {
   }
   return DAD_OK;
 }
-
-// Student ranges of the W-stationary encoder by a min-max assignment: every student workgroup
-// takes a contiguous run of strong jobs, then a contiguous run of clean jobs, filled up to a
-// common cost bound T (jobs priced by live 16-row sub-slabs: clean 1, strong wstrong); the
-// smallest T that places every job in ns workgroups (bisection).  The clean jobs (cost 2 or 1)
-// fill what the coarser strong jobs (2 wstrong) leave, so the slowest range sits about half a
-// clean job above the mean instead of up to a strong job (ws_split's contiguous ranges).
-// Cached per geometry: computed once, then copied into each launch's arguments.
-bool ws_student_table(const DadGeom& G, int Bn, int ns, float wstrong, DadEncodeArgs& ea) {
-  const int Jc = G.Bc * G.ncc, Js = Bn * G.ncn;
-  ea.ws_tab_n = 0;
-  if (ns <= 0 || ns > DAD_WS_TAB || Jc + Js == 0 || Jc > 65535 || Js > 65535) return false;
-  struct Key { int Bc, Tc, Bn, Tn, ns; float w; };
-  static thread_local Key key{-1, -1, -1, -1, -1, 0.0f};
-  static thread_local uint16_t tab[DAD_WS_TAB][4];
-  const Key k{G.Bc, G.Tc, Bn, G.Tn, ns, wstrong};
-  if (!(key.Bc == k.Bc && key.Tc == k.Tc && key.Bn == k.Bn && key.Tn == k.Tn && key.ns == k.ns && key.w == k.w)) {
-    auto live = [](int c, int T) { return (c * DAD_SLAB + 16 < T) ? 2 : 1; };   // live sub-slabs of slab c
-    auto cs = [&](int j) { return wstrong * (float)live(j % G.ncn, G.Tn); };
-    auto cc = [&](int j) { return (float)live(j % G.ncc, G.Tc); };
-    // greedy fill to T; returns the workgroups used (ns + 1 when T is too small)
-    auto fill = [&](float T, bool write) {
-      int sp = 0, cp = 0, k = 0;
-      for (; k < ns && (sp < Js || cp < Jc); ++k) {
-        float cost = 0.0f;
-        const int s0 = sp, c0 = cp;
-        while (sp < Js && sp - s0 < DAD_ENC_WS_MAXJ - 2 && cost + cs(sp) <= T) cost += cs(sp++);
-        while (cp < Jc && (sp - s0) + (cp - c0) < DAD_ENC_WS_MAXJ - 2 && cost + cc(cp) <= T) cost += cc(cp++);
-        if (sp == s0 && cp == c0) return ns + 1;   // a single job above T
-        if (write) { tab[k][0] = (uint16_t)s0; tab[k][1] = (uint16_t)sp; tab[k][2] = (uint16_t)c0; tab[k][3] = (uint16_t)cp; }
-      }
-      if (sp < Js || cp < Jc) return ns + 1;
-      if (write)
-        for (int r = k; r < ns; ++r) { tab[r][0] = tab[r][1] = (uint16_t)Js; tab[r][2] = tab[r][3] = (uint16_t)Jc; }
-      return k;
-    };
-    float tot = 0.0f, jmax = 0.0f;
-    for (int j = 0; j < Js; ++j) { tot += cs(j); jmax = std::max(jmax, cs(j)); }
-    for (int j = 0; j < Jc; ++j) { tot += cc(j); jmax = std::max(jmax, cc(j)); }
-    float lo = tot / (float)ns, hi = lo + 2.0f * jmax + 1.0f;
-    if (fill(hi, false) > ns) return false;
-    for (int it = 0; it < 24; ++it) {
-      const float mid = 0.5f * (lo + hi);
-      if (fill(mid, false) <= ns) hi = mid; else lo = mid;
-    }
-    fill(hi, true);
-    key = k;
+// The split is a pure function of (geometry, CU count) for the process's fixed weights: cached
+// per thread for the last key, so a steady-state step runs no range evaluations on the host.
+int ws_split(const DadGeom& G, int Bn, int cus, int& nt, int& ns) {
+  struct Entry { int Bc, Tc, Bn, Tn, cus, rc, nt, ns; };
+  static thread_local Entry last{-1, -1, -1, -1, -1, 0, 0, 0};
+  if (!(last.Bc == G.Bc && last.Tc == G.Tc && last.Bn == Bn && last.Tn == G.Tn && last.cus == cus)) {
+    Entry e{G.Bc, G.Tc, Bn, G.Tn, cus, 0, 0, 0};
+    e.rc = ws_split_uncached(G, Bn, cus, e.nt, e.ns);
+    last = e;
   }
-  memcpy(ea.ws_tab, tab, sizeof(uint16_t) * 4 * (size_t)ns);
-  ea.ws_tab_n = ns;
-  return true;
+  nt = last.nt;
+  ns = last.ns;
+  return last.rc;
 }
 
 // Per-kernel timing of the fused step (dad_timing_start / dad_timing_stop): every `every`-th
 // step (counted at its encoder call) records hip events at the kernel boundaries of the
-// caller's stream (and around the side-stream GEMM of the FP32 step).  Events are created up
-// front by dad_timing_start, so a timed region only records them.  Not for graph capture.
-enum { TK_E0, TK_E1, TK_POOL, TK_TAIL, TK_WGRAD, TK_RED, TK_OPT0, TK_OPT1, TK_S0, TK_S1, TK_N };
+// caller's stream.  Events are created up front by dad_timing_start, so a timed region only
+// records them.  Not for graph capture.
+enum { TK_E0, TK_E1, TK_POOL, TK_TAIL, TK_WGRAD, TK_RED, TK_OPT0, TK_OPT1, TK_N };
 // (event-pair points of each DAD_TK_* kernel: dad_timing_stop's pairs)
 const int kTkPairs[DAD_TK_KERNELS][2] = {{TK_E0, TK_E1}, {TK_E1, TK_POOL}, {TK_POOL, TK_TAIL}, {TK_TAIL, TK_WGRAD},
-                                         {TK_WGRAD, TK_RED}, {TK_OPT0, TK_OPT1}, {TK_S0, TK_S1}};
+                                         {TK_WGRAD, TK_RED}, {TK_OPT0, TK_OPT1}};
 struct Timing {
   unsigned points = ~0u;               // TK points recorded (dad_timing_kernels)
   int every = 0;
@@ -306,6 +206,7 @@ extern "C" {
 int dad_timing_start(int every, int max_steps) {
   std::lock_guard<std::mutex> lk(g_tk_mu);
   if (every < 1 || max_steps < 1) return DAD_E_ARG;
+  if (g_tk.nset > 0) return DAD_E_ARG;   // a session is active: dad_timing_stop it first
   for (hipEvent_t e : g_tk.ev) (void)hipEventDestroy(e);
   g_tk = Timing();
   g_tk.ev.assign((size_t)max_steps * TK_N, nullptr);
@@ -419,10 +320,55 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   float* ecda_scratch = ws_ptr<float>(workspace, L.ecda);
   float* gzb = ws_ptr<float>(workspace, L.gzb);
   uint32_t* eflag = ws_ptr<uint32_t>(workspace, L.eflag);
-  __bf16* xs_bf16 = ws_ptr<__bf16>(workspace, L.xs_bf16);
-  const bool bf16 = cfg->precision == DAD_PREC_BF16;
+  uint16_t* xs16 = ws_ptr<uint16_t>(workspace, L.xs16);
+  const bool h16 = dad_prec16(cfg->precision);
+  const bool f16 = cfg->precision == DAD_PREC_FP16;
 
-  // pooling arguments (dad_pool, or the BF16 encoder's in-launch pooling)
+  // 1. fused augmentation + encoder GEMMs + pooling partials
+  DadEncodeArgs ea;
+  memset(&ea, 0, sizeof(ea));
+  ea.g = G; ea.warmup = cfg->warmup;
+  ea.mask_len = cfg->mask_len; ea.start_hi = cfg->start_hi;
+  ea.xc = bt->xc; ea.mc = bt->mc; ea.xn = bt->xn; ea.mn = bt->mn; ea.src = src;
+  ea.w1_student = st->student + DAD_OFF_W1; ea.b1_student = st->student + DAD_OFF_B1;
+  ea.w1_teacher = st->teacher + DAD_OFF_W1; ea.b1_teacher = st->teacher + DAD_OFF_B1;
+  ea.w1h_student = st->w1bf_student;
+  ea.w1h_teacher = st->w1bf_teacher;
+  if (explicit_rng) { ea.nw = bt->nw; ea.ns = bt->ns; ea.u = bt->u; ea.start = bt->start; }
+  ea.key_weak = k.weak; ea.key_strong = k.strong; ea.key_feat = k.feat; ea.key_tstart = k.tstart;
+  ea.weak_std = cfg->weak_std; ea.strong_std = cfg->strong_std; ea.feat_p = cfg->feat_p;
+  ea.part_sum = part_sum; ea.part_cnt = part_cnt; ea.bits = bits; ea.xs16 = xs16;
+  const int nwaves = G.Bc * G.ncc + Bn * G.ncn;
+  const dim3 egrid((nwaves + 3) / 4);
+  if (do_encode) {
+    tk_begin();
+    tk_mark(TK_E0, stream);
+    if (h16) {
+      int cus = 0;
+      const int rc = device_cus(&cus);
+      if (rc) return rc;
+      const int rs = ws_split(G, Bn, cus, ea.ws_nt, ea.ws_ns);
+      if (rs) return rs;
+      ea.ws_wstrong = ws_weights().strong;
+      if (ea.ws_nt + ea.ws_ns > 0) {
+        const dim3 grid(ea.ws_nt + ea.ws_ns), block(DAD_ENC_WS_THREADS);
+        if (f16) {
+          if (explicit_rng) hipLaunchKernelGGL(dad_encode_ws_f16_explicit, grid, block, 0, stream, ea);
+          else hipLaunchKernelGGL(dad_encode_ws_f16, grid, block, 0, stream, ea);
+        } else {
+          if (explicit_rng) hipLaunchKernelGGL(dad_encode_ws_explicit, grid, block, 0, stream, ea);
+          else hipLaunchKernelGGL(dad_encode_ws, grid, block, 0, stream, ea);
+        }
+      }
+    } else {
+      hipLaunchKernelGGL(dad_encode_f32, egrid, dim3(DAD_ENC_F32_THREADS), 0, stream, ea);
+    }
+    DAD_TRY(hipGetLastError());
+    tk_mark(TK_E1, stream);
+  }
+  if (!do_backward) return DAD_OK;
+
+  // 2. pooled embeddings + classifier logits
   DadPoolArgs pa;
   memset(&pa, 0, sizeof(pa));
   pa.g = G; pa.warmup = cfg->warmup;
@@ -434,99 +380,12 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   pa.emb = st->emb; pa.vlen = vlen; pa.logits = st->logits;
   pa.part_cnt = part_cnt; pa.cnt_tot = cnt_tot;
   pa.eflag = eflag; pa.tail_terms = st->tail + DAD_T_ECDA_TERM;
-  // (split calls: the encode call pooled, so the backward call launches no dad_pool)
-  const bool pool_fused = bf16 && pool_fuse_on();
-
-  // 1. fused augmentation + encoder GEMMs + pooling partials
-  DadEncodeArgs ea;
-  memset(&ea, 0, sizeof(ea));
-  ea.g = G; ea.warmup = cfg->warmup;
-  ea.mask_len = cfg->mask_len; ea.start_hi = cfg->start_hi;
-  ea.xc = bt->xc; ea.mc = bt->mc; ea.xn = bt->xn; ea.mn = bt->mn; ea.src = src;
-  ea.w1_student = st->student + DAD_OFF_W1; ea.b1_student = st->student + DAD_OFF_B1;
-  ea.w1_teacher = st->teacher + DAD_OFF_W1; ea.b1_teacher = st->teacher + DAD_OFF_B1;
-  ea.w1bf_student = reinterpret_cast<const __bf16*>(st->w1bf_student);
-  ea.w1bf_teacher = reinterpret_cast<const __bf16*>(st->w1bf_teacher);
-  if (explicit_rng) { ea.nw = bt->nw; ea.ns = bt->ns; ea.u = bt->u; ea.start = bt->start; }
-  ea.key_weak = k.weak; ea.key_strong = k.strong; ea.key_feat = k.feat; ea.key_tstart = k.tstart;
-  ea.weak_std = cfg->weak_std; ea.strong_std = cfg->strong_std; ea.feat_p = cfg->feat_p;
-  ea.part_sum = part_sum; ea.part_cnt = part_cnt; ea.bits = bits; ea.xs_bf16 = xs_bf16;
-  if (pool_fused) { ea.pool = pa; ea.pool_cnt = ws_ptr<uint32_t>(workspace, L.pool_cnt); }
-  const int nwaves = G.Bc * G.ncc + Bn * G.ncn;
-  const dim3 egrid((nwaves + 3) / 4);
-  if (do_encode) {
-    tk_begin();
-    tk_mark(TK_E0, stream);
-    if (bf16) {
-      int cus = 0;
-      const int rc = device_cus(&cus);
-      if (rc) return rc;
-      const int rs = ws_split(G, Bn, cus, ea.ws_nt, ea.ws_ns);
-      if (rs) return rs;
-      ea.ws_wstrong = ws_weights().strong;
-      if (ws_table_on()) ws_student_table(G, Bn, ea.ws_ns, ea.ws_wstrong, ea);
-      if (ea.ws_nt + ea.ws_ns > 0) {
-        if (explicit_rng) hipLaunchKernelGGL(dad_encode_ws_explicit, dim3(ea.ws_nt + ea.ws_ns), dim3(DAD_ENC_WS_THREADS), 0,
-                                             stream, ea);
-        else hipLaunchKernelGGL(dad_encode_ws, dim3(ea.ws_nt + ea.ws_ns), dim3(DAD_ENC_WS_THREADS), 0, stream, ea);
-      }
-    } else {
-      hipLaunchKernelGGL(dad_encode_f32, egrid, dim3(DAD_ENC_F32_THREADS), 0, stream, ea);
-    }
-    DAD_TRY(hipGetLastError());
-    tk_mark(TK_E1, stream);
-  }
-  if (!do_backward) return DAD_OK;
-
-  // 2. The loss-independent factor of dW1 on the side stream, S_u = bits_u^T X_u per
-  //    utterance (clean rows, then the strong-augmented noisy rows; BF16: the encoder's bf16
-  //    copies, S_u stored in bf16), concurrent with 3-5, for FP32 and for BF16 with DAD_WGRAD=su.
-  //    BF16 default: one direct GEMM after ECDA (6) with dL/de folded into its A operand.
-  const int nutt = G.Bc + Bn;
-  float* sbuf = ws_ptr<float>(workspace, L.sbuf);
-  DadWgradArgs wa;
-  memset(&wa, 0, sizeof(wa));
-  wa.g = G; wa.warmup = cfg->warmup;
-  wa.mask_len = cfg->mask_len; wa.start_hi = cfg->start_hi;
-  wa.xc = bt->xc; wa.xn = bt->xn; wa.src = src;
-  if (explicit_rng) { wa.ns = bt->ns; wa.u = bt->u; wa.start = bt->start; }
-  wa.key_strong = k.strong; wa.key_feat = k.feat; wa.key_tstart = k.tstart;
-  wa.strong_std = cfg->strong_std; wa.feat_p = cfg->feat_p;
-  wa.bits = bits; wa.ge = ge; wa.vlen = vlen; wa.xs_bf16 = xs_bf16;
-  SideStream* side = nullptr;
-  const bool factorised = bf16 ? !wgrad_direct() : !wgrad_f32_direct();
-  if (factorised) {
-    const int rc = side_stream(&side);
-    if (rc) return rc;
-    wa.splits = nutt; wa.per_utt = 1; wa.wpart = sbuf;
-    DAD_TRY(hipEventRecord(side->fork, stream));
-    DAD_TRY(hipStreamWaitEvent(side->s, side->fork, 0));
-    tk_mark(TK_S0, side->s);
-    if (bf16) {
-      wa.su = reinterpret_cast<__bf16*>(sbuf);
-      wa.ntiles = WGD_NDB * nutt;
-      const int sgrid = std::max(1, std::min(wa.ntiles, side->cus - kReservedCUs));
-      hipLaunchKernelGGL(dad_wgrad_su, dim3(sgrid), dim3(WGD_THREADS), 0, side->s, wa);
-    } else {
-      wa.ntiles = 6 * nutt;
-      const int sgrid = std::max(1, std::min(wa.ntiles, side->cus - kReservedCUs));
-      DadReduceArgs none;
-      memset(&none, 0, sizeof(none));
-      hipLaunchKernelGGL(dad_wgrad_f32, dim3(sgrid), dim3(DAD_WGRAD_THREADS), 0, side->s, wa, none);
-    }
-    DAD_TRY(hipGetLastError());
-    tk_mark(TK_S1, side->s);
-    DAD_TRY(hipEventRecord(side->join, side->s));
-  }
-
-  // 3. pooled embeddings + classifier logits (BF16: pooled inside the encoder launch)
-  if (!pool_fused) {
-    hipLaunchKernelGGL(dad_pool, dim3(G.Bc + 2 * Bn), dim3(DAD_POOL_THREADS), 0, stream, pa);
-    DAD_TRY(hipGetLastError());
-  }
+  pa.range_flag = reinterpret_cast<uint32_t*>(st->tail + DAD_T_RANGE);
+  hipLaunchKernelGGL(dad_pool, dim3(G.Bc + 2 * Bn), dim3(DAD_POOL_THREADS), 0, stream, pa);
+  DAD_TRY(hipGetLastError());
   tk_mark(TK_POOL, stream);
 
-  // 4. losses, DACP mask, analytic backward to dL/de and the classifier grads
+  // 3. losses, DACP mask, analytic backward to dL/de and the classifier grads
   DadTailArgs ta;
   memset(&ta, 0, sizeof(ta));
   ta.cfg = *cfg; ta.yc = bt->yc; ta.logits = st->logits; ta.emb = st->emb; ta.student = st->student;
@@ -534,7 +393,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   ta.key_drop1 = k.drop1; ta.key_drop2 = k.drop2;
   ta.dacp = st->dacp; ta.tailf = st->tail; ta.ge = ge; ta.ge_ecda = ge_ecda; ta.grad = st->grad;
   ta.gzb = gzb; ta.eflag = eflag;
-  // 5. ECDA (class-aware MMD + compactness + repulsion) and its embedding grads: after the
+  // 4. ECDA (class-aware MMD + compactness + repulsion) and its embedding grads: after the
   //    warm-up, in the same launch as the tail (block 0 = tail, blocks 1..C = classes)
   DadEcdaArgs ca;
   memset(&ca, 0, sizeof(ca));
@@ -556,10 +415,21 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
       DAD_TRY(hipGetLastError());
     }
   }
-
   tk_mark(TK_TAIL, stream);
-  // 6. dW1 (join, then sum_u (dL/de_u / len_u) * S_u; or the direct split-K GEMM), db1,
-  //    dW2, loss totals, squared-norm partials
+
+  // 5. dW1 as one direct split-K GEMM (G = ReLU' * dL/de / len rebuilt from the tail's dL/dz
+  //    and the ECDA rows), then the split sums with db1, dW2, loss totals, squared-norm partials
+  DadWgradArgs wa;
+  memset(&wa, 0, sizeof(wa));
+  wa.g = G; wa.warmup = cfg->warmup;
+  wa.mask_len = cfg->mask_len; wa.start_hi = cfg->start_hi;
+  wa.xc = bt->xc; wa.xn = bt->xn; wa.src = src;
+  if (explicit_rng) { wa.ns = bt->ns; wa.u = bt->u; wa.start = bt->start; }
+  wa.key_strong = k.strong; wa.key_feat = k.feat; wa.key_tstart = k.tstart;
+  wa.strong_std = cfg->strong_std; wa.feat_p = cfg->feat_p;
+  wa.bits = bits; wa.ge = ge; wa.vlen = vlen; wa.xs16 = xs16;
+  wa.splits = splits;
+  wa.wpart = ws_ptr<float>(workspace, L.wpart);
   DadReduceArgs ra;
   memset(&ra, 0, sizeof(ra));
   ra.g = G; ra.warmup = cfg->warmup;
@@ -571,40 +441,28 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   ra.key_drop1 = k.drop1; ra.key_drop2 = k.drop2; ra.p_drop = cfg->p_drop; ra.drop_scale = cfg->drop_scale;
   ra.ge = ge; ra.vlen = vlen; ra.cnt_tot = cnt_tot; ra.tailf = st->tail;
   ra.grad = st->grad; ra.normpart = normpart;
-  if (!factorised && !bf16) {
-    // FP32 direct: G = ReLU' * dL/de / len rebuilt per slab from the tail's dL/dz and the
-    // ECDA rows; one tile = (split, 128 columns); then every reduce block (dW1 sums and the
+  ra.splits = splits; ra.wpart = wa.wpart;
+  if (!h16) {
+    // FP32: one tile = (split, 128 columns); then every reduce block (dW1 sums and the
     // db1 / dW2 / totals blocks)
-    wa.splits = splits; wa.per_utt = 0;
-    wa.wpart = ws_ptr<float>(workspace, L.wpart);
     wa.ntiles = 6 * splits;
     hipLaunchKernelGGL(dad_wgrad_f32, dim3(wa.ntiles), dim3(DAD_WGRAD_THREADS), 0, stream, wa, ra);
     DAD_TRY(hipGetLastError());
     tk_mark(TK_WGRAD, stream);
-    ra.splits = splits; ra.wpart = wa.wpart;
     hipLaunchKernelGGL(dad_reduce, dim3(DAD_REDUCE_BLOCKS), dim3(DAD_REDUCE_THREADS), 0, stream, ra);
     DAD_TRY(hipGetLastError());
     tk_mark(TK_RED, stream);
-  } else if (!factorised) {
-    wa.splits = splits; wa.per_utt = 0;
-    wa.wpart = ws_ptr<float>(workspace, L.wpart);
+  } else {
     wa.ntiles = WGD_NDB * splits;
     // multiple of 8 (XCD-aware tile order) with WGD_XWG spare workgroups for the extra blocks
-    const int grid = (wa.ntiles + WGD_XWG + 7) / 8 * 8;
-    hipLaunchKernelGGL(dad_wgrad_direct, dim3(grid), dim3(WGD_THREADS), 0, stream, wa, ra);
+    const dim3 grid((wa.ntiles + WGD_XWG + 7) / 8 * 8);
+    if (f16) hipLaunchKernelGGL(dad_wgrad_direct_f16, grid, dim3(WGD_THREADS), 0, stream, wa, ra);
+    else hipLaunchKernelGGL(dad_wgrad_direct, grid, dim3(WGD_THREADS), 0, stream, wa, ra);
     DAD_TRY(hipGetLastError());
     tk_mark(TK_WGRAD, stream);
-    ra.splits = splits; ra.wpart = wa.wpart;
     hipLaunchKernelGGL(dad_reduce_w, dim3(DAD_REDUCE_BLOCKS - DAD_REDUCE_XBLK), dim3(64), 0, stream, ra);
     DAD_TRY(hipGetLastError());
     tk_mark(TK_RED, stream);
-  } else {
-    DAD_TRY(hipStreamWaitEvent(stream, side->join, 0));
-    ra.splits = nutt; ra.wpart = sbuf;
-    if (bf16) ra.su = wa.su;
-    hipLaunchKernelGGL(dad_wsum, dim3(DAD_REDUCE_BLOCKS), dim3(DAD_REDUCE_THREADS), 0, stream, ra);
-    DAD_TRY(hipGetLastError());
-    tk_mark(TK_WGRAD, stream);
   }
   return DAD_OK;
 }
@@ -645,8 +503,8 @@ int dad_step_apply(const dad_config* cfg, const dad_state* st, void* workspace, 
   oa.cfg = *cfg;
   oa.student = st->student; oa.teacher = st->teacher; oa.exp_avg = st->exp_avg; oa.exp_avg_sq = st->exp_avg_sq;
   oa.grad = st->grad;
-  oa.w1bf_student = reinterpret_cast<__bf16*>(st->w1bf_student);
-  oa.w1bf_teacher = reinterpret_cast<__bf16*>(st->w1bf_teacher);
+  oa.w1h_student = st->w1bf_student;
+  oa.w1h_teacher = st->w1bf_teacher;
   oa.dacp = st->dacp; oa.tailf = st->tail; oa.normpart = normpart; oa.nnorm = nnorm;
   oa.losses_out = st->losses;
   tk_mark(TK_OPT0, stream);
@@ -688,11 +546,11 @@ int dad_epoch_end(const dad_config* cfg, const dad_state* st, void* stream_) {
   return DAD_OK;
 }
 
-int dad_refresh_shadow(const dad_state* st, void* stream_) {
+int dad_refresh_shadow(const dad_state* st, int precision, void* stream_) {
   if (!st || !st->student || !st->teacher || !st->w1bf_student || !st->w1bf_teacher) return DAD_E_ARG;
+  if (precision != DAD_PREC_FP32 && !dad_prec16(precision)) return DAD_E_ARG;
   hipLaunchKernelGGL(dad_shadow_kernel, dim3((DAD_H * DAD_D + 255) / 256), dim3(256), 0, (hipStream_t)stream_,
-                     st->student, st->teacher, reinterpret_cast<__bf16*>(st->w1bf_student),
-                     reinterpret_cast<__bf16*>(st->w1bf_teacher));
+                     st->student, st->teacher, st->w1bf_student, st->w1bf_teacher, precision == DAD_PREC_FP16 ? 1 : 0);
   DAD_TRY(hipGetLastError());
   return DAD_OK;
 }
@@ -758,11 +616,11 @@ int dad_rng_draws(const dad_config* cfg, int which, uint64_t first, size_t n, fl
 // ----------------------------------------------------------------- modular encoder ops
 }  // extern "C"
 
-// The modular encoder ops' workspace: the FP32 layout plus the bf16 row-copy region, so the
-// BF16 encoder writes its copies to scratch instead of testing for a missing buffer in the
+// The modular encoder ops' workspace: the FP32 layout plus the 16-bit row-copy region, so the
+// 16-bit encoder writes its copies to scratch instead of testing for a missing buffer in the
 // conversion units it interleaves with the MFMA k-steps (a branch there splits the schedule).
 static DadWs enc_layout(const DadGeom& G) {
-  return dad_ws_layout(G, dad_auto_splits(G, DAD_PREC_FP32, 1), DAD_PREC_BF16, false);
+  return dad_ws_layout(G, dad_auto_splits(G, DAD_PREC_FP32, 1), DAD_PREC_BF16);
 }
 
 extern "C" {
@@ -792,38 +650,41 @@ __global__ __launch_bounds__(256) void dad_embed_kernel(const float* part_sum, c
   if (h == 0 && vlen) vlen[b] = len;
 }
 
-// bf16 copy of W1 in the W-stationary encoder's fragment order (dad_w1frag_index)
-__global__ __launch_bounds__(256) void dad_w1bf_kernel(const float* w, __bf16* out) {
+// 16-bit copy of W1 in the W-stationary encoder's fragment order (dad_w1frag_index)
+__global__ __launch_bounds__(256) void dad_w1h_kernel(const float* w, uint16_t* out, int f16) {
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (i < (size_t)DAD_H * DAD_D) out[dad_w1frag_index((uint32_t)(i / DAD_D), (uint32_t)(i % DAD_D))] = (__bf16)w[i];
+  if (i < (size_t)DAD_H * DAD_D)
+    out[dad_w1frag_index((uint32_t)(i / DAD_D), (uint32_t)(i % DAD_D))] = dad_half_bits(w[i], f16 != 0);
 }
 
 int encoder_forward_impl(const float* x, const uint8_t* pad, int B, int T, const float* w1, const float* b1,
                          int precision, void* workspace, hipStream_t stream, const DadWs& L, float* vlen_out,
                          float* e_out) {
-  __bf16* w1bf = ws_ptr<__bf16>(workspace, L.w1bf);
-  if (precision == DAD_PREC_BF16) {
-    hipLaunchKernelGGL(dad_w1bf_kernel, dim3((DAD_H * DAD_D + 255) / 256), dim3(256), 0, stream, w1, w1bf);
+  uint16_t* w1h = ws_ptr<uint16_t>(workspace, L.w1h);
+  const bool f16 = precision == DAD_PREC_FP16;
+  if (dad_prec16(precision)) {
+    hipLaunchKernelGGL(dad_w1h_kernel, dim3((DAD_H * DAD_D + 255) / 256), dim3(256), 0, stream, w1, w1h, f16 ? 1 : 0);
     DAD_TRY(hipGetLastError());
   }
   const DadGeom G = dad_geom(B, T, 0, 0);
   DadEncodeArgs ea;
   memset(&ea, 0, sizeof(ea));
   ea.g = G; ea.warmup = 1;
-  ea.xc = x; ea.mc = pad; ea.w1_student = w1; ea.b1_student = b1; ea.w1bf_student = w1bf;
+  ea.xc = x; ea.mc = pad; ea.w1_student = w1; ea.b1_student = b1; ea.w1h_student = w1h;
   ea.part_sum = ws_ptr<float>(workspace, L.part_sum);
   ea.part_cnt = ws_ptr<float>(workspace, L.part_cnt);
   ea.bits = ws_ptr<uint32_t>(workspace, L.bits);
-  ea.xs_bf16 = ws_ptr<__bf16>(workspace, L.xs_bf16);
+  ea.xs16 = ws_ptr<uint16_t>(workspace, L.xs16);
   const dim3 egrid((B * G.ncc + 3) / 4);
-  if (precision == DAD_PREC_BF16) {
+  if (dad_prec16(precision)) {
     int cus = 0;
     const int rc = device_cus(&cus);
     if (rc) return rc;
     const int rs = ws_split(G, 0, cus, ea.ws_nt, ea.ws_ns);
     if (rs) return rs;
     ea.ws_wstrong = ws_weights().strong;
-    hipLaunchKernelGGL(dad_encode_ws, dim3(ea.ws_nt + ea.ws_ns), dim3(DAD_ENC_WS_THREADS), 0, stream, ea);
+    if (f16) hipLaunchKernelGGL(dad_encode_ws_f16, dim3(ea.ws_nt + ea.ws_ns), dim3(DAD_ENC_WS_THREADS), 0, stream, ea);
+    else hipLaunchKernelGGL(dad_encode_ws, dim3(ea.ws_nt + ea.ws_ns), dim3(DAD_ENC_WS_THREADS), 0, stream, ea);
   } else {
     hipLaunchKernelGGL(dad_encode_f32, egrid, dim3(DAD_ENC_F32_THREADS), 0, stream, ea);
   }
@@ -859,7 +720,7 @@ int dad_encoder_forward(const float* x, const uint8_t* pad, int B, int T, const 
                         float* e_out, int precision, void* workspace, void* stream) {
   if (!x || !pad || !w1 || !b1 || !e_out || !workspace) return DAD_E_ARG;
   if (B < 1 || B > DAD_MAX_BATCH || T < 1) return DAD_E_SHAPE;
-  if (precision != DAD_PREC_FP32 && precision != DAD_PREC_BF16) return DAD_E_ARG;
+  if (precision != DAD_PREC_FP32 && !dad_prec16(precision)) return DAD_E_ARG;
   const DadGeom G = dad_geom(B, T, 0, 0);
   const DadWs L = enc_layout(G);
   return encoder_forward_impl(x, pad, B, T, w1, b1, precision, workspace, (hipStream_t)stream, L,

@@ -3,7 +3,8 @@
 // Layout contract (see DESIGN.md "Data layout in HBM"):
 //   features   f32 [B][T][768] row-major (the reference collator's padded layout,
 //              I/dataload_noisy.py:111-129), padding mask u8 [B][T] (1 = pad)
-//   W1         f32 [256][768] (nn.Linear weight, I/model.py:13), bf16 shadow [256][768]
+//   W1         f32 [256][768] (nn.Linear weight, I/model.py:13), 16-bit shadow [256][768]
+//              (fp16 or bf16 by the step's precision)
 //   rows are processed in 32-row "slabs" that never cross an utterance: slab (b, c)
 //   covers frames 32c .. 32c+31 of utterance b (frames >= T are masked).
 #pragma once
@@ -24,9 +25,26 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));   // register-promotable (unlike HIP uint4)
 
 __device__ __forceinline__ int dad_nchunk(int T) { return (T + DAD_SLAB - 1) / DAD_SLAB; }
+
+// 16-bit MFMA operands of the throughput modes: fp16 (DAD_PREC_FP16, 11-bit significand) or
+// bf16 (DAD_PREC_BF16, 8-bit), both rounded to nearest even.  Two floats -> one packed word
+// (v_cvt_pk_f16_f32 / v_cvt_pk_bf16_f32 on gfx950).
+template <bool F16>
+__device__ __forceinline__ uint32_t dad_pack2(float a, float b) {
+  if constexpr (F16) return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, f16x2));
+  else return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, bf16x2));
+}
+__device__ __forceinline__ uint16_t dad_half_bits(float x, bool f16) {
+  return f16 ? __builtin_bit_cast(uint16_t, (_Float16)x) : __builtin_bit_cast(uint16_t, (__bf16)x);
+}
+static inline __host__ __device__ bool dad_prec16(int precision) {
+  return precision == DAD_PREC_BF16 || precision == DAD_PREC_FP16;
+}
 
 // ---------------------------------------------------------------------------------
 // Counter-based RNG (production mode).  Each random value is a pure function of
@@ -127,8 +145,8 @@ __device__ __forceinline__ size_t dad_src_row(const DadStoreRows& s, bool noisy,
   return (size_t)(base[b] + min(t, max(len, 1) - 1));
 }
 
-// W1 bf16 shadow layout = the B-fragment order of the W-stationary encoder (encode_ws.hip):
-// fragment ((w*4 + t)*24 + ks) is 64 lanes x 8 bf16, lane l holding
+// W1 16-bit shadow layout = the B-fragment order of the W-stationary encoder (encode_ws.hip):
+// fragment ((w*4 + t)*24 + ks) is 64 lanes x 8 halves, lane l holding
 // W1[h = 64w + 16t + (l & 15)][k = 32ks + 8(l >> 4) + j], so each wave loads its resident
 // W1 with fully coalesced 1 KB reads.
 __host__ __device__ __forceinline__ uint32_t dad_w1frag_index(uint32_t h, uint32_t k) {
@@ -140,7 +158,7 @@ __device__ __forceinline__ float dad_uniform_at(uint32_t key, uint32_t idx) {
   return dad_u01(dad_rng32(idx, key));
 }
 
-// Augmentation noise std*N of elements 2*pair, 2*pair+1 as the BF16 encoder adds it: the scale
+// Augmentation noise std*N of elements 2*pair, 2*pair+1 as the 16-bit encoder adds it: the scale
 // folded into the Box-Muller radius constant (c = -2 ln2 std^2).
 __device__ __forceinline__ void dad_aug_noise_pair(uint32_t key, uint32_t pair, float sd, float& z0, float& z1) {
   dad_normal_pair_c(key, pair, DAD_NEG2LN2 * sd * sd, z0, z1);
@@ -261,7 +279,7 @@ static inline __host__ __device__ DadGeom dad_geom(int Bc, int Tc, int Bn, int T
   return g;
 }
 
-// Job ranges of the W-stationary BF16 encoder (encode_ws.hip), shared by the kernel and the
+// Job ranges of the W-stationary 16-bit encoder (encode_ws.hip), shared by the kernel and the
 // host (ws_split sizes the grid with it, so host and kernel count work in the same units).
 // Jobs are 32-row slabs; teacher workgroups [0, nt) split the weak slabs, student workgroups
 // [nt, nt + ns) the clean slabs (cost 1 per live 16-row sub-slab) then the strong slabs (cost
@@ -319,11 +337,9 @@ struct DadWs {
   size_t wpart;      // f32 [S][H][D]               split-K weight-gradient partial slabs
   size_t normpart;   // f32 [DAD_NORM_BLOCKS]       squared-norm partials
   size_t ecda;       // f32 [C][Bc+Bn][Bc+Bn]       ECDA pairwise scratch for large member sets
-  size_t xs_bf16;    // bf16 [Bc*Tc + Bn*Tn][768]   BF16 mode: the student's MFMA input, clean rows then strong rows (wgrad operand)
-  size_t w1bf;       // bf16 [H][D]                 modular encoder ops: bf16 copy of W1
+  size_t xs16;       // f16/bf16 [Bc*Tc + Bn*Tn][768]  16-bit modes: the student's MFMA input, clean rows then strong rows (wgrad operand)
+  size_t w1h;        // f16/bf16 [H][D]             modular encoder ops: 16-bit copy of W1
   size_t gflat;      // f32 [DAD_GRAD_FLOATS]       modular encoder backward: scratch grad vector
-  size_t sbuf;       // [Bc + Bn][H][D]             S_u = bits_u^T X_u, the loss-independent factor of dW1 (f32; bf16 in BF16 mode)
-  size_t pool_cnt;   // [3][DAD_MAX_BATCH] u32      in-launch pooling arrival counters (dad_encode_ws); zero at allocation
   size_t bytes;
   int splits;
 };
@@ -331,7 +347,7 @@ struct DadWs {
 static inline size_t dad_align(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // weight-gradient split-K factor.  FP32 (dad_wgrad_f32, 6 column blocks per split): 42
-// splits -> 252 tiles.  BF16 (dad_wgrad_direct, 12 column blocks per split): 21 splits -> 252 workgroups,
+// splits -> 252 tiles.  FP16/BF16 (dad_wgrad_direct, 12 column blocks per split): 21 splits -> 252 workgroups,
 // one per CU, and never more than WGD_MAXU = 64 slabs per split (its dL/de table in LDS).
 // Both are bounded by the number of 32-row slabs.
 #ifndef WGD_SPLITS
@@ -341,14 +357,13 @@ static inline int dad_wgd_min_splits(int total) { return (total + 63) / 64; }
 static inline int dad_auto_splits(const DadGeom& g, int precision, int warmup) {
   const int total = g.Bc * g.ncc + (warmup ? 0 : g.Bn * g.ncn);
   // FP32: 42 splits x 6 column blocks = 252 tiles, one per CU
-  const int target = precision == DAD_PREC_BF16 ? WGD_SPLITS : 42;
+  const int target = dad_prec16(precision) ? WGD_SPLITS : 42;
   int s = total < target ? total : target;
-  if (precision == DAD_PREC_BF16 && s < dad_wgd_min_splits(total)) s = dad_wgd_min_splits(total);
+  if (dad_prec16(precision) && s < dad_wgd_min_splits(total)) s = dad_wgd_min_splits(total);
   return s;
 }
 
-// fused = the train step's layout (with the S_u buffer); the modular encoder ops pass false.
-static inline DadWs dad_ws_layout(const DadGeom& g, int splits, int precision, bool fused = true) {
+static inline DadWs dad_ws_layout(const DadGeom& g, int splits, int precision) {
   DadWs w;
   const size_t nsc = (size_t)g.Bc * g.ncc, nsn = (size_t)g.Bn * g.ncn;
   const size_t nb = (size_t)g.Bc + g.Bn;
@@ -366,11 +381,9 @@ static inline DadWs dad_ws_layout(const DadGeom& g, int splits, int precision, b
   w.wpart = off;    off = dad_align(off + sizeof(float) * (size_t)splits * DAD_H * DAD_D);
   w.normpart = off; off = dad_align(off + sizeof(float) * DAD_NORM_BLOCKS);
   w.ecda = off;     off = dad_align(off + sizeof(float) * DAD_C * nb * nb);
-  w.xs_bf16 = off;  off = dad_align(off + (precision == DAD_PREC_BF16 ? 2 * ((size_t)g.Bc * g.Tc + (size_t)g.Bn * g.Tn) * DAD_D : 0));
-  w.w1bf = off;     off = dad_align(off + 2 * (size_t)DAD_H * DAD_D);
+  w.xs16 = off;     off = dad_align(off + (dad_prec16(precision) ? 2 * ((size_t)g.Bc * g.Tc + (size_t)g.Bn * g.Tn) * DAD_D : 0));
+  w.w1h = off;      off = dad_align(off + 2 * (size_t)DAD_H * DAD_D);
   w.gflat = off;    off = dad_align(off + sizeof(float) * DAD_GRAD_FLOATS);
-  w.sbuf = off;     off = dad_align(off + (fused ? (precision == DAD_PREC_BF16 ? 2 : sizeof(float)) * nb * DAD_H * DAD_D : 0));
-  w.pool_cnt = off; off = dad_align(off + sizeof(uint32_t) * 3 * DAD_MAX_BATCH);
   w.bytes = off;
   return w;
 }

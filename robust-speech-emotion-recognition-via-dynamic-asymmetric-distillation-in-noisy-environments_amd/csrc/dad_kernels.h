@@ -5,9 +5,8 @@
 // Block sizes: kernels index with these, launches use them; every kernel whose indexing
 // depends on its block size exits uniformly if launched with another one.
 #define DAD_ENC_F32_THREADS 256
-#define DAD_ENC_WS_THREADS 512                               // W-stationary bf16 encoder (8 waves, two per SIMD)
+#define DAD_ENC_WS_THREADS 512                               // W-stationary 16-bit encoder (8 waves, two per SIMD)
 #define DAD_ENC_WS_MAXJ 256                                  // max 32-row jobs per encoder workgroup
-#define DAD_WS_TAB 256                                       // student workgroups of the host range table
 #define DAD_POOL_THREADS 64
 #define DAD_TAIL_THREADS 512
 #define DAD_ECDA_THREADS 512
@@ -18,8 +17,8 @@
 #define DAD_FUSED_TAIL 1
 #endif
 #define DAD_WGRAD_THREADS 256
-// dad_wgrad_direct (BF16): 64-column blocks, slab-range splits of at most WGD_MAXU slabs,
-// WGD_DEPTH slabs in flight per group, x tile row pitch WGD_XP bf16 (192 B)
+// dad_wgrad_direct (FP16/BF16): 64-column blocks, slab-range splits of at most WGD_MAXU slabs,
+// WGD_DEPTH slabs in flight per group, x tile row pitch WGD_XP halves (192 B)
 #define WGD_DB 64
 #define WGD_NDB (DAD_D / WGD_DB)
 #define WGD_MAXU 64
@@ -54,6 +53,7 @@ struct DadPoolArgs {
   const float* part_cnt; float* cnt_tot;
   uint32_t* eflag;        // [Bc+Bn] ECDA row flags, zeroed here (ECDA flags the rows it writes)
   float* tail_terms;      // per-class ECDA terms + gates, zeroed here (block 0)
+  uint32_t* range_flag;   // sticky: set when a pooled embedding is not finite (tail header DAD_T_RANGE)
 };
 
 struct DadEncodeArgs {
@@ -64,24 +64,15 @@ struct DadEncodeArgs {
   DadStoreRows src;         // store mode (dad_batch.rowc..lenn) or all NULL
   const float* w1_student; const float* b1_student;
   const float* w1_teacher; const float* b1_teacher;
-  const __bf16* w1bf_student; const __bf16* w1bf_teacher;
+  const uint16_t* w1h_student; const uint16_t* w1h_teacher;   // 16-bit W1 shadows (fragment-major)
   // explicit draws (parity mode) or NULL -> counter RNG
   const float* nw; const float* ns; const float* u; const int64_t* start;
   uint32_t key_weak, key_strong, key_feat, key_tstart;
   float weak_std, strong_std, feat_p;
   float* part_sum; float* part_cnt; uint32_t* bits;
-  __bf16* xs_bf16;          // BF16 mode: the student's MFMA input, clean rows then strong rows (for wgrad)
+  uint16_t* xs16;           // 16-bit modes: the student's MFMA input, clean rows then strong rows (for wgrad)
   int ws_nt, ws_ns;         // dad_encode_ws: teacher / student workgroups
   float ws_wstrong;         // dad_encode_ws: cost of a strong slab relative to a clean one
-  // dad_encode_ws student ranges from the host's min-max assignment (ws_tab_n = ws_ns, else 0 and
-  // the closed-form split): student k runs strong jobs [t[k][0], t[k][1]) then clean [t[k][2], t[k][3])
-  int ws_tab_n;
-  uint16_t ws_tab[DAD_WS_TAB][4];
-  // dad_encode_ws with pool_cnt set: the slab partials are pooled in the same launch (the last
-  // workgroup to finish an utterance's slabs of one kind pools them: dad_pool's outputs), so the
-  // step has no dad_pool launch.  pool_cnt: [3][DAD_MAX_BATCH] arrival counters, zero between steps.
-  DadPoolArgs pool;
-  uint32_t* pool_cnt;
 };
 
 
@@ -122,11 +113,9 @@ struct DadWgradArgs {
   uint32_t key_strong, key_feat, key_tstart;
   float strong_std, feat_p;
   const uint32_t* bits; const float* ge; const float* vlen;
-  const __bf16* xs_bf16;
+  const uint16_t* xs16;    // the encoder's 16-bit copies of the student's MFMA input
   float* wpart;
-  int per_utt;         // 1: one split per utterance with G = ReLU' bits (S_u = bits_u^T X_u into wpart[u])
   int ntiles;          // column blocks x splits; workgroups stride over them (grid may be smaller)
-  __bf16* su;          // dad_wgrad_su: S_u = bits_u^T X_u, bf16 [Bc + Bn][H][D]
 };
 
 struct DadReduceArgs {
@@ -134,7 +123,6 @@ struct DadReduceArgs {
   int splits, warmup, want_norm;
   float w_kl, w_ecda;
   const float* wpart; const float* ge; const float* vlen; const float* cnt_tot;
-  const __bf16* su;           // dad_wsum (BF16 step): bf16 S_u instead of the fp32 wpart slabs
   const float* ge_ecda;       // ECDA part of dL/de, added where eflag is set
   // fused step: dL/de is not materialised; the classifier part is rebuilt per (utterance, h)
   // as keep(u,h) * sum_c W2[c][h] gzb[u][c] (nn.Linear + dropout backward, I/model.py:62-63)
@@ -150,7 +138,7 @@ struct DadReduceArgs {
 struct DadOptimArgs {
   dad_config cfg;
   float* student; float* teacher; float* exp_avg; float* exp_avg_sq;
-  float* grad; __bf16* w1bf_student; __bf16* w1bf_teacher;
+  float* grad; uint16_t* w1h_student; uint16_t* w1h_teacher;   // shadows: fp16 if cfg.precision is FP16, else bf16
   float* dacp; float* tailf; const float* normpart; int nnorm;
   float* losses_out;
 };
@@ -167,24 +155,25 @@ struct DadCollateArgs {
 __global__ void dad_collate_kernel(DadCollateArgs a);
 int dad_collate_grid(long B, long T);
 __global__ void dad_encode_f32(DadEncodeArgs a);
-__global__ void dad_encode_ws(DadEncodeArgs a);            // counter RNG
-__global__ void dad_encode_ws_explicit(DadEncodeArgs a);   // explicit noise tensors (parity)
+__global__ void dad_encode_ws(DadEncodeArgs a);                // bf16 operands, counter RNG
+__global__ void dad_encode_ws_explicit(DadEncodeArgs a);       // bf16, explicit noise tensors (parity)
+__global__ void dad_encode_ws_f16(DadEncodeArgs a);            // fp16 operands, counter RNG
+__global__ void dad_encode_ws_f16_explicit(DadEncodeArgs a);   // fp16, explicit noise tensors
 __global__ void dad_pool(DadPoolArgs a);
 __global__ void dad_tail(DadTailArgs a);
 __global__ void dad_ecda(DadEcdaArgs a);
 __global__ void dad_tail_ecda(DadTailArgs ta, DadEcdaArgs ca);
 __global__ void dad_tail_ecda_w(DadTailArgs ta, DadEcdaArgs ca);   // B, Bn <= 64, class-aware
 __global__ void dad_wgrad_f32(DadWgradArgs a, DadReduceArgs r);   // r: the fused step's dL/de sources (gzb) or zeroed
-__global__ void dad_wgrad_direct(DadWgradArgs a, DadReduceArgs r);
-__global__ void dad_wgrad_su(DadWgradArgs a);
-__global__ void dad_wsum(DadReduceArgs a);
+__global__ void dad_wgrad_direct(DadWgradArgs a, DadReduceArgs r);       // bf16 operands
+__global__ void dad_wgrad_direct_f16(DadWgradArgs a, DadReduceArgs r);   // fp16 operands
 __global__ void dad_reduce(DadReduceArgs a);
 __global__ void dad_reduce_w(DadReduceArgs a);
 __global__ void dad_norm(float* grad, float* normpart, float inv_world);
 __global__ void dad_optim(DadOptimArgs a);
 __global__ void dad_commit_kernel(dad_config cfg, const float* grad, float* dacp, float* tailf, float* losses_out);
 __global__ void dad_epoch_end_kernel(float* dacp, float beta, float one_m_beta);
-__global__ void dad_shadow_kernel(const float* student, const float* teacher, __bf16* ws, __bf16* wt);
+__global__ void dad_shadow_kernel(const float* student, const float* teacher, uint16_t* ws, uint16_t* wt, int f16);
 // helper-type drop-ins (DACPManager / ECDALoss, tail.hip; DataAugmentation, utils_abi.hip)
 __global__ void dad_certainty_kernel(const float* probs, int B, int use_entropy, float* score, int64_t* pred);
 __global__ void dad_dacp_mask_kernel(dad_config cfg, const float* probs, int Bn, float* dacp, uint8_t* mask,

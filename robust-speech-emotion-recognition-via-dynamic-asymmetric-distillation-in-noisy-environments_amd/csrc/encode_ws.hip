@@ -1,22 +1,23 @@
-// W-stationary BF16 encoder: the throughput-mode forward of all three encoder passes.
+// W-stationary 16-bit encoder: the throughput-mode forward of all three encoder passes, with
+// fp16 (default throughput mode, 11-bit significand) or bf16 MFMA operands and fp32 accumulation.
 //
 // Replaces, per step (I/train.py:399,406-410,439):
 //   student_encoder(clean)                         Emotion2VecEncoder.forward, I/model.py:18-41
 //   teacher_encoder(weak_augment(noisy))           + DataAugmentation.weak_augment, I/utils.py:328-331
 //   student_encoder(strong_augment(noisy))         + strong_augment/_apply_temporal_masking, I/utils.py:333-375
 // and emits what the rest of the step consumes: per-32-row-slab pooled ReLU sums and active
-// counts, the ReLU'-and-valid row masks, and the bf16 student inputs (clean and strong-augmented
+// counts, the ReLU'-and-valid row masks, and the 16-bit student inputs (clean and strong-augmented
 // rows, the weight gradient's operand).
 //
 // Shape of the work: out[rows][256] = x[rows][768] . W1^T with tens of thousands of rows and
-// W1 only 384 KB in bf16.  So W1 is STATIONARY: a persistent workgroup holds all 256 hidden
+// W1 only 384 KB in 16 bits.  So W1 is STATIONARY: a persistent workgroup holds all 256 hidden
 // units of ONE network's W1 in its register file (each wave 256/WAVES hidden units x 768 k,
 // read in place as MFMA B operands) and streams 16-row sub-slabs of x through LDS:
 //
 //   HBM fp32 rows --LDS-DMA (global_load_lds_dwordx4, 2 stages x 48 KB in flight)--> raw ring
-//   raw ring --augment (counter-RNG Box-Muller, feature mask, temporal zero) + cvt bf16-->
-//      bf16 tile ring (2 x 24 KB; 16-B chunks XOR-swizzled by row: conflict-free A reads)
-//   bf16 tile --ds_read_b128 A fragments--> v_mfma_f32_16x16x32_bf16 against the resident W1
+//   raw ring --augment (counter-RNG Box-Muller, feature mask, temporal zero) + cvt f16/bf16-->
+//      16-bit tile ring (2 x 24 KB; 16-B chunks XOR-swizzled by row: conflict-free A reads)
+//   tile --ds_read_b128 A fragments--> v_mfma_f32_16x16x32_{f16,bf16} against the resident W1
 //   accumulators --bias, ReLU, valid mask, row sums, ballots--> slab partials + ReLU' bits
 //
 // Each x element is fetched once per network that consumes it and augmented once.  Roles are
@@ -59,7 +60,7 @@ DAD_PROBE_BUFFER(ws_stamps, 4096 * 10)
 namespace {
 
 constexpr int kSub = 16;                       // rows per sub-slab (one MFMA M tile)
-constexpr int kKS = DAD_D / 32;                // 24 k-steps of v_mfma_f32_16x16x32_bf16
+constexpr int kKS = DAD_D / 32;                // 24 k-steps of v_mfma_f32_16x16x32_{f16,bf16}
 constexpr int kRawRow = DAD_D * 4;             // 3072 B
 constexpr int kRawStage = kSub * kRawRow;      // 48 KB
 constexpr int kTileRow = DAD_D * 2;            // 1536 B
@@ -89,7 +90,7 @@ struct Ctx {
   uint32_t key_weak, key_strong, key_feat, key_tstart;
   float wstd, sstd, feat_p;
   float* part_sum; float* part_cnt; uint32_t* bits;
-  __bf16* xs; __bf16* xsn;   // bf16 copies of the student's MFMA input: clean rows, strong rows
+  uint16_t* xs; uint16_t* xsn;   // 16-bit copies of the student's MFMA input: clean rows, strong rows
 };
 
 __device__ __forceinline__ Ctx ctx_of(const DadEncodeArgs& a) {
@@ -106,7 +107,7 @@ __device__ __forceinline__ Ctx ctx_of(const DadEncodeArgs& a) {
   c.key_weak = a.key_weak; c.key_strong = a.key_strong; c.key_feat = a.key_feat; c.key_tstart = a.key_tstart;
   c.wstd = a.weak_std; c.sstd = a.strong_std; c.feat_p = a.feat_p;
   c.part_sum = a.part_sum; c.part_cnt = a.part_cnt; c.bits = a.bits;
-  c.xs = a.xs_bf16; c.xsn = a.xs_bf16 + (size_t)c.Bc * c.Tc * DAD_D;
+  c.xs = a.xs16; c.xsn = a.xs16 + (size_t)c.Bc * c.Tc * DAD_D;
   return c;
 }
 
@@ -153,11 +154,10 @@ __device__ __forceinline__ void job_range(const Ctx& C, int wg, int nt, int ns, 
   dad_ws_job_range(wg, nt, ns, wstrong, C.Bc, C.Tc, C.ncc, C.Bn, C.Tn, C.ncn, C.Js, teacher, j0, j1);
 }
 
-// a workgroup's jobs: local job l is job a0 + l for l < na, then b0 + (l - na) (student ranges
-// of the host table: strong jobs, then clean jobs; otherwise one contiguous range)
+// a workgroup's jobs: local job l is job a0 + l (one contiguous range)
 struct JobMap {
-  int a0, na, b0;
-  __device__ __forceinline__ int operator()(int l) const { return l < na ? a0 + l : b0 + (l - na); }
+  int a0;
+  __device__ __forceinline__ int operator()(int l) const { return a0 + l; }
 };
 
 template <int NOISE>
@@ -189,7 +189,7 @@ struct Shape {
   static constexpr int HW = 16 * NT;           // hidden units per wave
   static constexpr int RPW = kSub / WAVES;     // rows converted per wave
   static constexpr int kDma = 3 * RPW;         // LDS-DMA instructions per wave per sub-slab
-  static constexpr int kXsRow = 3;             // bf16 x-copy stores per converted row (student)
+  static constexpr int kXsRow = 3;             // 16-bit x-copy stores per converted row (student)
   // 4 waves (one per SIMD, 512 registers): 256 of the 384 W1 registers in AGPRs.
   // 8 waves (two per SIMD, 256 registers): all 192 in VGPRs, no AGPRs at all.
   static constexpr bool AGPR_W = WAVES == 4;
@@ -221,41 +221,15 @@ __device__ __forceinline__ int live_rows(const Job& J, int half, int w) {
   return n < 0 ? 0 : (n > S::RPW ? S::RPW : n);
 }
 
-// Convert the wave's rows of sub-slab (J, HALF): raw stage -> bf16 tile; CLEAN / STRONG also store
-// the bf16 row to HBM for the weight gradient.  Straight-line code per KIND (one basic block,
-// so the 3*RPW independent RNG chains interleave): rows past the utterance are converted as
-// copies of its last row (identical bytes to the same xs address), temporally masked rows
-// are selected to zero after the RNG.  Noise comes pre-scaled (dad_normal_pair_c).
-#ifndef WS_REGION
-#define WS_REGION 1
-#endif
-#ifndef WS_WT
-#define WS_WT 1        // bf16 copy stores write-through (sc1): no dirty L2 lines at the kernel end (A/B: -0.5 us)
-#endif
-#ifndef WS_LDS_FIRST
-#define WS_LDS_FIRST 0
-#endif
-#ifndef WS_PRIO
-#define WS_PRIO 0      // static s_setprio 1 for: 0 no wave, 1 waves WAVES/2.., 2 waves ..WAVES/2-1
-#endif
-// Floor knockouts (diagnostic builds only, tools/gpu_ws_floor.sh; results are wrong by design):
-// WS_FLOOR_NO_RNG  constant noise instead of the counter RNG (the add and the masks stay)
-// WS_FLOOR_NO_XS   no bf16 copy stores
-// WS_FLOOR_NO_MFMA no MFMAs (accumulators stay zero)
-// WS_FLOOR_NO_DMA  no row DMA after the first two sub-slabs (stale LDS rows)
-#ifndef WS_FLOOR_NO_RNG
-#define WS_FLOOR_NO_RNG 0
-#endif
-#ifndef WS_FLOOR_NO_XS
-#define WS_FLOOR_NO_XS 0
-#endif
-#ifndef WS_FLOOR_NO_MFMA
-#define WS_FLOOR_NO_MFMA 0
-#endif
-#ifndef WS_FLOOR_NO_DMA
-#define WS_FLOOR_NO_DMA 0
-#endif
-template <class S, int NOISE, int KIND, int HALF>
+// Convert the wave's rows of sub-slab (J, HALF): raw stage -> 16-bit tile; CLEAN / STRONG also
+// store the 16-bit row to HBM for the weight gradient (write-through, sc1: no dirty L2 lines are
+// left for the kernel-end release, A/B -0.5 us per launch).  Straight-line code per KIND (one
+// basic block, so the 3*RPW independent RNG chains interleave): rows past the utterance are
+// converted as copies of its last row (identical bytes to the same xs address), temporally
+// masked rows are selected to zero after the RNG.  Noise comes pre-scaled (dad_normal_pair_c).
+// F16: v_cvt_pk_f16_f32 (round to nearest even; |x| > 65504 becomes inf, which makes the row's
+// pre-activations non-finite and is reported by dad_pool's range flag), else v_cvt_pk_bf16_f32.
+template <class S, int NOISE, int KIND, int HALF, bool F16>
 struct WsConv {
   static constexpr bool strong = KIND == KIND_STRONG;
   static constexpr int kUnits = 3 * S::RPW;   // (row i, 256-column chunk k) units of 4 elements per lane
@@ -291,18 +265,12 @@ struct WsConv {
     f32x4 v = *reinterpret_cast<const f32x4*>(rrow + 256 * k);
     [[maybe_unused]] f32x4 kp;
     if constexpr (strong) kp = *reinterpret_cast<const f32x4*>(fk + d);
-#if WS_LDS_FIRST
-    // the unit's LDS reads go out before its RNG chain, which then covers their latency
-    if constexpr (KIND != KIND_CLEAN) __builtin_amdgcn_sched_barrier(0);
-#endif
     if constexpr (KIND != KIND_CLEAN) {
       f32x4 n;
       if constexpr (NOISE) {
         n = *reinterpret_cast<const f32x4*>(nsrc + (size_t)grow * DAD_D + d);
 #pragma unroll
         for (int e = 0; e < 4; ++e) n[e] *= sd;
-      } else if constexpr (WS_FLOOR_NO_RNG) {
-        n = f32x4{sd, sd, sd, sd};
       } else {
         const uint32_t p = ((uint32_t)grow * (uint32_t)DAD_D + (uint32_t)d) >> 1;
         float z0, z1, z2, z3;
@@ -319,27 +287,24 @@ struct WsConv {
         for (int e = 0; e < 4; ++e) v[e] = v[e] * kp[e];
       }
     }
-    // two v_cvt_pk_bf16_f32 per 4 elements; the temporal zero selects the packed words
-    uint2 o = uint2{__builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{v[0], v[1]}, bf16x2)),
-                    __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{v[2], v[3]}, bf16x2))};
+    // two packed converts per 4 elements; the temporal zero selects the packed words
+    uint2 o = uint2{dad_pack2<F16>(v[0], v[1]), dad_pack2<F16>(v[2], v[3])};
     if constexpr (strong) o = tzero ? uint2{0u, 0u} : o;
     *reinterpret_cast<uint2*>(trow + 512 * k) = o;             // chunk 32k + (lane>>1), swizzled by row
-    if constexpr (KIND != KIND_WEAK && !WS_FLOOR_NO_XS) {
+    if constexpr (KIND != KIND_WEAK) {
       // 32-bit byte offset from the uniform base (saddr store, no 64-bit address math)
       const uint32_t boff = ((uint32_t)grow * (uint32_t)DAD_D + (uint32_t)d) * 2u;
-      if constexpr (WS_WT)
-        __hip_atomic_store(reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(strong ? C.xsn : C.xs) + boff),
-                           __builtin_bit_cast(uint64_t, o), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else *reinterpret_cast<uint2*>(reinterpret_cast<char*>(strong ? C.xsn : C.xs) + boff) = o;
+      __hip_atomic_store(reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(strong ? C.xsn : C.xs) + boff),
+                         __builtin_bit_cast(uint64_t, o), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   template <int U = 0>
   __device__ __forceinline__ void all() const {
     if constexpr (U < kUnits) {
       unit<U>();
-      // WS_REGION units per scheduling region: the wave's partner on the SIMD covers the rest
-      // of the dependent latency, and nothing is hoisted across regions
-      if constexpr ((U % 3 + 1) % WS_REGION == 0 || U % 3 == 2) __builtin_amdgcn_sched_barrier(0);
+      // one unit per scheduling region: the wave's partner on the SIMD covers the rest of the
+      // dependent latency, and nothing is hoisted across regions
+      __builtin_amdgcn_sched_barrier(0);
       all<U + 1>();
     }
   }
@@ -351,22 +316,17 @@ struct WsNoConv {
   __device__ __forceinline__ void unit() const {}
 };
 
-// Convert the wave's rows of sub-slab (J, HALF): raw stage -> bf16 tile; CLEAN / STRONG also store
-// the bf16 row to HBM for the weight gradient.  Straight-line code per KIND (one basic block,
-// so the 3*RPW independent RNG chains interleave): rows past the utterance are converted as
-// copies of its last row (identical bytes to the same xs address), temporally masked rows
-// are selected to zero after the RNG.  Noise comes pre-scaled (dad_normal_pair_c).
-template <class S, int NOISE, int KIND, int HALF>
+template <class S, int NOISE, int KIND, int HALF, bool F16>
 __device__ __forceinline__ void ws_convert(const Ctx& C, const Job& J, int w, int lane_, const float* raw, char* tile,
                                            const float* fk) {
-  WsConv<S, NOISE, KIND, HALF>(C, J, w, lane_, raw, tile, fk).all();
+  WsConv<S, NOISE, KIND, HALF, F16>(C, J, w, lane_, raw, tile, fk).all();
 }
 
-// bf16 copies of an empty sub-slab's rows that lie inside the utterance (padded frames): zeros.
+// 16-bit copies of an empty sub-slab's rows that lie inside the utterance (padded frames): zeros.
 // Rows past the utterance alias its last row's copy and are left alone.
 template <class S, int HALF>
 __device__ __forceinline__ void ws_zero_xs(const Ctx& C, const Job& J, int w, int lane) {
-  __bf16* xs = J.kind == KIND_STRONG ? C.xsn : C.xs;
+  uint16_t* xs = J.kind == KIND_STRONG ? C.xsn : C.xs;
 #pragma unroll
   for (int i = 0; i < S::RPW; ++i) {
     const int t = J.c * DAD_SLAB + HALF * kSub + S::RPW * w + i;
@@ -380,21 +340,25 @@ __device__ __forceinline__ void ws_zero_xs(const Ctx& C, const Job& J, int w, in
 // One MFMA against a resident W1 fragment, as inline asm so the fragment is read in place as
 // the B operand (the compiler otherwise parks W1 in the accumulator file and copies 4
 // registers back per MFMA).  AGPR-resident fragments: "a"; VGPR-resident: "v".  The first
-// k-step takes C = 0; a chain on one accumulator needs no wait states.
-template <bool AGPR, bool FIRST>
-__device__ __forceinline__ void mfma1(f32x4& acc, const bf16x8& xa, const bf16x8& wfr) {
-  if constexpr (WS_FLOOR_NO_MFMA) {
-    if constexpr (FIRST) acc = f32x4{};
-    return;
+// k-step takes C = 0; a chain on one accumulator needs no wait states.  Operands are 8 x 16-bit
+// (bf16x8 is only the register container; F16 selects the fp16 instruction).
+#define DAD_WS_MFMA(OP)                                                                            \
+  if constexpr (AGPR) {                                                                            \
+    if constexpr (FIRST) asm(OP " %0, %1, %2, 0" : "=&v"(acc) : "v"(xa), "a"(wfr));                 \
+    else asm(OP " %0, %1, %2, %0" : "+v"(acc) : "v"(xa), "a"(wfr));                                 \
+  } else {                                                                                         \
+    if constexpr (FIRST) asm(OP " %0, %1, %2, 0" : "=&v"(acc) : "v"(xa), "v"(wfr));                 \
+    else asm(OP " %0, %1, %2, %0" : "+v"(acc) : "v"(xa), "v"(wfr));                                 \
   }
-  if constexpr (AGPR) {
-    if constexpr (FIRST) asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(acc) : "v"(xa), "a"(wfr));
-    else asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(xa), "a"(wfr));
+template <bool AGPR, bool FIRST, bool F16>
+__device__ __forceinline__ void mfma1(f32x4& acc, const bf16x8& xa, const bf16x8& wfr) {
+  if constexpr (F16) {
+    DAD_WS_MFMA("v_mfma_f32_16x16x32_f16")
   } else {
-    if constexpr (FIRST) asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(acc) : "v"(xa), "v"(wfr));
-    else asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(xa), "v"(wfr));
+    DAD_WS_MFMA("v_mfma_f32_16x16x32_bf16")
   }
 }
+#undef DAD_WS_MFMA
 
 // A fragment of k-step KS: rows lane&15, k = 32KS + 8(lane>>4) .. +7.  The XOR swizzle only
 // touches the low 4 bits of the chunk index, so chunk (4KS + g) ^ row = 16(KS>>2) +
@@ -404,30 +368,22 @@ __device__ __forceinline__ bf16x8 afrag(const char* tile, const int (&aoff)[4]) 
   return *reinterpret_cast<const bf16x8*>(tile + aoff[KS & 3] + 256 * (KS >> 2));
 }
 
-// acc[t] = x_tile(16 rows) . W1[hw + 16t .. +15]^T over K = 768.  A fragments are read
-// WS_LA k-steps ahead of their MFMAs: one k-step's MFMAs (NT x 16 cycles) are shorter than an
-// LDS read under load, so a one-step lookahead left every k-step waiting on its fragment.
-#ifndef WS_LA
-#define WS_LA 1   // 1 or 2 (2 with the interleaved conversion spills W1 fragments)
-#endif
-static_assert(WS_LA == 1 || WS_LA == 2, "A-fragment lookahead: 1 or 2 k-steps");
-// CV: conversion units of the next sub-slab riding along the MFMA chain (WS_INTERLEAVE): unit
-// u is issued after k-step (u + 1) * kKS / kUnits - 1, between scheduling barriers, so the
-// VALU work of the RNG fills the matrix pipe's cycles inside ONE wave.
-#ifndef WS_INTERLEAVE
-#define WS_INTERLEAVE 1   // measured 0.6-0.8 us per launch faster than the MFMA-then-convert order alone
-#endif
-template <class S, int KS, class CV>
+// acc[t] = x_tile(16 rows) . W1[hw + 16t .. +15]^T over K = 768.  The A fragment of k-step
+// KS+1 is read while the MFMAs of k-step KS issue.  CV: conversion units of the next sub-slab
+// riding along the MFMA chain: unit u is issued after k-step (u + 1) * kKS / kUnits - 1, between
+// scheduling barriers, so the VALU work of the RNG fills the matrix pipe's cycles inside ONE
+// wave (measured 0.6-0.8 us per launch faster than the MFMA-then-convert order alone).
+template <class S, int KS, bool F16, class CV>
 __device__ __forceinline__ void ws_mfma_from(const char* tile, const int (&aoff)[4], const bf16x8 (&wf)[S::NT][kKS],
-                                             f32x4 (&acc)[S::NT], bf16x8 x0, bf16x8 x1, const CV& cv) {
+                                             f32x4 (&acc)[S::NT], bf16x8 x0, const CV& cv) {
   if constexpr (KS < kKS) {
     bf16x8 xn;
-    if constexpr (KS + WS_LA < kKS) xn = afrag<KS + WS_LA>(tile, aoff);
+    if constexpr (KS + 1 < kKS) xn = afrag<KS + 1>(tile, aoff);
 #pragma unroll
     for (int t = 0; t < S::NT; ++t) {
       const bool agpr = S::AGPR_W && (t < 2 || (t == 2 && KS < 16));
-      if (agpr) mfma1<true, KS == 0>(acc[t], x0, wf[t][KS]);
-      else mfma1<false, KS == 0>(acc[t], x0, wf[t][KS]);
+      if (agpr) mfma1<true, KS == 0, F16>(acc[t], x0, wf[t][KS]);
+      else mfma1<false, KS == 0, F16>(acc[t], x0, wf[t][KS]);
     }
     if constexpr (CV::kUnits > 0) {
       constexpr int U = (KS + 1) * CV::kUnits / kKS;        // units due after this k-step
@@ -438,15 +394,13 @@ __device__ __forceinline__ void ws_mfma_from(const char* tile, const int (&aoff)
         __builtin_amdgcn_sched_barrier(0);
       }
     }
-    if constexpr (WS_LA == 1) ws_mfma_from<S, KS + 1>(tile, aoff, wf, acc, xn, xn, cv);
-    else ws_mfma_from<S, KS + 1>(tile, aoff, wf, acc, x1, xn, cv);
+    ws_mfma_from<S, KS + 1, F16>(tile, aoff, wf, acc, xn, cv);
   }
 }
-template <class S, class CV = WsNoConv>
+template <class S, bool F16, class CV = WsNoConv>
 __device__ __forceinline__ void ws_mfma(const char* tile, const int (&aoff)[4], const bf16x8 (&wf)[S::NT][kKS],
                                         f32x4 (&acc)[S::NT], const CV& cv = CV{}) {
-  if constexpr (WS_LA == 1) ws_mfma_from<S, 0>(tile, aoff, wf, acc, afrag<0>(tile, aoff), afrag<0>(tile, aoff), cv);
-  else ws_mfma_from<S, 0>(tile, aoff, wf, acc, afrag<0>(tile, aoff), afrag<1>(tile, aoff), cv);
+  ws_mfma_from<S, 0, F16>(tile, aoff, wf, acc, afrag<0>(tile, aoff), cv);
   // MFMA D -> VALU readers of the epilogue (hipcc pads nothing after an asm MFMA)
   if constexpr (S::NT == 4) asm volatile("s_nop 7\n\ts_nop 7" ::"v"(acc[0]), "v"(acc[1]), "v"(acc[2]), "v"(acc[3]));
   else asm volatile("s_nop 7\n\ts_nop 7" ::"v"(acc[0]), "v"(acc[1]));
@@ -533,7 +487,7 @@ __device__ __forceinline__ void ws_epilogue(const Ctx& C, const Job& J, int w, i
 // VMEM instructions one wave issues per sub-slab (the counted vmcnt waits depend on them)
 template <class S>
 __device__ __forceinline__ constexpr int n_xs(int kind) {
-  return (kind != KIND_WEAK && !WS_FLOOR_NO_XS) ? S::kXsRow * S::RPW : 0;
+  return kind != KIND_WEAK ? S::kXsRow * S::RPW : 0;
 }
 template <bool TEACHER, int HALF>
 __device__ __forceinline__ constexpr int n_epi() { return TEACHER ? HALF : 3 * HALF; }
@@ -552,7 +506,7 @@ __device__ __forceinline__ void wait_vm_sw(int n) {
 
 }  // namespace
 
-template <int WAVES, int NOISE, bool TEACHER>
+template <int WAVES, int NOISE, bool TEACHER, bool F16>
 __device__ __forceinline__ void ws_loop(const Ctx& C, const JobMap jm, const int Q, const int w, const int lane,
                                         char* smem, const uint32_t sbase, const bf16x8* W, const float* bias,
                                         const float* fk, const uint32_t* vb) {
@@ -576,7 +530,7 @@ __device__ __forceinline__ void ws_loop(const Ctx& C, const JobMap jm, const int
   // 0 even where it zeroes padded rows' copies: under-counting younger stores only waits longer)
   auto xs_of = [&](int q) -> int { return vmask_of(q) ? n_xs<S>(jobq(q).kind) : 0; };
   auto dma = [&](int q) {
-    if (q < Q && !(WS_FLOOR_NO_DMA && q >= 2)) {
+    if (q < Q) {
       const Job J = jobq(q);
       dma_rows<S>(J.kind == KIND_CLEAN ? C.xc : C.xn, J, q & 1, w, sbase + kOffRaw + (q & 1) * kRawStage, lane);
     }
@@ -585,16 +539,16 @@ __device__ __forceinline__ void ws_loop(const Ctx& C, const JobMap jm, const int
   auto convert = [&](auto hn_tag, const Job& J, uint32_t vm) {
     constexpr int HN = decltype(hn_tag)::value;
     if (vm == 0) {
-      // nothing to multiply; the student's bf16 copies of padded frames inside the utterance
+      // nothing to multiply; the student's 16-bit copies of padded frames inside the utterance
       // still get finite bytes (the weight gradient multiplies them by a zero mask)
       if constexpr (!TEACHER) ws_zero_xs<S, HN>(C, J, w, lane);
       return;
     }
     const float* rawp = HN ? raw1 : raw0;
     char* tl = HN ? tile1 : tile0;
-    if constexpr (TEACHER) ws_convert<S, NOISE, KIND_WEAK, HN>(C, J, w, lane, rawp, tl, fk);
-    else if (J.kind == KIND_CLEAN) ws_convert<S, NOISE, KIND_CLEAN, HN>(C, J, w, lane, rawp, tl, fk);
-    else ws_convert<S, NOISE, KIND_STRONG, HN>(C, J, w, lane, rawp, tl, fk);
+    if constexpr (TEACHER) ws_convert<S, NOISE, KIND_WEAK, HN, F16>(C, J, w, lane, rawp, tl, fk);
+    else if (J.kind == KIND_CLEAN) ws_convert<S, NOISE, KIND_CLEAN, HN, F16>(C, J, w, lane, rawp, tl, fk);
+    else ws_convert<S, NOISE, KIND_STRONG, HN, F16>(C, J, w, lane, rawp, tl, fk);
   };
   // sub-slab q (half H): MFMA on tile H, convert sub-slab q+1 (half 1-H), epilogue, DMA q+3
   auto iter = [&](auto h_tag, int q) {
@@ -610,7 +564,7 @@ __device__ __forceinline__ void ws_loop(const Ctx& C, const JobMap jm, const int
     const uint32_t vmask = vmask_of(q);
     auto mfma = [&]() {
       if (vmask) {
-        ws_mfma<S>(H ? tile1 : tile0, aoff, wf, acc);
+        ws_mfma<S, F16>(H ? tile1 : tile0, aoff, wf, acc);
       } else {
 #pragma unroll
         for (int t = 0; t < S::NT; ++t) acc[t] = f32x4{};
@@ -623,18 +577,18 @@ __device__ __forceinline__ void ws_loop(const Ctx& C, const JobMap jm, const int
       // most these younger VMEM ops remain: xs stores of convert(q), epilogue(q-1), DMA(q+2)
       wait_vm_sw<S::kDma>(xs_of(q) + (q > 0 ? n_epi<TEACHER, 1 - H>() : 0) + (q + 2 < Q ? S::kDma : 0));
       c1 = WS_CLK();
-      if (WS_INTERLEAVE && vmask && vmn) {
+      if (vmask && vmn) {
         // MFMA(q) with convert(q+1)'s units riding along the chain
         constexpr int HN = 1 - H;
         const float* rawp = HN ? raw1 : raw0;
         char* tl = HN ? tile1 : tile0;
         const char* tm = H ? tile1 : tile0;
         if constexpr (TEACHER) {
-          ws_mfma<S>(tm, aoff, wf, acc, WsConv<S, NOISE, KIND_WEAK, HN>(C, Jn, w, lane, rawp, tl, fk));
+          ws_mfma<S, F16>(tm, aoff, wf, acc, WsConv<S, NOISE, KIND_WEAK, HN, F16>(C, Jn, w, lane, rawp, tl, fk));
         } else if (Jn.kind == KIND_CLEAN) {
-          ws_mfma<S>(tm, aoff, wf, acc, WsConv<S, NOISE, KIND_CLEAN, HN>(C, Jn, w, lane, rawp, tl, fk));
+          ws_mfma<S, F16>(tm, aoff, wf, acc, WsConv<S, NOISE, KIND_CLEAN, HN, F16>(C, Jn, w, lane, rawp, tl, fk));
         } else {
-          ws_mfma<S>(tm, aoff, wf, acc, WsConv<S, NOISE, KIND_STRONG, HN>(C, Jn, w, lane, rawp, tl, fk));
+          ws_mfma<S, F16>(tm, aoff, wf, acc, WsConv<S, NOISE, KIND_STRONG, HN, F16>(C, Jn, w, lane, rawp, tl, fk));
         }
         c2 = WS_CLK();
       } else if (S::STAGGER && w >= WAVES / 2) {
@@ -660,11 +614,6 @@ __device__ __forceinline__ void ws_loop(const Ctx& C, const JobMap jm, const int
     lds_barrier();
     WS_PHASES(c0, c1, c2, c3, c4, c5);
   };
-#if WS_PRIO == 1
-  if (w >= WAVES / 2) __builtin_amdgcn_s_setprio(1);   // the second-dispatched half loses arbitration by age
-#elif WS_PRIO == 2
-  if (w < WAVES / 2) __builtin_amdgcn_s_setprio(1);
-#endif
   // the first two sub-slabs' DMAs go out ahead of the resident W1 (48 KB per wave), so
   // sub-slab 0 is converted while W1 streams in
   dma(0);
@@ -690,133 +639,8 @@ __device__ __forceinline__ void ws_loop(const Ctx& C, const JobMap jm, const int
   wait_vm<0>();
 }
 
-// ---------------------------------------------------------------- in-launch pooling
-// dad_pool's work for one (kind, utterance), by the workgroup whose slab partials completed it
-// (I/model.py:35-36 masked mean pool, I/model.py:54-64 classifier with dropout): the same
-// arithmetic and summation orders as dad_pool (tail.hip), so the outputs are identical.
-// Threads 0..255: the pooled sums (hidden unit h), the embedding and the logit partial dots;
-// threads 256..511: the active-count sums (student kinds).  scratch: 24 floats of LDS.
-__device__ __forceinline__ void ws_pool_one(const DadEncodeArgs& a, const Ctx& C, int key, float* scratch) {
-  const DadPoolArgs& p = a.pool;
-  const int kind = key / DAD_MAX_BATCH, b = key - kind * DAD_MAX_BATCH;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = tid & (DAD_H - 1), half = tid >> 8;
-  const bool noisy = kind != KIND_CLEAN, tch = kind == KIND_WEAK;
-  const int T = noisy ? C.Tn : C.Tc, nc = noisy ? C.ncn : C.ncc;
-  const uint8_t* pad = noisy ? C.mn : C.mc;
-  const size_t slab0 = kind == KIND_CLEAN ? (size_t)b * C.ncc
-                                          : (tch ? (size_t)C.nsc + (size_t)b * C.ncn : (size_t)C.nsc + C.nsn + (size_t)b * C.ncn);
-  const size_t cslab0 = noisy ? (size_t)C.nsc + (size_t)b * C.ncn : (size_t)b * C.ncc;
-  const int erow = kind == KIND_CLEAN ? b : (tch ? C.Bc + b : C.Bc + C.Bn + b);
-  const int vrow = noisy ? C.Bc + b : b;
-  float* red = scratch;            // [8] length partials
-  float* zred = scratch + 8;       // [4 classes][4 waves]
-  // every load first: length flags, slab partials (slab order), W2 columns
-  float len = 0.0f;
-  for (int t = tid; t < T; t += DAD_ENC_WS_THREADS) len += pad[(size_t)b * T + t] == 0 ? 1.0f : 0.0f;
-  const float* src = half == 0 ? p.part_sum + slab0 * DAD_H : p.part_cnt + cslab0 * DAD_H;
-  float sv = 0.0f;
-  if (half == 0 || !tch)
-    for (int c = 0; c < nc; ++c) sv += src[(size_t)c * DAD_H + h];
-  const float* pw = tch ? p.teacher : p.student;
-  float w2[4];
-#pragma unroll
-  for (int c = 0; c < 4; ++c) w2[c] = pw[DAD_OFF_W2 + c * DAD_H + h];
-  const float kv = tch ? 1.0f
-                       : (kind == KIND_CLEAN ? keep_value(p.keep1, p.key_drop1, b, h, p.p_drop, p.drop_scale)
-                                             : keep_value(p.keep2, p.key_drop2, b, h, p.p_drop, p.drop_scale));
-  len = dad_wave_sum(len);   // an integer count: exact in any order
-  if (lane == 0) red[w] = len;
-  __syncthreads();
-  len = 0.0f;
-#pragma unroll
-  for (int k = 0; k < DAD_ENC_WS_THREADS / 64; ++k) len += red[k];
-  if (half == 0) {
-    const float e = sv / fmaxf(len, 1.0f);
-    p.emb[(size_t)erow * DAD_H + h] = e;
-    const float d = tch ? e : e * kv;   // teacher classifier: dropout p = 0 (I/model.py:121)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const float z = dad_wave_sum(w2[c] * d);
-      if (lane == 0) zred[c * 4 + w] = z;
-    }
-  } else if (!tch) {
-    p.cnt_tot[(size_t)vrow * DAD_H + h] = sv;
-  }
-  if (tid == 0) p.vlen[vrow] = len;
-  __syncthreads();
-  if (tid < 4) {
-    const float dot = ((zred[tid * 4] + zred[tid * 4 + 1]) + zred[tid * 4 + 2]) + zred[tid * 4 + 3];
-    const float bias = (tch ? p.teacher : p.student)[DAD_OFF_B2 + tid];
-    p.logits[(size_t)erow * DAD_C + tid] = dot + bias;
-  }
-  __syncthreads();   // scratch free for the next task
-}
-
-// Arrival: each run of this workgroup's jobs on one (kind, utterance) adds its slab count to
-// that counter; the arrival that completes the utterance (count = its slabs) resets the counter
-// and pools.  Release: every wave has drained its stores (vmcnt(0) at the end of ws_loop), then
-// one agent-scope release fence before the counters; acquire: one agent fence before the reads
-// (MI355X guide, Guideline 16, counter form).
-// Measured (A/B, 400-step benches, same box): the encoder launch 62.5 -> 74.8 us with it (71.0
-// with write-through partial stores and no release fence instead, which cost the default path
-// ~0.5 us), the pool launch gone; the step 120.6 -> 128.4 us (123.9): the workgroups that finish
-// last are the ones that pool, each after a cross-XCD hand-off of its utterances' partials.  Off
-// by default (DAD_POOL_FUSE=1 enables it; parity tests pass either way).
-template <int WAVES>
-__device__ __forceinline__ void ws_pool_arrive(const DadEncodeArgs& a, const Ctx& C, bool teacher, const JobMap& jm,
-                                               int nj, char* smem) {
-  const int tid = threadIdx.x, lane = tid & 63;
-  int* tasks = reinterpret_cast<int*>(smem + kOffVB);              // the valid-bit table is free now
-  float* scratch = reinterpret_cast<float*>(smem + kOffFK);        // so is the feature-flag table
-  __syncthreads();
-  if (tid < 64) {
-    if (lane == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (keep: the fence's own wait can be dropped)
-    }
-    int ntask = 0;
-    for (int l0 = 0; l0 < nj; l0 += 64) {
-      const int l = l0 + lane;
-      int key = -1, nck = 1;
-      if (l < nj) {
-        const Job J = job_of(C, teacher, jm(l));
-        key = J.kind * DAD_MAX_BATCH + J.b;
-        nck = J.kind == KIND_CLEAN ? C.ncc : C.ncn;
-      }
-      const int prev = __shfl_up(key, 1, 64);
-      const bool head = (l < nj) && (lane == 0 || prev != key);
-      const uint64_t heads = __ballot(head);
-      const int nv = min(64, nj - l0);
-      int n = 0;
-      if (head) {
-        const uint64_t after = heads & ~((2ull << lane) - 1ull);   // heads above this lane
-        const int next = after ? (int)__builtin_ctzll(after) : nv;
-        n = next - lane;
-      }
-      bool last = false;
-      if (head) {
-        const uint32_t old = __hip_atomic_fetch_add(&a.pool_cnt[key], (uint32_t)n, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
-        last = old + (uint32_t)n == (uint32_t)nck;
-        if (last) __hip_atomic_store(&a.pool_cnt[key], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      const uint64_t lasts = __ballot(last);
-      if (last) tasks[1 + ntask + (int)__popcll(lasts & ((1ull << lane) - 1ull))] = key;
-      ntask += (int)__popcll(lasts);
-    }
-    if (lane == 0) {
-      tasks[0] = ntask;
-      if (ntask) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  const int ntask = tasks[0];
-  for (int t = 0; t < ntask; ++t) ws_pool_one(a, C, tasks[1 + t], scratch);
-}
-
 // NOISE: 0 = counter RNG, 1 = explicit noise tensors (parity mode)
-template <int WAVES, int NOISE>
+template <int WAVES, int NOISE, bool F16>
 __device__ __forceinline__ void encode_ws_body(const DadEncodeArgs& a, char* smem) {
   using S = Shape<WAVES>;
   WS_STAMP(0, DAD_PROBE_WALL());
@@ -824,23 +648,11 @@ __device__ __forceinline__ void encode_ws_body(const DadEncodeArgs& a, char* sme
   const Ctx C = ctx_of(a);
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  if (a.pool_cnt && blockIdx.x == 0) {
-    // dad_pool's zeroing: the ECDA row flags and per-class terms that the ECDA blocks then set
-    // (their readers, the previous step's wgrad and reduce, have finished: stream order)
-    for (int i = tid; i < C.Bc + C.Bn; i += S::kThreads) a.pool.eflag[i] = 0u;
-    if (tid < 2 * DAD_C) a.pool.tail_terms[tid] = 0.0f;
-  }
   bool teacher;
   int j0, j1;
   job_range(C, blockIdx.x, a.ws_nt, a.ws_ns, a.ws_wstrong, teacher, j0, j1);
-  JobMap jm{j0, j1 - j0, 0};
-  int nj = j1 - j0;
-  if (!teacher && a.ws_tab_n > 0) {
-    const int k = (int)blockIdx.x - a.ws_nt;
-    const int s0 = a.ws_tab[k][0], s1 = a.ws_tab[k][1], c0 = a.ws_tab[k][2], c1 = a.ws_tab[k][3];
-    jm = JobMap{C.Jc + s0, s1 - s0, c0};
-    nj = (s1 - s0) + (c1 - c0);
-  }
+  const JobMap jm{j0};
+  const int nj = j1 - j0;
   if (nj <= 0) return;
   const uint32_t sbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;   // LDS byte address
 
@@ -862,26 +674,26 @@ __device__ __forceinline__ void encode_ws_body(const DadEncodeArgs& a, char* sme
   __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): the pad / u loads retired (no DMA in flight yet)
   lds_barrier();                        // fk / vb visible
   WS_STAMP(1, DAD_PROBE_WALL());
-  const bf16x8* W = reinterpret_cast<const bf16x8*>(teacher ? a.w1bf_teacher : a.w1bf_student);
+  const bf16x8* W = reinterpret_cast<const bf16x8*>(teacher ? a.w1h_teacher : a.w1h_student);
   const float* bias = teacher ? a.b1_teacher : a.b1_student;
-  if (teacher) ws_loop<WAVES, NOISE, true>(C, jm, 2 * nj, w, lane, smem, sbase, W, bias, fk, vb);
-  else ws_loop<WAVES, NOISE, false>(C, jm, 2 * nj, w, lane, smem, sbase, W, bias, fk, vb);
-  if (a.pool_cnt) ws_pool_arrive<WAVES>(a, C, teacher, jm, nj, smem);
+  if (teacher) ws_loop<WAVES, NOISE, true, F16>(C, jm, 2 * nj, w, lane, smem, sbase, W, bias, fk, vb);
+  else ws_loop<WAVES, NOISE, false, F16>(C, jm, 2 * nj, w, lane, smem, sbase, W, bias, fk, vb);
   WS_STAMP(2, DAD_PROBE_WALL());
   WS_STAMP(3, ((unsigned long long)teacher << 16) | (unsigned long long)(2 * nj));
 }
 
 
 // Counter-RNG (throughput) and explicit-noise (parity) kernels are separate so the noise
-// loads do not share the register allocation of the throughput kernel.
-__global__ __launch_bounds__(DAD_ENC_WS_THREADS, 1) void dad_encode_ws(DadEncodeArgs a) {
-  DAD_GUARD_BLOCK(DAD_ENC_WS_THREADS);
-  __shared__ __attribute__((aligned(16))) char smem[kLds];
-  encode_ws_body<DAD_ENC_WS_THREADS / 64, 0>(a, smem);
-}
-
-__global__ __launch_bounds__(DAD_ENC_WS_THREADS, 1) void dad_encode_ws_explicit(DadEncodeArgs a) {
-  DAD_GUARD_BLOCK(DAD_ENC_WS_THREADS);
-  __shared__ __attribute__((aligned(16))) char smem[kLds];
-  encode_ws_body<DAD_ENC_WS_THREADS / 64, 1>(a, smem);
-}
+// loads do not share the register allocation of the throughput kernel; fp16 and bf16 operand
+// kernels likewise.
+#define DAD_WS_KERNEL(name, NOISE, F16)                                              \
+  __global__ __launch_bounds__(DAD_ENC_WS_THREADS, 1) void name(DadEncodeArgs a) {   \
+    DAD_GUARD_BLOCK(DAD_ENC_WS_THREADS);                                             \
+    __shared__ __attribute__((aligned(16))) char smem[kLds];                         \
+    encode_ws_body<DAD_ENC_WS_THREADS / 64, NOISE, F16>(a, smem);                    \
+  }
+DAD_WS_KERNEL(dad_encode_ws, 0, false)
+DAD_WS_KERNEL(dad_encode_ws_explicit, 1, false)
+DAD_WS_KERNEL(dad_encode_ws_f16, 0, true)
+DAD_WS_KERNEL(dad_encode_ws_f16_explicit, 1, true)
+#undef DAD_WS_KERNEL

@@ -7,8 +7,9 @@
 //
 // One elementwise pass over the flat [W1|b1|W2|b2] vectors; every block re-derives the
 // clip coefficient from the same squared-norm partials in the same order, so the result
-// is identical across blocks (and across data-parallel ranks).  The bf16 shadows of W1
-// used by the BF16 forward are refreshed in the same pass.
+// is identical across blocks (and across data-parallel ranks).  The 16-bit shadows of W1
+// used by the FP16/BF16 forward (fp16 when the step's precision is FP16, else bf16) are
+// refreshed in the same pass.
 #include "dad_common.h"
 #include "dad_kernels.h"
 
@@ -60,8 +61,8 @@ __device__ __forceinline__ void adam_load(size_t n0, const float* __restrict__ g
 __device__ __forceinline__ void adam_ema_apply(const dad_config& cfg, float coef, size_t n0, const AdamOperands& o,
                                                float* __restrict__ student,
                                                 float* __restrict__ teacher, float* __restrict__ exp_avg,
-                                                float* __restrict__ exp_avg_sq, __bf16* __restrict__ w1bf_s,
-                                                __bf16* __restrict__ w1bf_t) {
+                                                float* __restrict__ exp_avg_sq, uint16_t* __restrict__ w1bf_s,
+                                                uint16_t* __restrict__ w1bf_t, bool f16) {
   const int tid = threadIdx.x;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -86,15 +87,15 @@ __device__ __forceinline__ void adam_ema_apply(const dad_config& cfg, float coef
     }
     if (i < (size_t)DAD_H * DAD_D) {
       const uint32_t f = dad_w1frag_index((uint32_t)(i / DAD_D), (uint32_t)(i % DAD_D));
-      w1bf_s[f] = (__bf16)p;
-      w1bf_t[f] = (__bf16)t;
+      w1bf_s[f] = dad_half_bits(p, f16);
+      w1bf_t[f] = dad_half_bits(t, f16);
     }
   }
 }
 
 // The same update with 4 CONSECUTIVE parameters per thread (i = n0 + 4 tid .. +3; DAD_NPARAM and
 // the W1 size are multiples of 4): one 16-B load per stream and one 16-B store per written stream,
-// and the 4 bf16 shadow values of a thread are 4 consecutive k of one h, i.e. 8 contiguous bytes
+// and the 4 16-bit shadow values of a thread are 4 consecutive k of one h, i.e. 8 contiguous bytes
 // of the fragment-major shadow (dad_w1frag_index: k & 7 is the innermost index).  The scalar
 // form issued 20 loads and 24 stores per thread, 8 of them 2-byte stores to scattered shadow
 // slots; the kernel's length was set by issuing them.  Used when every stream is 16-B aligned.
@@ -118,7 +119,8 @@ __device__ __forceinline__ void adam_load4(size_t i0, const float* __restrict__ 
 __device__ __forceinline__ void adam_ema_apply4(const dad_config& cfg, float coef, size_t i0, const AdamOperands4& o,
                                                 float* __restrict__ student, float* __restrict__ teacher,
                                                 float* __restrict__ exp_avg, float* __restrict__ exp_avg_sq,
-                                                __bf16* __restrict__ w1bf_s, __bf16* __restrict__ w1bf_t) {
+                                                uint16_t* __restrict__ w1bf_s, uint16_t* __restrict__ w1bf_t,
+                                                bool f16) {
   if (i0 >= DAD_NPARAM) return;
   f32x4 mo, vo, po, to;
 #pragma unroll
@@ -144,14 +146,12 @@ __device__ __forceinline__ void adam_ema_apply4(const dad_config& cfg, float coe
   const f32x4 tt = cfg.warmup ? o.t : to;
   if (i0 < (size_t)DAD_H * DAD_D) {
     const uint32_t f = dad_w1frag_index((uint32_t)(i0 / DAD_D), (uint32_t)(i0 % DAD_D));
-    bf16x4 bs, bt;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      bs[e] = (__bf16)po[e];
-      bt[e] = (__bf16)tt[e];
-    }
-    *reinterpret_cast<bf16x4*>(w1bf_s + f) = bs;
-    *reinterpret_cast<bf16x4*>(w1bf_t + f) = bt;
+    const uint2 bs = f16 ? uint2{dad_pack2<true>(po[0], po[1]), dad_pack2<true>(po[2], po[3])}
+                         : uint2{dad_pack2<false>(po[0], po[1]), dad_pack2<false>(po[2], po[3])};
+    const uint2 bt = f16 ? uint2{dad_pack2<true>(tt[0], tt[1]), dad_pack2<true>(tt[2], tt[3])}
+                         : uint2{dad_pack2<false>(tt[0], tt[1]), dad_pack2<false>(tt[2], tt[3])};
+    *reinterpret_cast<uint2*>(w1bf_s + f) = bs;
+    *reinterpret_cast<uint2*>(w1bf_t + f) = bt;
   }
 }
 
@@ -193,11 +193,13 @@ __global__ __launch_bounds__(DAD_OPTIM_THREADS) void dad_optim(DadOptimArgs a) {
       for (int k = 0; k < 4; ++k) a.losses_out[k] = ex[12 + k];
   }
   if (blockIdx.x == 0) dacp_commit(cfg, a.grad, a.dacp, tid);
+  const bool f16 = cfg.precision == DAD_PREC_FP16;
   if (vec)
     adam_ema_apply4(cfg, coef, n0 + 4 * (size_t)tid, o4, a.student, a.teacher, a.exp_avg, a.exp_avg_sq,
-                    a.w1bf_student, a.w1bf_teacher);
+                    a.w1h_student, a.w1h_teacher, f16);
   else
-    adam_ema_apply(cfg, coef, n0, o, a.student, a.teacher, a.exp_avg, a.exp_avg_sq, a.w1bf_student, a.w1bf_teacher);
+    adam_ema_apply(cfg, coef, n0, o, a.student, a.teacher, a.exp_avg, a.exp_avg_sq, a.w1h_student, a.w1h_teacher,
+                   f16);
 }
 
 // DACPManager.update_class_quality_scores_epoch (I/utils.py:430-447)
@@ -211,13 +213,13 @@ __global__ void dad_epoch_end_kernel(float* dacp, float beta, float one_m_beta) 
   dacp[12 + c] = 0.0f;
 }
 
-__global__ __launch_bounds__(256) void dad_shadow_kernel(const float* student, const float* teacher, __bf16* ws,
-                                                         __bf16* wt) {
+__global__ __launch_bounds__(256) void dad_shadow_kernel(const float* student, const float* teacher, uint16_t* ws,
+                                                         uint16_t* wt, int f16) {
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (i < (size_t)DAD_H * DAD_D) {
     const uint32_t f = dad_w1frag_index((uint32_t)(i / DAD_D), (uint32_t)(i % DAD_D));
-    ws[f] = (__bf16)student[i];
-    wt[f] = (__bf16)teacher[i];
+    ws[f] = dad_half_bits(student[i], f16 != 0);
+    wt[f] = dad_half_bits(teacher[i], f16 != 0);
   }
 }
 

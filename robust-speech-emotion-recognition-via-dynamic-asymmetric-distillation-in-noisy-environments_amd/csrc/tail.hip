@@ -162,6 +162,13 @@ __global__ __launch_bounds__(DAD_POOL_THREADS) void dad_pool(DadPoolArgs a) {
   for (int c = 0; c < DAD_C; ++c)
     zp[c] = dad_wave_sum(((w2[c][0] * d[0] + w2[c][1] * d[1]) + w2[c][2] * d[2]) + w2[c][3] * d[3]);
   if (lane < DAD_C) a.logits[(size_t)erow * DAD_C + lane] = (lane == 0 ? zp[0] : (lane == 1 ? zp[1] : (lane == 2 ? zp[2] : zp[3]))) + bias;
+  // range check: a non-finite embedding or logit sets the sticky flag.  In FP16 steps an encoder
+  // operand beyond +-65504 converts to inf, which turns every pre-activation of its row into
+  // +-inf or NaN: the +inf units survive the ReLU into the pooled sum.
+  const bool fin = __builtin_isfinite(e[0]) & __builtin_isfinite(e[1]) & __builtin_isfinite(e[2]) &
+                   __builtin_isfinite(e[3]) & __builtin_isfinite(((zp[0] + zp[1]) + zp[2]) + zp[3]);
+  if (__ballot(!fin) != 0 && lane == 0 && a.range_flag)
+    __hip_atomic_fetch_or(a.range_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (!teacher) {
     // active-row count per (utterance, h) of the branch that gets a gradient (clean / strong);
     // the length, and the ECDA row flag (clean b / noisy Bc + b) starts at zero: the ECDA

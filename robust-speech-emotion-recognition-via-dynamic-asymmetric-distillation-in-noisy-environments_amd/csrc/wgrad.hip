@@ -8,13 +8,8 @@
 // G is rebuilt on the fly from the ReLU' bit mask written by the forward and the
 // per-(utterance, h) scale dL/de / len.  The strong branch's augmented input is
 //   FP32: regenerated exactly (same counter-RNG function, or re-read explicit noise);
-//   BF16: re-read from the bf16 copy the forward stored (the exact MFMA operand it used).
-//
-// FP32 fused step (per_utt = 1): the loss-dependent scale factors out of the row sum,
-//   dW1[h][:] = sum_u (dL/de_u[h] / len_u) * S_u[h][:],   S_u = bits_u^T X_u,
-// so the GEMM runs as soon as the forward has produced the bits (on a second stream) and
-// dad_wsum applies the scale.  BF16 fused step: dad_wgrad_direct after the losses, with the
-// scale folded into the A operand (one GEMM, no S_u round trip through HBM).
+//   FP16/BF16: re-read from the 16-bit copy the forward stored (the exact MFMA operand it used).
+// Both run after the losses as one direct split-K GEMM with the loss scale folded into G.
 #include <type_traits>
 
 #include "dad_common.h"
@@ -59,19 +54,12 @@ __device__ __forceinline__ int wg_total(const DadWgradArgs& a) {
   return a.g.Bc * a.g.ncc + (a.warmup ? 0 : a.g.Bn * a.g.ncn);
 }
 
-// slab range [s0, s1) of a split: contiguous share of all slabs, or (per_utt) the slabs
-// of utterance `split` (clean utterances first, then noisy)
+// slab range [s0, s1) of a split: a contiguous share of all slabs
 __device__ __forceinline__ void wg_range(const DadWgradArgs& a, int split, int& s0, int& s1) {
-  if (a.per_utt) {
-    const DadGeom& g = a.g;
-    if (split < g.Bc) { s0 = split * g.ncc; s1 = s0 + g.ncc; }
-    else { s0 = g.Bc * g.ncc + (split - g.Bc) * g.ncn; s1 = s0 + g.ncn; }
-  } else {
-    const int total = wg_total(a);
-    const int per = (total + a.splits - 1) / a.splits;
-    s0 = split * per;
-    s1 = min(total, s0 + per);
-  }
+  const int total = wg_total(a);
+  const int per = (total + a.splits - 1) / a.splits;
+  s0 = split * per;
+  s1 = min(total, s0 + per);
 }
 
 // Fused step: dL/de of utterance row u (clean u < Bc, strong Bc + b), hidden unit h: the
@@ -122,9 +110,9 @@ __device__ __forceinline__ float fused_ge1(const DadReduceArgs& a, int Bc, int u
 // The strong branch's augmentation is regenerated per element (counter RNG or explicit noise).
 constexpr int F32_GP = 36;   // G tile pitch per h: [kh][16 pairs] + 4 floats (conflict-free b128 reads)
 
-// the scale of G: 1 (S_u mode), dL/de / len from a dL/de buffer, or rebuilt from the tail's
-// dL/dz and the ECDA rows (fused step, fused_ge1)
-enum { F32_SU = 0, F32_GE = 1, F32_FUSED = 2 };
+// the scale of G: dL/de / len from a dL/de buffer (modular encoder backward), or rebuilt from
+// the tail's dL/dz and the ECDA rows (fused step, fused_ge1)
+enum { F32_GE = 1, F32_FUSED = 2 };
 
 struct F32X {
   float x[16], n[16];
@@ -186,10 +174,10 @@ template <int MODE, bool KEEPX>
 __device__ __forceinline__ void f32_gbuild(const DadWgradArgs& a, const DadReduceArgs& ra, int s, int h,
                                            const float (&w2h)[4], const F32GIn& gi, float* G) {
   const SlabIdx q = wg_slab(a, s);
-  float scale = 1.0f;
+  float scale = 0.0f;
   if constexpr (MODE == F32_GE) scale = gi.ec / fmaxf(a.vlen[q.erow], 1.0f);
   if constexpr (MODE == F32_FUSED) {
-    // dL/de_u[h] / max(1, len_u), as dad_wgrad_direct builds it (bf16 there, f32 here)
+    // dL/de_u[h] / max(1, len_u), as dad_wgrad_direct builds it (16-bit there, f32 here)
     const int u = q.erow;
     const f32x4 gz = *reinterpret_cast<const f32x4*>(ra.gzb + (size_t)u * DAD_C);
     scale = fused_ge1_v<KEEPX>(ra, a.g.Bc, u, h, w2h, gz, ra.eflag[u], gi.ec) / fmaxf(ra.vlen[u], 1.0f);
@@ -299,8 +287,7 @@ __device__ __forceinline__ void wgrad_f32_store(const DadWgradArgs& a, const Dad
 }
 template <bool EXPLICIT>
 __device__ __forceinline__ void wgrad_f32_mode(const DadWgradArgs& a, const DadReduceArgs& ra, float* Gs) {
-  if (a.per_utt) wgrad_f32_store<EXPLICIT, F32_SU, false>(a, ra, Gs);
-  else if (ra.gzb == nullptr) wgrad_f32_store<EXPLICIT, F32_GE, false>(a, ra, Gs);
+  if (ra.gzb == nullptr) wgrad_f32_store<EXPLICIT, F32_GE, false>(a, ra, Gs);
   else if (ra.keep1) wgrad_f32_store<EXPLICIT, F32_FUSED, true>(a, ra, Gs);
   else wgrad_f32_store<EXPLICIT, F32_FUSED, false>(a, ra, Gs);
 }
@@ -313,10 +300,10 @@ __global__ __launch_bounds__(DAD_WGRAD_THREADS) void dad_wgrad_f32(DadWgradArgs 
   else wgrad_f32_mode<false>(a, ra, Gs);
 }
 
-// ------------------------------------------------------------ BF16 (throughput mode)
+// ------------------------------------------------------- FP16 / BF16 (throughput modes)
 // Direct split-K GEMM after the losses: dW1 = sum_rows G[row]^T x[row] with
 //   G[row][h] = ReLU'(row, h) * valid(row) * dL/de_u[h] / max(1, len_u)      (u = row's utterance)
-// x is the encoder's bf16 copy of the student's MFMA input (clean rows, then the
+// x is the encoder's 16-bit copy of the student's MFMA input (clean rows, then the
 // strong-augmented rows), so one loop with one load type covers both branches.
 // One workgroup per (column block of WGD_DB d, split of the slab list), two groups of 4 waves
 // (two waves per SIMD): the groups take alternate slabs of the split and their accumulators
@@ -327,14 +314,18 @@ __global__ __launch_bounds__(DAD_WGRAD_THREADS) void dad_wgrad_f32(DadWgradArgs 
 //   G is never staged: each lane loads the ReLU' row masks (one u32 per h) of its own two
 //     hidden units straight into registers, and its A fragment (8 rows of one h) is byte
 //     (16 ks + 8 (lane/32)) of that mask, expanded through a 256-entry LDS table into four
-//     0xFFFF/0 dword masks and AND-ed with bf16(dL/de_u[h] / len_u) in both halves: one
+//     0xFFFF/0 dword masks and AND-ed with the 16-bit dL/de_u[h] / len_u in both halves: one
 //     bitfield extract, one table read and four ANDs per fragment.  (The loop is bound by
 //     vector issue, about ten VALU instructions per MFMA, so table reads replace arithmetic.)
+// FP16: the per-utterance scales are stored as fp16(v * 2^s) with one power of two 2^s per
+// workgroup (its largest |v| maps into [2^14, 2^15): 11 significant bits and no overflow or
+// subnormals for values within 2^-28 of the largest), and the partial is multiplied by 2^-s
+// (exact) before it is stored.
 // Software pipeline, one barrier per TWO rounds: round j computes slab j from LDS buffer j&3
 // while it stages slab j+2 into buffer (j+2)&3 and issues the loads of slab j+2+WGD_DEPTH,
 // all in one basic block so the staging VALU fills the MFMA gaps.  dL/de_u[h] / len_u of the
 // workgroup's utterances is rebuilt in the prologue (fused_ge1) while the first loads are in
-// flight.  Output: one f32 partial slab per split, summed in fixed order by dad_reduce.
+// flight.  Output: one f32 partial slab per split, summed in fixed order by dad_reduce_w.
 static_assert(WGD_THREADS == 256 * WGD_GROUPS && DAD_H == 256, "dad_wgrad_direct: groups of 256 threads, thread = h");
 static_assert(WGD_GROUPS == 1 || WGD_GROUPS == 2, "dad_wgrad_direct: one or two slab groups");
 static_assert(WGD_DB == 64 && DAD_D % WGD_DB == 0, "dad_wgrad_direct: 8 threads x 8 columns per row");
@@ -349,7 +340,8 @@ namespace {
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
-__device__ __forceinline__ bf16x8 tr_frag(const __bf16* tile, int pitch, int rowbase, int colbase) {
+// B fragment (k-major) of the x tile: 8 x 16-bit in a bf16x8 register container
+__device__ __forceinline__ bf16x8 tr_frag(const uint16_t* tile, int pitch, int rowbase, int colbase) {
   const int lane = threadIdx.x & 63;
   const int g = lane >> 4, li = lane & 15;
   const int q = li >> 2, p = li & 3;
@@ -370,14 +362,14 @@ __device__ __forceinline__ bf16x8 tr_frag(const __bf16* tile, int pitch, int row
 // for everyone) and the ReLU' row masks of its own A-fragment hidden units (kept in
 // registers); the slab's utterance slot and valid row count are wave-uniform
 struct WgdSlab {
-  bf16x8 x;
+  u32x4 x;
   uint32_t mw[2];
   int ul, nvalid;
 };
 
 // Slab table of one group, one slab per lane: lane l describes the group's slab j = l,
 // global slab s0 + grp + WGD_GROUPS l (clean slabs first, then strong): its first x row (rows of the
-// bf16 copy: clean [b][Tc], then strong [b][Tn]) and (utterance slot << 8 | valid rows).
+// 16-bit copy: clean [b][Tc], then strong [b][Tn]) and (utterance slot << 8 | valid rows).
 // A load reads its slab's entry with v_readlane, so no cursor arithmetic runs per slab.
 struct WgdTable {
   int row0, info;
@@ -406,30 +398,28 @@ __device__ __forceinline__ void wgd_load(const DadWgradArgs& a, const WgdTable& 
   r.nvalid = info & 255;
   r.ul = info >> 8;
   const int row = min(tid >> 3, r.nvalid - 1);
-  const __bf16* xb = a.xs_bf16 + (size_t)row0 * DAD_D + dbase;
+  const uint16_t* xb = a.xs16 + (size_t)row0 * DAD_D + dbase;
   const uint32_t* mb = a.bits + (size_t)(sfirst + WGD_GROUPS * j) * DAD_H;
-  r.x = *reinterpret_cast<const bf16x8*>(xb + row * DAD_D + (tid & 7) * 8);
+  r.x = *reinterpret_cast<const u32x4*>(xb + row * DAD_D + (tid & 7) * 8);
   // masks of h = 32 (2 wv + m) + lane % 32 (both 32-lane halves load the same words)
 #pragma unroll
   for (int m = 0; m < 2; ++m) r.mw[m] = mb[(2 * wv + m) * 32 + (tid & 31)];
 }
 
-__device__ __forceinline__ void wgd_stage(const WgdSlab& r, __bf16* Xt) {
+__device__ __forceinline__ void wgd_stage(const WgdSlab& r, uint16_t* Xt) {
   const int tid = threadIdx.x & 255;
   const int row = tid >> 3;
   // rows past the utterance hold a copy of its last row (finite); their ReLU' mask bits are 0
-  *reinterpret_cast<uint4*>(&Xt[row * WGD_XP + (tid & 7) * 8]) = __builtin_bit_cast(uint4, r.x);
+  *reinterpret_cast<u32x4*>(&Xt[row * WGD_XP + (tid & 7) * 8]) = r.x;
 }
 
-// A fragment of h tile ht, k rows 16 ks + 8 (lane/32) + 0..7: bit ? gb : 0 (bf16 bits).
+// A fragment of h tile ht, k rows 16 ks + 8 (lane/32) + 0..7: bit ? gb : 0 (16-bit pattern).
 // lut[b][s] = the 0xFFFF/0 halfword masks of the 8 bits of byte b (16 B), once per 16-B bank
 // slot s (64 KB): lane l reads slot l & 15, which is a different slot for every lane of each
 // ds_read_b128 lane group ({0-3,12-15,20-27}, {4-11,16-19,28-31}, and +32), so the
 // data-dependent bytes never meet on a bank (one table with one copy: 27 % of the kernel's
 // LDS cycles were bank conflicts).  One bitfield extract and one 16-B LDS read per fragment.
-#ifndef WGD_LUT_SLOTS
-#define WGD_LUT_SLOTS 16   // 1: one 4 KB table (27 % of the LDS cycles bank conflicts)
-#endif
+constexpr int WGD_LUT_SLOTS = 16;
 constexpr int WGD_LUT = 256 * WGD_LUT_SLOTS;
 __device__ __forceinline__ uint4 wgd_amask(uint32_t mask, const uint4* lut, int ks) {
   const int lane = threadIdx.x & 63;
@@ -451,13 +441,12 @@ struct WgdRaw {
   uint32_t gp[2];
 };
 
-template <bool SU>
-__device__ __forceinline__ WgdRaw wgd_read(const __bf16* Xt, const uint32_t (&mk)[2], const uint4* lut,
+__device__ __forceinline__ WgdRaw wgd_read(const uint16_t* Xt, const uint32_t (&mk)[2], const uint4* lut,
                                            const uint16_t* gs, int ul, int wv) {
   WgdRaw w;
   const int i = threadIdx.x & 31;
 #pragma unroll
-  for (int m = 0; m < 2; ++m) w.gp[m] = SU ? 0x3f80u : gs[ul * DAD_H + (2 * wv + m) * 32 + i];   // SU: bf16 1.0
+  for (int m = 0; m < 2; ++m) w.gp[m] = gs[ul * DAD_H + (2 * wv + m) * 32 + i];
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
 #pragma unroll
@@ -488,14 +477,20 @@ __device__ __forceinline__ WgdFrag wgd_finish(const WgdRaw& w) {
   return f;
 }
 
+template <bool F16>
 __device__ __forceinline__ void wgd_mma(const WgdFrag& f, f32x16 (&acc)[2][2]) {
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
-      for (int n = 0; n < 2; ++n)
-        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[ks][m], f.b[ks][n], acc[m][n], 0, 0, 0);
+      for (int n = 0; n < 2; ++n) {
+        if constexpr (F16)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, f.a[ks][m]),
+                                                             __builtin_bit_cast(f16x8, f.b[ks][n]), acc[m][n], 0, 0, 0);
+        else
+          acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[ks][m], f.b[ks][n], acc[m][n], 0, 0, 0);
+      }
 }
 
 __device__ __forceinline__ int wgd_utt(const DadGeom& g, int s) {
@@ -503,23 +498,23 @@ __device__ __forceinline__ int wgd_utt(const DadGeom& g, int s) {
   return s < nsc ? s / g.ncc : g.Bc + (s - nsc) / g.ncn;
 }
 
+// power of two 2^s with max_abs * 2^s in [2^14, 2^15) (1 for 0 or a non-finite max)
+__device__ __forceinline__ int wgd_f16_exp(float max_abs) {
+  if (!(max_abs > 0.0f) || !__builtin_isfinite(max_abs)) return 0;
+  int e = 0;
+  (void)frexpf(max_abs, &e);   // max_abs = f 2^e, f in [0.5, 1)
+  return min(max(15 - e, -126), 126);
+}
+
 }  // namespace
 
-#ifndef WGD_PRIO
-#define WGD_PRIO 0   // 1 / 2: s_setprio 1 for slab group 0 / 1 in the loop (A/B option)
-#endif
-#ifndef WGD_NBUF
-#define WGD_NBUF 4   // x-tile LDS buffers per slab group (8: staging 4 rounds ahead, a barrier every 4 rounds)
-#endif
-// WGD_WT: partial-slab stores write-through (sc1): no dirty L2 lines left for the kernel-end release
-#ifndef WGD_WT
-#define WGD_WT 0
-#endif
-// one 256 h x WGD_DB d tile over slabs [s0, s1): fp32 partial (direct) or bf16 S_u (SU)
-template <bool SU>
+// x-tile LDS buffers per slab group: a slab is staged two rounds before it is read, one barrier
+// per two rounds (eight buffers and a barrier every four rounds measured neutral, round 3)
+constexpr int WGD_NBUF = 4;
+// one 256 h x WGD_DB d tile over slabs [s0, s1): fp32 partial
+template <bool F16>
 __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceArgs& ra, int s0, int s1, int dbase,
-                                         float* outf, __bf16* outb, __bf16* Xt, const uint4* lut, uint16_t* gs,
-                                         float* red) {
+                                         float* outf, uint16_t* Xt, const uint4* lut, uint16_t* gs, float* red) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane((tid >> 6) & 3);
   const int grp = __builtin_amdgcn_readfirstlane(tid >> 8);
@@ -529,6 +524,7 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
   for (int m = 0; m < 2; ++m)
 #pragma unroll
     for (int n = 0; n < 2; ++n) acc[m][n] = f32x16{};
+  float unscale = 1.0f;   // FP16: 2^-s
   for (int k = 0; DAD_PROBE_ON && k < 10; ++k)
     if (tid == 0 && blockIdx.x < 512) DAD_PROBE_SET(wgd_stamps, blockIdx.x * 10 + k, 0);
   const unsigned long long t0 = WGD_CLK();
@@ -541,28 +537,26 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
     const int mine = (n - grp + WGD_GROUPS - 1) / WGD_GROUPS;   // group 1 may have one slab fewer
     const int cntmin = n / WGD_GROUPS;
     const int u0 = wgd_utt(g, s0), nu = wgd_utt(g, s1 - 1) - u0 + 1;
-    __bf16* Xg = Xt + grp * (WGD_NBUF * DAD_SLAB * WGD_XP);   // this group's WGD_NBUF LDS buffers
-    // dL/de_u[h] / max(1, len_u) of this split's utterances (thread = h of each group) as bf16;
+    uint16_t* Xg = Xt + grp * (WGD_NBUF * DAD_SLAB * WGD_XP);   // this group's WGD_NBUF LDS buffers
+    // dL/de_u[h] / max(1, len_u) of this split's utterances (thread = h of each group) as 16-bit;
     // the host bounds a split to WGD_MAXU slabs, hence utterances.  In each batch of eight
     // utterances group g builds entries 4g .. 4g+3 (KG per group).  The first batch's vector
     // loads (dL/dz, ECDA row and flag, length) go out before the slab prefetch, so their math
     // never waits on it.
     constexpr int KG = 8 / WGD_GROUPS;
     const int hh = tid & (DAD_H - 1);
-    float w2[4] = {0.0f, 0.0f, 0.0f, 0.0f}, ec0[KG], vl0[KG];
+    float w2[4], ec0[KG], vl0[KG];
     f32x4 gz0[KG];
     uint32_t ef0[KG];
-    if (!SU) {
 #pragma unroll
-      for (int c = 0; c < 4; ++c) w2[c] = ra.student[DAD_OFF_W2 + c * DAD_H + hh];
+    for (int c = 0; c < 4; ++c) w2[c] = ra.student[DAD_OFF_W2 + c * DAD_H + hh];
 #pragma unroll
-      for (int k = 0; k < KG; ++k) {
-        const int u = u0 + min(grp * KG + k, nu - 1);
-        ec0[k] = ra.ge_ecda[(size_t)u * DAD_H + hh];
-        gz0[k] = *reinterpret_cast<const f32x4*>(ra.gzb + (size_t)u * DAD_C);
-        ef0[k] = ra.eflag[u];
-        vl0[k] = ra.vlen[u];
-      }
+    for (int k = 0; k < KG; ++k) {
+      const int u = u0 + min(grp * KG + k, nu - 1);
+      ec0[k] = ra.ge_ecda[(size_t)u * DAD_H + hh];
+      gz0[k] = *reinterpret_cast<const f32x4*>(ra.gzb + (size_t)u * DAD_C);
+      ef0[k] = ra.eflag[u];
+      vl0[k] = ra.vlen[u];
     }
     const int sfirst = s0 + grp;
     const WgdTable tab = wgd_table(g, min(sfirst + WGD_GROUPS * lane, s1 - 1), u0);
@@ -573,32 +567,72 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
 #pragma unroll
     for (int k = 0; k < WGD_DEPTH; ++k) wgd_load(a, tab, min(k, jlast), sfirst, dbase, wv, r[k]);
     const unsigned long long ta = WGD_CLK();
+    // the table: the first batch's values stay in registers (v0); FP16 first takes the
+    // workgroup's largest |v| (a second pass recomputes later batches), then writes the
+    // scaled values
     auto ge_table = [&](auto ex_tag) {
       constexpr bool EX = decltype(ex_tag)::value;
-      for (int ul0 = 0; ul0 < nu; ul0 += 8) {
-        float v[KG];
+      auto batch = [&](int ul0, float (&v)[KG]) {
 #pragma unroll
         for (int k = 0; k < KG; ++k) {   // the group's utterances' loads in flight (index clamped)
           const int u = u0 + min(ul0 + grp * KG + k, nu - 1);
           v[k] = ul0 == 0 ? fused_ge1_v<EX>(ra, g.Bc, u, hh, w2, gz0[k], ef0[k], ec0[k]) / fmaxf(vl0[k], 1.0f)
                           : fused_ge1<EX>(ra, g.Bc, u, hh, w2) / fmaxf(ra.vlen[u], 1.0f);
         }
+      };
+      auto put = [&](int ul0, const float (&v)[KG], float scale) {
 #pragma unroll
         for (int k = 0; k < KG; ++k) {
           const int uk = ul0 + grp * KG + k;
-          if (uk < nu) gs[uk * DAD_H + hh] = __builtin_bit_cast(uint16_t, (__bf16)v[k]);
+          if (uk < nu) gs[uk * DAD_H + hh] = dad_half_bits(F16 ? v[k] * scale : v[k], F16);
+        }
+      };
+      float v0[KG];
+      batch(0, v0);
+      if constexpr (F16) {
+        float mx = 0.0f;
+#pragma unroll
+        for (int k = 0; k < KG; ++k) mx = fmaxf(mx, fabsf(v0[k]));
+        for (int ul0 = 8; ul0 < nu; ul0 += 8) {
+          float v[KG];
+          batch(ul0, v);
+#pragma unroll
+          for (int k = 0; k < KG; ++k) mx = fmaxf(mx, ul0 + grp * KG + k < nu ? fabsf(v[k]) : 0.0f);
+        }
+        // (values of clamped duplicate utterances equal a real one's: no effect on the max)
+        mx = dad_wave_max(mx);
+        float* wmx = reinterpret_cast<float*>(gs);   // 8 wave maxima in the table's first 32 B
+        if (lane == 0) wmx[tid >> 6] = mx;
+        __syncthreads();
+        float m8 = wmx[0];
+#pragma unroll
+        for (int k = 1; k < WGD_THREADS / 64; ++k) m8 = fmaxf(m8, wmx[k]);
+        __syncthreads();   // every wave has read the maxima before the table overwrites them
+        const int s = wgd_f16_exp(m8);
+        const float scale = __builtin_ldexpf(1.0f, s);
+        unscale = __builtin_ldexpf(1.0f, -s);
+        put(0, v0, scale);
+        for (int ul0 = 8; ul0 < nu; ul0 += 8) {
+          float v[KG];
+          batch(ul0, v);
+          put(ul0, v, scale);
+        }
+      } else {
+        put(0, v0, 1.0f);
+        for (int ul0 = 8; ul0 < nu; ul0 += 8) {
+          float v[KG];
+          batch(ul0, v);
+          put(ul0, v, 1.0f);
         }
       }
     };
-    if (!SU) {
-      if (ra.keep1) ge_table(std::true_type{});
-      else ge_table(std::false_type{});
-    }
+    if (ra.keep1) ge_table(std::true_type{});
+    else ge_table(std::false_type{});
     const unsigned long long tb = WGD_CLK();
     // slabs 0 .. SD-1 of each group into buffers 0 .. SD-1; their ring slots reload slabs
     // WGD_DEPTH .. WGD_DEPTH + SD - 1
     constexpr int NB = WGD_NBUF, SD = WGD_NBUF / 2;   // LDS buffers, staging distance (rounds)
-    static_assert(WGD_DEPTH == 4 && (NB == 4 || NB == 8), "dad_wgrad_direct: four ring slots, 4 or 8 LDS buffers");
+    static_assert(WGD_DEPTH == 4 && NB == 4, "dad_wgrad_direct: four ring slots, 4 LDS buffers");
     int ulq[SD];   // utterance slot and row masks of slabs j .. j+SD-1 (by j mod SD)
     uint32_t mwq[SD][2];
 #pragma unroll
@@ -612,11 +646,6 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
     for (int q = 0; q < SD; ++q) wgd_load(a, tab, min(WGD_DEPTH + q, jlast), sfirst, dbase, wv, r[q]);
     const unsigned long long tc = WGD_CLK();
     __syncthreads();
-#if WGD_PRIO
-    // static priority for one slab group: the two waves sharing a SIMD (one per group) leave each
-    // barrier in step; the favoured one issues its MFMAs first and the other fills the gaps
-    if (grp == WGD_PRIO - 1) __builtin_amdgcn_s_setprio(1);
-#endif
     t1 = WGD_CLK();
     WGD_ACC(3, ta - t0); WGD_ACC(6, tb - ta); WGD_ACC(7, tc - tb); (void)ta; (void)tb; (void)tc;
     // round j: read slab j's operands from buffer j % NB into registers | MFMAs of slab j-1 from
@@ -624,15 +653,15 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
     // buffer (j+SD) % NB from ring slot (j+SD) % 4 and reload that slot with slab j+SD+4.  A slab
     // is staged SD = NB/2 rounds before it is read, so one barrier per SD rounds (after rounds
     // j = SD-1 mod SD) orders every staging before its reads and every read before its buffer is
-    // restaged (NB = 4: a barrier every two rounds; NB = 8: every four).
+    // restaged.
     WgdFrag F;
     auto round = [&](int jr, int k, bool prev, bool comp, bool stage, bool bar) {
       const unsigned long long c0 = WGD_CLK();
       const int nk = (k + SD) % WGD_DEPTH;
       WgdRaw R;
-      if (comp) R = wgd_read<SU>(Xg + (k % NB) * (DAD_SLAB * WGD_XP), mwq[k % SD], lut, gs, ulq[k % SD], wv);
+      if (comp) R = wgd_read(Xg + (k % NB) * (DAD_SLAB * WGD_XP), mwq[k % SD], lut, gs, ulq[k % SD], wv);
       __builtin_amdgcn_sched_barrier(0);   // reads first, their latency under the MFMAs
-      if (prev) wgd_mma(F, acc);
+      if (prev) wgd_mma<F16>(F, acc);
       if (stage) wgd_stage(r[nk], Xg + ((k + SD) % NB) * (DAD_SLAB * WGD_XP));
       ulq[k % SD] = r[nk].ul;
       mwq[k % SD][0] = r[nk].mw[0];
@@ -660,7 +689,7 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
     for (int k = 0; k < NB + SD + 1; ++k)   // nround - j <= NB + SD
       if (j + k < nround)
         round(j + k, (k + 1) % NB, j + k - 1 < mine, j + k < mine, j + k + SD < mine, (k + 1) % SD == SD - 1);
-    if (nround - 1 < mine) wgd_mma(F, acc);
+    if (nround - 1 < mine) wgd_mma<F16>(F, acc);
     t2 = WGD_CLK();
   }
   const int kh = lane >> 5;
@@ -687,9 +716,7 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
           const int h = (2 * wv + m) * 32 + dad_acc_row(rr, kh);
           const int d = 32 * nn + (lane & 31);
           const float v = acc[m][nn][rr] + (WGD_GROUPS == 2 ? red[h * WGD_DB + d] : 0.0f);
-          if constexpr (SU) outb[(size_t)h * DAD_D + dbase + d] = (__bf16)v;
-          else if constexpr (WGD_WT) __hip_atomic_store(outf + (size_t)h * DAD_D + dbase + d, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          else outf[(size_t)h * DAD_D + dbase + d] = v;
+          outf[(size_t)h * DAD_D + dbase + d] = F16 ? v * unscale : v;
         }
   if constexpr (WGD_GROUPS == 2) __syncthreads();   // red free for the next tile
   WGD_ACC(0, t1 - t0); WGD_ACC(1, t2 - t1); WGD_ACC(2, WGD_CLK() - t2);
@@ -717,11 +744,11 @@ __device__ __forceinline__ void wgd_lut(uint4* lut) {
 // LDS of the weight-gradient workgroups (160 KB with the dL/de table): the x tiles, then the
 // mask table; the end-of-tile exchange (red, 64 KB) reuses the x tiles and the spare space
 // after them (the table stays intact for the next tile)
-constexpr int WGD_XT = WGD_GROUPS * WGD_NBUF * DAD_SLAB * WGD_XP;   // bf16 elements
+constexpr int WGD_XT = WGD_GROUPS * WGD_NBUF * DAD_SLAB * WGD_XP;   // 16-bit elements
 constexpr int WGD_RED = WGD_GROUPS == 2 ? DAD_H * WGD_DB : 1;
 struct __attribute__((aligned(16))) WgdSmem {
   union {
-    __bf16 xt[WGD_XT];
+    uint16_t xt[WGD_XT];
     float red[WGD_RED];
   } a;
   uint4 lut[WGD_LUT];
@@ -729,11 +756,11 @@ struct __attribute__((aligned(16))) WgdSmem {
 
 __device__ double extra_block(const DadReduceArgs& a, int e, int tid, float (*xs)[16][6]);
 
-__global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct(DadWgradArgs a, DadReduceArgs ra) {
-  DAD_GUARD_BLOCK(WGD_THREADS);
+template <bool F16>
+__device__ __forceinline__ void wgrad_direct_body(const DadWgradArgs& a, const DadReduceArgs& ra) {
   __shared__ WgdSmem S;
   __shared__ __attribute__((aligned(16))) uint16_t gs[WGD_MAXU * DAD_H];
-  __bf16* Xt = S.a.xt;
+  uint16_t* Xt = S.a.xt;
   // XCD-aware tile order (grid is a multiple of 8; workgroups go round-robin over the 8
   // XCDs): each XCD takes a consecutive run of tiles, so the column blocks of one split,
   // which read the same ReLU' row masks, share an L2
@@ -749,7 +776,7 @@ __global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct(DadWgradArgs 
     static_assert(sizeof(S.a) >= 2 * 16 * 16 * 6 * sizeof(float), "extra-block scratch fits the x tile");
     double* wred = reinterpret_cast<double*>(S.lut);   // (the mask table is not used here)
     const int half = threadIdx.x >> 8, htid = threadIdx.x & 255;
-    float (*xs)[16][6] = reinterpret_cast<float (*)[16][6]>(Xt) + 16 * half;
+    float (*xs)[16][6] = reinterpret_cast<float (*)[16][6]>(S.a.red) + 16 * half;
     constexpr int per_wg = DAD_REDUCE_XBLK / WGD_XWG;
     constexpr int NB = DAD_REDUCE_BLOCKS - DAD_REDUCE_XBLK;
     for (int r = 0; r < per_wg; r += 2) {
@@ -768,27 +795,16 @@ __global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct(DadWgradArgs 
   const int per = (total + a.splits - 1) / a.splits;
   const int s0 = split * per, s1 = min(total, s0 + per);
   wgd_lut(S.lut);   // (the tile's first barrier orders it before the first read)
-  wgd_tile<false>(a, ra, s0, s1, dblk * WGD_DB, a.wpart + (size_t)split * DAD_H * DAD_D, nullptr, Xt, S.lut, gs,
-                  S.a.red);
+  wgd_tile<F16>(a, ra, s0, s1, dblk * WGD_DB, a.wpart + (size_t)split * DAD_H * DAD_D, Xt, S.lut, gs, S.a.red);
 }
 
-// FP32-free loss-independent factor for the BF16 step: S_u = bits_u^T X_u (G = 0/1 exactly,
-// bf16 output) per (utterance, column block), persistent workgroups striding over the tiles.
-// Runs on a side stream concurrently with pool/tail/ECDA; dad_wsum applies dL/de_u / len_u.
-__global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_su(DadWgradArgs a) {
+__global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct(DadWgradArgs a, DadReduceArgs ra) {
   DAD_GUARD_BLOCK(WGD_THREADS);
-  __shared__ WgdSmem S;
-  DadReduceArgs unused;
-  const DadGeom& g = a.g;
-  const int nsc = g.Bc * g.ncc;
-  wgd_lut(S.lut);
-  for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
-    const int u = tile / WGD_NDB, dblk = tile - u * WGD_NDB;
-    const int s0 = u < g.Bc ? u * g.ncc : nsc + (u - g.Bc) * g.ncn;
-    const int s1 = s0 + (u < g.Bc ? g.ncc : g.ncn);
-    wgd_tile<true>(a, unused, s0, s1, dblk * WGD_DB, nullptr, a.su + (size_t)u * DAD_H * DAD_D, S.a.xt, S.lut,
-                   nullptr, S.a.red);
-  }
+  wgrad_direct_body<false>(a, ra);
+}
+__global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct_f16(DadWgradArgs a, DadReduceArgs ra) {
+  DAD_GUARD_BLOCK(WGD_THREADS);
+  wgrad_direct_body<true>(a, ra);
 }
 
 // ---------------------------------------------------------------- reduce + squared norms
@@ -927,14 +943,7 @@ __global__ __launch_bounds__(DAD_REDUCE_THREADS) void dad_reduce(DadReduceArgs a
   }
 }
 
-// Factorised weight-gradient finish (FP32 S_u in wpart, or BF16 S_u in su):
-// dW1[h][d] = sum_u g_u[h] * S_u[h][d],
-// g_u[h] = dL/de_u[h] / max(1, len_u).  Blocks [0, NB): DAD_REDUCE_COLS columns of one
-// row h; thread = (float4 column, utterance group ug), utterances ug, ug+4, ... with eight
-// loads in flight, the four groups combined in fixed order (deterministic).  Blocks NB + e:
-// db1, dW2, norm shares, loss totals (extra_block).  Every block: its squared-norm partial.
-static_assert(DAD_D % DAD_REDUCE_COLS == 0, "dad_wsum: whole blocks per dW1 row");
-// BF16 step (the extra blocks ran on spare dad_wgrad_direct workgroups): one wave per
+// FP16/BF16 step (the extra blocks ran on spare dad_wgrad_direct workgroups): one wave per
 // DAD_REDUCE_COLS columns, 4 per lane, the splits summed in split order with every partial's
 // load issued first (batches of 8, index clamped, +0 past the last split), the squared-norm
 // partial a wave reduction: no LDS, no barrier (dad_reduce's 4 row groups met through LDS
@@ -961,75 +970,6 @@ __global__ __launch_bounds__(64) void dad_reduce_w(DadReduceArgs a) {
   for (int e = 0; e < 4; ++e) sq += (double)t[e] * t[e];
   sq = dad_wave_sum_d(sq);
   if (lane == 0) a.normpart[blockIdx.x] = (float)sq;
-}
-
-__global__ __launch_bounds__(DAD_REDUCE_THREADS) void dad_wsum(DadReduceArgs a) {
-  DAD_GUARD_BLOCK(DAD_REDUCE_THREADS);
-  __shared__ double red[DAD_REDUCE_THREADS / 64];
-  __shared__ f32x4 part[4][DAD_H / 4];
-  __shared__ float gsh[2 * DAD_MAX_BATCH];
-  const int tid = threadIdx.x;
-  constexpr int NB = DAD_REDUCE_BLOCKS - DAD_REDUCE_XBLK;
-  double sq = 0.0;
-  if (blockIdx.x < NB) {
-    const DadGeom& g = a.g;
-    const int nutt = g.Bc + (a.warmup ? 0 : g.Bn);
-    const int h = blockIdx.x / (DAD_D / DAD_REDUCE_COLS);
-    const int dcol0 = (blockIdx.x % (DAD_D / DAD_REDUCE_COLS)) * DAD_REDUCE_COLS;
-    // dL/de = classifier part + ECDA part (where ECDA wrote the row this step)
-    const float w2h[4] = {a.student[DAD_OFF_W2 + h], a.student[DAD_OFF_W2 + DAD_H + h],
-                          a.student[DAD_OFF_W2 + 2 * DAD_H + h], a.student[DAD_OFF_W2 + 3 * DAD_H + h]};
-    for (int u = tid; u < nutt; u += DAD_REDUCE_THREADS)
-      gsh[u] = (a.keep1 ? fused_ge1<true>(a, g.Bc, u, h, w2h) : fused_ge1<false>(a, g.Bc, u, h, w2h)) /
-               fmaxf(a.vlen[u], 1.0f);
-    __syncthreads();
-    const int col = tid & (DAD_REDUCE_COLS / 4 - 1), ug = tid / (DAD_REDUCE_COLS / 4);
-    const size_t off = (size_t)h * DAD_D + dcol0 + (size_t)col * 4;
-    f32x4 s = f32x4{};
-    for (int u0 = ug; u0 < nutt; u0 += 4 * 8) {
-      f32x4 v[8];
-      if (a.su) {
-        bf16x4 vb[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const int u = min(u0 + 4 * k, nutt - 1);
-          vb[k] = *reinterpret_cast<const bf16x4*>(a.su + (size_t)u * DAD_H * DAD_D + off);
-        }
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[k][e] = (float)vb[k][e];
-      } else {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const int u = min(u0 + 4 * k, nutt - 1);
-          v[k] = *reinterpret_cast<const f32x4*>(a.wpart + (size_t)u * DAD_H * DAD_D + off);
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if (u0 + 4 * k < nutt) s += gsh[u0 + 4 * k] * v[k];
-    }
-    part[ug][col] = s;
-    __syncthreads();
-    if (ug == 0) {
-      const f32x4 t = ((part[0][col] + part[1][col]) + part[2][col]) + part[3][col];
-      *reinterpret_cast<f32x4*>(a.grad + DAD_OFF_W1 + off) = t;
-      for (int e = 0; e < 4; ++e) sq += (double)t[e] * t[e];
-    }
-  } else {
-    __shared__ float xsx[16][16][6];
-    sq = extra_block(a, blockIdx.x - NB, tid, xsx);
-  }
-  if (!a.want_norm) return;
-  double v = dad_wave_sum_d(sq);
-  if ((tid & 63) == 0) red[tid >> 6] = v;
-  __syncthreads();
-  if (tid == 0) {
-    double t = 0.0;
-    for (int k = 0; k < DAD_REDUCE_THREADS / 64; ++k) t += red[k];
-    a.normpart[blockIdx.x] = (float)t;
-  }
 }
 
 // Data-parallel path: after the SUM all-reduce, average (grads, thresholds, losses) and

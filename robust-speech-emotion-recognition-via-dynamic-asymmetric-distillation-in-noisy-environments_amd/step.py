@@ -21,7 +21,7 @@ from . import _lib
 from .config import ConfigView, dad_config_for
 from .data import StoreFeats
 
-PRECISIONS = {"fp32": _lib.PREC_FP32, "bf16": _lib.PREC_BF16}
+PRECISIONS = {"fp32": _lib.PREC_FP32, "bf16": _lib.PREC_BF16, "fp16": _lib.PREC_FP16}
 
 
 def _dev_batch(batch, device, labels=True):
@@ -84,7 +84,9 @@ class DADStep:
         model: `SSRLModel` (already on the target cuda device).
         cfg: reference-style config module / dict / object (read at every step), or None.
         flavor: 'iemocap' | 'casia' | 'emodb' (which ablation switches are honoured).
-        precision: 'fp32' (exact-f32 MFMA, parity mode) or 'bf16' (bf16 MFMA, fp32 accumulate).
+        precision: 'fp32' (exact-f32 MFMA, the reference's arithmetic), 'fp16' (fp16 MFMA operands,
+            fp32 accumulate: the throughput mode that keeps losses and logits within 1e-4) or
+            'bf16' (bf16 operands, fp32 accumulate).
         rng: 'counter' (in-kernel counter-based RNG) or 'explicit' (draws passed to step()).
         seed: counter-RNG seed.
         comm: optional `dist.DPComm` for data-parallel gradient averaging.
@@ -148,8 +150,8 @@ class DADStep:
 
         NOT detected: writes through `p.data` (`p.data.copy_(...)`, the style of the
         reference's model.py:204-223).  `.data` is a detached alias with a version counter of
-        its own, so such a write leaves this key unchanged and the next BF16 step would run on
-        the old bf16 W1 shadows.  Call `refresh_shadow()` after writing through `.data`
+        its own, so such a write leaves this key unchanged and the next FP16/BF16 step would run
+        on the old 16-bit W1 shadows.  Call `refresh_shadow()` after writing through `.data`
         (tests/test_gpu_shadow.py).  A per-step content check would cost a read of both W1
         copies (1.5 MB) on every step."""
         m = self.model
@@ -157,11 +159,11 @@ class DADStep:
         return (s.data_ptr(), t.data_ptr(), s._version, t._version, getattr(m, "param_writes", 0))
 
     def refresh_shadow(self):
-        """Re-derive the bf16 W1 shadows after the caller changed the model's parameters
+        """Re-derive the 16-bit W1 shadows after the caller changed the model's parameters
         (step() also does this by itself whenever `_param_key` changed; required after writes
         through `.data`, which `_param_key` cannot see)."""
         st = self._state_struct(0)
-        _lib.check(_lib.lib().dad_refresh_shadow(st, self._stream()), "dad_refresh_shadow")
+        _lib.check(_lib.lib().dad_refresh_shadow(st, self.precision, self._stream()), "dad_refresh_shadow")
         self._shadow_dirty = False
         self._shadow_key = self._param_key()
 
@@ -323,6 +325,16 @@ class DADStep:
         if self.view.flavor in ("casia", "emodb"):
             out["scl_loss"] = torch.zeros((), device=self.device)   # always 0 (C/train_CASIA.py:442)
         return out
+
+    def range_flag(self, clear=False):
+        """Device u32 scalar, nonzero once a step with the current batch shapes produced a non-finite
+        pooled embedding or logit (dad.h DAD_T_RANGE: in FP16 an encoder operand beyond +-65504;
+        in any mode non-finite features).  Sticky; `clear=True` resets it after reading."""
+        t = self._last["tail"]
+        v = t[_lib.T_RANGE:_lib.T_RANGE + 1].view(torch.int32).clone()[0]
+        if clear:
+            t[_lib.T_RANGE:_lib.T_RANGE + 1].zero_()
+        return v
 
     def outputs(self, Bc=None, Bn=None):
         """Per-step intermediates (device tensors) of the last step, for inspection/tests."""

@@ -35,7 +35,7 @@ def _state(step):
                                          step.exp_avg_sq, step.dacp, step.grad)]
 
 
-@pytest.mark.parametrize("precision,rng", [("fp32", "explicit"), ("bf16", "counter")])
+@pytest.mark.parametrize("precision,rng", [("fp32", "explicit"), ("bf16", "counter"), ("fp16", "counter")])
 def test_captured_step_replays_like_eager(precision, rng):
     cfg = dad_oracle.make_cfg("iemocap")
     inp = _problem(B=16, T=40, seed=21, Bn=12, Tn=50)

@@ -9,7 +9,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_bf16_parity.py tests/test_gpu_bf16.py -q -x \
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_throughput_parity.py tests/test_gpu_16bit.py -q -x \
   --timeout 120 --timeout-method thread > gpurun_out/iter_tests.log 2>&1
 rc=$?; tail -2 gpurun_out/iter_tests.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi

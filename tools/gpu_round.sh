@@ -1,11 +1,11 @@
-# GPU tests (all -m gpu, measured bf16 parity errors to gpurun_out/bf16_parity.json), then the
+# GPU tests (all -m gpu, measured fp16/bf16 parity errors to gpurun_out/parity16.json), then the
 # default bench line.  Test failures (pytest rc 1) still run the bench; a crash, abort or time
 # limit stops the script there.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-DAD_PARITY_JSON=gpurun_out/bf16_parity.json timeout -k 10 ${TEST_LIMIT:-420} python -u -m pytest tests -m gpu -v -rf \
+DAD_PARITY_JSON=gpurun_out/parity16.json timeout -k 10 ${TEST_LIMIT:-420} python -u -m pytest tests -m gpu -v -rf \
   --timeout 120 --timeout-method thread -s ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
 rc=$?
 grep -E "passed|failed|error" gpurun_out/pytest_gpu.log | tail -3
