@@ -411,6 +411,42 @@ def event_every(steps):
 TIMED_KERNELS = ["encode"]
 
 
+def capture_steps(step, data, epoch, split=None):
+    """One hipGraph (torch.cuda.CUDAGraph) per resident batch pair, each holding one full fused
+    step (the C ABI is enqueue-only; tests/test_gpu_graph.py proves replay == eager bit for bit).
+    A graph bakes its step's host scalars into the kernel arguments: the RNG step counter and the
+    Adam bias corrections of steps g0 .. g0+7, so replay k runs graph k mod 8 -- a full step on
+    batch k mod 8 with that graph's noise stream and Adam step, reading and updating the live
+    device state (parameters, moments, DACP).  Batch `split` is captured as two graphs, the
+    encoder launch and the rest of its step, so stream events recorded between their replays
+    time the encoder inside the timed region (HIP event nodes captured INSIDE a graph do not
+    report elapsed times).  Returns a list of graph tuples, or raises on a capture error."""
+    torch.cuda.synchronize()
+    graphs = []
+    for i, (c, nb) in enumerate(data):
+        if i != split:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                step.step(c, nb, epoch)
+            graphs.append((g,))
+            continue
+        ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+
+        def cut():
+            ga.capture_end()
+            gb.capture_begin(pool=ga.pool())
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            ga.capture_begin()
+            step.step(c, nb, epoch, after_encode=cut)
+            gb.capture_end()
+        torch.cuda.current_stream().wait_stream(s)
+        graphs.append((ga, gb))
+    torch.cuda.synchronize()
+    return graphs
+
+
 def kernel_pass(run1, n):
     """Per-kernel durations (all boundaries, every 2nd step) over n steps run after the timed
     region: the `kernels` table of the line (the encoder's own entry is the timed region's)."""
@@ -651,6 +687,8 @@ def main():
                     help="steps of the per-kernel timing pass after the timed region (0: none)")
     ap.add_argument("--no-data-path", action="store_true", help="skip the device collate measurement (N=1)")
     ap.add_argument("--no-parity", action="store_true", help="skip the 16-bit-vs-fp32 parity block (N=1)")
+    ap.add_argument("--launch", default="graph", choices=["graph", "eager"],
+                    help="timed steps as hipGraph replays (one graph per resident batch) or eager launches")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -730,21 +768,69 @@ def main():
         torch.cuda.synchronize()
         # every EVENT_EVERY-th timed step records hip events at its kernel boundaries (created
         # here, outside the timed region; the region only records them)
-        timer = PKG._lib.KernelTimer(event_every(args.steps), args.steps + 1, kernels=TIMED_KERNELS)
+        launch = args.launch
+        if launch == "graph" and isinstance(comm, PKG.ProcessGroupComm):
+            launch = "eager (the gloo all-reduce runs on the host: not capturable)"
+        graphs = None
+        timer = None
+        enc_events = []
+        if launch == "graph":
+            # the capture advances the host's step counters by len(data): the timed replays are
+            # steps warmup .. warmup+7 of the same run, cycled; the encoder of the last batch's
+            # graph is timed by stream events around its own graph (every 8th step)
+            split = len(data) - 1
+            try:
+                graphs = capture_steps(step, data, args.epoch, split=split)
+            except Exception as e:   # (e.g. a transport that refuses capture): eager, said so in the line
+                err = str(e).splitlines()[0][:200] if str(e) else type(e).__name__
+                restore(model, step, snap)
+                torch.cuda.synchronize()
+                launch = "eager (graph capture failed: %s)" % err
+            if graphs is not None:
+                n_ev = sum(1 for i in range(args.steps) if i % len(graphs) == split)
+                enc_events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                              for _ in range(n_ev)]
+                for e0, e1 in enc_events:   # first use outside the timed region
+                    e0.record()
+                    e1.record()
+                torch.cuda.synchronize()
+        if graphs is None:
+            timer = PKG._lib.KernelTimer(event_every(args.steps), args.steps + 1, kernels=TIMED_KERNELS)
+
+        def timed(n):
+            if graphs is None:
+                run(n)
+                return
+            k = 0
+            for i in range(n):
+                gs = graphs[i % len(graphs)]
+                if len(gs) == 1:
+                    gs[0].replay()
+                else:
+                    e0, e1 = enc_events[k]
+                    k += 1
+                    e0.record()
+                    gs[0].replay()
+                    e1.record()
+                    gs[1].replay()
         if dist:
             dist.barrier()
         t0 = time.perf_counter()
-        run(args.steps)
+        timed(args.steps)
         torch.cuda.synchronize()
         if dist:
             dist.barrier()
         elapsed = time.perf_counter() - t0
-        ktimes = timer.stop()
+        if timer is not None:
+            ktimes = timer.stop()
+        else:
+            ms_enc = [e0.elapsed_time(e1) for e0, e1 in enc_events]
+            ktimes = {"encode": (sum(ms_enc) / len(ms_enc), len(ms_enc))} if ms_enc else {}
         if dist:
             t = torch.tensor([elapsed], dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
-        losses = {k: float(v) for k, v in step.losses().items()}   # the last timed step's
+        losses = {k: float(v) for k, v in step.losses().items()}   # the last timed (or captured) step's
         nbc = step._last_shape
         msum = float(step.outputs(*nbc)["msum"])
         ecda_on = float(step.outputs(*nbc)["ecda_on"])
@@ -787,9 +873,11 @@ def main():
     kt.update(ktimes)
     rf, srf, kern = rooflines(kt, rows, rows, ms, args.precision,
                               tail_kernel(B, B, True if args.mixed else class_aware(view)))
-    kern["source"] = ("encoder: HIP events around it in the timed region (every %d-th step); the other "
-                      "kernels: a separate pass of %d steps after it (events at every boundary of every "
-                      "2nd step)" % (event_every(args.steps), args.kernel_steps))
+    kern["source"] = ("encoder: HIP events around it in the timed region (%s); the other kernels: a separate "
+                      "eager pass of %d steps after it (events at every boundary of every 2nd step)"
+                      % ("stream events around the encoder graph of every %d-th replayed step" % len(graphs)
+                         if not args.mixed and graphs else "every %d-th step" % event_every(args.steps),
+                         args.kernel_steps))
     line = {
         "metric": METRIC, "value": value, "unit": "utterances/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
@@ -802,6 +890,7 @@ def main():
                    "global_batch": B * world, "per_gpu_batch": B, "seq_len": T, "feature_dim": 768,
                    "parallelism": "dp%d" % world},
         "comm": {"transport": args.comm if world > 1 else None, "ranks_seen": ranks_seen},
+        "launch": launch if not args.mixed else "eager",
         "roofline": rf, "step_roofline": srf, "kernels": kern,
         "losses_last_step": losses, "mask_sum_last_step": msum, "ecda_on_last_step": ecda_on,
     }

@@ -147,6 +147,46 @@ int ws_split_uncached(const DadGeom& G, int Bn, int cus, int& nt, int& ns) {
   }
   return DAD_OK;
 }
+// XCD-sweep role counts (dad_ws_sweep_jobs): per XCD P = cus / 8 workgroups split into teachers,
+// strong students and clean students minimising the largest per-workgroup cost (live 16-row
+// sub-slabs x role weight), every range within DAD_ENC_WS_MAXJ jobs.  Off (all 0) when the
+// CUs do not divide over 8 XCDs, in warm-up (no noisy rows to share), when a role would get no
+// workgroup, or by DAD_WS_SWEEP=0 (A/B runs; read once).
+bool ws_sweep_on() {
+  static const bool on = [] { const char* e = getenv("DAD_WS_SWEEP"); return !(e && strcmp(e, "0") == 0); }();
+  return on;
+}
+DadWsSweep ws_sweep_uncached(const DadGeom& G, int Bn, int cus) {
+  DadWsSweep best{0, 0, 0};
+  const int P = cus / 8, Jc = G.Bc * G.ncc, Js = Bn * G.ncn;
+  if (!ws_sweep_on() || cus % 8 != 0 || P < 3 || Js < 8 || Jc < 8) return best;
+  const float kW = ws_weights().weak, kS = ws_weights().strong;
+  const int Lc = (G.Tc + 15) / 16, Ln = (G.Tn + 15) / 16;
+  const double cn = (double)Bn * Ln / 8.0, cc = (double)G.Bc * Lc / 8.0;   // live sub-slabs per XCD
+  double best_cost = 1e30;
+  for (int nt = 1; nt <= P - 2; ++nt)
+    for (int ns = 1; nt + ns <= P - 1; ++ns) {
+      const int nc = P - nt - ns;
+      const double cost = std::max(std::max(cn * kW / nt, cn * kS / ns), cc / nc);
+      if (cost < best_cost) { best_cost = cost; best = DadWsSweep{nt, ns, nc}; }
+    }
+  // the kernel's job tables hold DAD_ENC_WS_MAXJ jobs per workgroup
+  for (int wg = 0; wg < cus; ++wg) {
+    bool t = false;
+    int a0 = 0, st = 1, nj = 0;
+    dad_ws_sweep_jobs(wg, best, G.Bc, G.Tc, G.ncc, Jc, Js, t, a0, st, nj);
+    if (nj > DAD_ENC_WS_MAXJ) return DadWsSweep{0, 0, 0};
+  }
+  return best;
+}
+DadWsSweep ws_sweep(const DadGeom& G, int Bn, int cus) {
+  struct Entry { int Bc, Tc, Bn, Tn, cus; DadWsSweep s; };
+  static thread_local Entry last{-1, -1, -1, -1, -1, {0, 0, 0}};
+  if (!(last.Bc == G.Bc && last.Tc == G.Tc && last.Bn == Bn && last.Tn == G.Tn && last.cus == cus))
+    last = Entry{G.Bc, G.Tc, Bn, G.Tn, cus, ws_sweep_uncached(G, Bn, cus)};
+  return last.s;
+}
+
 // The split is a pure function of (geometry, CU count) for the process's fixed weights: cached
 // per thread for the last key, so a steady-state step runs no range evaluations on the host.
 int ws_split(const DadGeom& G, int Bn, int cus, int& nt, int& ns) {
@@ -276,6 +316,36 @@ int dad_encoder_ws_plan(const dad_config* cfg, int cus, int* nt, int* ns, int* m
   return DAD_OK;
 }
 
+int dad_encoder_ws_jobs(const dad_config* cfg, int cus, int* jobs) {
+  int rc = check_cfg(cfg);
+  if (rc) return rc;
+  if (cus < 2 || !jobs) return DAD_E_ARG;
+  const DadGeom G = geom_of(cfg);
+  const int Bn = cfg->warmup ? 0 : G.Bn;
+  int nt = 0, ns = 0;
+  rc = ws_split(G, Bn, cus, nt, ns);
+  if (rc) return rc;
+  const DadWsSweep sw = ws_sweep(G, Bn, cus);
+  const int Jc = G.Bc * G.ncc, Js = Bn * G.ncn;
+  const int grid = sw.nt > 0 ? cus : nt + ns;
+  for (int wg = 0; wg < grid; ++wg) {
+    bool t = false;
+    int a0 = 0, st = 1, nj = 0;
+    if (sw.nt > 0) {
+      dad_ws_sweep_jobs(wg, sw, G.Bc, G.Tc, G.ncc, Jc, Js, t, a0, st, nj);
+    } else {
+      int j1 = 0;
+      dad_ws_job_range(wg, nt, ns, ws_weights().strong, G.Bc, G.Tc, G.ncc, Bn, G.Tn, G.ncn, Js, t, a0, j1);
+      nj = j1 - a0;
+    }
+    jobs[4 * wg] = t ? 1 : 0;
+    jobs[4 * wg + 1] = a0;
+    jobs[4 * wg + 2] = st;
+    jobs[4 * wg + 3] = nj;
+  }
+  return grid;
+}
+
 int dad_workspace_bytes(const dad_config* cfg, size_t* bytes) {
   int rc = check_cfg(cfg);
   if (rc) return rc;
@@ -350,6 +420,8 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
       const int rs = ws_split(G, Bn, cus, ea.ws_nt, ea.ws_ns);
       if (rs) return rs;
       ea.ws_wstrong = ws_weights().strong;
+      ea.ws_sweep = ws_sweep(G, Bn, cus);
+      if (ea.ws_sweep.nt > 0) { ea.ws_nt = cus; ea.ws_ns = 0; }   // (grid = cus: one workgroup per CU)
       if (ea.ws_nt + ea.ws_ns > 0) {
         const dim3 grid(ea.ws_nt + ea.ws_ns), block(DAD_ENC_WS_THREADS);
         if (f16) {

@@ -322,6 +322,42 @@ static inline __host__ __device__ void dad_ws_job_range(int wg, int nt, int ns, 
   j1 = j[1];
 }
 
+// XCD-sweep job assignment of the 16-bit encoder (ws_sweep on the host): workgroup wg runs on
+// XCD wg & 7 (the dispatcher deals workgroups round-robin over the 8 XCDs) as local workgroup
+// l = wg >> 3 of that XCD, in one of three roles with per-XCD counts nt + ns + nc:
+//   l < nt           teacher: weak slabs g0 + l, g0 + l + nt, ... of the XCD's noisy group [g0, g1)
+//   nt <= l < nt+ns  strong student: strong slabs g0 + k, g0 + k + ns, ... (k = l - nt)
+//   else             clean student: a contiguous clean range (live-cost balanced over all 8 nc)
+// Teachers and strong students of an XCD sweep the SAME noisy rows at matching rates (the counts
+// follow the costs, nt / w_weak ~ ns / w_strong), so each noisy row is fetched from HBM once and
+// read by the second role from that XCD's L2 (the contiguous split read it twice, from different
+// XCDs).  Student jobs: j < Jc clean slab j, j >= Jc strong slab j - Jc (job_of).
+struct DadWsSweep {
+  int nt, ns, nc;   // per-XCD role counts (all 0: the contiguous split dad_ws_job_range)
+};
+static inline __host__ __device__ void dad_ws_sweep_jobs(int wg, const DadWsSweep& sw, int Bc, int Tc, int ncc, int Jc,
+                                                         int Js, bool& teacher, int& a0, int& stride, int& nj) {
+  const int x = wg & 7, l = wg >> 3;
+  const int g0 = (int)((long long)Js * x / 8), g1 = (int)((long long)Js * (x + 1) / 8);
+  if (l < sw.nt + sw.ns) {
+    teacher = l < sw.nt;
+    const int k = teacher ? l : l - sw.nt, n = teacher ? sw.nt : sw.ns;
+    a0 = (teacher ? 0 : Jc) + g0 + k;
+    stride = n;
+    nj = g0 + k < g1 ? (g1 - g0 - k + n - 1) / n : 0;
+    return;
+  }
+  teacher = false;
+  const int k = x * sw.nc + (l - sw.nt - sw.ns), N = 8 * sw.nc;
+  const int Lc = (Tc + 15) / 16;
+  const float tot = (float)Bc * (float)Lc;
+  const int c0 = dad_live_jobs_at(tot * (float)k / (float)N, ncc, Lc, Jc);
+  const int c1 = k + 1 >= N ? Jc : dad_live_jobs_at(tot * (float)(k + 1) / (float)N, ncc, Lc, Jc);
+  a0 = c0;
+  stride = 1;
+  nj = c1 - c0;
+}
+
 // Workspace layout (bytes), shared by host and device.  All offsets 256-B aligned.
 //   slab-indexed buffers: clean slabs [0, Bc*ncc), noisy slabs after them.
 struct DadWs {

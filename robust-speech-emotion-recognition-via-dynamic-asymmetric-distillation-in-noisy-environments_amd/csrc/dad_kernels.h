@@ -71,8 +71,9 @@ struct DadEncodeArgs {
   float weak_std, strong_std, feat_p;
   float* part_sum; float* part_cnt; uint32_t* bits;
   uint16_t* xs16;           // 16-bit modes: the student's MFMA input, clean rows then strong rows (for wgrad)
-  int ws_nt, ws_ns;         // dad_encode_ws: teacher / student workgroups
+  int ws_nt, ws_ns;         // dad_encode_ws: teacher / student workgroups (contiguous split)
   float ws_wstrong;         // dad_encode_ws: cost of a strong slab relative to a clean one
+  DadWsSweep ws_sweep;      // dad_encode_ws: XCD-sweep role counts per XCD (nt = ns = nc = 0: contiguous split)
 };
 
 

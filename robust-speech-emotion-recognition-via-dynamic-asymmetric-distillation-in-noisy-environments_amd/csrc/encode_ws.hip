@@ -154,10 +154,10 @@ __device__ __forceinline__ void job_range(const Ctx& C, int wg, int nt, int ns, 
   dad_ws_job_range(wg, nt, ns, wstrong, C.Bc, C.Tc, C.ncc, C.Bn, C.Tn, C.ncn, C.Js, teacher, j0, j1);
 }
 
-// a workgroup's jobs: local job l is job a0 + l (one contiguous range)
+// a workgroup's jobs: local job l is job a0 + l * stride (a contiguous range, or an XCD sweep)
 struct JobMap {
-  int a0;
-  __device__ __forceinline__ int operator()(int l) const { return a0 + l; }
+  int a0, stride;
+  __device__ __forceinline__ int operator()(int l) const { return a0 + l * stride; }
 };
 
 template <int NOISE>
@@ -649,10 +649,16 @@ __device__ __forceinline__ void encode_ws_body(const DadEncodeArgs& a, char* sme
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   bool teacher;
-  int j0, j1;
-  job_range(C, blockIdx.x, a.ws_nt, a.ws_ns, a.ws_wstrong, teacher, j0, j1);
-  const JobMap jm{j0};
-  const int nj = j1 - j0;
+  JobMap jm;
+  int nj;
+  if (a.ws_sweep.nt > 0) {
+    dad_ws_sweep_jobs(blockIdx.x, a.ws_sweep, C.Bc, C.Tc, C.ncc, C.Jc, C.Js, teacher, jm.a0, jm.stride, nj);
+  } else {
+    int j0, j1;
+    job_range(C, blockIdx.x, a.ws_nt, a.ws_ns, a.ws_wstrong, teacher, j0, j1);
+    jm = JobMap{j0, 1};
+    nj = j1 - j0;
+  }
   if (nj <= 0) return;
   const uint32_t sbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;   // LDS byte address
 

@@ -99,8 +99,8 @@ __device__ __forceinline__ void adam_ema_apply(const dad_config& cfg, float coef
 // of the fragment-major shadow (dad_w1frag_index: k & 7 is the innermost index).  The scalar
 // form issued 20 loads and 24 stores per thread, 8 of them 2-byte stores to scattered shadow
 // slots; the kernel's length was set by issuing them.  Used when every stream is 16-B aligned.
-static_assert(DAD_OPTIM_THREADS * 4 == 1024 && DAD_NPARAM % 4 == 0 && (DAD_H * DAD_D) % 4 == 0,
-              "dad_optim: 1024 parameters per block, 4 per thread, the W1 boundary on a 4-aligned index");
+static_assert(DAD_OPTIM_THREADS * 4 == 1024 && DAD_NPARAM % 4 == 0 && (DAD_H * DAD_D) % 1024 == 0,
+              "dad_optim: 1024 parameters per block, 4 per thread, whole blocks of W1");
 struct AdamOperands4 {
   f32x4 g, p, m, v, t;
 };
@@ -116,11 +116,11 @@ __device__ __forceinline__ void adam_load4(size_t i0, const float* __restrict__ 
   o.t = *reinterpret_cast<const f32x4*>(teacher + i);
 }
 
-__device__ __forceinline__ void adam_ema_apply4(const dad_config& cfg, float coef, size_t i0, const AdamOperands4& o,
-                                                float* __restrict__ student, float* __restrict__ teacher,
-                                                float* __restrict__ exp_avg, float* __restrict__ exp_avg_sq,
-                                                uint16_t* __restrict__ w1bf_s, uint16_t* __restrict__ w1bf_t,
-                                                bool f16) {
+__device__ __forceinline__ void adam_ema_apply4(const dad_config& cfg, float coef, size_t i0, uint32_t f,
+                                                const AdamOperands4& o, float* __restrict__ student,
+                                                float* __restrict__ teacher, float* __restrict__ exp_avg,
+                                                float* __restrict__ exp_avg_sq, uint16_t* __restrict__ w1bf_s,
+                                                uint16_t* __restrict__ w1bf_t, bool f16) {
   if (i0 >= DAD_NPARAM) return;
   f32x4 mo, vo, po, to;
 #pragma unroll
@@ -145,7 +145,6 @@ __device__ __forceinline__ void adam_ema_apply4(const dad_config& cfg, float coe
   if (!cfg.warmup) *reinterpret_cast<f32x4*>(teacher + i0) = to;
   const f32x4 tt = cfg.warmup ? o.t : to;
   if (i0 < (size_t)DAD_H * DAD_D) {
-    const uint32_t f = dad_w1frag_index((uint32_t)(i0 / DAD_D), (uint32_t)(i0 % DAD_D));
     const uint2 bs = f16 ? uint2{dad_pack2<true>(po[0], po[1]), dad_pack2<true>(po[2], po[3])}
                          : uint2{dad_pack2<false>(po[0], po[1]), dad_pack2<false>(po[2], po[3])};
     const uint2 bt = f16 ? uint2{dad_pack2<true>(tt[0], tt[1]), dad_pack2<true>(tt[2], tt[3])}
@@ -153,6 +152,19 @@ __device__ __forceinline__ void adam_ema_apply4(const dad_config& cfg, float coe
     *reinterpret_cast<uint2*>(w1bf_s + f) = bs;
     *reinterpret_cast<uint2*>(w1bf_t + f) = bt;
   }
+}
+
+// W1 parameter of shadow position f (f % 4 == 0: 4 consecutive k of one h), the inverse of
+// dad_w1frag_index: f = ((((h>>4)*24 + ks)*64) + (h & 15) + 16q)*8 + j, k = 32ks + 8q + j.
+// The 4-per-thread W1 blocks walk the SHADOW in order: a wave writes 512 contiguous shadow bytes
+// and a block 1024 consecutive fragment slots = 16 h x 64 k, i.e. whole 128-B lines of every
+// fp32 stream too.  (Walking the parameters in order wrote each shadow line as 16-B pieces from 8
+// blocks, partial lines left dirty in several XCD L2s: the optimizer's kernel-end writeback then
+// held the next launch ~5 us, measured as the optim -> encoder gap.)
+__device__ __forceinline__ size_t w1_param_of_frag(uint32_t f) {
+  const uint32_t j = f & 7u, lane = (f >> 3) & 63u, r2 = f >> 9;
+  const uint32_t n = lane & 15u, q = lane >> 4, ks = r2 % 24u, ht = r2 / 24u;
+  return (size_t)(16u * ht + n) * DAD_D + 32u * ks + 8u * q + j;
 }
 
 __global__ __launch_bounds__(DAD_OPTIM_THREADS) void dad_optim(DadOptimArgs a) {
@@ -166,7 +178,10 @@ __global__ __launch_bounds__(DAD_OPTIM_THREADS) void dad_optim(DadOptimArgs a) {
                      reinterpret_cast<uintptr_t>(a.exp_avg_sq)) & 15u) == 0;
   AdamOperands o;
   AdamOperands4 o4;
-  if (vec) adam_load4(n0 + 4 * (size_t)tid, a.grad, a.student, a.teacher, a.exp_avg, a.exp_avg_sq, o4);
+  // vector path: W1 blocks walk the shadow's fragment order (w1_param_of_frag), the rest linearly
+  const uint32_t f4 = (uint32_t)(n0 + 4 * (size_t)tid);
+  const size_t i4 = n0 < (size_t)DAD_H * DAD_D ? w1_param_of_frag(f4) : n0 + 4 * (size_t)tid;
+  if (vec) adam_load4(i4, a.grad, a.student, a.teacher, a.exp_avg, a.exp_avg_sq, o4);
   else adam_load(n0, a.grad, a.student, a.teacher, a.exp_avg, a.exp_avg_sq, o);
   // global norm from the squared-norm partials: EVERY wave sums all of them in the same fixed
   // order (lane-strided, then the wave reduction), so every wave of every block derives the
@@ -195,8 +210,8 @@ __global__ __launch_bounds__(DAD_OPTIM_THREADS) void dad_optim(DadOptimArgs a) {
   if (blockIdx.x == 0) dacp_commit(cfg, a.grad, a.dacp, tid);
   const bool f16 = cfg.precision == DAD_PREC_FP16;
   if (vec)
-    adam_ema_apply4(cfg, coef, n0 + 4 * (size_t)tid, o4, a.student, a.teacher, a.exp_avg, a.exp_avg_sq,
-                    a.w1h_student, a.w1h_teacher, f16);
+    adam_ema_apply4(cfg, coef, i4, f4, o4, a.student, a.teacher, a.exp_avg, a.exp_avg_sq, a.w1h_student,
+                    a.w1h_teacher, f16);
   else
     adam_ema_apply(cfg, coef, n0, o, a.student, a.teacher, a.exp_avg, a.exp_avg_sq, a.w1h_student, a.w1h_teacher,
                    f16);

@@ -275,8 +275,12 @@ class DADStep:
         self._keepalive = (xc, mc, yc, xn, mn, keep, rc, lc, rn, ln)
         return cfg, bt, st
 
-    def step(self, clean_batch, noisy_batch, epoch, lr=None, draws=None):
-        """One full training step; returns the reference's loss dict as 0-d device tensors."""
+    def step(self, clean_batch, noisy_batch, epoch, lr=None, draws=None, after_encode=None):
+        """One full training step; returns the reference's loss dict as 0-d device tensors.
+
+        after_encode: optional callable run on the host between the encoder launch and the rest
+        of the step (e.g. to split a graph capture there and time the encoder with stream events).
+        """
         if self._shadow_dirty or self._param_key() != self._shadow_key:
             self.refresh_shadow()
         cfg, bt, st = self._prepare(clean_batch, noisy_batch, epoch, lr, draws)
@@ -284,6 +288,9 @@ class DADStep:
         stream = self._stream()
         L = _lib.lib()
         _lib.check(L.dad_step_encode(cfg, bt, st, _lib.ptr(ws), stream), "dad_step_encode")
+        if after_encode is not None:
+            after_encode()
+            stream = self._stream()
         _lib.check(L.dad_step_backward(cfg, bt, st, _lib.ptr(ws), stream), "dad_step_backward")
         if self.comm is not None and self.comm.world > 1:
             self.comm.allreduce_grad(st, stream, grad=self.grad)

@@ -68,6 +68,45 @@ def test_encoder_ws_plan_keeps_every_range_within_the_kernel_table(Bc, Tc, Bn, T
         assert ns.value >= 1 and (nt.value >= 1) == (epoch >= 30)
 
 
+@pytest.mark.parametrize("Bc,Tc,Bn,Tn,cus", [
+    (64, 300, 64, 300, 256),       # the bench geometry: XCD sweep
+    (64, 300, 48, 250, 256),       # Bc != Bn, Tc != Tn
+    (7, 20, 5, 33, 256),           # fewer noisy slabs than 8 XCDs: contiguous split
+    (1024, 300, 1024, 1280, 256),  # long noisy batch
+    (64, 300, 64, 300, 304),       # a CU count that is not 256
+    (64, 300, 64, 300, 252),       # CUs not divisible by 8: contiguous split
+])
+def test_encoder_job_assignment_covers_every_slab_once(Bc, Tc, Bn, Tn, cus):
+    """Every clean, weak and strong 32-row slab is run by exactly one encoder workgroup of the
+    right role, whichever assignment applies (XCD sweep or contiguous split), and no workgroup's
+    range exceeds the kernel's 256-job table.  In the sweep, a noisy slab's teacher and strong
+    student run on the same XCD (wg % 8), the point of the assignment."""
+    p = dadpkg.pkg()
+    L = p.lib()
+    for epoch in (0, 60):
+        cfg = p.dad_config_for(p.ConfigView(flavor="iemocap"), Bc, Tc, Bn, Tn, epoch, 1,
+                               precision=p._lib.PREC_FP16)
+        buf = (ctypes.c_int * (4 * max(cus, 2048)))()
+        grid = L.dad_encoder_ws_jobs(cfg, cus, buf)
+        assert grid > 0
+        ncc, ncn = -(-Tc // 32), -(-Tn // 32)
+        Jc, Js = Bc * ncc, (Bn * ncn if epoch >= 30 else 0)
+        seen_t, seen_s = {}, {}
+        for wg in range(grid):
+            t, a0, st, nj = buf[4 * wg:4 * wg + 4]
+            assert 0 <= nj <= 256 and st >= 1
+            for j in range(a0, a0 + nj * st, st):
+                d = seen_t if t else seen_s
+                assert j not in d, (wg, j)
+                d[j] = wg
+        assert sorted(seen_t) == list(range(Js))
+        assert sorted(seen_s) == list(range(Jc + Js))
+        sweep = grid == cus and cus % 8 == 0 and Js >= 8
+        if sweep:
+            for s in range(Js):
+                assert seen_t[s] % 8 == seen_s[Jc + s] % 8, s
+
+
 def test_ctypes_structs_match_c_layout(tmp_path):
     """Compile a C probe against include/dad.h and compare sizeof/offsetof with ctypes."""
     p = dadpkg.pkg()

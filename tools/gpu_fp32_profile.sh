@@ -9,13 +9,13 @@ TITLE=${TITLE:-fp32}
 mkdir -p gpurun_out/p32 gpurun_out/p32pmc
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/p32/prof" -o run -- \
-  python "$R/bench.py" --precision fp32 --steps 20 --warmup 5 --no-cpu-baseline --no-parity --fp32-steps 0 --no-data-path \
+  python "$R/bench.py" --precision fp32 --steps 20 --warmup 5 --no-cpu-baseline --no-parity --fp32-steps 0 --bf16-steps 0 --no-data-path \
   > "$R/gpurun_out/p32/prof.log" 2>&1 || { echo PROF_FAIL; tail -20 "$R/gpurun_out/p32/prof.log"; exit 1; }
 pass() {
   name=$1; shift
   timeout -s KILL 240 rocprofv3 --pmc "$@" --kernel-trace --kernel-include-regex "dad_" --output-format csv \
     -d "$R/gpurun_out/p32pmc/$name" -o run -- python "$R/bench.py" --precision fp32 --steps 3 --warmup 1 \
-    --no-cpu-baseline --no-parity --fp32-steps 0 --no-data-path > "$R/gpurun_out/p32pmc/$name.log" 2>&1
+    --no-cpu-baseline --no-parity --fp32-steps 0 --bf16-steps 0 --no-data-path > "$R/gpurun_out/p32pmc/$name.log" 2>&1
 }
 pass time SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_VALU_MFMA_COEXEC_CYCLES && \
 pass insts SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE && \

@@ -9,7 +9,7 @@ cd /tmp
 pass() {
   name=$1; shift
   timeout -s KILL 240 rocprofv3 --pmc "$@" --kernel-trace --kernel-include-regex "${PMC_REGEX:-dad_(encode|wgrad)_f32|dad_wsum}" --output-format csv \
-    -d "$R/gpurun_out/pmc32/$name" -o run -- python "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-parity --fp32-steps 6 --no-data-path \
+    -d "$R/gpurun_out/pmc32/$name" -o run -- python "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-parity --fp32-steps 6 --bf16-steps 0 --no-data-path \
     > "$R/gpurun_out/pmc32/$name.log" 2>&1 && python "$R/tools/pmc_brief.py" "$R/gpurun_out/pmc32/$name/run_counter_collection.csv"
 }
 if [ -n "${PMC_SETS:-}" ]; then
