@@ -1602,9 +1602,8 @@ struct __attribute__((aligned(16))) EcdaW {
   float nz[2 * TW_MAXB], wz[2 * TW_MAXB], rs[2 * TW_MAXB];
   int rowz[2 * TW_MAXB], mem[2 * TW_MAXB];
   int cnt[DAD_C];                       // masked noisy rows per class (pseudo-label)
-  float repg[DAD_H];
   float pd[DAD_C][DAD_C];
-  double bwp[ECDA_THREADS / 64];
+  float msp[ECDA_THREADS / 64][DAD_H];   // per-wave member-row sums (the bandwidth identity)
   double t3p[ECDA_THREADS / 64][3];
   float cmp[ECDA_THREADS / 64];
 };
@@ -1627,10 +1626,10 @@ __device__ __forceinline__ void ew_pair_inv(int pr, int nt, int& ti, int& tj) {
 // (the phase was bound by issuing the 32 KB of stores, not by the MFMA chain).
 #define EW_TP 40
 static_assert(ECDA_NG * 32 * EW_TP <= sizeof(EcdaW::b) / sizeof(float), "ew_member_grads: a 32 x EW_TP tile per wave in S.b");
-template <int NP>
+template <int NP, class RG>
 __device__ __forceinline__ void ew_member_grads(EcdaW& S, const float* db, int dp, int c, int ncs, int ncand_all,
                                                 float mmd_scale, float comp_scale, float* ge_c, float* ge_s,
-                                                float* sink) {
+                                                float* sink, const RG& repg_at) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int g = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int kh = lane >> 5, l32 = lane & 31;
@@ -1655,7 +1654,7 @@ __device__ __forceinline__ void ew_member_grads(EcdaW& S, const float* db, int d
       zi[r] = S.a.zc[i * EW_ZP + d];
       rsv[r] = S.rs[ic];
     }
-    const float mu = S.cent[c][d], rg = S.repg[d];
+    const float mu = S.cent[c][d], rg = repg_at(d);
     f32x16 acc = f32x16{};
 #pragma unroll
     for (int q = 0; q < NK; ++q)
@@ -1718,12 +1717,16 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
     else return S.a.zc[i * EW_ZP + col];
   };
   if (gc) {
-    // squared norms of the candidate rows (a runtime loop: only the candidates are summed)
+    // squared norms of the candidate rows (a runtime loop: only the candidates are summed), and
+    // this wave's sum of its member rows (lane = 4 hidden units) for the bandwidth
+    f32x4 ms = f32x4{};
     for (int r = g; r < ncand_all; r += ECDA_NG) {
       const f32x4 v = *reinterpret_cast<const f32x4*>(rowp(r) + 4 * lane);
       const float nr = dad_wave_sum(((v[0] * v[0] + v[1] * v[1]) + v[2] * v[2]) + v[3] * v[3]);
       if (lane == 0) S.nz[r] = nr;
+      ms += S.mem[r] ? v : f32x4{};
     }
+    *reinterpret_cast<f32x4*>(&S.msp[g][4 * lane]) = ms;
     // Gram partials: tile pair (ti, tj) over a K slice, fp32 matrix cores
     for (int item = g; item < npt * ks; item += ECDA_NG) {
       const int pr = item / ks, sl = item - pr * ks;
@@ -1764,24 +1767,6 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
   const int ept = npad * npad / ECDA_THREADS;     // 2, 8 or 32
   const int tpr = npad / ept;                     // threads per row: 16, 8 or 4
   const int ei = tid / tpr, ej0 = (tid - ei * tpr) * ept;
-  double bwpart = 0.0;
-  if (gc) {
-    // branch-free: every element computed, invalid ones selected to 0
-    const int mi = S.mem[ei < ncand_all ? ei : 0] & (ei < ncand_all ? 1 : 0);
-    for (int e = 0; e < ept; ++e) {
-      const int i = ei, j = ej0 + e;
-      // G_ij read at (min, max) in the upper-triangle tiles: D is symmetric bit for bit
-      const int lo = i < j ? i : j, hi = i < j ? j : i;
-      const int pr = ew_pair(lo >> 5, hi >> 5, nt);
-      float gsum = 0.0f;
-      for (int s2 = 0; s2 < ks; ++s2) gsum += S.b.gp[pr * ks + s2][(lo & 31) * EW_GP + (hi & 31)];
-      const bool ok = (i < ncand_all) & (j < ncand_all) & (i != j);
-      const float d = ok ? fmaxf((S.nz[lo] + S.nz[hi]) - 2.0f * gsum, 0.0f) : 0.0f;
-      const int mj = S.mem[j < ncand_all ? j : 0];
-      bwpart += (ok & (mi != 0) & (mj != 0)) ? (double)d : 0.0;
-      db[i * dp + j] = d;
-    }
-  }
   // centroid distances (I/utils.py:582-595): 32 threads per (p, q) pair, pair-symmetric order
   {
     const int pair = tid / 32, t32 = tid & 31;
@@ -1804,8 +1789,11 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
     d = dpp_seg_sum<32>(d);
     if (pair < DAD_C * DAD_C && t32 == 31) S.pd[pair / DAD_C][pair % DAD_C] = sqrtf(d);
   }
-  // compactness partial (I/utils.py:614-616): this wave's masked noisy rows of class c
+  const float Wss = (float)ncs * (float)ncs + 1e-8f;
+  const float Wtt = (float)(wsum_t * wsum_t) + 1e-8f;
+  const float Wst = (float)((double)ncs * wsum_t) + 1e-8f;
   if (gc) {
+    // compactness partial (I/utils.py:614-616): this wave's masked noisy rows of class c
     float cpart = 0.0f;
     const f32x4 mu = *reinterpret_cast<const f32x4*>(&S.cent[c][4 * lane]);
 #pragma unroll
@@ -1818,11 +1806,78 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
       }
     }
     cpart = dad_wave_sum(cpart);
-    bwpart = dad_wave_sum_d(bwpart);
-    if (lane == 0) { S.cmp[g] = cpart; S.bwp[g] = bwpart; }
+    // detached bandwidth (I/utils.py:538-544) without the distance matrix: over the nmem member
+    // rows, sum_ij |z_i - z_j|^2 = 2 nmem sum_i |z_i|^2 - 2 |sum_i z_i|^2, from the candidates'
+    // norms and the waves' member-row sums (every wave alike, in double), so the kernel values
+    // and coefficients follow the distances in the same pass (the distance matrix no longer
+    // makes a round trip through LDS and a barrier before them)
+    f32x4 m = f32x4{};
+#pragma unroll
+    for (int gg = 0; gg < ECDA_NG; ++gg) m += *reinterpret_cast<const f32x4*>(&S.msp[gg][4 * lane]);
+    const double msq = dad_wave_sum_d(((double)m[0] * m[0] + (double)m[1] * m[1]) + ((double)m[2] * m[2] + (double)m[3] * m[3]));
+    double nsq = 0.0;
+    for (int i0 = 0; i0 < ncand_all; i0 += 64) {
+      const int i = i0 + lane;
+      const int ic = i < ncand_all ? i : 0;
+      nsq += ((i < ncand_all) & (S.mem[ic] != 0)) ? (double)S.nz[ic] : 0.0;
+    }
+    nsq = dad_wave_sum_d(nsq);
+    const double bws = fmax(2.0 * (double)nmem * nsq - 2.0 * msq, 0.0);
+    float bw = nmem > 1 ? (float)(bws / (double)(nmem * nmem - nmem)) : 1.0f;
+    bw = bw / 4.0f;
+    float ibw[5];
+#pragma unroll
+    for (int mm = 0; mm < 5; ++mm) ibw[mm] = 1.0f / (bw * (float)(1 << mm) + 1e-8f);
+    // the weighted kernel terms (I/utils.py:546-563): every ordered member pair (i, j); the
+    // symmetric coefficients Csym_ij = dmmd/dD_ij + dmmd/dD_ji; branch-free, invalid elements 0
+    double t3[3] = {0.0, 0.0, 0.0};
+    float rsp = 0.0f;
+    const int ic = ei < ncand_all ? ei : 0;
+    const bool mi = (ei < ncand_all) & (S.mem[ic] != 0);
+    const float wi = S.wz[ic];
+    const bool si = ei < ncs;
+    const float css = 2.0f / Wss, ctt = 2.0f / Wtt, cst = -2.0f / Wst;
+    for (int e = 0; e < ept; ++e) {
+      const int i = ei, j = ej0 + e;
+      // G_ij read at (min, max) in the upper-triangle tiles: D is symmetric bit for bit
+      const int lo = i < j ? i : j, hi = i < j ? j : i;
+      const int pr = ew_pair(lo >> 5, hi >> 5, nt);
+      float gsum = 0.0f;
+      for (int s2 = 0; s2 < ks; ++s2) gsum += S.b.gp[pr * ks + s2][(lo & 31) * EW_GP + (hi & 31)];
+      const bool ok = (i < ncand_all) & (j < ncand_all) & (i != j);
+      const float d = ok ? fmaxf((S.nz[lo] + S.nz[hi]) - 2.0f * gsum, 0.0f) : 0.0f;
+      const int jc = j < ncand_all ? j : 0;
+      const bool on = mi & (j < ncand_all) & (S.mem[jc] != 0);
+      const float wj = S.wz[jc];
+      float K = 0.0f, dK = 0.0f;
+#pragma unroll
+      for (int mm = 0; mm < 5; ++mm) {
+        const float ex = __expf(-d * ibw[mm]);
+        K += ex;
+        dK -= ex * ibw[mm];
+      }
+      const bool sj = j < ncs;
+      const bool ss = on & si & sj, tt = on & !si & !sj, st = on & si & !sj, ts = on & !si & sj;
+      const float ww = wi * wj;
+      t3[0] += ss ? (double)K : 0.0;
+      t3[1] += tt ? (double)K * ww : 0.0;
+      t3[2] += st ? (double)K * wj : 0.0;
+      // Csym: SS 2/Wss dK, TT 2 w_i w_j/Wtt dK, ST -2 w_j/Wst dK, TS -2 w_i/Wst dK
+      const float vss = css * dK, vtt = (ctt * ww) * dK, vst = (cst * wj) * dK, vts = (cst * wi) * dK;
+      float v = ss ? vss : (tt ? vtt : (st ? vst : (ts ? vts : 0.0f)));
+      v = i == j ? 0.0f : v;
+      db[i * dp + j] = v;
+      rsp += v;
+    }
+    // row sums of the coefficients: the tpr threads of a row are adjacent lanes
+    rsp = tpr == 16 ? dpp_seg_sum<16>(rsp) : (tpr == 8 ? dpp_seg_sum<8>(rsp) : dpp_seg_sum<4>(rsp));
+    if ((tid & (tpr - 1)) == tpr - 1) S.rs[ei] = rsp;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) t3[k] = dad_wave_sum_d(t3[k]);
+    if (lane == 0) { S.t3p[g][0] = t3[0]; S.t3p[g][1] = t3[1]; S.t3p[g][2] = t3[2]; S.cmp[g] = cpart; }
   }
   __syncthreads();   // ---------------------------------------------------------------- 3
-  ECDA_STAMP(6);
+  ECDA_STAMP(7);
   const float wscale = cfg.w_ecda;
   float pd[DAD_C][DAD_C];
 #pragma unroll
@@ -1842,83 +1897,26 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
       }
     rep = -sp / (float)npairs;
   }
-  // repulsion grad of the class's noisy members, per hidden unit (d rep / d mu_c / n_c)
-  if (tid < DAD_H) {
-    float rep_g = 0.0f;
-    if (rep_on) {
-      float ce[DAD_C];
+  // repulsion grad of the class's noisy members at hidden unit d (d rep / d mu_c / n_c), each
+  // lane for its own columns: rk * sum_q fq (cent_c[d] - cent_q[d]) with uniform fq = 1 / pd_cq
+  // over the valid other classes, in the reference's class order
+  float fq[DAD_C];
 #pragma unroll
-      for (int q = 0; q < DAD_C; ++q) ce[q] = S.cent[q][tid];
-      float gsum = 0.0f;
-#pragma unroll
-      for (int q = 0; q < DAD_C; ++q) {
-        const int nq = S.cnt[q];
-        if (q == c || q >= ncls || nq == 0) continue;
-        const float nd = S.pd[c][q];
-        if (nd > 0.0f) gsum += (sel4(ce, c) - ce[q]) / nd;
-      }
-      rep_g = wscale * rep_coef * (-gsum / (float)npairs / (float)cnc);
-    }
-    S.repg[tid] = rep_g;
+  for (int q = 0; q < DAD_C; ++q) {
+    const int nq = S.cnt[q];
+    const float nd = S.pd[c][q];
+    fq[q] = (rep_on && q != c && q < ncls && nq > 0 && nd > 0.0f) ? nd : 0.0f;
   }
-  const float Wss = (float)ncs * (float)ncs + 1e-8f;
-  const float Wtt = (float)(wsum_t * wsum_t) + 1e-8f;
-  const float Wst = (float)((double)ncs * wsum_t) + 1e-8f;
-  if (gc) {
-    // detached bandwidth (I/utils.py:540-544) and the weighted kernel terms (I/utils.py:546-563):
-    // every ordered member pair (i, j); the symmetric coefficients Csym_ij = dmmd/dD_ij + dmmd/dD_ji
-    double bws = 0.0;
+  const float rk = rep_on ? wscale * rep_coef : 0.0f;
+  auto repg_at = [&](int d) -> float {
+    if (!rep_on) return 0.0f;
+    const float cc0 = S.cent[c][d];
+    float gsum = 0.0f;
 #pragma unroll
-    for (int gg = 0; gg < ECDA_NG; ++gg) bws += S.bwp[gg];
-    float bw = nmem > 1 ? (float)(bws / (double)(nmem * nmem - nmem)) : 1.0f;
-    bw = bw / 4.0f;
-    float ibw[5];
-#pragma unroll
-    for (int m = 0; m < 5; ++m) ibw[m] = 1.0f / (bw * (float)(1 << m) + 1e-8f);
-    double t3[3] = {0.0, 0.0, 0.0};
-    float rsp = 0.0f;
-    // branch-free: every element's K and coefficient computed, selected by pair type
-    const int ic = ei < ncand_all ? ei : 0;
-    const bool mi = (ei < ncand_all) & (S.mem[ic] != 0);
-    const float wi = S.wz[ic];
-    const bool si = ei < ncs;
-    const float css = 2.0f / Wss, ctt = 2.0f / Wtt, cst = -2.0f / Wst;
-    for (int e = 0; e < ept; ++e) {
-      const int j = ej0 + e;
-      const int jc = j < ncand_all ? j : 0;
-      const bool on = mi & (j < ncand_all) & (S.mem[jc] != 0);
-      const float wj = S.wz[jc];
-      const float d = db[ei * dp + j];
-      float K = 0.0f, dK = 0.0f;
-#pragma unroll
-      for (int m = 0; m < 5; ++m) {
-        const float ex = __expf(-d * ibw[m]);
-        K += ex;
-        dK -= ex * ibw[m];
-      }
-      const bool sj = j < ncs;
-      const bool ss = on & si & sj, tt = on & !si & !sj, st = on & si & !sj, ts = on & !si & sj;
-      const float ww = wi * wj;
-      t3[0] += ss ? (double)K : 0.0;
-      t3[1] += tt ? (double)K * ww : 0.0;
-      t3[2] += st ? (double)K * wj : 0.0;
-      // Csym: SS 2/Wss dK, TT 2 w_i w_j/Wtt dK, ST -2 w_j/Wst dK, TS -2 w_i/Wst dK
-      const float vss = css * dK, vtt = (ctt * ww) * dK, vst = (cst * wj) * dK, vts = (cst * wi) * dK;
-      float v = ss ? vss : (tt ? vtt : (st ? vst : (ts ? vts : 0.0f)));
-      v = ei == j ? 0.0f : v;
-      db[ei * dp + j] = v;
-      rsp += v;
-    }
-
-    // row sums of the coefficients: the tpr threads of a row are adjacent lanes
-    rsp = tpr == 16 ? dpp_seg_sum<16>(rsp) : (tpr == 8 ? dpp_seg_sum<8>(rsp) : dpp_seg_sum<4>(rsp));
-    if ((tid & (tpr - 1)) == tpr - 1) S.rs[ei] = rsp;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) t3[k] = dad_wave_sum_d(t3[k]);
-    if (lane == 0) { S.t3p[g][0] = t3[0]; S.t3p[g][1] = t3[1]; S.t3p[g][2] = t3[2]; }
-  }
-  __syncthreads();   // ---------------------------------------------------------------- 4
-  ECDA_STAMP(7);
+    for (int q = 0; q < DAD_C; ++q)
+      if (fq[q] > 0.0f) gsum += (cc0 - S.cent[q][d]) / fq[q];
+    return rk * (-gsum / (float)npairs / (float)cnc);
+  };
   float* ge_c = a.ge;
   float* ge_s = a.ge + (size_t)B * DAD_H;
   if (gc) {
@@ -1944,8 +1942,8 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
     // member grads 2 sum_j Csym_ij (z_i - z_j) = 2 (rs_i z_i - (Csym Z)_i): (Csym Z) on the
     // matrix cores, 32 candidates x 32 hidden units per item
     if constexpr (!WIDE) {
-      if (npad == 32) ew_member_grads<32>(S, db, dp, c, ncs, ncand_all, mmd_scale, comp_scale, ge_c, ge_s, a.sink);
-      else ew_member_grads<64>(S, db, dp, c, ncs, ncand_all, mmd_scale, comp_scale, ge_c, ge_s, a.sink);
+      if (npad == 32) ew_member_grads<32>(S, db, dp, c, ncs, ncand_all, mmd_scale, comp_scale, ge_c, ge_s, a.sink, repg_at);
+      else ew_member_grads<64>(S, db, dp, c, ncs, ncand_all, mmd_scale, comp_scale, ge_c, ge_s, a.sink, repg_at);
     }
     for (int item = g; WIDE && item < nt * (DAD_H / 32); item += ECDA_NG) {
       const int ti = item >> 3, tc = item & 7;
@@ -1961,7 +1959,7 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
 #pragma unroll
         for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[e], bv[e], acc, 0, 0, 0);
       }
-      const float mu = S.cent[c][d], rg = S.repg[d];
+      const float mu = S.cent[c][d], rg = repg_at(d);
       // every accumulator row stored: members to their ge row, the rest to the sink (no branch)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -1980,8 +1978,10 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
     const int nct = ncand_all - ncs;
     for (int e = tid; e < nct * (DAD_H / 4); e += ECDA_THREADS) {
       const int i = ncs + e / (DAD_H / 4), q = e % (DAD_H / 4);
-      if (S.mem[i])
-        reinterpret_cast<f32x4*>(ge_s + (size_t)S.rowz[i] * DAD_H)[q] = reinterpret_cast<const f32x4*>(S.repg)[q];
+      if (S.mem[i]) {
+        const f32x4 v = f32x4{repg_at(4 * q), repg_at(4 * q + 1), repg_at(4 * q + 2), repg_at(4 * q + 3)};
+        reinterpret_cast<f32x4*>(ge_s + (size_t)S.rowz[i] * DAD_H)[q] = v;
+      }
     }
   }
   for (int i = tid; i < ncand_all; i += ECDA_THREADS)

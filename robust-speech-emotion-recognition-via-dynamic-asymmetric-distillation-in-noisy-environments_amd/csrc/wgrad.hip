@@ -317,10 +317,10 @@ __global__ __launch_bounds__(DAD_WGRAD_THREADS) void dad_wgrad_f32(DadWgradArgs 
 //     0xFFFF/0 dword masks and AND-ed with the 16-bit dL/de_u[h] / len_u in both halves: one
 //     bitfield extract, one table read and four ANDs per fragment.  (The loop is bound by
 //     vector issue, about ten VALU instructions per MFMA, so table reads replace arithmetic.)
-// FP16: the per-utterance scales are stored as fp16(v * 2^s) with one power of two 2^s per
-// workgroup (its largest |v| maps into [2^14, 2^15): 11 significant bits and no overflow or
-// subnormals for values within 2^-28 of the largest), and the partial is multiplied by 2^-s
-// (exact) before it is stored.
+// FP16: the per-utterance scales of hidden unit h are stored as fp16(v * 2^s_h), one power of
+// two per h (its largest |v| over the split's utterances maps into [2^14, 2^15): 11 significant
+// bits and no overflow or subnormals for values within 2^-28 of the largest), and row h of the
+// partial is multiplied by 2^-s_h (exact) before it is stored.
 // Software pipeline, one barrier per TWO rounds: round j computes slab j from LDS buffer j&3
 // while it stages slab j+2 into buffer (j+2)&3 and issues the loads of slab j+2+WGD_DEPTH,
 // all in one basic block so the staging VALU fills the MFMA gaps.  dL/de_u[h] / len_u of the
@@ -524,7 +524,7 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
   for (int m = 0; m < 2; ++m)
 #pragma unroll
     for (int n = 0; n < 2; ++n) acc[m][n] = f32x16{};
-  float unscale = 1.0f;   // FP16: 2^-s
+  float unscale = 1.0f;   // FP16: 2^-s_h of row h = 64 wv + lane
   for (int k = 0; DAD_PROBE_ON && k < 10; ++k)
     if (tid == 0 && blockIdx.x < 512) DAD_PROBE_SET(wgd_stamps, blockIdx.x * 10 + k, 0);
   const unsigned long long t0 = WGD_CLK();
@@ -543,16 +543,23 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
     // utterances group g builds entries 4g .. 4g+3 (KG per group).  The first batch's vector
     // loads (dL/dz, ECDA row and flag, length) go out before the slab prefetch, so their math
     // never waits on it.
+    // FP16: row h of G is stored as fp16(v * 2^s_h), with 2^s_h putting max_u |v[u][h]| in
+    // [2^14, 2^15) (wgd_f16_exp); both groups evaluate all KL = 8 utterances of a batch for that
+    // max (the same arithmetic: identical s_h in both), so no barrier is needed, and the row
+    // of the partial is multiplied back by 2^-s_h when it is stored.  Thread hh is lane hh & 63
+    // of wave (hh >> 6) & 3 of its group: the wave that owns rows 64 wv .. 64 wv + 63.
     constexpr int KG = 8 / WGD_GROUPS;
+    constexpr int KL = F16 ? 8 : KG;
+    auto slot = [&](int k) { return F16 ? k : grp * KG + k; };   // utterance slot of evaluation k
     const int hh = tid & (DAD_H - 1);
-    float w2[4], ec0[KG], vl0[KG];
-    f32x4 gz0[KG];
-    uint32_t ef0[KG];
+    float w2[4], ec0[KL], vl0[KL];
+    f32x4 gz0[KL];
+    uint32_t ef0[KL];
 #pragma unroll
     for (int c = 0; c < 4; ++c) w2[c] = ra.student[DAD_OFF_W2 + c * DAD_H + hh];
 #pragma unroll
-    for (int k = 0; k < KG; ++k) {
-      const int u = u0 + min(grp * KG + k, nu - 1);
+    for (int k = 0; k < KL; ++k) {
+      const int u = u0 + min(slot(k), nu - 1);
       ec0[k] = ra.ge_ecda[(size_t)u * DAD_H + hh];
       gz0[k] = *reinterpret_cast<const f32x4*>(ra.gzb + (size_t)u * DAD_C);
       ef0[k] = ra.eflag[u];
@@ -567,63 +574,48 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
 #pragma unroll
     for (int k = 0; k < WGD_DEPTH; ++k) wgd_load(a, tab, min(k, jlast), sfirst, dbase, wv, r[k]);
     const unsigned long long ta = WGD_CLK();
-    // the table: the first batch's values stay in registers (v0); FP16 first takes the
-    // workgroup's largest |v| (a second pass recomputes later batches), then writes the
-    // scaled values
+    // the table: the first batch's values stay in registers (v0); FP16 takes the row's largest
+    // |v| first (a second pass recomputes later batches), then writes the scaled values
     auto ge_table = [&](auto ex_tag) {
       constexpr bool EX = decltype(ex_tag)::value;
-      auto batch = [&](int ul0, float (&v)[KG]) {
+      auto batch = [&](int ul0, float (&v)[KL]) {
 #pragma unroll
-        for (int k = 0; k < KG; ++k) {   // the group's utterances' loads in flight (index clamped)
-          const int u = u0 + min(ul0 + grp * KG + k, nu - 1);
+        for (int k = 0; k < KL; ++k) {   // the batch's loads in flight (index clamped)
+          const int u = u0 + min(ul0 + slot(k), nu - 1);
           v[k] = ul0 == 0 ? fused_ge1_v<EX>(ra, g.Bc, u, hh, w2, gz0[k], ef0[k], ec0[k]) / fmaxf(vl0[k], 1.0f)
                           : fused_ge1<EX>(ra, g.Bc, u, hh, w2) / fmaxf(ra.vlen[u], 1.0f);
         }
       };
-      auto put = [&](int ul0, const float (&v)[KG], float scale) {
+      auto put = [&](int ul0, const float (&v)[KL], float scale) {
 #pragma unroll
         for (int k = 0; k < KG; ++k) {
           const int uk = ul0 + grp * KG + k;
-          if (uk < nu) gs[uk * DAD_H + hh] = dad_half_bits(F16 ? v[k] * scale : v[k], F16);
+          const float x = v[F16 ? grp * KG + k : k];
+          if (uk < nu) gs[uk * DAD_H + hh] = dad_half_bits(F16 ? x * scale : x, F16);
         }
       };
-      float v0[KG];
+      float v0[KL];
       batch(0, v0);
+      float scale = 1.0f;
       if constexpr (F16) {
         float mx = 0.0f;
 #pragma unroll
-        for (int k = 0; k < KG; ++k) mx = fmaxf(mx, fabsf(v0[k]));
+        for (int k = 0; k < KL; ++k) mx = fmaxf(mx, fabsf(v0[k]));   // (clamped slots repeat a real one)
         for (int ul0 = 8; ul0 < nu; ul0 += 8) {
-          float v[KG];
+          float v[KL];
           batch(ul0, v);
 #pragma unroll
-          for (int k = 0; k < KG; ++k) mx = fmaxf(mx, ul0 + grp * KG + k < nu ? fabsf(v[k]) : 0.0f);
+          for (int k = 0; k < KL; ++k) mx = fmaxf(mx, ul0 + k < nu ? fabsf(v[k]) : 0.0f);
         }
-        // (values of clamped duplicate utterances equal a real one's: no effect on the max)
-        mx = dad_wave_max(mx);
-        float* wmx = reinterpret_cast<float*>(gs);   // 8 wave maxima in the table's first 32 B
-        if (lane == 0) wmx[tid >> 6] = mx;
-        __syncthreads();
-        float m8 = wmx[0];
-#pragma unroll
-        for (int k = 1; k < WGD_THREADS / 64; ++k) m8 = fmaxf(m8, wmx[k]);
-        __syncthreads();   // every wave has read the maxima before the table overwrites them
-        const int s = wgd_f16_exp(m8);
-        const float scale = __builtin_ldexpf(1.0f, s);
+        const int s = wgd_f16_exp(mx);
+        scale = __builtin_ldexpf(1.0f, s);
         unscale = __builtin_ldexpf(1.0f, -s);
-        put(0, v0, scale);
-        for (int ul0 = 8; ul0 < nu; ul0 += 8) {
-          float v[KG];
-          batch(ul0, v);
-          put(ul0, v, scale);
-        }
-      } else {
-        put(0, v0, 1.0f);
-        for (int ul0 = 8; ul0 < nu; ul0 += 8) {
-          float v[KG];
-          batch(ul0, v);
-          put(ul0, v, 1.0f);
-        }
+      }
+      put(0, v0, scale);
+      for (int ul0 = 8; ul0 < nu; ul0 += 8) {
+        float v[KL];
+        batch(ul0, v);
+        put(ul0, v, scale);
       }
     };
     if (ra.keep1) ge_table(std::true_type{});
@@ -716,7 +708,8 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
           const int h = (2 * wv + m) * 32 + dad_acc_row(rr, kh);
           const int d = 32 * nn + (lane & 31);
           const float v = acc[m][nn][rr] + (WGD_GROUPS == 2 ? red[h * WGD_DB + d] : 0.0f);
-          outf[(size_t)h * DAD_D + dbase + d] = F16 ? v * unscale : v;
+          // FP16: 2^-s_h of row h, held by lane h - 64 wv of this wave (ds_bpermute)
+          outf[(size_t)h * DAD_D + dbase + d] = F16 ? v * __shfl(unscale, h - 64 * wv, 64) : v;
         }
   if constexpr (WGD_GROUPS == 2) __syncthreads();   // red free for the next tile
   WGD_ACC(0, t1 - t0); WGD_ACC(1, t2 - t1); WGD_ACC(2, WGD_CLK() - t2);

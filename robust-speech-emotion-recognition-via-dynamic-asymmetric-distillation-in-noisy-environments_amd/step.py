@@ -217,7 +217,7 @@ class DADStep:
         _lib.check(_lib.lib().dad_workspace_bytes(cfg, ctypes.byref(nbytes)), "dad_workspace_bytes")
         need = int(nbytes.value)
         if self._ws is None or self._ws.numel() < need:
-            # zero-filled once: the in-launch pooling's arrival counters live in it (dad.h)
+            # zero-filled once (finite bytes everywhere; the step needs no initialisation)
             self._ws = torch.zeros(need, dtype=torch.uint8, device=self.device)
         return self._ws
 
