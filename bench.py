@@ -687,8 +687,9 @@ def main():
                     help="steps of the per-kernel timing pass after the timed region (0: none)")
     ap.add_argument("--no-data-path", action="store_true", help="skip the device collate measurement (N=1)")
     ap.add_argument("--no-parity", action="store_true", help="skip the 16-bit-vs-fp32 parity block (N=1)")
-    ap.add_argument("--launch", default="graph", choices=["graph", "eager"],
-                    help="timed steps as hipGraph replays (one graph per resident batch) or eager launches")
+    ap.add_argument("--launch", default="eager", choices=["graph", "eager"],
+                    help="timed steps as eager launches (default) or hipGraph replays (one graph per resident batch; "
+                         "measured no faster on this ROCm, DESIGN.md §5)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:

@@ -19,7 +19,7 @@ def main():
     B, T = 64, 300
     model = PKG.SSRLModel().cuda()
     P = bench.init_model_weights(model, seed=0)
-    step = PKG.DADStep(model, flavor="iemocap", precision="bf16", rng="counter", seed=1)
+    step = PKG.DADStep(model, flavor="iemocap", precision=os.environ.get("STAMP_PREC", "fp16"), rng="counter", seed=1)
     data = bench.make_batches(P, 2, B, T, seed=17, device=torch.device("cuda"))
     for i in range(6):
         step.step(data[i % 2][0], data[i % 2][1], 60)
