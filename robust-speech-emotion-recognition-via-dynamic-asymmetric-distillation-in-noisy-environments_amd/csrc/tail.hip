@@ -21,7 +21,7 @@
 
 // ECDA per-class phase wall clocks (100 MHz) of the stamps build (dad_probe.h): 16 slots per
 // class, then the tail block's phases
-#define ECDA_SLOTS 24
+#define ECDA_SLOTS 32
 DAD_PROBE_BUFFER(ecda_stamps, DAD_C * ECDA_SLOTS + 16)
 #define ECDA_STAMP(k) \
   if (threadIdx.x == 0) DAD_PROBE_SET(ecda_stamps, (gridDim.x > DAD_C ? blockIdx.x - 1 : blockIdx.x) * ECDA_SLOTS + (k), DAD_PROBE_WALL())
@@ -1660,6 +1660,7 @@ __device__ __forceinline__ void ew_member_grads(EcdaW& S, const float* db, int d
     for (int q = 0; q < NK; ++q)
 #pragma unroll
       for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[q][e], bv[q][e], acc, 0, 0, 0);
+    ECDA_CYC(25);
     float* stg = &S.b.gp[0][0] + g * (32 * EW_TP);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -1669,6 +1670,7 @@ __device__ __forceinline__ void ew_member_grads(EcdaW& S, const float* db, int d
           mmd_scale * (2.0f * (rsv[r] * zi[r] - acc[r])) + (noisy ? comp_scale * (zi[r] - mu) + rg : 0.0f);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // (the wave's own tile: LDS ops are in order)
+    ECDA_CYC(26);
     // every row stored: members to their ge row, the rest to the sink (no branch)
     const int rl = lane >> 3, c4 = 4 * (lane & 7);
 #pragma unroll
@@ -1681,6 +1683,7 @@ __device__ __forceinline__ void ew_member_grads(EcdaW& S, const float* db, int d
       *reinterpret_cast<f32x4*>(dst) = v;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // tile reads done before the next item's writes
+    ECDA_CYC(27);
   }
 }
 
@@ -1763,6 +1766,7 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
   ECDA_STAMP(4);
   __syncthreads();   // ---------------------------------------------------------------- 2
   ECDA_STAMP(5);
+  ECDA_CYC(6);
   // element ownership of the [npad x npad] matrices: row ei, columns ej0 .. ej0 + ept - 1
   const int ept = npad * npad / ECDA_THREADS;     // 2, 8 or 32
   const int tpr = npad / ept;                     // threads per row: 16, 8 or 4
@@ -1789,6 +1793,7 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
     d = dpp_seg_sum<32>(d);
     if (pair < DAD_C * DAD_C && t32 == 31) S.pd[pair / DAD_C][pair % DAD_C] = sqrtf(d);
   }
+  ECDA_CYC(20);
   const float Wss = (float)ncs * (float)ncs + 1e-8f;
   const float Wtt = (float)(wsum_t * wsum_t) + 1e-8f;
   const float Wst = (float)((double)ncs * wsum_t) + 1e-8f;
@@ -1828,6 +1833,7 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
     float ibw[5];
 #pragma unroll
     for (int mm = 0; mm < 5; ++mm) ibw[mm] = 1.0f / (bw * (float)(1 << mm) + 1e-8f);
+    ECDA_CYC(21);
     // the weighted kernel terms (I/utils.py:546-563): every ordered member pair (i, j); the
     // symmetric coefficients Csym_ij = dmmd/dD_ij + dmmd/dD_ji; branch-free, invalid elements 0
     double t3[3] = {0.0, 0.0, 0.0};
@@ -1869,12 +1875,14 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
       db[i * dp + j] = v;
       rsp += v;
     }
+    ECDA_CYC(22);
     // row sums of the coefficients: the tpr threads of a row are adjacent lanes
     rsp = tpr == 16 ? dpp_seg_sum<16>(rsp) : (tpr == 8 ? dpp_seg_sum<8>(rsp) : dpp_seg_sum<4>(rsp));
     if ((tid & (tpr - 1)) == tpr - 1) S.rs[ei] = rsp;
 #pragma unroll
     for (int k = 0; k < 3; ++k) t3[k] = dad_wave_sum_d(t3[k]);
     if (lane == 0) { S.t3p[g][0] = t3[0]; S.t3p[g][1] = t3[1]; S.t3p[g][2] = t3[2]; S.cmp[g] = cpart; }
+    ECDA_CYC(23);
   }
   __syncthreads();   // ---------------------------------------------------------------- 3
   ECDA_STAMP(7);
@@ -1898,24 +1906,23 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
     rep = -sp / (float)npairs;
   }
   // repulsion grad of the class's noisy members at hidden unit d (d rep / d mu_c / n_c), each
-  // lane for its own columns: rk * sum_q fq (cent_c[d] - cent_q[d]) with uniform fq = 1 / pd_cq
-  // over the valid other classes, in the reference's class order
-  float fq[DAD_C];
+  // lane for its own columns: rk * sum_q (cent_c[d] - cent_q[d]) / pd_cq over the valid other
+  // classes in the reference's class order; the reciprocals are wave-uniform, taken once
+  float rq[DAD_C];
 #pragma unroll
   for (int q = 0; q < DAD_C; ++q) {
     const int nq = S.cnt[q];
     const float nd = S.pd[c][q];
-    fq[q] = (rep_on && q != c && q < ncls && nq > 0 && nd > 0.0f) ? nd : 0.0f;
+    rq[q] = (rep_on && q != c && q < ncls && nq > 0 && nd > 0.0f) ? 1.0f / nd : 0.0f;
   }
-  const float rk = rep_on ? wscale * rep_coef : 0.0f;
+  const float rk = rep_on ? -wscale * rep_coef / (float)npairs / (float)cnc : 0.0f;
   auto repg_at = [&](int d) -> float {
     if (!rep_on) return 0.0f;
     const float cc0 = S.cent[c][d];
     float gsum = 0.0f;
 #pragma unroll
-    for (int q = 0; q < DAD_C; ++q)
-      if (fq[q] > 0.0f) gsum += (cc0 - S.cent[q][d]) / fq[q];
-    return rk * (-gsum / (float)npairs / (float)cnc);
+    for (int q = 0; q < DAD_C; ++q) gsum += rq[q] != 0.0f ? (cc0 - S.cent[q][d]) * rq[q] : 0.0f;
+    return rk * gsum;
   };
   float* ge_c = a.ge;
   float* ge_s = a.ge + (size_t)B * DAD_H;
@@ -1937,6 +1944,7 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
       a.tail_terms[c] = att_c * (mmd + cfg.ecda_gamma * comp + cfg.ecda_delta * rep);
       a.tail_terms[DAD_T_ECDA_GATE - DAD_T_ECDA_TERM + c] = 1.0f;
     }
+    ECDA_CYC(24);
     const float mmd_scale = wscale * att_c;
     const float comp_scale = wscale * att_c * cfg.ecda_gamma * (2.0f / (float)cnc);
     // member grads 2 sum_j Csym_ij (z_i - z_j) = 2 (rs_i z_i - (Csym Z)_i): (Csym Z) on the

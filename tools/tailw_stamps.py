@@ -22,7 +22,7 @@ def main():
     P = bench.init_model_weights(model, seed=0)
     step = PKG.DADStep(model, flavor="iemocap", precision=os.environ.get("STAMP_PREC", "fp16"), rng="counter", seed=1)
     data = bench.make_batches(P, 2, B, T, seed=17, device=torch.device("cuda"))
-    S = 24  # slots per ECDA class (tail.hip ECDA_SLOTS)
+    S = 32  # slots per ECDA class (tail.hip ECDA_SLOTS)
     L = PKG.lib()
     reps = int(os.environ.get("STAMP_REPS", "15"))
     raw = []
@@ -52,7 +52,13 @@ def main():
         if all(on[o + a] and on[o + b] for a, b, _ in cyc):
             print("ecda class %d staging cycles: %s" % (c, "  ".join(
                 "%s %d" % (n, int(np.median(raw[:, o + b] - raw[:, o + a]))) for a, b, n in cyc)))
-    names = ["start", "dacp", "staged", "b1", "gram+cent", "b2", "b3", "b4", "end", "rows-landed", "", "", "norms"]
+    cyc2 = [(6, 20, "cent-dist"), (20, 21, "comp+bw"), (21, 22, "pairs"), (22, 23, "sums"), (23, 24, "b3+terms"),
+            (24, 25, "mg-reads+mfma"), (25, 26, "mg-stage"), (26, 27, "mg-stores"), (27, 28, "flags")]
+    for c in range(4):
+        o = c * S
+        print("ecda class %d coef/grad cycles: %s" % (c, "  ".join(
+            "%s %d" % (n, int(np.median(raw[:, o + b] - raw[:, o + a]))) for a, b, n in cyc2 if on[o + a] and on[o + b])))
+    names = ["start", "dacp", "staged", "b1", "gram+cent", "b2", "b3", "b4", "end", "rows-landed", "", "", "cand-stored"]
     for c in range(4):
         o = c * S
         print("ecda class %d (cand %d, clean %d): %s" % (c, raw[-1, o + 10], raw[-1, o + 11], "  ".join(
