@@ -687,6 +687,8 @@ def main():
                     help="steps of the per-kernel timing pass after the timed region (0: none)")
     ap.add_argument("--no-data-path", action="store_true", help="skip the device collate measurement (N=1)")
     ap.add_argument("--no-parity", action="store_true", help="skip the 16-bit-vs-fp32 parity block (N=1)")
+    ap.add_argument("--no-ahead", action="store_true",
+                    help="16-bit modes: every step prepares its own rows (no next-batch preparation in the tail launch)")
     ap.add_argument("--launch", default="eager", choices=["graph", "eager"],
                     help="timed steps as eager launches (default) or hipGraph replays (one graph per resident batch; "
                          "measured no faster on this ROCm, DESIGN.md §5)")
@@ -741,10 +743,16 @@ def main():
         data = make_batches(P, N_BATCHES, B, T, seed=17 + rank, device=dev, snr_db=args.snr)
         torch.cuda.synchronize()
 
+        pos = [0]
+
         def run(n):
-            for i in range(n):
+            # each step names the next resident batch: its augmentation + 16-bit conversion run in
+            # this step's tail launch (DADStep.step(next_batch=...)); bit-identical either way
+            for _ in range(n):
+                i = pos[0]
+                pos[0] += 1
                 c, nb = data[i % len(data)]
-                step.step(c, nb, args.epoch)
+                step.step(c, nb, args.epoch, next_batch=None if args.no_ahead else data[(i + 1) % len(data)])
 
         run(args.warmup)
         torch.cuda.synchronize()

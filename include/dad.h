@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define DAD_ABI_VERSION 3
+#define DAD_ABI_VERSION 4
 
 /* error codes (besides hipError_t values) */
 #define DAD_OK 0
@@ -117,7 +117,10 @@ typedef struct dad_config {
   float ema_m, ema_one_m;       /* EMA_MOMENTUM, 1-EMA_MOMENTUM (I/model.py:219) */
   float dacp_beta, dacp_one_m_beta;   /* epoch-end quality smoothing (I/utils.py:433-436) */
   int32_t splits;               /* weight-gradient split-K factor (0 = auto) */
-  int32_t reserved[5];
+  int32_t prepped;              /* FP16/BF16: 1 = the previous step's dad_step_backward_ahead prepared this
+                                   batch's 16-bit rows (it reported *prepped = 1 for this cfg and batch), so
+                                   the encoder skips the preparation; 0 = prepare them in this step */
+  int32_t reserved[4];
 } dad_config;
 
 /* One clean + one noisy collated batch (I/dataload_noisy.py:124-129 format). */
@@ -196,6 +199,17 @@ int dad_step_encode(const dad_config* cfg, const dad_batch* batch, const dad_sta
                     void* workspace, void* stream);
 int dad_step_backward(const dad_config* cfg, const dad_batch* batch, const dad_state* st,
                       void* workspace, void* stream);
+/* dad_step_backward + the NEXT step's row preparation (FP16/BF16: the augmentation and 16-bit
+ * conversion of next_batch under next_cfg, weight-independent) on the CUs this step's tail launch
+ * leaves idle.  *prepped = 1 when it was enqueued: the next step then passes cfg->prepped = 1 with
+ * the same next_cfg scalars and next_batch pointers, whose contents must not change in between.
+ * *prepped = 0 (and nothing extra enqueued) unless: 16-bit precision, the tail runs as the
+ * wave-centric launch (B, Bn <= 64, class-aware MMD), next_cfg has this cfg's geometry and
+ * precision and the other counter parity.  Replaces nothing in the reference: its loop draws the
+ * augmentation inside train_step (I/train.py:406-410,439); the draws are the same streams. */
+int dad_step_backward_ahead(const dad_config* cfg, const dad_batch* batch, const dad_state* st,
+                            void* workspace, void* stream, const dad_config* next_cfg,
+                            const dad_batch* next_batch, int* prepped);
 int dad_step_apply(const dad_config* cfg, const dad_state* st, void* workspace, void* stream);
 int dad_step(const dad_config* cfg, const dad_batch* batch, const dad_state* st,
              void* workspace, void* stream);

@@ -13,8 +13,8 @@ CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_DIR = os.path.join(PKG_DIR, "lib")
 OBJ_DIR = os.path.join(PKG_DIR, "build")
 LIB_PATH = os.path.join(LIB_DIR, "libdad_hip.so")
-SOURCES = ["encode.hip", "encode_ws.hip", "tail.hip", "wgrad.hip", "optim.hip", "dad_abi.hip", "rccl_dp.hip", "collate.hip", "eval.hip", "utils_abi.hip"]
-HEADERS = ["dad_common.h", "dad_kernels.h", "dad_probe.h", os.path.join("..", "..", "include", "dad.h")]
+SOURCES = ["encode.hip", "encode_ws.hip", "tail.hip", "wgrad.hip", "optim.hip", "dad_abi.hip", "rccl_dp.hip", "collate.hip", "eval.hip", "utils_abi.hip", "prep.hip"]
+HEADERS = ["dad_common.h", "dad_kernels.h", "dad_probe.h", "dad_prep.h", os.path.join("..", "..", "include", "dad.h")]
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")
 ARCH = os.environ.get("DAD_OFFLOAD_ARCH", "gfx950")

@@ -49,7 +49,7 @@ class DadConfig(ctypes.Structure):
         ("one_m_beta2", ctypes.c_float), ("adam_eps", ctypes.c_float), ("weight_decay", ctypes.c_float),
         ("ema_m", ctypes.c_float), ("ema_one_m", ctypes.c_float),
         ("dacp_beta", ctypes.c_float), ("dacp_one_m_beta", ctypes.c_float),
-        ("splits", ctypes.c_int32), ("reserved", ctypes.c_int32 * 5),
+        ("splits", ctypes.c_int32), ("prepped", ctypes.c_int32), ("reserved", ctypes.c_int32 * 4),
     ]
 
 
@@ -79,6 +79,10 @@ EXPORTS = {
                                        ctypes.POINTER(DadState), ctypes.c_void_p, ctypes.c_void_p]),
     "dad_step_backward": (ctypes.c_int, [ctypes.POINTER(DadConfig), ctypes.POINTER(DadBatch),
                                          ctypes.POINTER(DadState), ctypes.c_void_p, ctypes.c_void_p]),
+    "dad_step_backward_ahead": (ctypes.c_int, [ctypes.POINTER(DadConfig), ctypes.POINTER(DadBatch),
+                                               ctypes.POINTER(DadState), ctypes.c_void_p, ctypes.c_void_p,
+                                               ctypes.POINTER(DadConfig), ctypes.POINTER(DadBatch),
+                                               ctypes.POINTER(ctypes.c_int)]),
     "dad_step_apply": (ctypes.c_int, [ctypes.POINTER(DadConfig), ctypes.POINTER(DadState),
                                       ctypes.c_void_p, ctypes.c_void_p]),
     "dad_step": (ctypes.c_int, [ctypes.POINTER(DadConfig), ctypes.POINTER(DadBatch), ctypes.POINTER(DadState),

@@ -202,6 +202,69 @@ int ws_split(const DadGeom& G, int Bn, int cus, int& nt, int& ns) {
   return last.rc;
 }
 
+// Split of the prepared-row encoder (dad_encode_wp): every live sub-slab costs the same (no
+// augmentation in the launch), so teacher : student workgroups follow the live sub-slab counts.
+int wp_split(const DadGeom& G, int Bn, int cus, int& nt, int& ns) {
+  struct Entry { int Bc, Tc, Bn, Tn, cus, rc, nt, ns; };
+  static thread_local Entry last{-1, -1, -1, -1, -1, 0, 0, 0};
+  if (!(last.Bc == G.Bc && last.Tc == G.Tc && last.Bn == Bn && last.Tn == G.Tn && last.cus == cus)) {
+    Entry e{G.Bc, G.Tc, Bn, G.Tn, cus, 0, 0, 0};
+    const int Jt = Bn * G.ncn, Jc = G.Bc * G.ncc, Js = Jt;
+    const double lt = (double)Bn * ((G.Tn + 15) / 16), lc = (double)G.Bc * ((G.Tc + 15) / 16);
+    if (Jt == 0) {
+      e.nt = 0;
+      e.ns = std::min(cus, Jc);
+    } else {
+      e.nt = (int)(cus * lt / (2.0 * lt + lc) + 0.5);
+      e.nt = std::max(1, std::min(cus - 1, std::min(e.nt, Jt)));
+      e.ns = std::min(cus - e.nt, Jc + Js);
+    }
+    e.nt = std::max(e.nt, (Jt + DAD_ENC_WS_MAXJ - 1) / DAD_ENC_WS_MAXJ);
+    e.ns = std::max(e.ns, (Jc + Js + DAD_ENC_WS_MAXJ - 1) / DAD_ENC_WS_MAXJ);
+    while (e.rc == DAD_OK && e.nt > 0 && ws_max_range(G, Bn, e.nt, e.ns, 1.0f, true) > DAD_ENC_WS_MAXJ)
+      if (++e.nt > Jt) e.rc = DAD_E_SHAPE;
+    while (e.rc == DAD_OK && ws_max_range(G, Bn, e.nt, e.ns, 1.0f, false) > DAD_ENC_WS_MAXJ)
+      if (++e.ns > Jc + Js) e.rc = DAD_E_SHAPE;
+    last = e;
+  }
+  nt = last.nt;
+  ns = last.ns;
+  return last.rc;
+}
+
+// DAD_WP_WAVES=4: the prepared-row encoder with one wave per SIMD (A/B runs; read once)
+int wp_waves() {
+  static const int w = [] { const char* e = getenv("DAD_WP_WAVES"); return (e && strcmp(e, "4") == 0) ? 4 : 8; }();
+  return w;
+}
+
+// Row-preparation arguments (dad_prep.h) of the step described by (cfg, bt) into set x16.
+DadPrepArgs prep_args(const dad_config* cfg, const dad_batch* bt, uint16_t* x16) {
+  DadPrepArgs p;
+  memset(&p, 0, sizeof(p));
+  const Keys k = keys_of(cfg);
+  p.g = geom_of(cfg);
+  p.warmup = cfg->warmup; p.mask_len = cfg->mask_len; p.start_hi = cfg->start_hi;
+  p.f16 = cfg->precision == DAD_PREC_FP16 ? 1 : 0;
+  p.xc = bt->xc; p.xn = bt->xn;
+  p.src = DadStoreRows{bt->rowc, bt->lenc, bt->rown, bt->lenn};
+  if (cfg->rng_mode == DAD_RNG_EXPLICIT) { p.nw = bt->nw; p.ns = bt->ns; p.u = bt->u; p.start = bt->start; }
+  p.key_weak = k.weak; p.key_strong = k.strong; p.key_feat = k.feat; p.key_tstart = k.tstart;
+  p.weak_std = cfg->weak_std; p.strong_std = cfg->strong_std; p.feat_p = cfg->feat_p;
+  p.x16 = x16;
+  return p;
+}
+
+// standalone preparation of one set: ~4 workgroups of 4 waves per CU, two rows in flight per wave
+int launch_prep(const DadPrepArgs& p, hipStream_t stream) {
+  int cus = 0;
+  const int rc = device_cus(&cus);
+  if (rc) return rc;
+  hipLaunchKernelGGL(dad_prep, dim3(4 * cus), dim3(DAD_PREP_THREADS), 0, stream, p);
+  DAD_TRY(hipGetLastError());
+  return DAD_OK;
+}
+
 // Per-kernel timing of the fused step (dad_timing_start / dad_timing_stop): every `every`-th
 // step (counted at its encoder call) records hip events at the kernel boundaries of the
 // caller's stream.  Events are created up front by dad_timing_start, so a timed region only
@@ -356,8 +419,27 @@ int dad_workspace_bytes(const dad_config* cfg, size_t* bytes) {
 
 }  // extern "C"
 
+// The next step's batch may be prepared in this step's tail launch when the tail runs as
+// dad_tail_ecda_w and the next step has this step's workspace layout (so its prepared set sits
+// where the next step will look) and the other set parity.
+static bool can_prepare_ahead(const dad_config* cfg, const dad_config* ncfg, const dad_batch* nbt) {
+  if (!ncfg || !nbt || check_cfg(ncfg) != DAD_OK) return false;
+  if (!dad_prec16(cfg->precision) || ncfg->precision != cfg->precision) return false;
+  if (ncfg->B != cfg->B || ncfg->T != cfg->T || ncfg->Bn != cfg->Bn || ncfg->Tn != cfg->Tn) return false;
+  if (((ncfg->counter ^ cfg->counter) & 1u) == 0) return false;
+  if (max_splits_of(ncfg) != max_splits_of(cfg)) return false;
+  if (!nbt->xc || !nbt->mc) return false;
+  if (!ncfg->warmup && (!nbt->xn || !nbt->mn)) return false;
+  if (ncfg->rng_mode == DAD_RNG_EXPLICIT && !ncfg->warmup && (!nbt->nw || !nbt->ns || !nbt->u || !nbt->start))
+    return false;
+  if ((nbt->rowc == nullptr) != (nbt->lenc == nullptr) || (nbt->rown == nullptr) != (nbt->lenn == nullptr)) return false;
+  return true;
+}
+
 static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const dad_state* st, void* workspace,
-                               void* stream_, bool do_encode, bool do_backward) {
+                               void* stream_, bool do_encode, bool do_backward, const dad_config* ncfg = nullptr,
+                               const dad_batch* nbt = nullptr, int* prepped = nullptr) {
+  if (prepped) *prepped = 0;
   int rc = check_cfg(cfg);
   if (rc) return rc;
   if (!bt || !st || !workspace) return DAD_E_ARG;
@@ -390,9 +472,12 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   float* ecda_scratch = ws_ptr<float>(workspace, L.ecda);
   float* gzb = ws_ptr<float>(workspace, L.gzb);
   uint32_t* eflag = ws_ptr<uint32_t>(workspace, L.eflag);
-  uint16_t* xs16 = ws_ptr<uint16_t>(workspace, L.xs16);
   const bool h16 = dad_prec16(cfg->precision);
   const bool f16 = cfg->precision == DAD_PREC_FP16;
+  // 16-bit modes: this step's prepared set (parity of the step counter; the next step's set is
+  // the other one, so preparing it in this step's tail launch leaves this one intact for wgrad)
+  uint16_t* xs16 = ws_ptr<uint16_t>(workspace, L.xs16 + (cfg->counter & 1u) * L.x16set);
+  const size_t nrc = (size_t)G.Bc * G.Tc, nrn = (size_t)G.Bn * G.Tn;
 
   // 1. fused augmentation + encoder GEMMs + pooling partials
   DadEncodeArgs ea;
@@ -414,22 +499,27 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
     tk_begin();
     tk_mark(TK_E0, stream);
     if (h16) {
+      // augmentation + 16-bit conversion (unless the previous step's tail launch prepared this
+      // batch: cfg->prepped), then the W-stationary GEMM on the prepared set
+      if (!cfg->prepped) {
+        const int rp = launch_prep(prep_args(cfg, bt, xs16), stream);
+        if (rp) return rp;
+      }
       int cus = 0;
       const int rc = device_cus(&cus);
       if (rc) return rc;
-      const int rs = ws_split(G, Bn, cus, ea.ws_nt, ea.ws_ns);
+      const int rs = wp_split(G, Bn, cus, ea.ws_nt, ea.ws_ns);
       if (rs) return rs;
-      ea.ws_wstrong = ws_weights().strong;
-      ea.ws_sweep = ws_sweep(G, Bn, cus);
-      if (ea.ws_sweep.nt > 0) { ea.ws_nt = cus; ea.ws_ns = 0; }   // (grid = cus: one workgroup per CU)
+      ea.ws_wstrong = 1.0f;
+      ea.x16c = xs16; ea.x16s = xs16 + nrc * DAD_D; ea.x16w = ea.x16s + (cfg->warmup ? 0 : nrn) * DAD_D;
       if (ea.ws_nt + ea.ws_ns > 0) {
-        const dim3 grid(ea.ws_nt + ea.ws_ns), block(DAD_ENC_WS_THREADS);
-        if (f16) {
-          if (explicit_rng) hipLaunchKernelGGL(dad_encode_ws_f16_explicit, grid, block, 0, stream, ea);
-          else hipLaunchKernelGGL(dad_encode_ws_f16, grid, block, 0, stream, ea);
+        const dim3 grid(ea.ws_nt + ea.ws_ns);
+        if (wp_waves() == 4) {
+          if (f16) hipLaunchKernelGGL(dad_encode_wp4_f16, grid, dim3(256), 0, stream, ea);
+          else hipLaunchKernelGGL(dad_encode_wp4, grid, dim3(256), 0, stream, ea);
         } else {
-          if (explicit_rng) hipLaunchKernelGGL(dad_encode_ws_explicit, grid, block, 0, stream, ea);
-          else hipLaunchKernelGGL(dad_encode_ws, grid, block, 0, stream, ea);
+          if (f16) hipLaunchKernelGGL(dad_encode_wp_f16, grid, dim3(DAD_ENC_WS_THREADS), 0, stream, ea);
+          else hipLaunchKernelGGL(dad_encode_wp, grid, dim3(DAD_ENC_WS_THREADS), 0, stream, ea);
         }
       }
     } else {
@@ -474,9 +564,21 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   ca.sink = ws_ptr<float>(workspace, L.gflat);
   if (!cfg->warmup && DAD_FUSED_TAIL) {
     // batches of at most 64 utterances per side, class-aware MMD: the wave-centric launch
-    if (G.Bc <= 64 && Bn <= 64 && cfg->class_aware && tail_w_on())
-      hipLaunchKernelGGL(dad_tail_ecda_w, dim3(1 + DAD_C), dim3(DAD_TAIL_THREADS), 0, stream, ta, ca);
-    else
+    if (G.Bc <= 64 && Bn <= 64 && cfg->class_aware && tail_w_on()) {
+      // + the next step's row preparation on the CUs the tail and class blocks leave idle
+      DadPrepArgs pa;
+      memset(&pa, 0, sizeof(pa));
+      int nblk = 1 + DAD_C;
+      if (can_prepare_ahead(cfg, ncfg, nbt)) {
+        int cus = 0;
+        const int rc = device_cus(&cus);
+        if (rc) return rc;
+        pa = prep_args(ncfg, nbt, ws_ptr<uint16_t>(workspace, L.xs16 + (ncfg->counter & 1u) * L.x16set));
+        nblk = std::max(cus, 2 * (1 + DAD_C));
+        if (prepped) *prepped = 1;
+      }
+      hipLaunchKernelGGL(dad_tail_ecda_w, dim3(nblk), dim3(DAD_TAIL_THREADS), 0, stream, ta, ca, pa);
+    } else
       hipLaunchKernelGGL(dad_tail_ecda, dim3(1 + DAD_C), dim3(DAD_TAIL_THREADS), 0, stream, ta, ca);
     DAD_TRY(hipGetLastError());
   } else {
@@ -554,6 +656,11 @@ int dad_step_encode(const dad_config* cfg, const dad_batch* bt, const dad_state*
 int dad_step_backward(const dad_config* cfg, const dad_batch* bt, const dad_state* st, void* workspace,
                       void* stream) {
   return step_compute_phases(cfg, bt, st, workspace, stream, false, true);
+}
+
+int dad_step_backward_ahead(const dad_config* cfg, const dad_batch* bt, const dad_state* st, void* workspace,
+                            void* stream, const dad_config* next_cfg, const dad_batch* next_batch, int* prepped) {
+  return step_compute_phases(cfg, bt, st, workspace, stream, false, true, next_cfg, next_batch, prepped);
 }
 
 int dad_step_apply(const dad_config* cfg, const dad_state* st, void* workspace, void* stream_) {
@@ -746,17 +853,24 @@ int encoder_forward_impl(const float* x, const uint8_t* pad, int B, int T, const
   ea.part_sum = ws_ptr<float>(workspace, L.part_sum);
   ea.part_cnt = ws_ptr<float>(workspace, L.part_cnt);
   ea.bits = ws_ptr<uint32_t>(workspace, L.bits);
-  ea.xs16 = ws_ptr<uint16_t>(workspace, L.xs16);
   const dim3 egrid((B * G.ncc + 3) / 4);
   if (dad_prec16(precision)) {
+    // 16-bit rows of x (a clean-only prepared set), then the W-stationary GEMM on them
+    DadPrepArgs pp;
+    memset(&pp, 0, sizeof(pp));
+    pp.g = G; pp.warmup = 1; pp.f16 = f16 ? 1 : 0; pp.xc = x;
+    pp.x16 = ws_ptr<uint16_t>(workspace, L.xs16);
+    const int rp = launch_prep(pp, stream);
+    if (rp) return rp;
+    ea.x16c = pp.x16;
     int cus = 0;
     const int rc = device_cus(&cus);
     if (rc) return rc;
-    const int rs = ws_split(G, 0, cus, ea.ws_nt, ea.ws_ns);
+    const int rs = wp_split(G, 0, cus, ea.ws_nt, ea.ws_ns);
     if (rs) return rs;
-    ea.ws_wstrong = ws_weights().strong;
-    if (f16) hipLaunchKernelGGL(dad_encode_ws_f16, dim3(ea.ws_nt + ea.ws_ns), dim3(DAD_ENC_WS_THREADS), 0, stream, ea);
-    else hipLaunchKernelGGL(dad_encode_ws, dim3(ea.ws_nt + ea.ws_ns), dim3(DAD_ENC_WS_THREADS), 0, stream, ea);
+    ea.ws_wstrong = 1.0f;
+    if (f16) hipLaunchKernelGGL(dad_encode_wp_f16, dim3(ea.ws_nt + ea.ws_ns), dim3(DAD_ENC_WS_THREADS), 0, stream, ea);
+    else hipLaunchKernelGGL(dad_encode_wp, dim3(ea.ws_nt + ea.ws_ns), dim3(DAD_ENC_WS_THREADS), 0, stream, ea);
   } else {
     hipLaunchKernelGGL(dad_encode_f32, egrid, dim3(DAD_ENC_F32_THREADS), 0, stream, ea);
   }

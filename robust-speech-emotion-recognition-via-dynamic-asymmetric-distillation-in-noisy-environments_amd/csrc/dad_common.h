@@ -373,7 +373,10 @@ struct DadWs {
   size_t wpart;      // f32 [S][H][D]               split-K weight-gradient partial slabs
   size_t normpart;   // f32 [DAD_NORM_BLOCKS]       squared-norm partials
   size_t ecda;       // f32 [C][Bc+Bn][Bc+Bn]       ECDA pairwise scratch for large member sets
-  size_t xs16;       // f16/bf16 [Bc*Tc + Bn*Tn][768]  16-bit modes: the student's MFMA input, clean rows then strong rows (wgrad operand)
+  size_t xs16;       // 16-bit modes: two prepared sets (dad_prep.h), set s at xs16 + s * x16set, each
+                     // f16/bf16 [Bc*Tc clean | Bn*Tn strong | Bn*Tn weak][768] (the encoder's input;
+                     // clean + strong are the weight gradient's operand)
+  size_t x16set;     // bytes per prepared set
   size_t w1h;        // f16/bf16 [H][D]             modular encoder ops: 16-bit copy of W1
   size_t gflat;      // f32 [DAD_GRAD_FLOATS]       modular encoder backward: scratch grad vector
   size_t bytes;
@@ -417,7 +420,8 @@ static inline DadWs dad_ws_layout(const DadGeom& g, int splits, int precision) {
   w.wpart = off;    off = dad_align(off + sizeof(float) * (size_t)splits * DAD_H * DAD_D);
   w.normpart = off; off = dad_align(off + sizeof(float) * DAD_NORM_BLOCKS);
   w.ecda = off;     off = dad_align(off + sizeof(float) * DAD_C * nb * nb);
-  w.xs16 = off;     off = dad_align(off + (dad_prec16(precision) ? 2 * ((size_t)g.Bc * g.Tc + (size_t)g.Bn * g.Tn) * DAD_D : 0));
+  w.x16set = dad_align(dad_prec16(precision) ? 2 * ((size_t)g.Bc * g.Tc + 2 * (size_t)g.Bn * g.Tn) * DAD_D : 0);
+  w.xs16 = off;     off = dad_align(off + 2 * w.x16set);
   w.w1h = off;      off = dad_align(off + 2 * (size_t)DAD_H * DAD_D);
   w.gflat = off;    off = dad_align(off + sizeof(float) * DAD_GRAD_FLOATS);
   w.bytes = off;

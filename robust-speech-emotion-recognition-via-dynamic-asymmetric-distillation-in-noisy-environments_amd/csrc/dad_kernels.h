@@ -74,6 +74,25 @@ struct DadEncodeArgs {
   int ws_nt, ws_ns;         // dad_encode_ws: teacher / student workgroups (contiguous split)
   float ws_wstrong;         // dad_encode_ws: cost of a strong slab relative to a clean one
   DadWsSweep ws_sweep;      // dad_encode_ws: XCD-sweep role counts per XCD (nt = ns = nc = 0: contiguous split)
+  // dad_encode_wp: the prepared 16-bit rows (dad_prep) of the clean, strong and weak branches,
+  // [B][T][768] each (padded layout whatever the source mode)
+  const uint16_t* x16c; const uint16_t* x16s; const uint16_t* x16w;
+};
+
+// The weight-independent half of the 16-bit encoder (prep.hip, dad_prep.h): augmentation
+// (I/utils.py:328-375) and the 16-bit conversion of every row of one step, written as one
+// "prepared set" [clean Bc*Tc | strong Bn*Tn | weak Bn*Tn][768] of 16-bit rows (padded layout).
+// Runs standalone before the encoder, or -- for the NEXT step -- on the spare workgroups of the
+// current step's tail launch (dad_tail_ecda_w blocks > DAD_C).
+struct DadPrepArgs {
+  DadGeom g;
+  int warmup, mask_len, start_hi, f16;
+  const float* xc; const float* xn;
+  DadStoreRows src;
+  const float* nw; const float* ns; const float* u; const int64_t* start;   // explicit draws, or NULL
+  uint32_t key_weak, key_strong, key_feat, key_tstart;
+  float weak_std, strong_std, feat_p;
+  uint16_t* x16;            // the set; NULL: nothing to prepare (tail launch without a next batch)
 };
 
 
@@ -160,11 +179,18 @@ __global__ void dad_encode_ws(DadEncodeArgs a);                // bf16 operands,
 __global__ void dad_encode_ws_explicit(DadEncodeArgs a);       // bf16, explicit noise tensors (parity)
 __global__ void dad_encode_ws_f16(DadEncodeArgs a);            // fp16 operands, counter RNG
 __global__ void dad_encode_ws_f16_explicit(DadEncodeArgs a);   // fp16, explicit noise tensors
+__global__ void dad_encode_wp(DadEncodeArgs a);                // bf16 operands from a prepared set
+__global__ void dad_encode_wp_f16(DadEncodeArgs a);            // fp16 operands from a prepared set
+__global__ void dad_encode_wp4(DadEncodeArgs a);               // 4 waves (one per SIMD, W1 partly in AGPRs)
+__global__ void dad_encode_wp4_f16(DadEncodeArgs a);
+#define DAD_PREP_THREADS 256
+__global__ void dad_prep(DadPrepArgs a);                       // one prepared set, standalone
 __global__ void dad_pool(DadPoolArgs a);
 __global__ void dad_tail(DadTailArgs a);
 __global__ void dad_ecda(DadEcdaArgs a);
 __global__ void dad_tail_ecda(DadTailArgs ta, DadEcdaArgs ca);
-__global__ void dad_tail_ecda_w(DadTailArgs ta, DadEcdaArgs ca);   // B, Bn <= 64, class-aware
+// B, Bn <= 64, class-aware; blocks > DAD_C prepare the next step's set (pa.x16 != NULL)
+__global__ void dad_tail_ecda_w(DadTailArgs ta, DadEcdaArgs ca, DadPrepArgs pa);
 __global__ void dad_wgrad_f32(DadWgradArgs a, DadReduceArgs r);   // r: the fused step's dL/de sources (gzb) or zeroed
 __global__ void dad_wgrad_direct(DadWgradArgs a, DadReduceArgs r);       // bf16 operands
 __global__ void dad_wgrad_direct_f16(DadWgradArgs a, DadReduceArgs r);   // fp16 operands

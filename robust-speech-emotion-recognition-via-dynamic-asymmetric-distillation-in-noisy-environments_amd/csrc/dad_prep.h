@@ -1,0 +1,122 @@
+// The weight-independent half of the 16-bit encoder: the reference's augmentation
+//   weak_augment   x + weak_std * N                          (I/utils.py:328-331)
+//   strong_augment (x + strong_std * N) * (u > p), then frames [start, start + mask_len) zeroed
+//                                                            (I/utils.py:333-375)
+// and the conversion of every MFMA input row to 16 bits (fp16 or bf16, round to nearest even), for
+// the three encoder passes of one step (I/train.py:399,406-410,439).  None of it depends on the
+// weights, so it need not sit between the previous step's optimizer and this step's GEMMs: the
+// step launches it either standalone before the encoder (dad_prep), or -- when the caller names
+// the next batch -- for the NEXT step on the ~250 workgroups the current step's tail launch
+// leaves idle (dad_tail_ecda_w blocks > DAD_C), where it overlaps the latency-bound tail/ECDA.
+//
+// Output: one prepared set [clean Bc*Tc | strong Bn*Tn | weak Bn*Tn][768] of 16-bit rows in the
+// padded layout (row b*T + t), whatever the source mode.  The strong and clean parts are also the
+// weight gradient's operand (they replace the encoder's old 16-bit copies).
+//
+// One wave per row; lane l owns columns 256k + 4l .. +3 (k = 0..2): the element pairs the fused
+// encoder converted per lane, so the counter RNG draws the same values (pair (row*768 + d) / 2 of
+// the stream, dad_aug_noise_pair) and the bytes equal what the fused encoder multiplied.  Each
+// wave loads R rows before converting any (R x 3 KB in flight per wave; rows past the end are
+// clamped to the last one and not stored, so no load sits under a condition).
+#pragma once
+#include "dad_kernels.h"
+
+template <int NOISE>
+__device__ __forceinline__ int dad_prep_tstart(const DadPrepArgs& a, int b) {
+  if (NOISE) return (int)a.start[b];
+  return dad_tstart_at(a.key_tstart, b, a.start_hi);
+}
+
+// waves [wave, wave + nwaves, ...) of the prepared set; wave index wave-uniform
+template <int NOISE, bool F16, int R>
+__device__ __forceinline__ void dad_prep_rows(const DadPrepArgs& a, int wave, int nwaves, int lane) {
+  const DadGeom& G = a.g;
+  const int Nc = G.Bc * G.Tc;
+  const int Nn = a.warmup ? 0 : G.Bn * G.Tn;
+  const int N = Nc + Nn;
+  uint16_t* const oc = a.x16;
+  uint16_t* const os = a.x16 + (size_t)Nc * DAD_D;
+  uint16_t* const ow = os + (size_t)Nn * DAD_D;
+  // feature keep flags of the lane's 12 columns (one [768] mask per step, I/utils.py:343)
+  float kp[3][4];
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) kp[k][e] = dad_feat_keep(a.u, a.key_feat, 256 * k + 4 * lane + e, a.feat_p);
+  for (int base = wave; base < N; base += R * nwaves) {
+    f32x4 v[R][3];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int u = min(base + r * nwaves, N - 1);
+      const bool noisy = u >= Nc;
+      const int un = noisy ? u - Nc : u;
+      const int T = noisy ? G.Tn : G.Tc;
+      const int b = un / T, t = un - b * T;
+      const float* x = (noisy ? a.xn : a.xc) + dad_src_row(a.src, noisy, b, T, t) * DAD_D + 4 * lane;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) v[r][k] = *reinterpret_cast<const f32x4*>(x + 256 * k);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int u = base + r * nwaves;
+      if (u >= N) break;
+      if (u < Nc) {
+        char* o = reinterpret_cast<char*>(oc + (size_t)u * DAD_D + 4 * lane);
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+          *reinterpret_cast<uint2*>(o + 512 * k) =
+              uint2{dad_pack2<F16>(v[r][k][0], v[r][k][1]), dad_pack2<F16>(v[r][k][2], v[r][k][3])};
+        continue;
+      }
+      const int un = u - Nc;
+      const int b = un / G.Tn, t = un - b * G.Tn;
+      const int st = a.mask_len > 0 ? dad_prep_tstart<NOISE>(a, b) : -(1 << 30);
+      const bool tzero = t >= st && t < st + a.mask_len;      // I/utils.py:365-372 (padded Tmax)
+      char* o_w = reinterpret_cast<char*>(ow + (size_t)un * DAD_D + 4 * lane);
+      char* o_s = reinterpret_cast<char*>(os + (size_t)un * DAD_D + 4 * lane);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int d = 256 * k + 4 * lane;
+        f32x4 nw, ns;
+        if constexpr (NOISE) {
+          nw = *reinterpret_cast<const f32x4*>(a.nw + (size_t)un * DAD_D + d);
+          ns = *reinterpret_cast<const f32x4*>(a.ns + (size_t)un * DAD_D + d);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { nw[e] *= a.weak_std; ns[e] *= a.strong_std; }
+        } else {
+          const uint32_t p = ((uint32_t)un * (uint32_t)DAD_D + (uint32_t)d) >> 1;
+          float z[8];
+          dad_aug_noise_pair(a.key_weak, p, a.weak_std, z[0], z[1]);
+          dad_aug_noise_pair(a.key_weak, p + 1u, a.weak_std, z[2], z[3]);
+          dad_aug_noise_pair(a.key_strong, p, a.strong_std, z[4], z[5]);
+          dad_aug_noise_pair(a.key_strong, p + 1u, a.strong_std, z[6], z[7]);
+          nw = f32x4{z[0], z[1], z[2], z[3]};
+          ns = f32x4{z[4], z[5], z[6], z[7]};
+        }
+        // reference op order: x + std*N, then * feature mask, then temporal zero
+        f32x4 w, s;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          w[e] = v[r][k][e] + nw[e];
+          s[e] = (v[r][k][e] + ns[e]) * kp[k][e];
+        }
+        *reinterpret_cast<uint2*>(o_w + 512 * k) = uint2{dad_pack2<F16>(w[0], w[1]), dad_pack2<F16>(w[2], w[3])};
+        const uint2 so = uint2{dad_pack2<F16>(s[0], s[1]), dad_pack2<F16>(s[2], s[3])};
+        *reinterpret_cast<uint2*>(o_s + 512 * k) = tzero ? uint2{0u, 0u} : so;
+      }
+    }
+  }
+}
+
+// runtime dispatch on the set's precision and draw source (wave-uniform)
+template <int R>
+__device__ __forceinline__ void dad_prep_dispatch(const DadPrepArgs& a, int wave, int nwaves, int lane) {
+  const bool noise = a.nw != nullptr;
+  if (a.f16) {
+    if (noise) dad_prep_rows<1, true, R>(a, wave, nwaves, lane);
+    else dad_prep_rows<0, true, R>(a, wave, nwaves, lane);
+  } else {
+    if (noise) dad_prep_rows<1, false, R>(a, wave, nwaves, lane);
+    else dad_prep_rows<0, false, R>(a, wave, nwaves, lane);
+  }
+}

@@ -703,3 +703,162 @@ DAD_WS_KERNEL(dad_encode_ws_explicit, 1, false)
 DAD_WS_KERNEL(dad_encode_ws_f16, 0, true)
 DAD_WS_KERNEL(dad_encode_ws_f16_explicit, 1, true)
 #undef DAD_WS_KERNEL
+
+// ------------------------------------------------------------ prepared-row encoder (wp)
+// dad_encode_wp: the same W-stationary GEMM + epilogue on a PREPARED set (dad_prep.h: the
+// augmentation and the 16-bit conversion already done, weight-independent, off this launch).
+// What is left per 16-row sub-slab is data movement and matrix work only:
+//   HBM 16-bit rows --LDS-DMA (3 x 1 KB per wave, straight into the XOR-swizzled tile: lane l of
+//   a piece loads the source chunk that lands at its slot)--> one of kPS = 6 tile stages
+//   --ds_read_b128 A fragments--> 48 MFMAs per wave against the resident W1 --> epilogue.
+// Five sub-slabs are in flight ahead of the one being multiplied (120 KB per CU), one barrier per
+// sub-slab, no VALU conversion, no raw stage, no 16-bit copy stores (the set is the copy).
+namespace {
+
+constexpr int kPS = 6;                                   // 24-KB tile stages
+constexpr int kOffPVB = kPS * kTile;                     // valid bits u32[DAD_ENC_WS_MAXJ]
+constexpr int kLdsP = kOffPVB + 4 * DAD_ENC_WS_MAXJ;
+static_assert(kLdsP <= 160 * 1024, "LDS budget");
+
+// one 1-KB LDS-DMA piece: 16 B per lane from `src` to lds_dst + 16 * lane (see dad_glds16x3)
+__device__ __forceinline__ void dad_glds16(const void* src, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep) : "v"(src), "s"(lds_dst) : "memory");
+}
+
+// vmcnt(D + n) for the counts the prepared-row pipeline produces: D = NP (kPS - 2) DMA
+// instructions plus n = 0..3 odd iterations' epilogue stores (1 teacher, 3 student)
+template <int D>
+__device__ __forceinline__ void wp_wait(int n) {
+  switch (n) {
+    case 1: wait_vm<D + 1>(); break;  case 2: wait_vm<D + 2>(); break;  case 3: wait_vm<D + 3>(); break;
+    case 6: wait_vm<D + 6>(); break;  case 9: wait_vm<D + 9>(); break;
+    default: wait_vm<D>(); break;
+  }
+}
+
+}  // namespace
+
+template <int WAVES, bool TEACHER, bool F16>
+__device__ __forceinline__ void wp_loop(const Ctx& C, const JobMap jm, const int Q, const int w, const int lane,
+                                        char* smem, const uint32_t sbase, const bf16x8* W, const float* bias,
+                                        const uint32_t* vb, const DadEncodeArgs& a) {
+  using S = Shape<WAVES>;
+  constexpr int NP = 24 / WAVES;   // 1-KB DMA pieces per wave per sub-slab
+  bf16x8 wf[S::NT][kKS];
+  float bh[S::NT];
+  float ssum[S::NT], scnt[S::NT];
+  uint32_t bw[S::NT];
+  // resident W1 and bias before any DMA: every later sub-slab wait covers them too
+  const int hw = S::HW * w;
+#pragma unroll
+  for (int t = 0; t < S::NT; ++t)   // fragment-major shadow (dad_w1frag_index): 1 KB coalesced loads
+#pragma unroll
+    for (int ks = 0; ks < kKS; ++ks) wf[t][ks] = W[(size_t)(((hw >> 4) + t) * kKS + ks) * 64 + lane];
+#pragma unroll
+  for (int t = 0; t < S::NT; ++t) bh[t] = bias[hw + 16 * t + (lane & 15)];
+  // the wave's pieces p = NP w + i of a sub-slab tile: lane slot 1024p + 16 lane = row prow[i],
+  // swizzled position P; it loads source chunk P ^ (row & 15) (byte offset pcol[i] in the row)
+  int prow[NP], pcol[NP];
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    const int o = 1024 * (NP * w + i) + 16 * lane;
+    prow[i] = o / kTileRow;
+    pcol[i] = 16 * (((o - kTileRow * prow[i]) >> 4) ^ (prow[i] & 15));
+  }
+  // DMA of sub-slab q into stage s (sub-slabs past the range re-read the last one's rows, so
+  // every iteration issues the same VMEM count; their stages are never read)
+  auto dma = [&](int q, int s) {
+    const int qq = min(q, Q - 1);
+    const Job J = job_of(C, TEACHER, jm(qq >> 1));
+    const char* base = reinterpret_cast<const char*>(J.kind == KIND_CLEAN ? a.x16c : (J.kind == KIND_STRONG ? a.x16s : a.x16w));
+    const uint32_t dst = sbase + (uint32_t)(s * kTile) + 1024u * NP * (uint32_t)w;
+    const int t0 = J.c * DAD_SLAB + (qq & 1) * kSub;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const int t = min(t0 + prow[i], J.T - 1);
+      dad_glds16(base + (size_t)(J.row0 + t) * (DAD_D * 2) + pcol[i], dst + 1024u * (uint32_t)i);
+    }
+  };
+  auto vmask_of = [&](int q) -> uint32_t {
+    return __builtin_amdgcn_readfirstlane((vb[q >> 1] >> (16 * (q & 1))) & 0xffffu);
+  };
+  constexpr int E = TEACHER ? 1 : 3;   // epilogue stores of an odd (HALF 1) iteration
+  int s_cur = 0;                       // stage of sub-slab q
+  auto iter = [&](auto h_tag, int q) {
+    constexpr int H = decltype(h_tag)::value;
+    // DMA(q) has landed once at most these younger VMEM ops remain: DMA(q+1 .. q+kPS-2) and the
+    // epilogue stores of iterations max(0, q-kPS+1) .. q-1 (stores only in odd iterations)
+    const int lo = max(0, q - (kPS - 1));
+    wp_wait<NP * (kPS - 2)>(E * ((q >> 1) - (lo >> 1)));
+    lds_barrier();   // every wave's pieces of q visible; stage of q-1 free (its reads retired)
+    dma(q + kPS - 1, s_cur == 0 ? kPS - 1 : s_cur - 1);
+    f32x4 acc[S::NT];
+    const uint32_t vmask = vmask_of(q);
+    if (vmask) {
+      int aoff[4];
+      const int ln = opaque(lane);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) aoff[m] = (ln & 15) * kTileRow + 16 * ((4 * m + (ln >> 4)) ^ (ln & 15));
+      ws_mfma<S, F16>(smem + s_cur * kTile, aoff, wf, acc);
+    } else {
+#pragma unroll
+      for (int t = 0; t < S::NT; ++t) acc[t] = f32x4{};
+    }
+    ws_epilogue<S, TEACHER, H>(C, job_of(C, TEACHER, jm(q >> 1)), w, lane, vmask, bh, acc, ssum, scnt, bw);
+    s_cur = s_cur == kPS - 1 ? 0 : s_cur + 1;
+  };
+#pragma unroll
+  for (int q = 0; q < kPS - 1; ++q) dma(q, q);
+  for (int q = 0; q < Q; q += 2) {   // Q is even: a job is two sub-slabs
+    iter(std::integral_constant<int, 0>{}, q);
+    iter(std::integral_constant<int, 1>{}, q + 1);
+  }
+  wait_vm<0>();   // no DMA may still target this workgroup's LDS when it exits
+}
+
+template <int WAVES, bool F16>
+__device__ __forceinline__ void encode_wp_body(const DadEncodeArgs& a, char* smem) {
+  const Ctx C = ctx_of(a);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  bool teacher;
+  int j0, j1;
+  job_range(C, blockIdx.x, a.ws_nt, a.ws_ns, a.ws_wstrong, teacher, j0, j1);
+  const JobMap jm{j0, 1};
+  const int nj = j1 - j0;
+  if (nj <= 0) return;
+  const uint32_t sbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  // valid bits of every job (bit r = row r of the 32-row slab is a frame of the utterance)
+  uint32_t* vb = reinterpret_cast<uint32_t*>(smem + kOffPVB);
+  for (int p = tid; p < nj * DAD_SLAB; p += 64 * WAVES) {
+    const Job J = job_of(C, teacher, jm(p / DAD_SLAB));
+    const int t = J.c * DAD_SLAB + (p & (DAD_SLAB - 1));
+    const uint8_t* pad = J.kind == KIND_CLEAN ? C.mc : C.mn;
+    const bool v = t < J.T && pad[J.row0 + t] == 0;
+    const uint64_t bal = __ballot(v);
+    if ((lane & 31) == 0) vb[p / DAD_SLAB] = (uint32_t)(bal >> (lane & 32));
+  }
+  __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): the pad loads retired (no DMA in flight yet)
+  lds_barrier();                        // vb visible
+  const bf16x8* W = reinterpret_cast<const bf16x8*>(teacher ? a.w1h_teacher : a.w1h_student);
+  const float* bias = teacher ? a.b1_teacher : a.b1_student;
+  if (teacher) wp_loop<WAVES, true, F16>(C, jm, 2 * nj, w, lane, smem, sbase, W, bias, vb, a);
+  else wp_loop<WAVES, false, F16>(C, jm, 2 * nj, w, lane, smem, sbase, W, bias, vb, a);
+}
+
+#define DAD_WP_KERNEL(name, WAVES, F16)                                        \
+  __global__ __launch_bounds__(64 * WAVES, 1) void name(DadEncodeArgs a) {     \
+    DAD_GUARD_BLOCK(64 * WAVES);                                               \
+    __shared__ __attribute__((aligned(16))) char smem[kLdsP];                  \
+    encode_wp_body<WAVES, F16>(a, smem);                                       \
+  }
+DAD_WP_KERNEL(dad_encode_wp, 8, false)
+DAD_WP_KERNEL(dad_encode_wp_f16, 8, true)
+DAD_WP_KERNEL(dad_encode_wp4, 4, false)
+DAD_WP_KERNEL(dad_encode_wp4_f16, 4, true)
+#undef DAD_WP_KERNEL

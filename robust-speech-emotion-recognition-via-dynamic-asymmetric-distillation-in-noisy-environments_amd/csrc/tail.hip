@@ -17,6 +17,7 @@
 
 #include "dad_common.h"
 #include "dad_kernels.h"
+#include "dad_prep.h"
 #include "dad_probe.h"
 
 // ECDA per-class phase wall clocks (100 MHz) of the stamps build (dad_probe.h): 16 slots per
@@ -2166,13 +2167,25 @@ __device__ __forceinline__ void ecda_block_w(const DadEcdaArgs& a, const DadTail
 }
 
 // block 0: the wave-centric tail; blocks 1..C: ECDA class blockIdx.x - 1.  Host contract:
-// B <= 64, Bn <= 64, class-aware MMD (dad_tail_ecda otherwise).
-__global__ __launch_bounds__(TAIL_THREADS) void dad_tail_ecda_w(DadTailArgs ta, DadEcdaArgs ca) {
+// B <= 64, Bn <= 64, class-aware MMD (dad_tail_ecda otherwise).  Blocks > C (when pa.x16 is set):
+// the NEXT step's row preparation (dad_prep.h) on the CUs the tail and the class blocks leave
+// idle; it reads only the next batch and writes only the other prepared set, so it overlaps this
+// step's latency-bound tail and ECDA.  The tail and class blocks have the lowest block ids, so
+// they are dispatched first and never wait for a CU behind the preparation blocks.
+__global__ __launch_bounds__(TAIL_THREADS) void dad_tail_ecda_w(DadTailArgs ta, DadEcdaArgs ca, DadPrepArgs pa) {
   DAD_GUARD_BLOCK(TAIL_THREADS);
   __shared__ union UW {
     TailW t;
     EcdaW e;
   } u;
+  if ((int)blockIdx.x > DAD_C) {
+    if (!pa.x16) return;
+    constexpr int kWaves = TAIL_THREADS / 64;
+    const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    dad_prep_dispatch<4>(pa, ((int)blockIdx.x - 1 - DAD_C) * kWaves + w, ((int)gridDim.x - 1 - DAD_C) * kWaves,
+                         (int)threadIdx.x & 63);
+    return;
+  }
   if (ta.cfg.B > TW_MAXB || ta.cfg.Bn > TW_MAXB) return;
   if (blockIdx.x == 0) tail_block_w(ta, u.t);
   else ecda_block_w(ca, ta, (int)blockIdx.x - 1, u.e);

@@ -121,6 +121,9 @@ class DADStep:
         self.global_step = 0
         self._ws = None
         self._bufs = {}
+        self._prepped_key = None       # identity of the batch the last step's tail launch prepared
+        self.last_prepped = False
+        self._next_keep = None
         self._shadow_dirty = False
         self.refresh_shadow()
 
@@ -222,15 +225,34 @@ class DADStep:
         return self._ws
 
     # ------------------------------------------------------------------------------- step
-    def make_config(self, Bc, Tc, Bn, Tn, epoch, lr=None, adam_step=None):
+    def make_config(self, Bc, Tc, Bn, Tn, epoch, lr=None, adam_step=None, counter=None):
         return dad_config_for(self.view, Bc, Tc, Bn, Tn, epoch,
                               adam_step if adam_step is not None else self.adam_step + 1, lr=lr,
                               precision=self.precision, rng_mode=self.rng_mode, seed=self.seed,
-                              counter=self.global_step,
+                              counter=self.global_step if counter is None else counter,
                               dp_world=self.comm.world if self.comm is not None else 1, splits=self.splits)
+
+    _PREP_CFG = ("B", "T", "Bn", "Tn", "precision", "rng_mode", "seed", "counter", "warmup", "mask_len",
+                 "start_hi", "weak_std", "strong_std", "feat_p")
+    _PREP_BT = ("xc", "mc", "xn", "mn", "nw", "ns", "u", "start", "rowc", "lenc", "rown", "lenn")
+
+    @classmethod
+    def _prep_key(cls, cfg, bt):
+        """Everything the 16-bit row preparation of a step reads (dad_prep.h): the config scalars
+        and the batch's device pointers."""
+        return tuple(getattr(cfg, f) for f in cls._PREP_CFG) + tuple(getattr(bt, f) for f in cls._PREP_BT)
 
     def _prepare(self, clean_batch, noisy_batch, epoch, lr, draws):
         """Device batch + POD structs for one step (shared by step() and train_step())."""
+        cfg, bt, keep = self._batch_structs(clean_batch, noisy_batch, epoch, lr, draws)
+        st = self._state_struct(cfg.Bn, cfg.B)
+        self._loss_vec = torch.empty(4, device=self.device)     # written by the optimizer/commit kernel
+        st.losses = self._loss_vec.data_ptr()
+        self._keepalive = keep
+        return cfg, bt, st
+
+    def _batch_structs(self, clean_batch, noisy_batch, epoch, lr, draws, counter=None, adam_step=None):
+        """(dad_config, dad_batch, keepalive) of one step's batch."""
         dev = self.device
         xc, mc, yc, rc, lc = _dev_batch(clean_batch, dev)
         warm = epoch < self.view.WARMUP_EPOCHS
@@ -244,7 +266,7 @@ class DADStep:
         else:
             raise ValueError("post-warm-up steps need a noisy batch")
         Bc, Tc = mc.shape[0], mc.shape[1]
-        cfg = self.make_config(Bc, Tc, Bn, Tn, epoch, lr=lr)
+        cfg = self.make_config(Bc, Tc, Bn, Tn, epoch, lr=lr, adam_step=adam_step, counter=counter)
         bt = _lib.DadBatch()
         bt.xc, bt.mc, bt.yc = xc.data_ptr(), mc.data_ptr(), yc.data_ptr()
         if rc is not None:
@@ -269,29 +291,46 @@ class DADStep:
             for k, v in dd.items():
                 setattr(bt, k, v.data_ptr())
             keep.append(dd)
-        st = self._state_struct(Bn, Bc)
-        self._loss_vec = torch.empty(4, device=dev)          # written by the optimizer/commit kernel
-        st.losses = self._loss_vec.data_ptr()
-        self._keepalive = (xc, mc, yc, xn, mn, keep, rc, lc, rn, ln)
-        return cfg, bt, st
+        return cfg, bt, (xc, mc, yc, xn, mn, keep, rc, lc, rn, ln)
 
-    def step(self, clean_batch, noisy_batch, epoch, lr=None, draws=None, after_encode=None):
+    def step(self, clean_batch, noisy_batch, epoch, lr=None, draws=None, after_encode=None, next_batch=None):
         """One full training step; returns the reference's loss dict as 0-d device tensors.
 
         after_encode: optional callable run on the host between the encoder launch and the rest
         of the step (e.g. to split a graph capture there and time the encoder with stream events).
+        next_batch: optional (clean_batch, noisy_batch[, draws]) of the NEXT step (same epoch and
+        lr).  FP16/BF16: its augmentation and 16-bit conversion then run inside this step's tail
+        launch, on the CUs the tail leaves idle (dad_step_backward_ahead), and the next step()
+        with that batch skips them.  Results are bit-identical with or without it.  The next
+        batch's device tensors must keep their contents until that step (device-resident
+        batches; host tensors are copied again by the next step, which then prepares itself).
         """
         if self._shadow_dirty or self._param_key() != self._shadow_key:
             self.refresh_shadow()
         cfg, bt, st = self._prepare(clean_batch, noisy_batch, epoch, lr, draws)
+        pk, self._prepped_key = self._prepped_key, None
+        cfg.prepped = 1 if (pk is not None and pk == self._prep_key(cfg, bt)) else 0
+        self.last_prepped = bool(cfg.prepped)   # diagnostics: this step's rows came from the last tail launch
         ws = self._workspace(cfg)
         stream = self._stream()
         L = _lib.lib()
         _lib.check(L.dad_step_encode(cfg, bt, st, _lib.ptr(ws), stream), "dad_step_encode")
+        self._next_keep = None           # (the rows it prepared were read on this stream before)
         if after_encode is not None:
             after_encode()
             stream = self._stream()
-        _lib.check(L.dad_step_backward(cfg, bt, st, _lib.ptr(ws), stream), "dad_step_backward")
+        if next_batch is not None and self.precision != _lib.PREC_FP32:
+            nd = next_batch[2] if len(next_batch) > 2 else None
+            ncfg, nbt, nkeep = self._batch_structs(next_batch[0], next_batch[1], epoch, lr, nd,
+                                                   counter=self.global_step + 1, adam_step=self.adam_step + 2)
+            done = ctypes.c_int(0)
+            _lib.check(L.dad_step_backward_ahead(cfg, bt, st, _lib.ptr(ws), stream, ncfg, nbt, ctypes.byref(done)),
+                       "dad_step_backward_ahead")
+            if done.value:
+                self._prepped_key = self._prep_key(ncfg, nbt)
+                self._next_keep = nkeep          # the preparation reads these until it has run
+        else:
+            _lib.check(L.dad_step_backward(cfg, bt, st, _lib.ptr(ws), stream), "dad_step_backward")
         if self.comm is not None and self.comm.world > 1:
             self.comm.allreduce_grad(st, stream, grad=self.grad)
         _lib.check(L.dad_step_apply(cfg, st, _lib.ptr(ws), stream), "dad_step_apply")
@@ -311,6 +350,7 @@ class DADStep:
         if self.comm is not None and self.comm.world > 1:
             raise RuntimeError("train_step is the single-process shim; use step() with a DPComm")
         self.refresh_shadow()        # the caller's optimizer/EMA changed the fp32 params
+        self._prepped_key = None     # (this step prepares its own rows into the workspace)
         cfg, bt, st = self._prepare(clean_batch, noisy_batch, epoch, None, draws)
         ws = self._workspace(cfg)
         stream = self._stream()

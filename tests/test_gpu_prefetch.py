@@ -1,0 +1,66 @@
+"""Next-batch row preparation inside the tail launch (DADStep.step(next_batch=...), C ABI
+dad_step_backward_ahead + dad_config.prepped).
+
+The 16-bit steps' augmentation and conversion (dad_prep.h) are weight-independent, so a step can
+prepare the NEXT batch's rows on the CUs its tail launch leaves idle.  A chain of steps over
+rotating device-resident batches that names each next batch must equal the same chain without it
+bit for bit (same RNG streams, same bytes, same GEMMs); the later steps must really have skipped
+their own preparation; a step whose batch is not the one named falls back to preparing itself."""
+import pytest
+import torch
+
+import gpu_harness as gh
+from oracle import dad_oracle, synth
+from test_gpu_graph import _device_batches, _state
+from test_gpu_parity import _problem
+
+pytestmark = pytest.mark.gpu
+K = 7
+
+
+def _chain(cfg, precision, batches, st, ahead, wrong_at=None):
+    step = gh.make_step(cfg, precision=precision, rng="counter", seed=5)
+    gh.load_state(step, st)
+    losses, prepped = [], []
+    for k in range(K):
+        c, n = batches[k % len(batches)]
+        nxt = None
+        if ahead:
+            nxt = batches[(k + 1) % len(batches)] if k != wrong_at else batches[(k + 2) % len(batches)]
+        out = step.step(c, n, 60, next_batch=nxt)
+        losses.append({key: float(v) for key, v in out.items()})
+        prepped.append(step.last_prepped)
+    torch.cuda.synchronize()
+    return _state(step), losses, prepped
+
+
+@pytest.mark.parametrize("precision", ["fp16", "bf16"])
+def test_prefetch_chain_equals_plain_chain(precision):
+    cfg = dad_oracle.make_cfg("iemocap")
+    batches = [_device_batches(_problem(B=16, T=40, seed=31 + i, Bn=12, Tn=50))[:2] for i in range(3)]
+    st = synth.make_state(31, 1)
+    want, want_losses, plain_prepped = _chain(cfg, precision, batches, st, ahead=False)
+    assert not any(plain_prepped)
+    got, got_losses, prepped = _chain(cfg, precision, batches, st, ahead=True, wrong_at=3)
+    # step 0 prepares itself; steps 1..K-1 use the previous tail launch's rows, except step 4,
+    # whose batch is not the one step 3 named (it prepares itself)
+    assert prepped == [False, True, True, True, False, True, True], prepped
+    for name, a, b in zip(("student", "teacher", "exp_avg", "exp_avg_sq", "dacp", "grad"), got, want):
+        assert torch.equal(a, b), "%s differs (max %.3g)" % (name, float((a - b).abs().max()))
+    assert got_losses == want_losses
+
+
+def test_prefetch_refused_for_other_geometry():
+    """A next batch of another shape is not prepared ahead (its set would not sit where the next
+    step looks); the step runs as without it."""
+    cfg = dad_oracle.make_cfg("iemocap")
+    a = _device_batches(_problem(B=16, T=40, seed=41, Bn=12, Tn=50))[:2]
+    b = _device_batches(_problem(B=16, T=44, seed=42, Bn=12, Tn=50))[:2]
+    st = synth.make_state(41, 1)
+    step = gh.make_step(cfg, precision="fp16", rng="counter", seed=5)
+    gh.load_state(step, st)
+    step.step(a[0], a[1], 60, next_batch=b)
+    assert step._prepped_key is None
+    step.step(b[0], b[1], 60)
+    torch.cuda.synchronize()
+    assert not step.last_prepped
