@@ -86,156 +86,43 @@ int device_cus(int* out) {
   return DAD_OK;
 }
 
-// Workgroup split of the W-stationary encoder (encode_ws.hip): one persistent workgroup per
-// CU, teacher : student in proportion to their work (32-row slab costs: clean 1, weak
-// kWsWeak, strong kWsStrong -- the augmentation RNG dominates a noisy slab), more
-// workgroups than CUs only when a range would exceed DAD_ENC_WS_MAXJ jobs.
-constexpr float kWsWeak = 1.03f, kWsStrong = 1.55f;   // sweeps of 300-step benches (tools/gpu_ws_sweep.sh)
-// DAD_WS_WEIGHTS="weak,strong" overrides the two costs (tuning runs; read once per process)
-struct WsWeights { float weak, strong; };
-WsWeights ws_weights() {
-  static const WsWeights w = [] {
-    WsWeights v{kWsWeak, kWsStrong};
-    if (const char* e = getenv("DAD_WS_WEIGHTS")) {
-      float a = 0.0f, b = 0.0f;
-      if (sscanf(e, "%f,%f", &a, &b) == 2 && a > 0.0f && b > 0.0f) v = WsWeights{a, b};
-    }
-    return v;
-  }();
-  return w;
-}
-// the largest job range of the teacher (or student) workgroups of a split, by the kernel's own
-// range function (dad_ws_job_range)
-int ws_max_range(const DadGeom& G, int Bn, int nt, int ns, float wstrong, bool teacher_side) {
-  const int Js = Bn * G.ncn;
+// Roles of the prepared-row encoder (dad_encode_wp, dad_wp_job_range): nt teacher and ns student
+// workgroups, one per CU, in proportion to their live 16-row sub-slabs (every prepared sub-slab
+// costs the same); more workgroups than CUs only when a range would exceed the kernel's
+// DAD_ENC_WS_MAXJ-job table.
+int wp_max_range(const DadGeom& G, int Bn, int nt, int ns) {
   int worst = 0;
-  const int lo = teacher_side ? 0 : nt, hi = teacher_side ? nt : nt + ns;
-  for (int wg = lo; wg < hi; ++wg) {
+  for (int wg = 0; wg < nt + ns; ++wg) {
     bool t = false;
     int j0 = 0, j1 = 0;
-    dad_ws_job_range(wg, nt, ns, wstrong, G.Bc, G.Tc, G.ncc, Bn, G.Tn, G.ncn, Js, t, j0, j1);
+    dad_wp_job_range(wg, nt, ns, G.Bc, G.Tc, G.ncc, Bn, G.Tn, G.ncn, Bn * G.ncn, t, j0, j1);
     worst = std::max(worst, j1 - j0);
   }
   return worst;
 }
-// Returns DAD_E_SHAPE if no split keeps every range within DAD_ENC_WS_MAXJ jobs (cannot happen
-// for B <= DAD_MAX_BATCH: one job per workgroup always fits).
-int ws_split_uncached(const DadGeom& G, int Bn, int cus, int& nt, int& ns) {
-  const float kWsWeak = ws_weights().weak, kWsStrong = ws_weights().strong;
-  const int Jt = Bn * G.ncn, Jc = G.Bc * G.ncc, Js = Jt;
-  if (Jt == 0) {
-    nt = 0;
-    ns = std::min(cus, Jc);
-  } else {
-    const double tot = Jt * (double)kWsWeak + Jc + Js * (double)kWsStrong;
-    nt = (int)(cus * (Jt * (double)kWsWeak) / tot + 0.5);
-    nt = std::max(1, std::min(cus - 1, nt));
-    ns = cus - nt;
-    nt = std::min(nt, Jt);
-    ns = std::min(ns, Jc + Js);
-  }
-  // every range within DAD_ENC_WS_MAXJ jobs (the kernel's valid-bit table), checked with the
-  // kernel's range function: ranges are priced by live sub-slabs, so a job-count bound is not
-  // enough when clean and strong jobs hold different numbers of live sub-slabs (Tc != Tn)
-  nt = std::max(nt, (Jt + DAD_ENC_WS_MAXJ - 1) / DAD_ENC_WS_MAXJ);
-  ns = std::max(ns, (Jc + Js + DAD_ENC_WS_MAXJ - 1) / DAD_ENC_WS_MAXJ);
-  while (nt > 0 && ws_max_range(G, Bn, nt, ns, kWsStrong, true) > DAD_ENC_WS_MAXJ) {
-    if (++nt > Jt) return DAD_E_SHAPE;
-  }
-  while (ws_max_range(G, Bn, nt, ns, kWsStrong, false) > DAD_ENC_WS_MAXJ) {
-    if (++ns > Jc + Js) return DAD_E_SHAPE;
-  }
-  return DAD_OK;
-}
-// XCD-sweep role counts (dad_ws_sweep_jobs): per XCD P = cus / 8 workgroups split into teachers,
-// strong students and clean students minimising the largest per-workgroup cost (live 16-row
-// sub-slabs x role weight), every range within DAD_ENC_WS_MAXJ jobs.  Off (all 0) when the
-// CUs do not divide over 8 XCDs, in warm-up (no noisy rows to share), when a role would get no
-// workgroup, or by DAD_WS_SWEEP=0 (A/B runs; read once).
-bool ws_sweep_on() {
-  static const bool on = [] { const char* e = getenv("DAD_WS_SWEEP"); return !(e && strcmp(e, "0") == 0); }();
-  return on;
-}
-DadWsSweep ws_sweep_uncached(const DadGeom& G, int Bn, int cus) {
-  DadWsSweep best{0, 0, 0};
-  const int P = cus / 8, Jc = G.Bc * G.ncc, Js = Bn * G.ncn;
-  if (!ws_sweep_on() || cus % 8 != 0 || P < 3 || Js < 8 || Jc < 8) return best;
-  const float kW = ws_weights().weak, kS = ws_weights().strong;
-  const int Lc = (G.Tc + 15) / 16, Ln = (G.Tn + 15) / 16;
-  const double cn = (double)Bn * Ln / 8.0, cc = (double)G.Bc * Lc / 8.0;   // live sub-slabs per XCD
-  double best_cost = 1e30;
-  for (int nt = 1; nt <= P - 2; ++nt)
-    for (int ns = 1; nt + ns <= P - 1; ++ns) {
-      const int nc = P - nt - ns;
-      const double cost = std::max(std::max(cn * kW / nt, cn * kS / ns), cc / nc);
-      if (cost < best_cost) { best_cost = cost; best = DadWsSweep{nt, ns, nc}; }
-    }
-  // the kernel's job tables hold DAD_ENC_WS_MAXJ jobs per workgroup
-  for (int wg = 0; wg < cus; ++wg) {
-    bool t = false;
-    int a0 = 0, st = 1, nj = 0;
-    dad_ws_sweep_jobs(wg, best, G.Bc, G.Tc, G.ncc, Jc, Js, t, a0, st, nj);
-    if (nj > DAD_ENC_WS_MAXJ) return DadWsSweep{0, 0, 0};
-  }
-  return best;
-}
-DadWsSweep ws_sweep(const DadGeom& G, int Bn, int cus) {
-  struct Entry { int Bc, Tc, Bn, Tn, cus; DadWsSweep s; };
-  static thread_local Entry last{-1, -1, -1, -1, -1, {0, 0, 0}};
-  if (!(last.Bc == G.Bc && last.Tc == G.Tc && last.Bn == Bn && last.Tn == G.Tn && last.cus == cus))
-    last = Entry{G.Bc, G.Tc, Bn, G.Tn, cus, ws_sweep_uncached(G, Bn, cus)};
-  return last.s;
-}
-
-// The split is a pure function of (geometry, CU count) for the process's fixed weights: cached
-// per thread for the last key, so a steady-state step runs no range evaluations on the host.
-int ws_split(const DadGeom& G, int Bn, int cus, int& nt, int& ns) {
-  struct Entry { int Bc, Tc, Bn, Tn, cus, rc, nt, ns; };
-  static thread_local Entry last{-1, -1, -1, -1, -1, 0, 0, 0};
-  if (!(last.Bc == G.Bc && last.Tc == G.Tc && last.Bn == Bn && last.Tn == G.Tn && last.cus == cus)) {
-    Entry e{G.Bc, G.Tc, Bn, G.Tn, cus, 0, 0, 0};
-    e.rc = ws_split_uncached(G, Bn, cus, e.nt, e.ns);
-    last = e;
-  }
-  nt = last.nt;
-  ns = last.ns;
-  return last.rc;
-}
-
-// Split of the prepared-row encoder (dad_encode_wp): every live sub-slab costs the same (no
-// augmentation in the launch), so teacher : student workgroups follow the live sub-slab counts.
 int wp_split(const DadGeom& G, int Bn, int cus, int& nt, int& ns) {
   struct Entry { int Bc, Tc, Bn, Tn, cus, rc, nt, ns; };
   static thread_local Entry last{-1, -1, -1, -1, -1, 0, 0, 0};
   if (!(last.Bc == G.Bc && last.Tc == G.Tc && last.Bn == Bn && last.Tn == G.Tn && last.cus == cus)) {
     Entry e{G.Bc, G.Tc, Bn, G.Tn, cus, 0, 0, 0};
-    const int Jt = Bn * G.ncn, Jc = G.Bc * G.ncc, Js = Jt;
-    const double lt = (double)Bn * ((G.Tn + 15) / 16), lc = (double)G.Bc * ((G.Tc + 15) / 16);
-    if (Jt == 0) {
-      e.nt = 0;
+    const int Js = Bn * G.ncn, Jc = G.Bc * G.ncc;
+    const double ln = (double)Bn * ((G.Tn + 15) / 16), lc = (double)G.Bc * ((G.Tc + 15) / 16);
+    if (Js == 0) {
       e.ns = std::min(cus, Jc);
     } else {
-      e.nt = (int)(cus * lt / (2.0 * lt + lc) + 0.5);
-      e.nt = std::max(1, std::min(cus - 1, std::min(e.nt, Jt)));
+      e.nt = std::max(1, std::min(std::min(Js, cus - 1), (int)(cus * ln / (2.0 * ln + lc) + 0.5)));
       e.ns = std::min(cus - e.nt, Jc + Js);
     }
-    e.nt = std::max(e.nt, (Jt + DAD_ENC_WS_MAXJ - 1) / DAD_ENC_WS_MAXJ);
-    e.ns = std::max(e.ns, (Jc + Js + DAD_ENC_WS_MAXJ - 1) / DAD_ENC_WS_MAXJ);
-    while (e.rc == DAD_OK && e.nt > 0 && ws_max_range(G, Bn, e.nt, e.ns, 1.0f, true) > DAD_ENC_WS_MAXJ)
-      if (++e.nt > Jt) e.rc = DAD_E_SHAPE;
-    while (e.rc == DAD_OK && ws_max_range(G, Bn, e.nt, e.ns, 1.0f, false) > DAD_ENC_WS_MAXJ)
-      if (++e.ns > Jc + Js) e.rc = DAD_E_SHAPE;
+    while (e.rc == DAD_OK && wp_max_range(G, Bn, e.nt, e.ns) > DAD_ENC_WS_MAXJ) {
+      if (e.nt > 0 && e.nt < Js) ++e.nt;
+      if (e.ns < Jc + Js) ++e.ns;
+      if (e.nt + e.ns > Js + Jc + 2) e.rc = DAD_E_SHAPE;
+    }
     last = e;
   }
   nt = last.nt;
   ns = last.ns;
   return last.rc;
-}
-
-// DAD_WP_WAVES=4: the prepared-row encoder with one wave per SIMD (A/B runs; read once)
-int wp_waves() {
-  static const int w = [] { const char* e = getenv("DAD_WP_WAVES"); return (e && strcmp(e, "4") == 0) ? 4 : 8; }();
-  return w;
 }
 
 // Row-preparation arguments (dad_prep.h) of the step described by (cfg, bt) into set x16.
@@ -246,6 +133,7 @@ DadPrepArgs prep_args(const dad_config* cfg, const dad_batch* bt, uint16_t* x16)
   p.g = geom_of(cfg);
   p.warmup = cfg->warmup; p.mask_len = cfg->mask_len; p.start_hi = cfg->start_hi;
   p.f16 = cfg->precision == DAD_PREC_FP16 ? 1 : 0;
+  p.clean = 1;
   p.xc = bt->xc; p.xn = bt->xn;
   p.src = DadStoreRows{bt->rowc, bt->lenc, bt->rown, bt->lenn};
   if (cfg->rng_mode == DAD_RNG_EXPLICIT) { p.nw = bt->nw; p.ns = bt->ns; p.u = bt->u; p.start = bt->start; }
@@ -372,10 +260,9 @@ int dad_encoder_ws_plan(const dad_config* cfg, int cus, int* nt, int* ns, int* m
   if (cus < 2 || !nt || !ns || !max_jobs) return DAD_E_ARG;
   const DadGeom G = geom_of(cfg);
   const int Bn = cfg->warmup ? 0 : G.Bn;
-  rc = ws_split(G, Bn, cus, *nt, *ns);
+  rc = wp_split(G, Bn, cus, *nt, *ns);
   if (rc) return rc;
-  const float ws = ws_weights().strong;
-  *max_jobs = std::max(ws_max_range(G, Bn, *nt, *ns, ws, true), ws_max_range(G, Bn, *nt, *ns, ws, false));
+  *max_jobs = wp_max_range(G, Bn, *nt, *ns);
   return DAD_OK;
 }
 
@@ -386,27 +273,18 @@ int dad_encoder_ws_jobs(const dad_config* cfg, int cus, int* jobs) {
   const DadGeom G = geom_of(cfg);
   const int Bn = cfg->warmup ? 0 : G.Bn;
   int nt = 0, ns = 0;
-  rc = ws_split(G, Bn, cus, nt, ns);
+  rc = wp_split(G, Bn, cus, nt, ns);
   if (rc) return rc;
-  const DadWsSweep sw = ws_sweep(G, Bn, cus);
-  const int Jc = G.Bc * G.ncc, Js = Bn * G.ncn;
-  const int grid = sw.nt > 0 ? cus : nt + ns;
-  for (int wg = 0; wg < grid; ++wg) {
+  for (int wg = 0; wg < nt + ns; ++wg) {
     bool t = false;
-    int a0 = 0, st = 1, nj = 0;
-    if (sw.nt > 0) {
-      dad_ws_sweep_jobs(wg, sw, G.Bc, G.Tc, G.ncc, Jc, Js, t, a0, st, nj);
-    } else {
-      int j1 = 0;
-      dad_ws_job_range(wg, nt, ns, ws_weights().strong, G.Bc, G.Tc, G.ncc, Bn, G.Tn, G.ncn, Js, t, a0, j1);
-      nj = j1 - a0;
-    }
+    int j0 = 0, j1 = 0;
+    dad_wp_job_range(wg, nt, ns, G.Bc, G.Tc, G.ncc, Bn, G.Tn, G.ncn, Bn * G.ncn, t, j0, j1);
     jobs[4 * wg] = t ? 1 : 0;
-    jobs[4 * wg + 1] = a0;
-    jobs[4 * wg + 2] = st;
-    jobs[4 * wg + 3] = nj;
+    jobs[4 * wg + 1] = j0;
+    jobs[4 * wg + 2] = 1;
+    jobs[4 * wg + 3] = j1 - j0;
   }
-  return grid;
+  return nt + ns;
 }
 
 int dad_workspace_bytes(const dad_config* cfg, size_t* bytes) {
@@ -492,7 +370,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   if (explicit_rng) { ea.nw = bt->nw; ea.ns = bt->ns; ea.u = bt->u; ea.start = bt->start; }
   ea.key_weak = k.weak; ea.key_strong = k.strong; ea.key_feat = k.feat; ea.key_tstart = k.tstart;
   ea.weak_std = cfg->weak_std; ea.strong_std = cfg->strong_std; ea.feat_p = cfg->feat_p;
-  ea.part_sum = part_sum; ea.part_cnt = part_cnt; ea.bits = bits; ea.xs16 = xs16;
+  ea.part_sum = part_sum; ea.part_cnt = part_cnt; ea.bits = bits;
   const int nwaves = G.Bc * G.ncc + Bn * G.ncn;
   const dim3 egrid((nwaves + 3) / 4);
   if (do_encode) {
@@ -510,18 +388,10 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
       if (rc) return rc;
       const int rs = wp_split(G, Bn, cus, ea.ws_nt, ea.ws_ns);
       if (rs) return rs;
-      ea.ws_wstrong = 1.0f;
       ea.x16c = xs16; ea.x16s = xs16 + nrc * DAD_D; ea.x16w = ea.x16s + (cfg->warmup ? 0 : nrn) * DAD_D;
-      if (ea.ws_nt + ea.ws_ns > 0) {
-        const dim3 grid(ea.ws_nt + ea.ws_ns);
-        if (wp_waves() == 4) {
-          if (f16) hipLaunchKernelGGL(dad_encode_wp4_f16, grid, dim3(256), 0, stream, ea);
-          else hipLaunchKernelGGL(dad_encode_wp4, grid, dim3(256), 0, stream, ea);
-        } else {
-          if (f16) hipLaunchKernelGGL(dad_encode_wp_f16, grid, dim3(DAD_ENC_WS_THREADS), 0, stream, ea);
-          else hipLaunchKernelGGL(dad_encode_wp, grid, dim3(DAD_ENC_WS_THREADS), 0, stream, ea);
-        }
-      }
+      const dim3 grid(ea.ws_nt + ea.ws_ns);
+      if (f16) hipLaunchKernelGGL(dad_encode_wp_f16, grid, dim3(DAD_ENC_WS_THREADS), 0, stream, ea);
+      else hipLaunchKernelGGL(dad_encode_wp, grid, dim3(DAD_ENC_WS_THREADS), 0, stream, ea);
     } else {
       hipLaunchKernelGGL(dad_encode_f32, egrid, dim3(DAD_ENC_F32_THREADS), 0, stream, ea);
     }
@@ -795,9 +665,8 @@ int dad_rng_draws(const dad_config* cfg, int which, uint64_t first, size_t n, fl
 // ----------------------------------------------------------------- modular encoder ops
 }  // extern "C"
 
-// The modular encoder ops' workspace: the FP32 layout plus the 16-bit row-copy region, so the
-// 16-bit encoder writes its copies to scratch instead of testing for a missing buffer in the
-// conversion units it interleaves with the MFMA k-steps (a branch there splits the schedule).
+// The modular encoder ops' workspace: the FP32 layout plus a prepared-row region (the 16-bit
+// encoder's input: x converted by dad_prep).
 static DadWs enc_layout(const DadGeom& G) {
   return dad_ws_layout(G, dad_auto_splits(G, DAD_PREC_FP32, 1), DAD_PREC_BF16);
 }
@@ -855,10 +724,10 @@ int encoder_forward_impl(const float* x, const uint8_t* pad, int B, int T, const
   ea.bits = ws_ptr<uint32_t>(workspace, L.bits);
   const dim3 egrid((B * G.ncc + 3) / 4);
   if (dad_prec16(precision)) {
-    // 16-bit rows of x (a clean-only prepared set), then the W-stationary GEMM on them
+    // the rows of x prepared (16-bit conversion: a clean-only set), then the GEMM on them
     DadPrepArgs pp;
     memset(&pp, 0, sizeof(pp));
-    pp.g = G; pp.warmup = 1; pp.f16 = f16 ? 1 : 0; pp.xc = x;
+    pp.g = G; pp.warmup = 1; pp.clean = 1; pp.f16 = f16 ? 1 : 0; pp.xc = x;
     pp.x16 = ws_ptr<uint16_t>(workspace, L.xs16);
     const int rp = launch_prep(pp, stream);
     if (rp) return rp;
@@ -868,9 +737,9 @@ int encoder_forward_impl(const float* x, const uint8_t* pad, int B, int T, const
     if (rc) return rc;
     const int rs = wp_split(G, 0, cus, ea.ws_nt, ea.ws_ns);
     if (rs) return rs;
-    ea.ws_wstrong = 1.0f;
-    if (f16) hipLaunchKernelGGL(dad_encode_wp_f16, dim3(ea.ws_nt + ea.ws_ns), dim3(DAD_ENC_WS_THREADS), 0, stream, ea);
-    else hipLaunchKernelGGL(dad_encode_wp, dim3(ea.ws_nt + ea.ws_ns), dim3(DAD_ENC_WS_THREADS), 0, stream, ea);
+    const dim3 grid(ea.ws_nt + ea.ws_ns);
+    if (f16) hipLaunchKernelGGL(dad_encode_wp_f16, grid, dim3(DAD_ENC_WS_THREADS), 0, stream, ea);
+    else hipLaunchKernelGGL(dad_encode_wp, grid, dim3(DAD_ENC_WS_THREADS), 0, stream, ea);
   } else {
     hipLaunchKernelGGL(dad_encode_f32, egrid, dim3(DAD_ENC_F32_THREADS), 0, stream, ea);
   }

@@ -279,15 +279,10 @@ static inline __host__ __device__ DadGeom dad_geom(int Bc, int Tc, int Bn, int T
   return g;
 }
 
-// Job ranges of the W-stationary 16-bit encoder (encode_ws.hip), shared by the kernel and the
-// host (ws_split sizes the grid with it, so host and kernel count work in the same units).
-// Jobs are 32-row slabs; teacher workgroups [0, nt) split the weak slabs, student workgroups
-// [nt, nt + ns) the clean slabs (cost 1 per live 16-row sub-slab) then the strong slabs (cost
-// wstrong per live sub-slab).  The last slab of an utterance holds ceil(T/16) - 2(nc-1) live
-// sub-slabs (one at T = 300: rows 304..319 are skipped), so ranges are priced by the sub-slabs
-// they run, not by their job count.  Js = Bn * ncn, or 0 in warm-up.
-// live_jobs_at: the job boundary nearest to x cumulative live sub-slabs of one branch (nc slabs,
-// L live sub-slabs per utterance, J jobs).
+// live_jobs_at: the 32-row job boundary nearest to x cumulative live 16-row sub-slabs of one
+// branch (nc slabs and L live sub-slabs per utterance, J jobs).  The last slab of an utterance
+// holds ceil(T/16) - 2(nc-1) live sub-slabs (one at T = 300: rows 304..319 are skipped), so the
+// encoder's ranges are priced by the sub-slabs they run, not by their job count.
 static inline __host__ __device__ int dad_live_jobs_at(float x, int nc, int L, int J) {
   if (x <= 0.0f) return 0;
   const int b = (int)(x / (float)L);
@@ -297,65 +292,27 @@ static inline __host__ __device__ int dad_live_jobs_at(float x, int nc, int L, i
   const int j = b * nc + c;
   return j < J ? j : J;
 }
-static inline __host__ __device__ void dad_ws_job_range(int wg, int nt, int ns, float wstrong, int Bc, int Tc, int ncc,
-                                                        int Bn, int Tn, int ncn, int Js, bool& teacher, int& j0,
-                                                        int& j1) {
+// Job ranges of the prepared-row encoder (dad_encode_wp, encode_ws.hip), shared by the kernel and
+// the host.  Teachers [0, nt) split the weak slabs, students [nt, nt + ns) the clean slabs then the
+// strong slabs, all evenly by live 16-row sub-slabs (every prepared sub-slab costs the same).  Job
+// numbers: teacher j = weak slab j; student j < Jc clean slab j, j >= Jc strong slab j - Jc (job_of).
+static inline __host__ __device__ void dad_wp_job_range(int wg, int nt, int ns, int Bc, int Tc, int ncc, int Bn,
+                                                        int Tn, int ncn, int Js, bool& teacher, int& j0, int& j1) {
   const int Lc = (Tc + 15) / 16, Ln = (Tn + 15) / 16, Jc = Bc * ncc;
   teacher = wg < nt;
-  if (teacher) {
-    const float tot = (float)Bn * (float)Ln;
-    j0 = wg >= nt ? Js : dad_live_jobs_at(tot * (float)wg / (float)nt, ncn, Ln, Js);
-    j1 = wg + 1 >= nt ? Js : dad_live_jobs_at(tot * (float)(wg + 1) / (float)nt, ncn, Ln, Js);
-    return;
-  }
-  const int k = wg - nt;
-  const float cc = Jc ? (float)Bc * (float)Lc : 0.0f;      // clean cost
-  const float wtot = cc + (Js ? (float)Bn * (float)Ln * wstrong : 0.0f);
+  const int k = teacher ? wg : wg - nt, n = teacher ? nt : ns;
+  const float tn = Js ? (float)Bn * (float)Ln : 0.0f, tc = (float)Bc * (float)Lc;
+  const float tot = teacher ? tn : tc + tn;
   int j[2];
   for (int e = 0; e < 2; ++e) {
     const int kk = k + e;
-    if (kk >= ns) { j[e] = Jc + Js; continue; }
-    const float B = wtot * (float)kk / (float)ns;
-    j[e] = B <= cc ? dad_live_jobs_at(B, ncc, Lc, Jc) : Jc + dad_live_jobs_at((B - cc) / wstrong, ncn, Ln, Js);
+    if (kk >= n) { j[e] = teacher ? Js : Jc + Js; continue; }
+    const float x = tot * (float)kk / (float)n;
+    if (teacher) j[e] = dad_live_jobs_at(x, ncn, Ln, Js);
+    else j[e] = x <= tc ? dad_live_jobs_at(x, ncc, Lc, Jc) : Jc + dad_live_jobs_at(x - tc, ncn, Ln, Js);
   }
   j0 = j[0];
   j1 = j[1];
-}
-
-// XCD-sweep job assignment of the 16-bit encoder (ws_sweep on the host): workgroup wg runs on
-// XCD wg & 7 (the dispatcher deals workgroups round-robin over the 8 XCDs) as local workgroup
-// l = wg >> 3 of that XCD, in one of three roles with per-XCD counts nt + ns + nc:
-//   l < nt           teacher: weak slabs g0 + l, g0 + l + nt, ... of the XCD's noisy group [g0, g1)
-//   nt <= l < nt+ns  strong student: strong slabs g0 + k, g0 + k + ns, ... (k = l - nt)
-//   else             clean student: a contiguous clean range (live-cost balanced over all 8 nc)
-// Teachers and strong students of an XCD sweep the SAME noisy rows at matching rates (the counts
-// follow the costs, nt / w_weak ~ ns / w_strong), so each noisy row is fetched from HBM once and
-// read by the second role from that XCD's L2 (the contiguous split read it twice, from different
-// XCDs).  Student jobs: j < Jc clean slab j, j >= Jc strong slab j - Jc (job_of).
-struct DadWsSweep {
-  int nt, ns, nc;   // per-XCD role counts (all 0: the contiguous split dad_ws_job_range)
-};
-static inline __host__ __device__ void dad_ws_sweep_jobs(int wg, const DadWsSweep& sw, int Bc, int Tc, int ncc, int Jc,
-                                                         int Js, bool& teacher, int& a0, int& stride, int& nj) {
-  const int x = wg & 7, l = wg >> 3;
-  const int g0 = (int)((long long)Js * x / 8), g1 = (int)((long long)Js * (x + 1) / 8);
-  if (l < sw.nt + sw.ns) {
-    teacher = l < sw.nt;
-    const int k = teacher ? l : l - sw.nt, n = teacher ? sw.nt : sw.ns;
-    a0 = (teacher ? 0 : Jc) + g0 + k;
-    stride = n;
-    nj = g0 + k < g1 ? (g1 - g0 - k + n - 1) / n : 0;
-    return;
-  }
-  teacher = false;
-  const int k = x * sw.nc + (l - sw.nt - sw.ns), N = 8 * sw.nc;
-  const int Lc = (Tc + 15) / 16;
-  const float tot = (float)Bc * (float)Lc;
-  const int c0 = dad_live_jobs_at(tot * (float)k / (float)N, ncc, Lc, Jc);
-  const int c1 = k + 1 >= N ? Jc : dad_live_jobs_at(tot * (float)(k + 1) / (float)N, ncc, Lc, Jc);
-  a0 = c0;
-  stride = 1;
-  nj = c1 - c0;
 }
 
 // Workspace layout (bytes), shared by host and device.  All offsets 256-B aligned.

@@ -70,12 +70,10 @@ struct DadEncodeArgs {
   uint32_t key_weak, key_strong, key_feat, key_tstart;
   float weak_std, strong_std, feat_p;
   float* part_sum; float* part_cnt; uint32_t* bits;
-  uint16_t* xs16;           // 16-bit modes: the student's MFMA input, clean rows then strong rows (for wgrad)
-  int ws_nt, ws_ns;         // dad_encode_ws: teacher / student workgroups (contiguous split)
-  float ws_wstrong;         // dad_encode_ws: cost of a strong slab relative to a clean one
-  DadWsSweep ws_sweep;      // dad_encode_ws: XCD-sweep role counts per XCD (nt = ns = nc = 0: contiguous split)
-  // dad_encode_wp: the prepared 16-bit rows (dad_prep) of the clean, strong and weak branches,
-  // [B][T][768] each (padded layout whatever the source mode)
+  // dad_encode_wp roles (dad_wp_job_range): ws_nt teacher and ws_ns student workgroups
+  int ws_nt, ws_ns;
+  // the prepared 16-bit rows (dad_prep) of the clean, strong and weak branches, [B][T][768] each
+  // (padded layout whatever the source mode)
   const uint16_t* x16c; const uint16_t* x16s; const uint16_t* x16w;
 };
 
@@ -87,6 +85,7 @@ struct DadEncodeArgs {
 struct DadPrepArgs {
   DadGeom g;
   int warmup, mask_len, start_hi, f16;
+  int clean;                // 1: also the clean rows (else the encoder converts them itself)
   const float* xc; const float* xn;
   DadStoreRows src;
   const float* nw; const float* ns; const float* u; const int64_t* start;   // explicit draws, or NULL
@@ -175,14 +174,8 @@ struct DadCollateArgs {
 __global__ void dad_collate_kernel(DadCollateArgs a);
 int dad_collate_grid(long B, long T);
 __global__ void dad_encode_f32(DadEncodeArgs a);
-__global__ void dad_encode_ws(DadEncodeArgs a);                // bf16 operands, counter RNG
-__global__ void dad_encode_ws_explicit(DadEncodeArgs a);       // bf16, explicit noise tensors (parity)
-__global__ void dad_encode_ws_f16(DadEncodeArgs a);            // fp16 operands, counter RNG
-__global__ void dad_encode_ws_f16_explicit(DadEncodeArgs a);   // fp16, explicit noise tensors
 __global__ void dad_encode_wp(DadEncodeArgs a);                // bf16 operands from a prepared set
 __global__ void dad_encode_wp_f16(DadEncodeArgs a);            // fp16 operands from a prepared set
-__global__ void dad_encode_wp4(DadEncodeArgs a);               // 4 waves (one per SIMD, W1 partly in AGPRs)
-__global__ void dad_encode_wp4_f16(DadEncodeArgs a);
 #define DAD_PREP_THREADS 256
 __global__ void dad_prep(DadPrepArgs a);                       // one prepared set, standalone
 __global__ void dad_pool(DadPoolArgs a);

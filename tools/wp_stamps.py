@@ -1,0 +1,55 @@
+"""Diagnostic: per-workgroup timeline of dad_encode_wp (build variant 'stamps', -DDAD_PROBE_STAMPS;
+never the product library).  Runs bench-shaped steps (each naming the next batch, as the bench
+does), then reads the stamps of every workgroup of the last encoder launch and summarises them per
+role: start / prologue end / end (us after the first workgroup's start) and wave-0 cycles per
+32-row job in: DMA wait, barrier, DMA issue + valid mask, MFMA, epilogue."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ.setdefault("DAD_LIB_VARIANT", "stamps")
+import bench  # noqa: E402
+
+PKG = bench.PKG
+
+
+def main():
+    B, T = 64, 300
+    model = PKG.SSRLModel().cuda()
+    P = bench.init_model_weights(model, seed=0)
+    step = PKG.DADStep(model, flavor="iemocap", precision=os.environ.get("STAMP_PREC", "fp16"), rng="counter", seed=1)
+    data = bench.make_batches(P, 2, B, T, seed=17, device=torch.device("cuda"))
+    for i in range(8):
+        step.step(data[i % 2][0], data[i % 2][1], 60, next_batch=data[(i + 1) % 2])
+    torch.cuda.synchronize()
+    L = PKG.lib()
+    n = 256
+    buf = (ctypes.c_ulonglong * (10 * n))()
+    assert L.dad_probe_read_ws_stamps(buf, 10 * n) == 0
+    st = np.frombuffer(buf, dtype=np.uint64).reshape(n, 10).astype(np.int64)
+    st = st[st[:, 0] > 0]
+    t0 = st[:, 0].min()
+    start, pro, end = (st[:, 0] - t0) / 100.0, (st[:, 1] - t0) / 100.0, (st[:, 2] - t0) / 100.0
+    role = st[:, 3] >> 16
+    Q = st[:, 3] & 0xffff
+    for r, name in ((0, "teacher"), (1, "student")):
+        m = (role == r) & (Q > 0)
+        if not m.any():
+            continue
+        per = (end[m] - pro[m]) / Q[m]
+        print("%-7s n=%3d Q p50 %d  start p50/max %.1f/%.1f  prologue-end p50 %.1f  end p50/max %.1f/%.1f us  "
+              "loop us/sub-slab p50 %.3f" % (name, m.sum(), np.median(Q[m]), np.median(start[m]), start[m].max(),
+                                            np.median(pro[m]), np.median(end[m]), end[m].max(), np.median(per)))
+        if True:
+            cyc = st[m, 4:9].astype(np.float64) / (Q[m][:, None] / 2.0)
+            print("        wave-0 cycles per 32-row job p50: wait %.0f  barrier %.0f  dma+mask %.0f  mfma %.0f  epilogue %.0f" %
+                  tuple(np.median(cyc, axis=0)))
+
+
+if __name__ == "__main__":
+    main()
