@@ -469,7 +469,7 @@ def merge_ktimes(parts):
     return {k: (t / c, c) for k, (t, c) in acc.items() if c}
 
 
-ENC_KERNEL = {"fp16": "dad_encode_ws_f16", "bf16": "dad_encode_ws", "fp32": "dad_encode_f32"}
+ENC_KERNEL = {"fp16": "dad_encode_wp_f16", "bf16": "dad_encode_wp", "fp32": "dad_encode_f32"}
 WGRAD_KERNEL = {"fp16": ("wgrad", "dad_wgrad_direct_f16"), "bf16": ("wgrad", "dad_wgrad_direct"),
                 "fp32": ("wgrad", "dad_wgrad_f32")}
 KNAMES = {p: {"encode": ENC_KERNEL[p], "pool": "dad_pool", "wgrad": WGRAD_KERNEL[p][1],
@@ -489,17 +489,45 @@ def tail_kernel(B, Bn, class_aware=True):
     return "dad_tail_ecda_w" if w else "dad_tail_ecda"
 
 
-def rooflines(ktimes, rows_c, rows_n, ms_step, precision, tail_name="dad_tail_ecda_w"):
-    """`roofline` of the dominant kernel (the encoder), `step_roofline` of the whole step and the
-    per-kernel table (live HIP-event durations of dad_timing_start) with MFMA utilisation of the
-    encoder linears.  Algorithmic work:
-      encoder:  bytes = (rows_c + rows_n) x 768 x 4 (both fp32 feature tensors, read once),
-                flops = 2 x 768 x 256 x (rows_c + 2 rows_n)  (student-clean, teacher-weak, student-strong)
+def _roof(kernel, ms, bytes_, flops, peak_tf, bound=None, note=None):
+    """One kernel's roofline block: algorithmic bytes (or FLOPs) per launch / mean launch time."""
+    ridge = peak_tf * 1e12 / (HBM_PEAK_GBS * 1e9)
+    intensity = flops / bytes_ if bytes_ else float("inf")
+    bound = bound or ("mfma" if intensity > ridge else "hbm")
+    if bound == "hbm":
+        achieved, peak, unit = bytes_ / (ms * 1e-3) / 1e9, HBM_PEAK_GBS, "GB/s"
+    else:
+        achieved, peak, unit = flops / (ms * 1e-3) / 1e12, peak_tf, "TFLOP/s"
+    pmc = pmc_counters(kernel)
+    r = {"bound": bound, "kernel": kernel, "achieved": achieved, "peak": peak, "unit": unit, "frac": achieved / peak,
+         "traffic": pmc["hbm_bytes_per_launch"] if pmc and "hbm_bytes_per_launch" in pmc else None,
+         "avg_launch_ms": ms, "algorithmic_bytes_per_launch": bytes_, "algorithmic_flops_per_launch": flops,
+         "arithmetic_intensity_flop_per_byte": intensity, "ridge_flop_per_byte": ridge,
+         "traffic_source": None if pmc is None else pmc["source"],
+         "traffic_stale": None if pmc is None else pmc["stale"]}
+    if note:
+        r["note"] = note
+    return r
+
+
+def rooflines(ktimes, rows_c, rows_n, ms_step, precision, tail_name="dad_tail_ecda_w", prepped_ahead=False):
+    """`roofline` of the dominant launch, the encoder's own roofline, `step_roofline` of the whole
+    step and the per-kernel table (live HIP-event durations of dad_timing_start) with MFMA
+    utilisation of the encoder linears.  Algorithmic work:
+      FP32 encoder: bytes = (rows_c + rows_n) x 768 x 4 (both fp32 feature tensors, read once);
+      16-bit encoder (dad_encode_wp): bytes = (rows_c + 2 rows_n) x 768 x 2 (its prepared rows);
+        flops = 2 x 768 x 256 x (rows_c + 2 rows_n) (student-clean, teacher-weak, student-strong)
+      row preparation (16-bit, in the tail launch when the next batch is prepared ahead):
+        bytes = (rows_c + rows_n) x 768 x 4 read + (rows_c + 2 rows_n) x 768 x 2 written
       dW1:      flops = 2 x 768 x 256 x (rows_c + rows_n)
-      step:     t_roof = max(F / P_mfma, Q / BW) with F = 2 x 768 x 256 x (2 rows_c + 3 rows_n).
-    bound: the encoder's arithmetic intensity against the ridge point P_mfma / BW."""
+      step:     t_roof = max(F / P_mfma, Q / BW) with F = 2 x 768 x 256 x (2 rows_c + 3 rows_n) and
+                Q = the fp32 features read once.
+    bound: the kernel's arithmetic intensity against the ridge point P_mfma / BW."""
     peak_tf = PEAK_TFLOPS.get(precision, FP32_PEAK_TFLOPS)
-    enc_bytes = int((rows_c + rows_n) * 768 * 4)
+    h16 = precision != "fp32"
+    src_bytes = int((rows_c + rows_n) * 768 * 4)
+    prep_bytes = int((rows_c + 2 * rows_n) * 768 * 2)
+    enc_bytes = prep_bytes if h16 else src_bytes
     enc_flops = 2 * 768 * 256 * (rows_c + 2 * rows_n)
     wg_flops = 2 * 768 * 256 * (rows_c + rows_n)
     step_flops = 2 * 768 * 256 * (2 * rows_c + 3 * rows_n)
@@ -512,25 +540,20 @@ def rooflines(ktimes, rows_c, rows_n, ms_step, precision, tail_name="dad_tail_ec
     enc = ktimes["encode"][0]
     wkey, wname = WGRAD_KERNEL[precision]
     wg = ktimes.get(wkey, (float("nan"), 0))[0]
-    ridge = peak_tf * 1e12 / (HBM_PEAK_GBS * 1e9)
-    intensity = enc_flops / enc_bytes
-    bound = "mfma" if intensity > ridge else "hbm"
     ekn = ENC_KERNEL[precision]
-    pmc = pmc_counters(ekn)
-    traffic = pmc["hbm_bytes_per_launch"] if pmc and "hbm_bytes_per_launch" in pmc else None
-    if bound == "hbm":
-        achieved, peak, unit, work = enc_bytes / (enc * 1e-3) / 1e9, HBM_PEAK_GBS, "GB/s", enc_bytes
-    else:
-        achieved, peak, unit, work = enc_flops / (enc * 1e-3) / 1e12, peak_tf, "TFLOP/s", enc_flops
-    rf = {"bound": bound, "kernel": ekn, "achieved": achieved, "peak": peak, "unit": unit, "frac": achieved / peak,
-          "traffic": traffic, "avg_launch_ms": enc, "timed_launches": ktimes.get("encode", (0, 0))[1],
-          "algorithmic_bytes_per_launch": enc_bytes, "algorithmic_flops_per_launch": enc_flops,
-          "arithmetic_intensity_flop_per_byte": intensity, "ridge_flop_per_byte": ridge,
-          "traffic_source": None if pmc is None else pmc["source"],
-          "traffic_stale": None if pmc is None else pmc["stale"]}
-    t_roof = max(step_flops / (peak_tf * 1e12), enc_bytes / (HBM_PEAK_GBS * 1e9))
+    enc_rf = _roof(ekn, enc, enc_bytes, enc_flops, peak_tf)
+    enc_rf["timed_launches"] = ktimes["encode"][1]
+    rf = enc_rf
+    if h16 and prepped_ahead and "tail" in ktimes and ktimes["tail"][0] > enc:
+        # the dominant launch is the tail launch carrying the next batch's row preparation: an
+        # HBM stream (the tail and ECDA blocks on 5 CUs run inside it)
+        rf = _roof(tail_name, ktimes["tail"][0], src_bytes + prep_bytes, 0.0, peak_tf, bound="hbm",
+                   note="tail + ECDA blocks and the next batch's row preparation (dad_prep) in one launch; "
+                        "bytes = the next batch's fp32 rows read + its 16-bit prepared rows written")
+        rf["timed_launches"] = ktimes["tail"][1]
+    t_roof = max(step_flops / (peak_tf * 1e12), src_bytes / (HBM_PEAK_GBS * 1e9))
     srf = {"t_roof_us": t_roof * 1e6, "t_step_us": ms_step * 1e3, "frac": t_roof / (ms_step * 1e-3),
-           "flops_per_step": step_flops, "bytes_per_step": enc_bytes, "mfma_peak_tflops": peak_tf}
+           "flops_per_step": step_flops, "bytes_per_step": src_bytes, "mfma_peak_tflops": peak_tf}
     # MFMA utilisation of the encoder linears (north_star: >= 40 %): algorithmic FLOPs / time / peak
     enc_tf = enc_flops / (enc * 1e-3) / 1e12
     wg_tf = wg_flops / (wg * 1e-3) / 1e12
@@ -546,6 +569,7 @@ def rooflines(ktimes, rows_c, rows_n, ms_step, precision, tail_name="dad_tail_ec
             mf[kn]["pmc_matrix_busy_frac"] = pk["mfma_busy_frac"]
             mf[kn]["pmc_stale"] = pk["stale"]
     kern["mfma_util"] = mf
+    kern["encoder_roofline"] = enc_rf
     return rf, srf, kern
 
 
@@ -599,19 +623,27 @@ def side_mode(model, view, data, B, T, args, precision, n):
     launches), with its own per-kernel timing and rooflines: fp32 (the reference's arithmetic,
     exact-f32 MFMA, f32 peak) or bf16 (BASELINE configs[1]'s named dtype, bf16 peak)."""
     s32 = PKG.DADStep(model, view, precision=precision, rng="counter", seed=5)
-    for i in range(3):
-        s32.step(data[i % 4][0], data[i % 4][1], args.epoch)
+    ahead = precision != "fp32" and not args.no_ahead
+    pos = [0]
+
+    def run1():
+        i = pos[0]
+        pos[0] += 1
+        s32.step(data[i % 4][0], data[i % 4][1], args.epoch, next_batch=data[(i + 1) % 4] if ahead else None)
+    for _ in range(3):
+        run1()
     torch.cuda.synchronize()
     timer = PKG._lib.KernelTimer(4, n // 4 + 1, kernels=TIMED_KERNELS)
     t1 = time.perf_counter()
-    for i in range(n):
-        s32.step(data[i % 4][0], data[i % 4][1], args.epoch)
+    for _ in range(n):
+        run1()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t1) / n
     enc = timer.stop()          # (one timer at a time: dad_timing_start refuses a second)
-    kt = kernel_pass(lambda: s32.step(data[0][0], data[0][1], args.epoch), max(8, n // 2))
+    kt = kernel_pass(run1, max(8, n // 2))
     kt.update(enc)
-    rf, srf, kern = rooflines(kt, B * T, B * T, dt * 1e3, precision, tail_kernel(B, B, class_aware(view)))
+    rf, srf, kern = rooflines(kt, B * T, B * T, dt * 1e3, precision, tail_kernel(B, B, class_aware(view)),
+                              prepped_ahead=ahead)
     return {"value": B / dt, "ms_per_step": dt * 1e3, "steps": n, "dtype": "f32" if precision == "fp32" else precision,
             "launch": "eager", "roofline": rf, "step_roofline": srf, "kernels": kern}
 
@@ -870,18 +902,21 @@ def main():
                     "store-mode loaders, epoch %d, counter-RNG augmentation" % (B, 100, 300, args.folds, args.epoch))
     elif args.flavor == "iemocap":
         workload = ("IEMOCAP DAD train step (configs[%d]): batch=64/GPU, T=300x768 synthetic emotion2vec-shaped "
-                    "features, post-warm-up epoch %d (CE+KL+ECDA active), counter-RNG augmentation in-kernel"
+                    "features, post-warm-up epoch %d (CE+KL+ECDA active), counter-RNG augmentation (16-bit modes: prepared for "
+                    "each next step inside the tail launch)"
                     % (1 if world == 1 else 2, args.epoch))
     else:
         workload = ("%s DAD train step%s: batch=%d/GPU, T=%dx768 synthetic features, noisy branch at SNR %g dB, "
-                    "post-warm-up epoch %d, counter-RNG augmentation in-kernel"
+                    "post-warm-up epoch %d, counter-RNG augmentation (16-bit modes: prepared for each next step inside the "
+                    "tail launch)"
                     % (args.flavor.upper(), " (configs[3]: DACP+ECDA forced on; SCL is 0 in the reference)"
                        if args.force_ecda else "", B, T, args.snr, args.epoch))
     # per-kernel table: the separate pass, with the timed region's encoder entry
     kt = dict(table)
     kt.update(ktimes)
     rf, srf, kern = rooflines(kt, rows, rows, ms, args.precision,
-                              tail_kernel(B, B, True if args.mixed else class_aware(view)))
+                              tail_kernel(B, B, True if args.mixed else class_aware(view)),
+                              prepped_ahead=not args.mixed and not args.no_ahead and graphs is None)
     kern["source"] = ("encoder: HIP events around it in the timed region (%s); the other kernels: a separate "
                       "eager pass of %d steps after it (events at every boundary of every 2nd step)"
                       % ("stream events around the encoder graph of every %d-th replayed step" % len(graphs)

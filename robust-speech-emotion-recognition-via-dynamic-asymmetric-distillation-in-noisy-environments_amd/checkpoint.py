@@ -131,13 +131,18 @@ def train_epoch(step, clean_loader, noisy_loader, epoch, lr=None):
     """Trainer.train_epoch (I/train.py:474-520): min(len) batch pairs through the fused step at
     the epoch's cosine learning rate (CosineAnnealingLR(T_max=EPOCHS) stepped once per epoch),
     then the DACP epoch-end update after warm-up.  Returns the mean of each loss over the
-    epoch (one device->host read, at the end)."""
+    epoch (one device->host read, at the end).  Batches are drawn one ahead, so each step names
+    the next one (16-bit modes prepare its rows inside the tail launch; the loaders hand out fresh
+    device tensors per batch, and the results are the same either way)."""
     lr = step.view.lr_at(epoch) if lr is None else lr
     n = min(len(clean_loader), len(noisy_loader))
     ci, ni = iter(clean_loader), iter(noisy_loader)
     tot = None
-    for _ in range(n):
-        losses = step.step(next(ci), next(ni), epoch, lr=lr)
+    cur = (next(ci), next(ni)) if n else None
+    for i in range(n):
+        nxt = (next(ci), next(ni)) if i + 1 < n else None
+        losses = step.step(cur[0], cur[1], epoch, lr=lr, next_batch=nxt)
+        cur = nxt
         vec = torch.stack([losses[k].float().reshape(()) for k in sorted(losses)])
         tot = vec if tot is None else tot + vec
     if epoch >= step.view.WARMUP_EPOCHS:

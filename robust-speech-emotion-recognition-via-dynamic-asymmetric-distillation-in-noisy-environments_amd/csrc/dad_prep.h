@@ -20,7 +20,12 @@
 // encoder converted per lane, so the counter RNG draws the same values (pair (row*768 + d) / 2 of
 // the stream, dad_aug_noise_pair) and the bytes equal what the fused encoder multiplied.  Each
 // wave loads R rows before converting any (R x 3 KB in flight per wave; rows past the end are
-// clamped to the last one and not stored, so no load sits under a condition).
+// clamped to the last one and not stored, so no load sits under a condition).  The fp32 source
+// rows are read once: non-temporal loads keep them out of the caches, so the prepared rows this
+// pass writes stay in the 256 MB Infinity Cache for the encoder and the weight gradient (A/B: step
+// 114.1-114.5 -> 110.3-110.6 us, encoder 38.5 -> 36.7 us, weight gradient 26.0 -> 25.0 us).  In
+// the tail launch (8 waves per CU) R = 2 measured best: 111.3-112.0 us against 112.7-113.3 (R = 4),
+// 113.5 (R = 3), 111.7-113.2 (R = 1), 119 (R = 8).
 #pragma once
 #include "dad_kernels.h"
 
@@ -57,13 +62,7 @@ __device__ __forceinline__ void dad_prep_rows(const DadPrepArgs& a, int wave, in
       const int b = un / T, t = un - b * T;
       const float* x = (noisy ? a.xn : a.xc) + dad_src_row(a.src, noisy, b, T, t) * DAD_D + 4 * lane;
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
-#ifdef PREP_NT
-        v[r][k] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(x + 256 * k));
-#else
-        v[r][k] = *reinterpret_cast<const f32x4*>(x + 256 * k);
-#endif
-      }
+      for (int k = 0; k < 3; ++k) v[r][k] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(x + 256 * k));
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) {

@@ -2182,10 +2182,7 @@ __global__ __launch_bounds__(TAIL_THREADS) void dad_tail_ecda_w(DadTailArgs ta, 
     if (!pa.x16) return;
     constexpr int kWaves = TAIL_THREADS / 64;
     const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-#ifndef PREP_R
-#define PREP_R 4
-#endif
-    dad_prep_dispatch<PREP_R>(pa, ((int)blockIdx.x - 1 - DAD_C) * kWaves + w, ((int)gridDim.x - 1 - DAD_C) * kWaves,
+    dad_prep_dispatch<2>(pa, ((int)blockIdx.x - 1 - DAD_C) * kWaves + w, ((int)gridDim.x - 1 - DAD_C) * kWaves,
                          (int)threadIdx.x & 63);
     return;
   }
