@@ -34,10 +34,12 @@ def _chain(cfg, precision, batches, st, ahead, wrong_at=None):
     return _state(step), losses, prepped
 
 
-@pytest.mark.parametrize("precision", ["fp16", "bf16"])
-def test_prefetch_chain_equals_plain_chain(precision):
+@pytest.mark.parametrize("precision,B,T", [("fp16", 16, 40), ("bf16", 16, 40), ("fp16", 64, 300)])
+def test_prefetch_chain_equals_plain_chain(precision, B, T):
+    """(B=64, T=300: the bench geometry, 251 preparation workgroups in the tail launch.)"""
     cfg = dad_oracle.make_cfg("iemocap")
-    batches = [_device_batches(_problem(B=16, T=40, seed=31 + i, Bn=12, Tn=50))[:2] for i in range(3)]
+    Bn, Tn = (12, 50) if B == 16 else (B, T)
+    batches = [_device_batches(_problem(B=B, T=T, seed=31 + i, Bn=Bn, Tn=Tn))[:2] for i in range(3)]
     st = synth.make_state(31, 1)
     want, want_losses, plain_prepped = _chain(cfg, precision, batches, st, ahead=False)
     assert not any(plain_prepped)
