@@ -411,7 +411,7 @@ def event_every(steps):
 TIMED_KERNELS = ["encode"]
 
 
-def capture_steps(step, data, epoch, split=None):
+def capture_steps(step, data, epoch, split=None, ahead=False):
     """One hipGraph (torch.cuda.CUDAGraph) per resident batch pair, each holding one full fused
     step (the C ABI is enqueue-only; tests/test_gpu_graph.py proves replay == eager bit for bit).
     A graph bakes its step's host scalars into the kernel arguments: the RNG step counter and the
@@ -420,14 +420,29 @@ def capture_steps(step, data, epoch, split=None):
     device state (parameters, moments, DACP).  Batch `split` is captured as two graphs, the
     encoder launch and the rest of its step, so stream events recorded between their replays
     time the encoder inside the timed region (HIP event nodes captured INSIDE a graph do not
-    report elapsed times).  Returns a list of graph tuples, or raises on a capture error."""
+    report elapsed times).
+    ahead (16-bit): every graph also prepares the next graph's rows in its tail launch, the last
+    one for the first graph's counter (next_counter), and one eager step on the last batch first
+    prepares the first graph's rows -- so the cycle of replays is the eager prepared-ahead chain
+    with its counters repeating.  Returns a list of graph tuples, or raises on a capture error."""
     torch.cuda.synchronize()
+    n = len(data)
+    if ahead:
+        c, nb = data[-1]
+        step.step(c, nb, epoch, next_batch=data[0])
+        torch.cuda.synchronize()
+    g0 = step.global_step
     graphs = []
     for i, (c, nb) in enumerate(data):
+        kw = {}
+        if ahead:
+            kw = {"next_batch": data[(i + 1) % n], "next_counter": g0 if i == n - 1 else None}
         if i != split:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                step.step(c, nb, epoch)
+                step.step(c, nb, epoch, **kw)
+            if ahead and not step.last_prepped:
+                raise RuntimeError("graph %d was captured without its prepared rows" % i)
             graphs.append((g,))
             continue
         ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
@@ -439,9 +454,11 @@ def capture_steps(step, data, epoch, split=None):
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             ga.capture_begin()
-            step.step(c, nb, epoch, after_encode=cut)
+            step.step(c, nb, epoch, after_encode=cut, **kw)
             gb.capture_end()
         torch.cuda.current_stream().wait_stream(s)
+        if ahead and not step.last_prepped:
+            raise RuntimeError("graph %d was captured without its prepared rows" % i)
         graphs.append((ga, gb))
     torch.cuda.synchronize()
     return graphs
@@ -821,7 +838,8 @@ def main():
             # graph is timed by stream events around its own graph (every 8th step)
             split = len(data) - 1
             try:
-                graphs = capture_steps(step, data, args.epoch, split=split)
+                graphs = capture_steps(step, data, args.epoch, split=split,
+                                       ahead=args.precision != "fp32" and not args.no_ahead)
             except Exception as e:   # (e.g. a transport that refuses capture): eager, said so in the line
                 err = str(e).splitlines()[0][:200] if str(e) else type(e).__name__
                 restore(model, step, snap)

@@ -251,8 +251,11 @@ class DADStep:
         self._keepalive = keep
         return cfg, bt, st
 
-    def _batch_structs(self, clean_batch, noisy_batch, epoch, lr, draws, counter=None, adam_step=None):
-        """(dad_config, dad_batch, keepalive) of one step's batch."""
+    def _batch_structs(self, clean_batch, noisy_batch, epoch, lr, draws, like=None, counter=None):
+        """(dad_config, dad_batch, keepalive) of one step's batch.  like: the current step's config;
+        then this is the NEXT step's batch: its config is a copy with the next counter (`counter`,
+        default like's + 1; only what the row preparation reads must be right, and the preparation
+        ahead needs the same geometry), or None when its geometry differs (no preparation ahead)."""
         dev = self.device
         xc, mc, yc, rc, lc = _dev_batch(clean_batch, dev)
         warm = epoch < self.view.WARMUP_EPOCHS
@@ -266,7 +269,14 @@ class DADStep:
         else:
             raise ValueError("post-warm-up steps need a noisy batch")
         Bc, Tc = mc.shape[0], mc.shape[1]
-        cfg = self.make_config(Bc, Tc, Bn, Tn, epoch, lr=lr, adam_step=adam_step, counter=counter)
+        if like is None:
+            cfg = self.make_config(Bc, Tc, Bn, Tn, epoch, lr=lr)
+        elif (like.B, like.T, like.Bn, like.Tn) == (Bc, Tc, Bn, Tn):
+            cfg = _lib.DadConfig.from_buffer_copy(like)
+            cfg.counter = like.counter + 1 if counter is None else counter
+            cfg.prepped = 0
+        else:
+            return None, None, None
         bt = _lib.DadBatch()
         bt.xc, bt.mc, bt.yc = xc.data_ptr(), mc.data_ptr(), yc.data_ptr()
         if rc is not None:
@@ -293,7 +303,8 @@ class DADStep:
             keep.append(dd)
         return cfg, bt, (xc, mc, yc, xn, mn, keep, rc, lc, rn, ln)
 
-    def step(self, clean_batch, noisy_batch, epoch, lr=None, draws=None, after_encode=None, next_batch=None):
+    def step(self, clean_batch, noisy_batch, epoch, lr=None, draws=None, after_encode=None, next_batch=None,
+             next_counter=None):
         """One full training step; returns the reference's loss dict as 0-d device tensors.
 
         after_encode: optional callable run on the host between the encoder launch and the rest
@@ -304,6 +315,9 @@ class DADStep:
         with that batch skips them.  Results are bit-identical with or without it.  The next
         batch's device tensors must keep their contents until that step (device-resident
         batches; host tensors are copied again by the next step, which then prepares itself).
+        next_counter: the next step's RNG step counter (default this step's + 1).  Graph replays
+        that cycle a fixed set of captured steps pass the first captured step's counter from the
+        last one (bench.capture_steps), so the cycle stays consistent.
         """
         if self._shadow_dirty or self._param_key() != self._shadow_key:
             self.refresh_shadow()
@@ -321,8 +335,11 @@ class DADStep:
             stream = self._stream()
         if next_batch is not None and self.precision != _lib.PREC_FP32:
             nd = next_batch[2] if len(next_batch) > 2 else None
-            ncfg, nbt, nkeep = self._batch_structs(next_batch[0], next_batch[1], epoch, lr, nd,
-                                                   counter=self.global_step + 1, adam_step=self.adam_step + 2)
+            ncfg, nbt, nkeep = self._batch_structs(next_batch[0], next_batch[1], epoch, lr, nd, like=cfg,
+                                                   counter=next_counter)
+        else:
+            ncfg = None
+        if ncfg is not None:
             done = ctypes.c_int(0)
             _lib.check(L.dad_step_backward_ahead(cfg, bt, st, _lib.ptr(ws), stream, ncfg, nbt, ctypes.byref(done)),
                        "dad_step_backward_ahead")

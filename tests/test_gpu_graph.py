@@ -82,3 +82,46 @@ def test_captured_step_replays_like_eager(precision, rng):
     # the replays really stepped: the parameters moved from the start state
     s0 = torch.from_numpy(gh.flat(st["student"])).cuda()
     assert not torch.equal(got[0], s0)
+
+
+@pytest.mark.parametrize("precision", ["fp16", "bf16"])
+def test_cycled_graphs_with_rows_prepared_ahead(precision):
+    """bench.py --launch graph with the next batch prepared in each tail launch: graphs of the
+    steps g0, g0+1 on batches A, B, each preparing the next graph's rows (the last one for g0:
+    next_counter), after one eager priming step that prepares A's.  Replays cycle the two graphs;
+    the eager side runs the same chain with its counters pinned (global_step reset per step)."""
+    import bench
+    cfg = dad_oracle.make_cfg("iemocap")
+    ins = [_problem(B=16, T=40, seed=s, Bn=12, Tn=50) for s in (31, 32)]
+    st = synth.make_state(21, 1)
+    data = []
+    for inp in ins:
+        c, n, _ = _device_batches(inp)
+        data.append((c, n))
+    epoch, R = 60, 6
+
+    eager = gh.make_step(cfg, precision=precision, rng="counter", seed=3)
+    gh.load_state(eager, st)
+    g0 = eager.global_step + 1
+    eager.step(*data[1], epoch, next_batch=data[0])            # the priming step (counter g0 - 1)
+    a0 = eager.adam_step
+    seen = []
+    for k in range(R):
+        i = k % 2
+        eager.global_step, eager.adam_step = g0 + i, a0 + i
+        eager.step(*data[i], epoch, next_batch=data[1 - i], next_counter=g0 if i == 1 else None)
+        seen.append(eager.last_prepped)
+    torch.cuda.synchronize()
+    assert all(seen)
+    want = _state(eager)
+
+    cap = gh.make_step(cfg, precision=precision, rng="counter", seed=3)
+    gh.load_state(cap, st)
+    graphs = bench.capture_steps(cap, data, epoch, ahead=True)
+    assert len(graphs) == 2 and cap.global_step == g0 + 2
+    for k in range(R):
+        graphs[k % 2][0].replay()
+    torch.cuda.synchronize()
+    got = _state(cap)
+    for name, a, b in zip(("student", "teacher", "exp_avg", "exp_avg_sq", "dacp", "grad"), got, want):
+        assert torch.equal(a, b), "%s differs after %d replays (max %.3g)" % (name, R, float((a - b).abs().max()))

@@ -1,4 +1,4 @@
-# A/B of environment switches on one box: AB_ENVS="DAD_WS_SWEEP=1 DAD_WS_SWEEP=0" (one token per
+# A/B of environment switches on one box: AB_ENVS="DAD_WP_SCOST=1.0 DAD_WP_SCOST=1.1" (one token per
 # variant; "base" = no change), AB_ROUNDS alternating eager benches each (per-kernel times), then
 # one FETCH_SIZE PMC pass per variant for the kernels in PMC_REGEX.
 set -o pipefail
