@@ -411,6 +411,14 @@ def event_every(steps):
 TIMED_KERNELS = ["encode"]
 
 
+def timed_kernels(precision, ahead):
+    """The kernel the timed region records events around: the line's dominant launch -- the tail
+    launch when it also prepares the next step's rows (16-bit with next-batch preparation: the
+    longest launch of the step), else the encoder.  The other kernels' times come from the
+    separate eager pass after the timed region."""
+    return ["tail"] if precision != "fp32" and ahead else TIMED_KERNELS
+
+
 def capture_steps(step, data, epoch, split=None, ahead=False):
     """One hipGraph (torch.cuda.CUDAGraph) per resident batch pair, each holding one full fused
     step (the C ABI is enqueue-only; tests/test_gpu_graph.py proves replay == eager bit for bit).
@@ -650,7 +658,7 @@ def side_mode(model, view, data, B, T, args, precision, n):
     for _ in range(3):
         run1()
     torch.cuda.synchronize()
-    timer = PKG._lib.KernelTimer(4, n // 4 + 1, kernels=TIMED_KERNELS)
+    timer = PKG._lib.KernelTimer(4, n // 4 + 1, kernels=timed_kernels(precision, ahead))
     t1 = time.perf_counter()
     for _ in range(n):
         run1()
@@ -803,27 +811,28 @@ def main():
                 c, nb = data[i % len(data)]
                 step.step(c, nb, args.epoch, next_batch=None if args.no_ahead else data[(i + 1) % len(data)])
 
+        # The side legs of the line (the FP32 mode, the BF16 mode, the data path) run first, from the
+        # initial state, which is restored after them; then the W warm-up steps, right before the
+        # timed region: it starts on a GPU that has been busy for ~100 ms (steady clocks) with the
+        # warm-up's prepared rows and caches in place.  (The driver's --steps 20 --warmup 5 line had
+        # measured the clock ramp: 137 -> 130 -> 124 us per step over consecutive 20-step segments,
+        # round 2.)  The parity block runs after the timed region, from the state it started in.
+        parity = fp32 = bf16 = data_path = None
+        side = rank == 0 and world == 1
+        if side:
+            snap0 = snapshot(model, step)
+            if args.precision != "fp32":
+                if args.fp32_steps > 0:
+                    fp32 = side_mode(model, view, data, B, T, args, "fp32", args.fp32_steps)
+                if args.precision == "fp16" and args.bf16_steps > 0:
+                    bf16 = side_mode(model, view, data, B, T, args, "bf16", args.bf16_steps)
+            if not args.no_data_path:
+                data_path = data_path_bench(step, B, T, args.epoch, dev)
+            restore(model, step, snap0)
+            del snap0
         run(args.warmup)
         torch.cuda.synchronize()
         snap = snapshot(model, step)          # the state the first timed step starts from
-        # The side legs of the line (bf16-vs-fp32 parity on the first timed batch, the FP32 mode,
-        # the data path) run here, between the warm-up and the timed region, and the state is
-        # restored after them: the timed region then starts on a GPU that has been busy for
-        # ~100 ms (steady clocks) instead of 5 warm-up steps after model setup.  (The driver's
-        # --steps 20 --warmup 5 line had measured the clock ramp: 137 -> 130 -> 124 us per step
-        # over consecutive 20-step segments, round 2.)
-        parity = fp32 = bf16 = data_path = None
-        if rank == 0 and world == 1 and args.precision != "fp32":
-            if not args.no_parity:
-                parity = parity_block(model, step, view, snap, data[0], args.epoch, args.precision)
-            if args.fp32_steps > 0:
-                fp32 = side_mode(model, view, data, B, T, args, "fp32", args.fp32_steps)
-            if args.precision == "fp16" and args.bf16_steps > 0:
-                bf16 = side_mode(model, view, data, B, T, args, "bf16", args.bf16_steps)
-        if rank == 0 and world == 1 and not args.no_data_path:
-            data_path = data_path_bench(step, B, T, args.epoch, dev)
-        restore(model, step, snap)
-        torch.cuda.synchronize()
         # every EVENT_EVERY-th timed step records hip events at its kernel boundaries (created
         # here, outside the timed region; the region only records them)
         launch = args.launch
@@ -854,7 +863,8 @@ def main():
                     e1.record()
                 torch.cuda.synchronize()
         if graphs is None:
-            timer = PKG._lib.KernelTimer(event_every(args.steps), args.steps + 1, kernels=TIMED_KERNELS)
+            timer = PKG._lib.KernelTimer(event_every(args.steps), args.steps + 1,
+                                         kernels=timed_kernels(args.precision, not args.no_ahead))
 
         def timed(n):
             if graphs is None:
@@ -894,6 +904,9 @@ def main():
         msum = float(step.outputs(*nbc)["msum"])
         ecda_on = float(step.outputs(*nbc)["ecda_on"])
         table = kernel_pass(lambda: run(1), args.kernel_steps)
+        if side and args.precision != "fp32" and not args.no_parity:
+            parity = parity_block(model, step, view, snap, data[args.warmup % len(data)], args.epoch,
+                                  args.precision)
         timed_steps = args.steps
         total_utts = B * world * args.steps
         rows_per_step = 2 * B * T
@@ -934,12 +947,15 @@ def main():
     kt.update(ktimes)
     rf, srf, kern = rooflines(kt, rows, rows, ms, args.precision,
                               tail_kernel(B, B, True if args.mixed else class_aware(view)),
-                              prepped_ahead=not args.mixed and not args.no_ahead and graphs is None)
-    kern["source"] = ("encoder: HIP events around it in the timed region (%s); the other kernels: a separate "
-                      "eager pass of %d steps after it (events at every boundary of every 2nd step)"
-                      % ("stream events around the encoder graph of every %d-th replayed step" % len(graphs)
-                         if not args.mixed and graphs else "every %d-th step" % event_every(args.steps),
-                         args.kernel_steps))
+                              prepped_ahead=not args.mixed and not args.no_ahead)
+    if not args.mixed and graphs:
+        src = "encoder: stream events around the encoder graph of every %d-th replayed step" % len(graphs)
+    else:
+        tk = timed_kernels(args.precision, not args.mixed and not args.no_ahead)[0]
+        src = "%s: HIP events around it in the timed region (every %d-th step)" % (
+            {"tail": "tail launch (the dominant launch)", "encode": "encoder"}[tk], event_every(args.steps))
+    kern["source"] = ("%s; the other kernels: a separate eager pass of %d steps after it (events at every "
+                      "boundary of every 2nd step)" % (src, args.kernel_steps))
     line = {
         "metric": METRIC, "value": value, "unit": "utterances/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",

@@ -11,10 +11,9 @@
 //
 // Output: one prepared set [clean Bc*Tc | strong Bn*Tn | weak Bn*Tn][768] of 16-bit rows in the
 // padded layout (row b*T + t), whatever the source mode.  The strong and clean parts are also the
-// weight gradient's operand.  The fused step prepares only the noisy rows (a.clean = 0): the
-// encoder's clean-student workgroups convert the clean rows themselves (no augmentation there, so
-// no RNG) and store the clean part, which keeps this pass's HBM traffic (118 MB at B=64, T=300)
-// within the tail launch it overlaps.
+// weight gradient's operand.  The step prepares all three parts (a.clean = 1; 206 MB of HBM
+// traffic at B=64, T=300: 118 MB of fp32 rows read, 88.5 MB of 16-bit rows written); a.clean = 0
+// (noisy rows only) is kept for callers whose clean rows are converted elsewhere.
 //
 // One wave per row; lane l owns columns 256k + 4l .. +3 (k = 0..2): the element pairs the fused
 // encoder converted per lane, so the counter RNG draws the same values (pair (row*768 + d) / 2 of
@@ -25,7 +24,10 @@
 // pass writes stay in the 256 MB Infinity Cache for the encoder and the weight gradient (A/B: step
 // 114.1-114.5 -> 110.3-110.6 us, encoder 38.5 -> 36.7 us, weight gradient 26.0 -> 25.0 us).  In
 // the tail launch (8 waves per CU) R = 2 measured best: 111.3-112.0 us against 112.7-113.3 (R = 4),
-// 113.5 (R = 3), 111.7-113.2 (R = 1), 119 (R = 8).
+// 113.5 (R = 3), 111.7-113.2 (R = 1), 119 (R = 8).  Loading the next group's rows before converting
+// the current one (software pipelining, 2 x R x 12 VGPRs) measured no faster: tail launch 42.7-42.9
+// against 41.2 us (R = 2), 45.0 (R = 4), 42.7-42.8 (R = 1): the pass is bound by HBM at ~5 TB/s
+// of mixed read/write traffic, not by the loads in flight per wave.
 #pragma once
 #include "dad_kernels.h"
 
