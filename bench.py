@@ -405,9 +405,11 @@ def event_every(steps):
     return max(1, min(EVENT_EVERY, steps // 4))
 
 
-# The timed region records events around the encoder only (the roofline kernel): every recorded
-# event costs the stream ~3 us (measured: events at every boundary of every 8th step put 3.2 us
-# on the mean step), so the per-kernel table comes from a separate pass after the timed region.
+# The timed region records events around one kernel only (the roofline kernel, timed_kernels):
+# with the default system-scope fence every recorded event had cost the stream ~3 us (events at
+# every boundary of every 8th step put 3.2 us on the mean step); the library's timing events are
+# now created without that fence (hipEventDisableSystemFence), and the per-kernel table still
+# comes from a separate pass after the timed region.
 TIMED_KERNELS = ["encode"]
 
 

@@ -202,7 +202,10 @@ int dad_timing_start(int every, int max_steps) {
   g_tk = Timing();
   g_tk.ev.assign((size_t)max_steps * TK_N, nullptr);
   g_tk.rec.assign((size_t)max_steps * TK_N, 0);
-  for (auto& e : g_tk.ev) DAD_TRY(hipEventCreate(&e));
+  // timing-only events: no system-scope fence (no L2 writeback / invalidate at each record, which had
+  // cost the stream ~3 us per event and slowed the kernel after it); dad_timing_stop reads them after
+  // a device synchronize
+  for (auto& e : g_tk.ev) DAD_TRY(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
   g_tk.every = every;
   g_tk.nset = max_steps;
   return DAD_OK;
