@@ -884,6 +884,7 @@ def main():
                     gs[0].replay()
                     e1.record()
                     gs[1].replay()
+        torch.cuda.synchronize()
         if dist:
             dist.barrier()
         t0 = time.perf_counter()
