@@ -120,6 +120,7 @@ class DADStep:
         self.adam_step = 0
         self.global_step = 0
         self._ws = None
+        self._ws_need = {}       # workspace bytes per layout key (_workspace)
         self._bufs = {}
         self._prepped_key = None       # identity of the batch the last step's tail launch prepared
         self.last_prepped = False
@@ -216,9 +217,14 @@ class DADStep:
         return s
 
     def _workspace(self, cfg):
-        nbytes = ctypes.c_size_t(0)
-        _lib.check(_lib.lib().dad_workspace_bytes(cfg, ctypes.byref(nbytes)), "dad_workspace_bytes")
-        need = int(nbytes.value)
+        # dad_workspace_bytes depends on the geometry, the split count, the precision and the
+        # warm-up flag only (dad_abi.hip: dad_ws_layout(geom_of, max_splits_of, precision))
+        key = (cfg.B, cfg.T, cfg.Bn, cfg.Tn, cfg.splits, cfg.precision, cfg.warmup)
+        need = self._ws_need.get(key)
+        if need is None:
+            nbytes = ctypes.c_size_t(0)
+            _lib.check(_lib.lib().dad_workspace_bytes(cfg, ctypes.byref(nbytes)), "dad_workspace_bytes")
+            need = self._ws_need[key] = int(nbytes.value)
         if self._ws is None or self._ws.numel() < need:
             # zero-filled once (finite bytes everywhere; the step needs no initialisation)
             self._ws = torch.zeros(need, dtype=torch.uint8, device=self.device)

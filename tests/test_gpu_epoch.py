@@ -64,3 +64,44 @@ def test_train_epoch_runs_loaders_and_epoch_end(tmp_path):
     assert not torch.equal(step.class_quality_scores, q0)   # DACP quality updated at epoch end
     warm = CK.train_epoch(step, clean, noisy, 3)              # warm-up: no epoch-end update
     assert np.isfinite(warm["total_loss"])
+
+
+def _store_batches(seed, k, length=30, mode="batch_index"):
+    """Batches of equal-length utterances from a data.FeatureStore, so consecutive batches share
+    their geometry and the next batch's rows can be prepared ahead: store mode (batch_index: rows
+    gathered from the store) or padded copies (collate)."""
+    rs = np.random.RandomState(seed)
+    sizes = np.full(64, length)
+    feats = rs.standard_normal((int(sizes.sum()), 768)).astype(np.float32)
+    offsets = np.concatenate([[0], np.cumsum(sizes)[:-1]])
+    st = PKG.data.FeatureStore(feats, sizes, offsets, rs.randint(0, 4, size=64))
+    f = getattr(st, mode)
+    return [(f(rs.choice(64, 12, replace=False)), f(rs.choice(64, 10, replace=False), with_labels=False))
+            for _ in range(k)]
+
+
+@pytest.mark.parametrize("mode", ["batch_index", "collate"])
+def test_store_mode_prefetch_chain_is_bit_exact(mode):
+    """Store-mode batches (rows gathered from the feature store through dad_batch.rowc..lenn) with
+    the next batch prepared in each tail launch: the same parameters, moments, DACP state and
+    losses as the chain that prepares every batch itself (fp16)."""
+    cfg = dad_oracle.make_cfg("iemocap")
+    data = _store_batches(51, 5, mode=mode)
+    state = synth.make_state(51, 1)
+    runs = []
+    for ahead in (False, True):
+        s = gh.make_step(cfg, precision="fp16", rng="counter", seed=6)
+        gh.load_state(s, state)
+        flags = []
+        for i in range(len(data)):
+            nxt = data[i + 1] if ahead and i + 1 < len(data) else None
+            l = s.step(*data[i], 60, next_batch=nxt)
+            flags.append(s.last_prepped)
+        torch.cuda.synchronize()
+        runs.append((s, {k: float(v) for k, v in l.items()}, flags))
+    (a, la, fa), (b, lb, fb) = runs
+    assert fa == [False] * 5 and fb == [False, True, True, True, True]
+    assert la == lb
+    for x, y in ((a.model.student_flat, b.model.student_flat), (a.model.teacher_flat, b.model.teacher_flat),
+                 (a.exp_avg, b.exp_avg), (a.exp_avg_sq, b.exp_avg_sq), (a.dacp, b.dacp)):
+        assert torch.equal(x, y)
