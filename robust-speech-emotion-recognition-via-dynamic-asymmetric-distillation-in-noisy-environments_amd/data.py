@@ -40,7 +40,9 @@ def _device(device):
     d = torch.device(device if device is not None else "cuda")
     if d.type != "cuda" or not torch.cuda.is_available():
         raise RuntimeError("the device-resident data path needs the MI355X (got device %s)" % d)
-    return d
+    # an explicit index: DADStep compares the store's device with its own ("cuda:0"), and a bare
+    # "cuda" would compare unequal and send every store-mode batch through a padded copy
+    return d if d.index is not None else torch.device("cuda", torch.cuda.current_device())
 
 
 class FeatureStore:

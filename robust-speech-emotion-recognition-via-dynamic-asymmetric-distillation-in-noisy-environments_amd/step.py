@@ -31,7 +31,7 @@ def _dev_batch(batch, device, labels=True):
     feats = ni["feats"]
     rows = lens = None
     if isinstance(feats, StoreFeats):
-        if feats.store.feats.dtype == torch.float32 and feats.device == device:
+        if feats.store.feats.dtype == torch.float32 and feats.store.feats.device == device:
             x, rows, lens = feats.store.feats, feats.rows, feats.lens
         else:                      # the encoders read f32 rows: other stores are widened by dad_collate
             x = feats.materialize().to(device)
