@@ -248,12 +248,19 @@ def data_path_bench(step, B, T, epoch, dev, n_utt=1024, reps=40, steps=20):
         noisy = PKG.data.DeviceLoader(store.subset(np.arange(n_utt), with_labels=False), batch_size=B,
                                       shuffle=True, fused=fused)
         ci, ni = epochs(clean), epochs(noisy)
+        # batches drawn one ahead, each step naming the next (checkpoint.train_epoch's loop): the
+        # 16-bit modes prepare the next batch's rows inside the tail launch
+        nxt = [(next(ci), next(ni))]
+
+        def one():
+            cur, nxt[0] = nxt[0], (next(ci), next(ni))
+            step.step(cur[0], cur[1], epoch, next_batch=nxt[0])
         for _ in range(3):
-            step.step(next(ci), next(ni), epoch)
+            one()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(steps):
-            step.step(next(ci), next(ni), epoch)
+            one()
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / steps
         return {"value": B / dt, "unit": "utterances/s", "ms_per_step": dt * 1e3, "steps": steps}

@@ -257,7 +257,11 @@ class _DeviceLoaderIter:
             # the sampler draws its permutation at the first next(), as in the reference
             self._batches = [np.asarray(b, dtype=np.int64) for b in self._it]
             flat = np.concatenate(self._batches) if self._batches else np.zeros(0, np.int64)
-            self._index_d = torch.from_numpy(flat).to(L.store.device)
+            # one upload per epoch, from pinned memory and asynchronous: a pageable copy would
+            # wait for every step already queued on the stream (a pipeline drain per epoch)
+            host = torch.from_numpy(flat)
+            dev = torch.device(L.store.device)
+            self._index_d = (host.pin_memory() if dev.type == "cuda" else host).to(dev, non_blocking=True)
             self._starts = np.concatenate([[0], np.cumsum([len(b) for b in self._batches])])
             self._T = [int(L.store.sizes[b].max()) if len(b) else 0 for b in self._batches]
         if self._k >= len(self._batches):
