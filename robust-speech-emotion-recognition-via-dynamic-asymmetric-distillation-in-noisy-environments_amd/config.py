@@ -178,3 +178,86 @@ def dad_config_for(view, Bc, Tc, Bn, Tn, epoch, adam_step, lr=None, precision=_l
     c.dacp_beta, c.dacp_one_m_beta = beta, 1 - beta
     c.splits = int(splits)
     return c
+
+
+# Every attribute dad_config_for (and the ConfigView methods it calls) reads: the key of
+# ConfigCache.  tests/test_config_model_cpu.py records the attributes a dad_config_for call
+# actually reads and checks that they are all here.
+CONFIG_KEYS = (
+    "INPUT_DIM", "HIDDEN_DIM", "NUM_CLASSES",
+    "USE_DACP", "USE_ECDA", "USE_ENTROPY_IN_SCORE", "USE_CLASS_AWARE_MMD",
+    "WARMUP_EPOCHS", "PROGRESSIVE_TRAINING", "INITIAL_CONSISTENCY_WEIGHT", "FINAL_CONSISTENCY_WEIGHT",
+    "WEIGHT_RAMP_EPOCHS", "WEIGHT_CONSISTENCY", "ECDA_START_EPOCH", "WEIGHT_ECDA",
+    "LEARNING_RATE_SCHEDULER", "LEARNING_RATE", "EPOCHS",
+    "DACP_QUANTILE_START", "DACP_QUANTILE_END", "DACP_THRESHOLD_SMOOTHING_ALPHA", "DACP_SENSITIVITY_K",
+    "DACP_CALIBRATION_STRENGTH_LAMBDA", "FIXED_CONFIDENCE_THRESHOLD", "ECDA_CLASS_ATTENTION_LAMBDA",
+    "ECDA_COMPACTNESS_WEIGHT_GAMMA", "ECDA_REPULSION_WEIGHT_DELTA", "LABEL_SMOOTHING_FACTOR",
+    "USE_LABEL_SMOOTHING", "DROPOUT_RATE", "WEAK_NOISE_STD", "STRONG_NOISE_STD", "TEMPORAL_MASK_RATIO",
+    "GRADIENT_CLIPPING", "MAX_GRAD_NORM", "WEIGHT_DECAY", "EMA_MOMENTUM", "DACP_QUALITY_SMOOTHING_BETA",
+)
+
+
+def _view_values(view):
+    """The CONFIG_KEYS values of a ConfigView in one pass (a sentinel for missing ones), or None
+    for another view type (then nothing is cached)."""
+    if type(view) is not ConfigView:
+        return None
+    d = view.__dict__
+    ov = d.get("overrides") or {}
+    src = d.get("source")
+    dd = FLAVOR_DEFAULTS[d["flavor"]]
+    out = []
+    if src is None:
+        for k in CONFIG_KEYS:
+            out.append(ov[k] if k in ov else dd.get(k, _MISSING))
+    elif isinstance(src, dict):
+        for k in CONFIG_KEYS:
+            out.append(ov[k] if k in ov else (src[k] if k in src else dd.get(k, _MISSING)))
+    else:
+        for k in CONFIG_KEYS:
+            if k in ov:
+                out.append(ov[k])
+            else:
+                v = getattr(src, k, _MISSING)
+                out.append(v if v is not _MISSING else dd.get(k, _MISSING))
+    return (d["flavor"],) + tuple(out)
+
+
+class ConfigCache:
+    """dad_config_for with its step-independent part cached: the config of a (view contents,
+    geometry, epoch, lr, precision, RNG, world, splits) key is built once by dad_config_for, and
+    each step copies it and sets only the Adam step's two scalars and the RNG counter, with
+    dad_config_for's own expressions, so the result is byte-identical.  The key holds every value
+    the view gives dad_config_for (CONFIG_KEYS, read in one pass each call), so a changed config
+    value is a new key.  (dad_config_for reads ~40 view attributes and sets ~60 ctypes fields:
+    ~20 us of host time per step, a third of DADStep.step's.)"""
+
+    def __init__(self, max_entries=64):
+        self._d = {}
+        self._max = max_entries
+
+    def config(self, view, Bc, Tc, Bn, Tn, epoch, adam_step, lr=None, precision=_lib.PREC_FP32,
+               rng_mode=_lib.RNG_COUNTER, seed=0, counter=0, dp_world=1, splits=0):
+        vals = _view_values(view)
+        key = (vals, Bc, Tc, Bn, Tn, epoch, lr, int(precision), int(rng_mode), int(seed), int(dp_world), int(splits))
+        try:
+            hit = self._d.get(key) if vals is not None else None
+        except TypeError:          # an unhashable config value: no caching
+            vals = None
+        if vals is None:
+            return dad_config_for(view, Bc, Tc, Bn, Tn, epoch, adam_step, lr=lr, precision=precision,
+                                  rng_mode=rng_mode, seed=seed, counter=counter, dp_world=dp_world, splits=splits)
+        if hit is None:
+            base = dad_config_for(view, Bc, Tc, Bn, Tn, epoch, 1, lr=lr, precision=precision, rng_mode=rng_mode,
+                                  seed=seed, counter=0, dp_world=dp_world, splits=splits)
+            lr_eff = lr if lr is not None else view.lr_at(epoch)
+            if len(self._d) >= self._max:
+                self._d.clear()
+            hit = self._d[key] = (base, lr_eff)
+        base, lr_eff = hit
+        c = _lib.DadConfig.from_buffer_copy(base)
+        c.counter = int(counter) & (2 ** 64 - 1)
+        b1, b2 = 0.9, 0.999
+        c.lr_step_size = lr_eff / (1 - b1 ** adam_step)
+        c.bc2_sqrt = math.sqrt(1 - b2 ** adam_step)
+        return c

@@ -18,7 +18,7 @@ import ctypes
 import torch
 
 from . import _lib
-from .config import ConfigView, dad_config_for
+from .config import ConfigCache, ConfigView
 from .data import StoreFeats
 
 PRECISIONS = {"fp32": _lib.PREC_FP32, "bf16": _lib.PREC_BF16, "fp16": _lib.PREC_FP16}
@@ -121,6 +121,7 @@ class DADStep:
         self.global_step = 0
         self._ws = None
         self._ws_need = {}       # workspace bytes per layout key (_workspace)
+        self._cfg_cache = ConfigCache()   # dad_config_for's step-independent part (config.py)
         self._bufs = {}
         self._prepped_key = None       # identity of the batch the last step's tail launch prepared
         self.last_prepped = False
@@ -232,11 +233,12 @@ class DADStep:
 
     # ------------------------------------------------------------------------------- step
     def make_config(self, Bc, Tc, Bn, Tn, epoch, lr=None, adam_step=None, counter=None):
-        return dad_config_for(self.view, Bc, Tc, Bn, Tn, epoch,
-                              adam_step if adam_step is not None else self.adam_step + 1, lr=lr,
-                              precision=self.precision, rng_mode=self.rng_mode, seed=self.seed,
-                              counter=self.global_step if counter is None else counter,
-                              dp_world=self.comm.world if self.comm is not None else 1, splits=self.splits)
+        return self._cfg_cache.config(self.view, Bc, Tc, Bn, Tn, epoch,
+                                      adam_step if adam_step is not None else self.adam_step + 1, lr=lr,
+                                      precision=self.precision, rng_mode=self.rng_mode, seed=self.seed,
+                                      counter=self.global_step if counter is None else counter,
+                                      dp_world=self.comm.world if self.comm is not None else 1,
+                                      splits=self.splits)
 
     _PREP_CFG = ("B", "T", "Bn", "Tn", "precision", "rng_mode", "seed", "counter", "warmup", "mask_len",
                  "start_hi", "weak_std", "strong_std", "feat_p")

@@ -43,6 +43,56 @@ def test_config_is_read_at_call_time():
     assert p.ConfigView(emod).effective_switches()[0] is True
 
 
+@pytest.mark.parametrize("flavor", ["iemocap", "casia", "emodb"])
+def test_config_cache_keys_cover_every_read(flavor, monkeypatch):
+    """ConfigCache keys a config on the CONFIG_KEYS values: every attribute dad_config_for reads
+    from a view (over warm-up, ramp, ECDA start and late epochs, with and without an lr) is there."""
+    p = dadpkg.pkg()
+    C = p.config
+    seen = set()
+    orig = C.ConfigView.__getattr__
+
+    def rec(self, name):
+        seen.add(name)
+        return orig(self, name)
+    monkeypatch.setattr(C.ConfigView, "__getattr__", rec)
+    view = C.ConfigView(flavor=flavor)
+    for epoch in (0, 29, 30, 35, 59, 60, 499):
+        for lr in (None, 1e-3):
+            C.dad_config_for(view, 4, 20, 4, 20, epoch, 3, lr=lr)
+    assert seen and seen <= set(C.CONFIG_KEYS), sorted(seen - set(C.CONFIG_KEYS))
+
+
+def test_config_cache_is_byte_identical_and_follows_config_changes():
+    """DADStep.make_config's ConfigCache: the same bytes as dad_config_for for every Adam step,
+    counter, geometry, epoch and lr, and a changed config value (module source, overrides) is
+    a new key, read at call time as dad_config_for reads it."""
+    p = dadpkg.pkg()
+    C = p.config
+    mod = types.ModuleType("config")
+    mod.WEIGHT_ECDA = 0.3
+    view = C.ConfigView(mod)
+    cache = C.ConfigCache()
+    for args in [(64, 300, 64, 300, 60, None), (16, 40, 12, 50, 3, 1e-3), (16, 40, None, None, 1, None),
+                 (64, 300, 64, 300, 35, None)]:
+        Bc, Tc, Bn, Tn, epoch, lr = args
+        for adam_step, counter in ((1, 0), (7, 123), (1000, 2 ** 40 + 5)):
+            for prec in (0, 1, 2):
+                kw = dict(lr=lr, precision=prec, rng_mode=1, seed=9, counter=counter)
+                a = C.dad_config_for(view, Bc, Tc, Bn, Tn, epoch, adam_step, **kw)
+                b = cache.config(view, Bc, Tc, Bn, Tn, epoch, adam_step, **kw)
+                assert bytes(a) == bytes(b), (args, adam_step, counter, prec)
+    mod.WEIGHT_ECDA = 0.5
+    view.overrides["DROPOUT_RATE"] = 0.25
+    a = C.dad_config_for(view, 64, 300, 64, 300, 60, 9, counter=4)
+    b = cache.config(view, 64, 300, 64, 300, 60, 9, counter=4)
+    assert bytes(a) == bytes(b) and abs(b.w_ecda - 0.5) < 1e-7 and abs(b.p_drop - 0.25) < 1e-7
+    mod.LIST_VALUE = [1, 2]                         # unrelated attributes do not matter
+    mod.WEAK_NOISE_STD = np.array(0.02)             # an unhashable value: computed without the cache
+    a = C.dad_config_for(view, 64, 300, 64, 300, 60, 9, counter=4)
+    assert bytes(a) == bytes(cache.config(view, 64, 300, 64, 300, 60, 9, counter=4))
+
+
 def test_float32_scalars_follow_torch_semantics():
     p = dadpkg.pkg()
     c = p.dad_config_for(p.ConfigView(flavor="iemocap"), 64, 300, 64, 300, 60, 7)
