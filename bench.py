@@ -385,7 +385,8 @@ def run_mixed(args, model, dev, rank, world, dist, comm):
             return rows, utts
         run(args.warmup if k == 0 else 3, False)
         torch.cuda.synchronize()
-        timer = PKG._lib.KernelTimer(event_every(args.steps), args.steps + 1, kernels=TIMED_KERNELS)
+        timer = PKG._lib.KernelTimer(event_every(args.steps), args.steps // event_every(args.steps) + 1,
+                                     kernels=TIMED_KERNELS)
         if dist:
             dist.barrier()
         t0 = time.perf_counter()
@@ -872,7 +873,9 @@ def main():
                     e1.record()
                 torch.cuda.synchronize()
         if graphs is None:
-            timer = PKG._lib.KernelTimer(event_every(args.steps), args.steps + 1,
+            # one event set per recorded step only (each set is 8 events created up front: sized
+            # for every step, a 200-step region had created 1,608 events right before its clock)
+            timer = PKG._lib.KernelTimer(event_every(args.steps), args.steps // event_every(args.steps) + 1,
                                          kernels=timed_kernels(args.precision, not args.no_ahead))
 
         def timed(n):
