@@ -241,6 +241,38 @@ def _identity(batch):
     return batch
 
 
+def _fast_batches(dl):
+    """The batches one epoch of DataLoader(range(n), batch_size, shuffle, generator, drop_last)
+    yields, without its per-index Python iteration (≈0.5 us per sample, ≈30 us per batch of 64):
+    for the default samplers, the same draws in the same order -- RandomSampler's seed from the
+    global RNG (or its generator) and one randperm -- cut into batch_size chunks as BatchSampler
+    does.  None for any other sampler (the caller drains the DataLoader).  The iterator's own base
+    seed was drawn when the caller created it (iter(DataLoader)), as before."""
+    bs = dl.batch_sampler
+    if type(bs) is not torch.utils.data.BatchSampler or dl.num_workers != 0:
+        return None
+    smp = bs.sampler
+    n = len(dl.dataset)
+    if type(smp) is torch.utils.data.SequentialSampler:
+        order = np.arange(n, dtype=np.int64)
+    elif (type(smp) is torch.utils.data.RandomSampler and not smp.replacement and smp.num_samples == n
+          and smp._num_samples is None):
+        g = smp.generator
+        if g is None:
+            seed = int(torch.empty((), dtype=torch.int64).random_().item())
+            g = torch.Generator()
+            g.manual_seed(seed)
+        order = torch.randperm(n, generator=g).numpy().astype(np.int64)
+        # RandomSampler's trailing `randperm(n)[: num_samples % n]` runs when the epoch is drained
+        # (an empty slice, but a caller's generator advances)
+        torch.randperm(n, generator=g)
+    else:
+        return None
+    k = bs.batch_size
+    stop = (n // k) * k if bs.drop_last else n
+    return [order[i:i + k] for i in range(0, stop, k)]
+
+
 class _DeviceLoaderIter:
     def __init__(self, loader):
         self.loader = loader
@@ -255,7 +287,9 @@ class _DeviceLoaderIter:
         L = self.loader
         if self._batches is None:
             # the sampler draws its permutation at the first next(), as in the reference
-            self._batches = [np.asarray(b, dtype=np.int64) for b in self._it]
+            self._batches = _fast_batches(L._index_loader)
+            if self._batches is None:
+                self._batches = [np.asarray(b, dtype=np.int64) for b in self._it]
             flat = np.concatenate(self._batches) if self._batches else np.zeros(0, np.int64)
             # one upload per epoch, from pinned memory and asynchronous: a pageable copy would
             # wait for every step already queued on the stream (a pipeline drain per epoch)

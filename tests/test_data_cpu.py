@@ -158,6 +158,29 @@ def test_device_loader_batch_order_matches_torch_dataloader(shuffle, drop_last):
         assert call[2] == sizes[r].max()                     # padded length = the batch max size
 
 
+@pytest.mark.parametrize("with_generator", [False, True])
+def test_device_loader_epochs_and_rng_state_match_torch_dataloader(with_generator):
+    """Two epochs of a shuffled DeviceLoader (its batch order drawn without the DataLoader's
+    per-index iteration) against torch's DataLoader: the same batches in both epochs and the same
+    global (and generator) RNG state afterwards."""
+    sizes = np.full(50, 4)
+    st = _HostStore(sizes, labels=np.zeros(50))
+    gen = (lambda: torch.Generator().manual_seed(9)) if with_generator else (lambda: None)
+    L = PKG.data.DeviceLoader(st, batch_size=7, shuffle=True, generator=gen())
+    torch.manual_seed(21)
+    got = [list(L), list(L)]
+    after = torch.rand(3)
+    ref_loader = torch.utils.data.DataLoader(range(50), batch_size=7, shuffle=True, generator=gen(),
+                                             collate_fn=lambda b: b)
+    torch.manual_seed(21)
+    ref = [[np.asarray(b) for b in ref_loader], [np.asarray(b) for b in ref_loader]]
+    assert torch.equal(after, torch.rand(3))
+    for ge, re in zip(got, ref):
+        assert len(ge) == len(re)
+        for g, r in zip(ge, re):
+            np.testing.assert_array_equal(g, r)
+
+
 def test_device_loader_draws_rng_like_the_reference_loop():
     """iter(a), iter(b), next(a), next(b) -- the reference's epoch start (I/train.py:479-483):
     each loader must take its sampler seed at its first next(), not at iter()."""
