@@ -206,6 +206,10 @@ int dad_timing_start(int every, int max_steps) {
   // cost the stream ~3 us per event and slowed the kernel after it); dad_timing_stop reads them after
   // a device synchronize
   for (auto& e : g_tk.ev) DAD_TRY(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
+  // first use outside the timed region: a HIP event's first record sets it up (host time the
+  // first recorded steps would otherwise pay)
+  for (auto& e : g_tk.ev) DAD_TRY(hipEventRecord(e, nullptr));
+  DAD_TRY(hipDeviceSynchronize());
   g_tk.every = every;
   g_tk.nset = max_steps;
   return DAD_OK;
