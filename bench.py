@@ -114,6 +114,13 @@ def pmc_counters(kernel):
     return out
 
 
+def pmc_summary_kernels():
+    try:
+        return set(json.load(open(PMC_SUMMARY)).get("kernels", {}))
+    except Exception:
+        return None
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -524,8 +531,10 @@ def tail_kernel(B, Bn, class_aware=True):
     return "dad_tail_ecda_w" if w else "dad_tail_ecda"
 
 
-def _roof(kernel, ms, bytes_, flops, peak_tf, bound=None, note=None):
-    """One kernel's roofline block: algorithmic bytes (or FLOPs) per launch / mean launch time."""
+def _roof(kernel, ms, bytes_, flops, peak_tf, bound=None, note=None, bytes_moved=None):
+    """One kernel's roofline block: algorithmic bytes (or FLOPs) per launch / mean launch time.
+    bytes_moved: what the launch's design reads and writes when that is more than the algorithmic
+    bytes (reported beside them, never in `frac`)."""
     ridge = peak_tf * 1e12 / (HBM_PEAK_GBS * 1e9)
     intensity = flops / bytes_ if bytes_ else float("inf")
     bound = bound or ("mfma" if intensity > ridge else "hbm")
@@ -540,9 +549,26 @@ def _roof(kernel, ms, bytes_, flops, peak_tf, bound=None, note=None):
          "arithmetic_intensity_flop_per_byte": intensity, "ridge_flop_per_byte": ridge,
          "traffic_source": None if pmc is None else pmc["source"],
          "traffic_stale": None if pmc is None else pmc["stale"]}
+    if bytes_moved is not None:
+        r["bytes_moved_per_launch"] = bytes_moved
+        r["bytes_moved_rate_gbs"] = bytes_moved / (ms * 1e-3) / 1e9
     if note:
         r["note"] = note
     return r
+
+
+def step_traffic(names):
+    """PMC HBM bytes per step summed over the step's kernels (one launch each), from the committed
+    summary: the whole step's fabric traffic against the survey's compulsory bytes."""
+    tot, parts, stale = 0.0, {}, False
+    for n in names:
+        pk = pmc_counters(n)
+        if not pk or "hbm_bytes_per_launch" not in pk:
+            return None
+        parts[n] = pk["hbm_bytes_per_launch"]
+        tot += pk["hbm_bytes_per_launch"]
+        stale = stale or bool(pk["stale"])
+    return {"bytes": tot, "per_kernel": parts, "stale": stale}
 
 
 def rooflines(ktimes, rows_c, rows_n, ms_step, precision, tail_name="dad_tail_ecda_w", prepped_ahead=False):
@@ -582,13 +608,22 @@ def rooflines(ktimes, rows_c, rows_n, ms_step, precision, tail_name="dad_tail_ec
     if h16 and prepped_ahead and "tail" in ktimes and ktimes["tail"][0] > enc:
         # the dominant launch is the tail launch carrying the next batch's row preparation: an
         # HBM stream (the tail and ECDA blocks on 5 CUs run inside it)
-        rf = _roof(tail_name, ktimes["tail"][0], src_bytes + prep_bytes, 0.0, peak_tf, bound="hbm",
+        rf = _roof(tail_name, ktimes["tail"][0], src_bytes, 0.0, peak_tf, bound="hbm",
+                   bytes_moved=src_bytes + prep_bytes,
                    note="tail + ECDA blocks and the next batch's row preparation (dad_prep) in one launch; "
-                        "bytes = the next batch's fp32 rows read + its 16-bit prepared rows written")
+                        "algorithmic bytes (SURVEY.md §8(d)) = one step's fp32 features read once; bytes_moved "
+                        "adds the 16-bit prepared rows the design writes")
         rf["timed_launches"] = ktimes["tail"][1]
     t_roof = max(step_flops / (peak_tf * 1e12), src_bytes / (HBM_PEAK_GBS * 1e9))
     srf = {"t_roof_us": t_roof * 1e6, "t_step_us": ms_step * 1e3, "frac": t_roof / (ms_step * 1e-3),
            "flops_per_step": step_flops, "bytes_per_step": src_bytes, "mfma_peak_tflops": peak_tf}
+    tr = step_traffic([names[k] for k in ("encode", "pool", "wgrad", "reduce", "optim")] +
+                      ([tail_name] if tail_name in (pmc_summary_kernels() or ()) else []))
+    if tr is not None:
+        srf["step_traffic_bytes"] = tr["bytes"]
+        srf["step_traffic_over_compulsory"] = tr["bytes"] / src_bytes
+        srf["step_traffic_per_kernel"] = tr["per_kernel"]
+        srf["step_traffic_stale"] = tr["stale"]
     # MFMA utilisation of the encoder linears (north_star: >= 40 %): algorithmic FLOPs / time / peak
     enc_tf = enc_flops / (enc * 1e-3) / 1e12
     wg_tf = wg_flops / (wg * 1e-3) / 1e12

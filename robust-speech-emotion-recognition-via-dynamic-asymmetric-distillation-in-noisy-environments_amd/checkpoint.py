@@ -14,6 +14,8 @@ optimizer and one written by the reference loads here.  The DACP state (ema_thre
 class_quality_scores, epoch statistics, anchors) rides along under 'dad_state'; the reference
 does not save it, and a checkpoint without it leaves the step's DACP state untouched.
 """
+import warnings
+
 import numpy as np
 import torch
 
@@ -149,5 +151,15 @@ def train_epoch(step, clean_loader, noisy_loader, epoch, lr=None):
         step.epoch_end()
     if tot is None:
         return {}
-    vals = (tot / n).cpu().tolist()
-    return dict(zip(sorted(losses), vals))
+    # the FP16 range flag (dad.h DAD_T_RANGE) rides in the epoch's one device->host read: an
+    # encoder operand beyond +-65504 makes that step's update non-finite, which the reference's
+    # fp32 path cannot do; it is reported (and cleared) instead of silently training on
+    flag = step.range_flag(clear=True).float().reshape(1)
+    vals = torch.cat([tot / n, flag]).cpu().tolist()
+    out = dict(zip(sorted(losses), vals[:-1]))
+    if vals[-1] != 0.0:
+        warnings.warn("train_epoch(epoch=%d): non-finite embeddings or logits in this epoch (fp16 operand "
+                      "range exceeded or non-finite features); the parameters are no longer finite" % epoch,
+                      RuntimeWarning)
+    out["range_flag"] = int(vals[-1] != 0.0)
+    return out

@@ -13,18 +13,25 @@
 // Shape of the work: out[rows][256] = x[rows][768] . W1^T with tens of thousands of rows and
 // W1 only 384 KB in 16 bits.  So W1 is STATIONARY: a persistent workgroup holds all 256 hidden
 // units of ONE network's W1 in its register file (each of 8 waves 32 hidden units x 768 k, 192
-// VGPRs, read in place as MFMA B operands) and streams 16-row sub-slabs through LDS:
+// VGPRs, read in place as MFMA B operands) and streams 32-row jobs through LDS:
 //
-//   HBM 16-bit rows --LDS-DMA (3 x 1 KB per wave, straight into the XOR-swizzled tile: lane l of
-//   a piece loads the source chunk that lands at its slot)--> one of 3 job stages (two 16-row
-//   tiles each) --ds_read_b128 A fragments (conflict-free)--> 96 v_mfma_f32_16x16x32_{f16,bf16}
-//   per wave per 32-row job
-//   --bias, ReLU, valid mask, row sums, ballots--> slab partials + ReLU' bits
+//   HBM 16-bit rows --LDS-DMA (6 x 1 KB per wave, straight into the XOR-swizzled tiles: lane l
+//   of a piece loads the source chunk that lands at its slot; per-lane offsets from an LDS
+//   table)--> one of 3 job stages (two 16-row tiles each) --ds_read_b128 A fragments
+//   (conflict-free, two k-steps ahead)--> 96 v_mfma_f32_16x16x32_{f16,bf16} per wave per job,
+//   accumulators starting at the bias --ReLU, valid mask, row sums, ReLU' words by lane
+//   swaps--> slab partials + ReLU' bits
+//
+// PING-PONG schedule (wp_loop_pp): the two waves sharing a SIMD alternate between an MFMA phase
+// (the SIMD's matrix pipe to themselves, s_setprio) and an overhead phase (the epilogue of the job
+// they just multiplied and the LDS-DMA issue two jobs ahead), one workgroup barrier per phase.
+// Round 4's loop (every wave: barrier, DMA issue, MFMAs, epilogue, per job) left the matrix pipe
+// idle during each wave's overhead: 35.3 -> 28.2 us per launch (A/B on one box, B = 64, T = 300).
 //
 // Roles are per workgroup: TEACHER workgroups (teacher W1) run the weak slabs, STUDENT workgroups
 // (student W1) the clean slabs and then the strong slabs, contiguous ranges balanced by live
-// sub-slabs (dad_wp_job_range; host: wp_split in dad_abi.hip).  Two jobs are in flight ahead of
-// the one being multiplied (96 KB per CU), one barrier per job.
+// sub-slabs (dad_wp_job_range; host: wp_split in dad_abi.hip); a job whose second 16 rows hold no
+// frame multiplies only the first.
 #include <type_traits>
 
 #include "dad_common.h"
@@ -32,8 +39,8 @@
 #include "dad_probe.h"
 
 // per-workgroup stamps of the stamps build (dad_probe.h): [start, after the valid-bit prologue,
-// end (100 MHz wall clock), role<<16 | sub-slabs, then wave-0 cycles summed over the loop in: DMA
-// wait, barrier, DMA issue + valid mask, first phase, second phase]
+// end (100 MHz wall clock), role<<16 | sub-slabs, then wave-0 cycles summed over the loop in: MFMA
+// phase, its end (vmcnt wait + barrier), epilogue + DMA issue, the overhead phase's barrier]
 DAD_PROBE_BUFFER(ws_stamps, 4096 * 10)
 #define WS_CLK() DAD_PROBE_CLK()
 #define WS_STAMP(k, v) \
@@ -151,36 +158,6 @@ __device__ __forceinline__ void mfma1(f32x4& acc, const bf16x8& xa, const bf16x8
 }
 #undef DAD_WS_MFMA
 
-// A fragment of k-step KS: rows lane&15, k = 32KS + 8(lane>>4) .. +7.  The XOR swizzle only
-// touches the low 4 bits of the chunk index, so chunk (4KS + g) ^ row = 16(KS>>2) +
-// ((4(KS&3) + g) ^ row): four per-lane offsets aoff[KS&3] plus an immediate 256(KS>>2).
-template <int KS>
-__device__ __forceinline__ bf16x8 afrag(const char* tile, const int (&aoff)[4]) {
-  return *reinterpret_cast<const bf16x8*>(tile + aoff[KS & 3] + 256 * (KS >> 2));
-}
-
-// acc[t] = x_tile(16 rows) . W1[hw + 16t .. +15]^T over K = 768.  The A fragment of k-step
-// KS+1 is read while the MFMAs of k-step KS issue.
-template <class S, int KS, bool F16>
-__device__ __forceinline__ void ws_mfma_from(const char* tile, const int (&aoff)[4], const bf16x8 (&wf)[S::NT][kKS],
-                                             f32x4 (&acc)[S::NT], bf16x8 x0) {
-  if constexpr (KS < kKS) {
-    bf16x8 xn;
-    if constexpr (KS + 1 < kKS) xn = afrag<KS + 1>(tile, aoff);
-#pragma unroll
-    for (int t = 0; t < S::NT; ++t) mfma1<false, KS == 0, F16>(acc[t], x0, wf[t][KS]);
-    ws_mfma_from<S, KS + 1, F16>(tile, aoff, wf, acc, xn);
-  }
-}
-template <class S, bool F16>
-__device__ __forceinline__ void ws_mfma(const char* tile, const int (&aoff)[4], const bf16x8 (&wf)[S::NT][kKS],
-                                        f32x4 (&acc)[S::NT]) {
-  ws_mfma_from<S, 0, F16>(tile, aoff, wf, acc, afrag<0>(tile, aoff));
-  // MFMA D -> VALU readers of the epilogue (hipcc pads nothing after an asm MFMA)
-  if constexpr (S::NT == 4) asm volatile("s_nop 7\n\ts_nop 7" ::"v"(acc[0]), "v"(acc[1]), "v"(acc[2]), "v"(acc[3]));
-  else asm volatile("s_nop 7\n\ts_nop 7" ::"v"(acc[0]), "v"(acc[1]));
-}
-
 // sum over the 4 row groups (lane >> 4) of a 16x16 C tile column: v_permlane32_swap and
 // v_permlane16_swap (gfx950) with both operands = x give [x_lo, x_lo] + [x_hi, x_hi]
 __device__ __forceinline__ float rowgroup_sum(float x) {
@@ -200,132 +177,179 @@ __device__ __forceinline__ uint32_t rowgroup_or(uint32_t x) {
   return b[0] | b[1];
 }
 
-// bias + ReLU + valid mask of one sub-slab.  Per-lane partial sums/counts (4 rows of the C
-// tile) accumulate over the job's two sub-slabs and are reduced across the 4 row groups only
-// at the job's end (HALF 1).  Student: the ReLU'-and-valid row mask of each hidden unit (bit
-// r = row r of the 32-row slab): a lane's 4 rows form a nibble, the 4 row groups are OR-ed
-// by lane swaps, the two halves meet in bw and one 32-lane store writes the job's words.
-// Stores: student 3 at HALF 1 (row masks, sums, counts); teacher 1 at HALF 1 (sums).
-template <class S, bool TEACHER, int HALF>
-__device__ __forceinline__ void ws_epilogue(const Ctx& C, const Job& J, int w, int lane, uint32_t vmask,
-                                            const float (&bh)[S::NT], const f32x4 (&acc)[S::NT], float (&ssum)[S::NT],
-                                            float (&scnt)[S::NT], uint32_t (&bw)[S::NT]) {
-  const int g = lane >> 4;
-#pragma unroll
-  for (int t = 0; t < S::NT; ++t) {
-    float s = 0.0f, n = 0.0f;
-    uint32_t nib = 0;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const bool v = (vmask >> (4 * g + r)) & 1u;     // C/D layout: row = 4(lane>>4) + r, col = lane&15
-      const float pre = acc[t][r] + bh[t];
-      const bool act = v && pre > 0.0f;
-      s += act ? pre : 0.0f;
-      if constexpr (!TEACHER) {
-        n += act ? 1.0f : 0.0f;
-        nib |= act ? (1u << r) : 0u;
-      }
-    }
-    ssum[t] = HALF ? ssum[t] + s : s;
-    if constexpr (!TEACHER) {
-      scnt[t] = HALF ? scnt[t] + n : n;
-      const uint32_t m16 = rowgroup_or(nib << (4 * g));   // rows 0..15 of the sub-slab, h = hw + 16t + col
-      bw[t] = HALF ? bw[t] | (m16 << 16) : m16;
-    }
-  }
-  const int hw = S::HW * w;
-  if constexpr (HALF == 1) {
-    const int t = lane >> 4;                           // h = hw + lane (lanes < HW)
-    float sv = 0.0f, cv = 0.0f;
-    uint32_t mv = 0;
-#pragma unroll
-    for (int k = 0; k < S::NT; ++k) {
-      const float a = rowgroup_sum(ssum[k]);
-      sv = t == k ? a : sv;
-      if constexpr (!TEACHER) {
-        const float c = rowgroup_sum(scnt[k]);
-        cv = t == k ? c : cv;
-        mv = t == k ? bw[k] : mv;
-      }
-    }
-    if (lane < S::HW) {
-      C.part_sum[(size_t)J.sum_slab * DAD_H + hw + lane] = sv;
-      if constexpr (!TEACHER) {
-        C.part_cnt[(size_t)J.cnt_slab * DAD_H + hw + lane] = cv;
-        C.bits[(size_t)J.cnt_slab * DAD_H + hw + lane] = mv;
-      }
-    }
-  }
-}
-
-
 }  // namespace
+
+#ifndef WP_PRIO
+#define WP_PRIO 2
+#endif
 
 namespace {
 
 constexpr int kJS = 3;                                   // 48-KB job stages (two 16-row tiles each)
 constexpr int kOffPVB = kJS * 2 * kTile;                 // valid bits u32[DAD_ENC_WS_MAXJ]
-constexpr int kLdsP = kOffPVB + 4 * DAD_ENC_WS_MAXJ;
+constexpr int kOffSimd = kOffPVB + 4 * DAD_ENC_WS_MAXJ;       // SIMD id per wave
+constexpr int kOffDMA = kOffSimd + 4 * 8;                      // per-lane DMA source offsets (12 KB)
+constexpr int kLdsP = kOffDMA + 8 * 6 * 64 * 4;
 static_assert(kLdsP <= 160 * 1024, "LDS budget");
-
-// one 1-KB LDS-DMA piece: 16 B per lane from `src` to lds_dst + 16 * lane (see dad_glds16x3)
-__device__ __forceinline__ void dad_glds16(const void* src, uint32_t lds_dst) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep) : "v"(src), "s"(lds_dst) : "memory");
-}
 
 }  // namespace
 
-// One 32-row job per iteration: its two 16-row sub-slab tiles are one 48-KB stage of three (two
-// jobs in flight ahead of the one multiplied), one barrier, one wait and one valid-mask read per
-// job, and every k-step issues 4 independent MFMAs (2 row tiles x 2 hidden-unit tiles) per A pair.
-// (The 16-row iteration, one barrier and one epilogue per sub-slab, measured 42.5 against 37.6-38.6
-// us per launch by events, step 118.4-119.2 against 114.6-115.0 us.)
-template <bool F16>
-__device__ __forceinline__ void wp_mfma2(const char* tile, const int (&aoff)[4], const bf16x8 (&wf)[2][kKS],
-                                         f32x4 (&acc)[2][2], uint32_t vm) {
-  const bool h0 = (vm & 0xffffu) != 0, h1 = (vm >> 16) != 0;
-  bf16x8 x0 = afrag<0>(tile, aoff), x1 = afrag<0>(tile + kTile, aoff);
-#pragma unroll
-  for (int ks = 0; ks < kKS; ++ks) {
-    bf16x8 n0, n1;
-    if (ks + 1 < kKS) {
-      n0 = *reinterpret_cast<const bf16x8*>(tile + aoff[(ks + 1) & 3] + 256 * ((ks + 1) >> 2));
-      n1 = *reinterpret_cast<const bf16x8*>(tile + kTile + aoff[(ks + 1) & 3] + 256 * ((ks + 1) >> 2));
-    }
+// ---- Ping-pong schedule -----------------------------------------------------------------------
+// The two waves that share a SIMD are in different groups (grp, from the hardware SIMD id).  Time
+// is cut into PHASES separated by one workgroup barrier each; a wave of group g multiplies job j in
+// phase 2j + g (the MFMA phase: 96 MFMAs, the SIMD's matrix pipe to itself) and runs job j's
+// epilogue and the LDS-DMA issue of job j + 2 in phase 2j + g + 1 (the overhead phase), while its
+// partner multiplies.  So each SIMD's matrix pipe alternates between its two waves and the
+// per-job overhead (epilogue, DMA issue, valid mask) hides under the partner's MFMAs instead of
+// stalling both.  Every wave executes 2 nj + 1 barriers (group 1 idles in phase 0, group 0 in
+// phase 2 nj).
+//
+// Stages: job J lives in stage J % 3.  Its pieces are issued by group 0 in phase 2J - 3 and by
+// group 1 in phase 2J - 2; the first reader is group 0 in phase 2J.  Every wave waits vmcnt(0) at
+// the end of its MFMA phase (it issued no memory op in it), i.e. group 0 at the end of phase
+// 2J - 2 and group 1 at the end of 2J - 1, so all pieces of J have landed before the barrier that
+// opens phase 2J.  Stage J % 3 last held job J - 3, read in phases 2J - 6 and 2J - 5, before either
+// group starts refilling it.
+// The fragment reads are inline asm with explicit lgkmcnt waits: left to the compiler, the reads
+// of k-step ks sank to right before its MFMAs (register pressure), exposing the LDS latency on
+// every k-step.  A wait names the fragments it guards as in/out operands, so no MFMA that reads
+// them can be scheduled above it.  addr[m] = this tile's LDS byte address + aoff[m].
+template <int OFF>
+__device__ __forceinline__ void lds_rd128(bf16x8& x, uint32_t addr) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(x) : "v"(addr), "i"(OFF));
+}
+template <int N>
+__device__ __forceinline__ void lgkm_wait2(bf16x8& x0, bf16x8& x1) {
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(x0), "+v"(x1) : "i"(N));
+}
+template <int KS, bool TWO>
+__device__ __forceinline__ void pp_read(bf16x8 (&xa)[3][2], const uint32_t (&addr)[4]) {
+  if constexpr (KS < kKS) {
+    lds_rd128<256 * (KS >> 2)>(xa[KS % 3][0], addr[KS & 3]);
+    if constexpr (TWO) lds_rd128<kTile + 256 * (KS >> 2)>(xa[KS % 3][1], addr[KS & 3]);
+  }
+}
+template <int KS, bool F16, bool TWO>
+__device__ __forceinline__ void pp_kstep(bf16x8 (&xa)[3][2], const uint32_t (&addr)[4], const bf16x8 (&wf)[2][kKS],
+                                         f32x4 (&acc)[2][2]) {
+  if constexpr (KS < kKS) {
+    pp_read<KS + 2, TWO>(xa, addr);
+    // reads younger than k-step KS's: those of KS + 1 and KS + 2 that exist
+    constexpr int younger = (KS + 1 < kKS ? 1 : 0) + (KS + 2 < kKS ? 1 : 0);
+    lgkm_wait2<younger * (TWO ? 2 : 1)>(xa[KS % 3][0], xa[KS % 3][1]);
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      if (ks == 0) {
-        mfma1<false, true, F16>(acc[0][t], x0, wf[t][0]);
-        mfma1<false, true, F16>(acc[1][t], x1, wf[t][0]);
-      } else {
-        mfma1<false, false, F16>(acc[0][t], x0, wf[t][ks]);
-        mfma1<false, false, F16>(acc[1][t], x1, wf[t][ks]);
-      }
+      mfma1<false, false, F16>(acc[0][t], xa[KS % 3][0], wf[t][KS]);
+      if constexpr (TWO) mfma1<false, false, F16>(acc[1][t], xa[KS % 3][1], wf[t][KS]);
     }
-    x0 = n0;
-    x1 = n1;
+    pp_kstep<KS + 1, F16, TWO>(xa, addr, wf, acc);
   }
-  asm volatile("s_nop 7\n\ts_nop 7" ::"v"(acc[0][0]), "v"(acc[0][1]), "v"(acc[1][0]), "v"(acc[1][1]));
-  if (!h0) { acc[0][0] = f32x4{}; acc[0][1] = f32x4{}; }
-  if (!h1) { acc[1][0] = f32x4{}; acc[1][1] = f32x4{}; }
+}
+// acc = bias + x . W1^T: the accumulators start at the bias (the epilogue adds nothing)
+template <bool F16, bool TWO>
+__device__ __forceinline__ void pp_mfma(const uint32_t (&addr)[4], const bf16x8 (&wf)[2][kKS], const float (&bh)[2],
+                                        f32x4 (&acc)[2][2]) {
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    acc[0][t] = f32x4{bh[t], bh[t], bh[t], bh[t]};
+    if constexpr (TWO) acc[1][t] = acc[0][t];
+  }
+  // A fragments two k-steps ahead of the MFMAs that use them (one MFMA wave per SIMD in this
+  // phase: the fragment reads' latency is not covered by a partner wave)
+  bf16x8 xa[3][2];
+  if constexpr (!TWO) xa[0][1] = xa[1][1] = xa[2][1] = bf16x8{};
+  pp_read<0, TWO>(xa, addr);
+  pp_read<1, TWO>(xa, addr);
+  pp_kstep<0, F16, TWO>(xa, addr, wf, acc);
+  // MFMA D -> VALU readers of the epilogue (hipcc pads nothing after an asm MFMA)
+  if constexpr (TWO) {
+    asm volatile("s_nop 7\n\ts_nop 7" ::"v"(acc[0][0]), "v"(acc[0][1]), "v"(acc[1][0]), "v"(acc[1][1]));
+  } else {
+    asm volatile("s_nop 7\n\ts_nop 7" ::"v"(acc[0][0]), "v"(acc[0][1]));
+    acc[1][0] = f32x4{};                           // rows 16..31 hold no frame (valid bits 0)
+    acc[1][1] = f32x4{};
+  }
+}
+
+// Epilogue of one 32-row job on bias-included accumulators: acc[half][t][r] is row 16 half + 4 g + r
+// (g = lane >> 4) of hidden unit hw + 16 t + (lane & 15).  Per element (integer ops on the float's
+// bits): m = max(bits, 0) = ReLU(pre), the ReLU' bit = min(m, 1) (pre > 0), the row sum += m; a lane's 8 bits of a hidden
+// unit sit at 16 half + r, moved to their rows by << 4g and OR-ed over the row groups; the
+// active-row count is the popcount of that 32-row word.  FULL: every row of the slab is a frame;
+// otherwise the valid bits gate each element.  Stores: lanes 16 t + col -> h = hw + lane.
+template <bool TEACHER, bool FULL>
+__device__ __forceinline__ void pp_epilogue(const Ctx& C, const Job& J, int hw, int lane, uint32_t vm,
+                                            const f32x4 (&acc)[2][2]) {
+  const int g = lane >> 4;
+  const uint32_t vg = vm >> (4 * g);
+  float sv[2];
+  uint32_t mv[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    float s = 0.0f;
+    uint32_t word = 0;
+#pragma unroll
+    for (int half = 0; half < 2; ++half)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        // ReLU on the bits: a float's int image is > 0 exactly when the float is > 0 (or a NaN of
+        // sign 0, which then reaches the sum and the range flag); no canonicalising v_max pairs
+        int mi = max(__float_as_int(acc[half][t][r]), 0);
+        if constexpr (!FULL) mi &= __builtin_amdgcn_sbfe((int)vg, 16 * half + r, 1);   // valid: all ones
+        s += __int_as_float(mi);
+        if constexpr (!TEACHER) word |= min((uint32_t)mi, 1u) << (16 * half + r);
+      }
+    sv[t] = rowgroup_sum(s);
+    if constexpr (!TEACHER) mv[t] = rowgroup_or(word << (4 * g));
+  }
+  if (lane < 32) {
+    // wave-uniform row bases + the lane (no per-lane 64-bit addresses held across the loop)
+    const int ln = opaque(lane);
+    const bool t1 = ln >= 16;
+    (C.part_sum + (size_t)J.sum_slab * DAD_H + hw)[ln] = t1 ? sv[1] : sv[0];
+    if constexpr (!TEACHER) {
+      const uint32_t m = t1 ? mv[1] : mv[0];
+      (C.part_cnt + (size_t)J.cnt_slab * DAD_H + hw)[ln] = (float)__popc(m);
+      (C.bits + (size_t)J.cnt_slab * DAD_H + hw)[ln] = m;
+    }
+  }
+}
+
+// six 1-KB LDS-DMA pieces: per lane, source base + off[i], off[i] read from the wave's LDS table
+// ([i][lane] u32 at tab = the lane's entry of piece 0) in the same asm block (the compiler would
+// otherwise forward the table's stores into six registers held across the loop); LDS destination
+// dst + 1024 i (dst: the wave's first piece in the stage); M0 saved and restored around them
+__device__ __forceinline__ void dad_glds16x6(const char* base, uint32_t tab, uint32_t dst) {
+  uint32_t keep, o0, o1, o2, o3, o4, o5;
+  asm volatile(
+      "ds_read_b32 %1, %9\n\t"
+      "ds_read_b32 %2, %9 offset:256\n\t"
+      "ds_read_b32 %3, %9 offset:512\n\t"
+      "ds_read_b32 %4, %9 offset:768\n\t"
+      "ds_read_b32 %5, %9 offset:1024\n\t"
+      "ds_read_b32 %6, %9 offset:1280\n\t"
+      "s_mov_b32 %0, m0\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "s_mov_b32 m0, %8\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %7\n\t"
+      "s_add_u32 m0, %8, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %7\n\t"
+      "s_add_u32 m0, %8, 0x800\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %3, %7\n\t"
+      "s_add_u32 m0, %8, 0xc00\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %4, %7\n\t"
+      "s_add_u32 m0, %8, 0x1000\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %5, %7\n\t"
+      "s_add_u32 m0, %8, 0x1400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %6, %7\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep), "=&v"(o0), "=&v"(o1), "=&v"(o2), "=&v"(o3), "=&v"(o4), "=&v"(o5)
+      : "s"(base), "s"(dst), "v"(tab)
+      : "memory", "scc");
 }
 
 template <bool TEACHER, bool F16>
-__device__ __forceinline__ void wp_loop(const Ctx& C, const JobMap jm, const int nj, const int w, const int lane,
-                                          char* smem, const uint32_t sbase, const bf16x8* W, const float* bias,
-                                          const uint32_t* vb, const DadEncodeArgs& a) {
+__device__ __forceinline__ void wp_loop_pp(const Ctx& C, const JobMap jm, const int nj, const int w, const int lane,
+                                           char* smem, const uint32_t sbase, const bf16x8* W, const float* bias,
+                                           const uint32_t* vb, const DadEncodeArgs& a, const int grp) {
   using S = Shape<8>;
   constexpr int NP = 6;                  // 1-KB DMA pieces per wave per job (48 per job)
-  constexpr int E = TEACHER ? 1 : 3;     // epilogue stores per job
   bf16x8 wf[S::NT][kKS];
   float bh[S::NT];
-  float ssum[S::NT], scnt[S::NT];
-  uint32_t bw[S::NT];
   const int hw = S::HW * w;
 #pragma unroll
   for (int t = 0; t < S::NT; ++t)
@@ -333,64 +357,75 @@ __device__ __forceinline__ void wp_loop(const Ctx& C, const JobMap jm, const int
     for (int ks = 0; ks < kKS; ++ks) wf[t][ks] = W[(size_t)(((hw >> 4) + t) * kKS + ks) * 64 + lane];
 #pragma unroll
   for (int t = 0; t < S::NT; ++t) bh[t] = bias[hw + 16 * t + (lane & 15)];
-  // pieces p = 6w + i of a job stage: tile p / 24 (rows 16 (p/24) ..), 1-KB piece p % 24 of it
-  int prow[NP], pcol[NP];
+  // Per-lane source offsets of the wave's pieces relative to the slab's first row: piece p = 6w + i
+  // of a stage lands at LDS byte 1024 (p % 24) + 16 lane of tile p / 24, i.e. row r, slot k of the
+  // XOR-swizzled tile, and loads source chunk k ^ r of row 16 (p / 24) + r.  Job-independent: kept
+  // in LDS ([w][i][lane] u32) and read by dad_glds16x6.  Rows past the utterance's
+  // end read the next rows of the prepared set (or the workspace after it): finite or not, they are
+  // masked by the valid bits in the epilogue, and a row's output depends on that row only.
+  uint32_t* dtab = reinterpret_cast<uint32_t*>(smem + kOffDMA) + w * (NP * 64);
 #pragma unroll
   for (int i = 0; i < NP; ++i) {
     const int p = NP * w + i;
     const int o = 1024 * (p % 24) + 16 * lane;
     const int r = o / kTileRow;
-    prow[i] = 16 * (p / 24) + r;
-    pcol[i] = 16 * (((o - kTileRow * r) >> 4) ^ (r & 15));
+    const int pc = 16 * (((o - kTileRow * r) >> 4) ^ (r & 15));
+    dtab[i * 64 + lane] = (uint32_t)((16 * (p / 24) + r) * kTileRow + pc);
   }
   auto dma = [&](int j, int s) {
-    const Job J = job_of(C, TEACHER, jm(min(j, nj - 1)));
-    const char* base = reinterpret_cast<const char*>(J.kind == KIND_CLEAN ? a.x16c : (J.kind == KIND_STRONG ? a.x16s : a.x16w));
-    const uint32_t dst = sbase + (uint32_t)(s * 2 * kTile) + 1024u * NP * (uint32_t)w;
-#pragma unroll
-    for (int i = 0; i < NP; ++i) {
-      const int t = min(J.c * DAD_SLAB + prow[i], J.T - 1);
-      dad_glds16(base + (size_t)(J.row0 + t) * (DAD_D * 2) + pcol[i], dst + 1024u * (uint32_t)i);
-    }
+    const Job J = job_of(C, TEACHER, jm(j));
+    const char* base = reinterpret_cast<const char*>(J.kind == KIND_CLEAN ? a.x16c : (J.kind == KIND_STRONG ? a.x16s : a.x16w)) +
+                       (size_t)(J.row0 + J.c * DAD_SLAB) * (DAD_D * 2);
+    dad_glds16x6(base, sbase + (uint32_t)(kOffDMA + 4 * (w * NP * 64) + 4 * opaque(lane)),
+                 sbase + (uint32_t)(s * 2 * kTile) + 1024u * NP * (uint32_t)w);
   };
-  int aoff[4];
-  {
-    const int ln = opaque(lane);
-#pragma unroll
-    for (int m = 0; m < 4; ++m) aoff[m] = (ln & 15) * kTileRow + 16 * ((4 * m + (ln >> 4)) ^ (ln & 15));
-  }
-  unsigned long long ph[5] = {0, 0, 0, 0, 0};
-  int s_cur = 0;
+  unsigned long long ph[4] = {0, 0, 0, 0};
   dma(0, 0);
-  dma(1, 1);
+  if (nj > 1) dma(1, 1);
+  wait_vm<0>();
+  lds_barrier();
+  if (grp) lds_barrier();                            // group 1: phase 0 idle
+  int s_cur = 0;
   for (int j = 0; j < nj; ++j) {
+    // MFMA phase of job j
     const unsigned long long c0 = WS_CLK();
-    // DMA(j) landed once at most these younger ops remain: DMA(j+1) and the epilogue stores of
-    // jobs max(0, j-2) .. j-1
-    const int ne = min(j, 2);
-    if (ne == 0) wait_vm<NP>();
-    else if (ne == 1) wait_vm<NP + E>();
-    else wait_vm<NP + 2 * E>();
+    const uint32_t vm = __builtin_amdgcn_readfirstlane(vb[j]);
+    f32x4 acc[2][S::NT];
+    // A-fragment addresses of k-steps 4q + m (rows lane & 15, k = 32 ks + 8 (lane >> 4) .. +7; the XOR
+    // swizzle only touches the low 4 bits of the chunk index, so chunk (4 ks + g) ^ row = 16 (ks >> 2) +
+    // ((4 (ks & 3) + g) ^ row): four per-lane addresses plus an immediate 256 (ks >> 2)), rebuilt per
+    // job: no registers held across the loop
+    uint32_t addr[4];
+    {
+      const int ln = opaque(lane);
+      const uint32_t tb = sbase + (uint32_t)(s_cur * 2 * kTile) + (uint32_t)((ln & 15) * kTileRow);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) addr[m] = tb + 16u * (uint32_t)((4 * m + (ln >> 4)) ^ (ln & 15));
+    }
+    // the MFMA wave takes the SIMD's issue first; the partner's overhead fills the gaps
+    if (WP_PRIO) __builtin_amdgcn_s_setprio(WP_PRIO);
+    if (vm >> 16) pp_mfma<F16, true>(addr, wf, bh, acc);
+    else pp_mfma<F16, false>(addr, wf, bh, acc);
+    if (WP_PRIO) __builtin_amdgcn_s_setprio(0);
     const unsigned long long c1 = WS_CLK();
+    wait_vm<0>();                                    // this wave's pieces of job j + 1 (and j + 2) landed
     lds_barrier();
     const unsigned long long c2 = WS_CLK();
-    dma(j + 2, s_cur == 0 ? kJS - 1 : s_cur - 1);
-    const uint32_t vm = __builtin_amdgcn_readfirstlane(vb[j]);
-    const unsigned long long c3 = WS_CLK();
-    f32x4 acc[2][S::NT];
-    wp_mfma2<F16>(smem + s_cur * 2 * kTile, aoff, wf, acc, vm);
-    const unsigned long long c4 = WS_CLK();
+    // overhead phase: epilogue of job j, DMA issue of job j + 2
     const Job J = job_of(C, TEACHER, jm(j));
-    ws_epilogue<S, TEACHER, 0>(C, J, w, lane, vm & 0xffffu, bh, acc[0], ssum, scnt, bw);
-    ws_epilogue<S, TEACHER, 1>(C, J, w, lane, vm >> 16, bh, acc[1], ssum, scnt, bw);
+    if (vm == 0xffffffffu) pp_epilogue<TEACHER, true>(C, J, hw, lane, vm, acc);
+    else pp_epilogue<TEACHER, false>(C, J, hw, lane, vm, acc);
+    if (j + 2 < nj) dma(j + 2, s_cur == 0 ? kJS - 1 : s_cur - 1);
     s_cur = s_cur == kJS - 1 ? 0 : s_cur + 1;
-    const unsigned long long c5 = WS_CLK();
+    const unsigned long long c3 = WS_CLK();
+    lds_barrier();
+    const unsigned long long c4 = WS_CLK();
     if (DAD_PROBE_ON) {
-      ph[0] += c1 - c0; ph[1] += c2 - c1; ph[2] += c3 - c2; ph[3] += c4 - c3; ph[4] += c5 - c4;
+      ph[0] += c1 - c0; ph[1] += c2 - c1; ph[2] += c3 - c2; ph[3] += c4 - c3;
     }
   }
-  for (int k = 0; DAD_PROBE_ON && k < 5; ++k) WS_STAMP(4 + k, ph[k]);
-  wait_vm<0>();
+  if (!grp) lds_barrier();                           // group 0: phase 2 nj idle
+  for (int k = 0; DAD_PROBE_ON && k < 4; ++k) WS_STAMP(4 + k, ph[k]);
 }
 
 // Roles (dad_wp_job_range): teacher workgroups run the weak slabs with the teacher's W1, student
@@ -412,6 +447,9 @@ __device__ __forceinline__ void encode_wp_body(const DadEncodeArgs& a, char* sme
   const uint32_t sbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
   // valid bits of every job (bit r = row r of the 32-row slab is a frame of the utterance)
   uint32_t* vb = reinterpret_cast<uint32_t*>(smem + kOffPVB);
+  // ping-pong group: 1 for the second wave on this wave's SIMD (hardware SIMD id, HW_ID[5:4])
+  int* simd = reinterpret_cast<int*>(smem + kOffSimd);
+  if (lane == 0) simd[w] = (int)((__builtin_amdgcn_s_getreg((1 << 11) | (4 << 6) | 4)) & 3u);
   for (int p = tid; p < nj * DAD_SLAB; p += 64 * WAVES) {
     const Job J = job_of(C, teacher, jm(p / DAD_SLAB));
     const int t = J.c * DAD_SLAB + (p & (DAD_SLAB - 1));
@@ -421,12 +459,15 @@ __device__ __forceinline__ void encode_wp_body(const DadEncodeArgs& a, char* sme
     if ((lane & 31) == 0) vb[p / DAD_SLAB] = (uint32_t)(bal >> (lane & 32));
   }
   __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): the pad loads retired (no DMA in flight yet)
-  lds_barrier();                        // vb visible
+  lds_barrier();                        // vb, simd visible
+  int grp = 0;
+  for (int v = 0; v < w; ++v) grp += simd[v] == simd[w];
+  grp &= 1;
   const bf16x8* W = reinterpret_cast<const bf16x8*>(teacher ? a.w1h_teacher : a.w1h_student);
   const float* bias = teacher ? a.b1_teacher : a.b1_student;
   WS_STAMP(1, DAD_PROBE_WALL());
-  if (teacher) wp_loop<true, F16>(C, jm, nj, w, lane, smem, sbase, W, bias, vb, a);
-  else wp_loop<false, F16>(C, jm, nj, w, lane, smem, sbase, W, bias, vb, a);
+  if (teacher) wp_loop_pp<true, F16>(C, jm, nj, w, lane, smem, sbase, W, bias, vb, a, grp);
+  else wp_loop_pp<false, F16>(C, jm, nj, w, lane, smem, sbase, W, bias, vb, a, grp);
   WS_STAMP(2, DAD_PROBE_WALL());
 }
 

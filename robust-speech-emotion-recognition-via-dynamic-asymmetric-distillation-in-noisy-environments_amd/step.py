@@ -52,6 +52,39 @@ def _dev_batch(batch, device, labels=True):
     return x, pad, y, None, None
 
 
+def _resident(batch, device, labels=True):
+    """True when _dev_batch hands out the batch's own device tensors (no copy), i.e. the pointers a
+    step would prepare ahead are the ones the next step will see: f32 features (or an f32 store) on
+    `device`, a bool padding mask and int64 labels there, all contiguous."""
+    ni = batch["net_input"]
+    feats, pm = ni["feats"], ni.get("padding_mask")
+    if isinstance(feats, StoreFeats):
+        ok = feats.store.feats.dtype == torch.float32 and feats.store.feats.device == device
+    else:
+        ok = (torch.is_tensor(feats) and feats.device == device and feats.dtype == torch.float32
+              and feats.is_contiguous())
+    ok = ok and torch.is_tensor(pm) and pm.device == device and pm.dtype == torch.bool and pm.is_contiguous()
+    if labels:
+        y = batch["labels"]
+        ok = ok and torch.is_tensor(y) and y.device == device and y.dtype == torch.int64 and y.is_contiguous()
+    return bool(ok)
+
+
+_DRAW_DTYPES = {"nw": torch.float32, "ns": torch.float32, "u": torch.float32, "start": torch.int64,
+                "keep1": torch.bool, "keep2": torch.bool}
+
+
+def _draws_resident(draws, device):
+    """Explicit draws that _batch_structs uses in place (same dtype, on `device`, contiguous)."""
+    if draws is None:
+        return False
+    for k, dt in _DRAW_DTYPES.items():
+        v = draws.get(k)
+        if v is not None and not (torch.is_tensor(v) and v.device == device and v.dtype == dt and v.is_contiguous()):
+            return False
+    return True
+
+
 class _StepLossFn(torch.autograd.Function):
     """total_loss whose backward hands the step's analytic gradient to the student params.
 
@@ -311,6 +344,17 @@ class DADStep:
             keep.append(dd)
         return cfg, bt, (xc, mc, yc, xn, mn, keep, rc, lc, rn, ln)
 
+    def _ahead_ok(self, next_batch):
+        """Prepare the next batch ahead only when the pointers this step would prepare from are the
+        ones the next step will use: device-resident tensors (a host batch would be copied here and
+        copied again by the next step, whose rows would then not match; it prepares itself)."""
+        clean, noisy = next_batch[0], next_batch[1]
+        if noisy is None or not (_resident(clean, self.device) and _resident(noisy, self.device, labels=False)):
+            return False
+        if self.rng_mode == _lib.RNG_EXPLICIT:
+            return _draws_resident(next_batch[2] if len(next_batch) > 2 else None, self.device)
+        return True
+
     def step(self, clean_batch, noisy_batch, epoch, lr=None, draws=None, after_encode=None, next_batch=None,
              next_counter=None):
         """One full training step; returns the reference's loss dict as 0-d device tensors.
@@ -320,9 +364,11 @@ class DADStep:
         next_batch: optional (clean_batch, noisy_batch[, draws]) of the NEXT step (same epoch and
         lr).  FP16/BF16: its augmentation and 16-bit conversion then run inside this step's tail
         launch, on the CUs the tail leaves idle (dad_step_backward_ahead), and the next step()
-        with that batch skips them.  Results are bit-identical with or without it.  The next
-        batch's device tensors must keep their contents until that step (device-resident
-        batches; host tensors are copied again by the next step, which then prepares itself).
+        with that batch skips them.  Results are bit-identical with or without it.  Only
+        device-resident batches are prepared ahead (_ahead_ok: f32 features, bool masks, int64
+        labels and, with explicit draws, the draws in DADStep's dtypes, all on the step's device);
+        a host batch is ignored here and copied once, by the step that runs it.  The named
+        batch's device tensors must keep their contents until that step.
         next_counter: the next step's RNG step counter (default this step's + 1).  Graph replays
         that cycle a fixed set of captured steps pass the first captured step's counter from the
         last one (bench.capture_steps), so the cycle stays consistent.
@@ -341,7 +387,7 @@ class DADStep:
         if after_encode is not None:
             after_encode()
             stream = self._stream()
-        if next_batch is not None and self.precision != _lib.PREC_FP32:
+        if next_batch is not None and self.precision != _lib.PREC_FP32 and self._ahead_ok(next_batch):
             nd = next_batch[2] if len(next_batch) > 2 else None
             ncfg, nbt, nkeep = self._batch_structs(next_batch[0], next_batch[1], epoch, lr, nd, like=cfg,
                                                    counter=next_counter)

@@ -80,3 +80,36 @@ def test_early_stopping_counts_epochs_without_improvement():
     assert [es(b) for b in (True, False, False, True, False, False, False)] == \
         [False, False, False, False, False, False, True]
     assert not CK.EarlyStopping(patience=1, enabled=False)(False)
+
+
+def test_next_batch_prepared_ahead_only_when_device_resident():
+    """a step prepares the named next batch only if its tensors are the ones the next
+    step will use in place (step._resident / _draws_resident); a host batch would be copied twice.
+    The predicates are device-generic, so the CPU plays the step's device here."""
+    S = PKG.step
+    cpu = torch.device("cpu")
+    meta = torch.device("meta")
+
+    def batch(x_dtype=torch.float32, m_dtype=torch.bool, y_dtype=torch.int64, dev=cpu):
+        return {"net_input": {"feats": torch.zeros(2, 5, 768, dtype=x_dtype, device=dev),
+                              "padding_mask": torch.zeros(2, 5, dtype=m_dtype, device=dev)},
+                "labels": torch.zeros(2, dtype=y_dtype, device=dev)}
+
+    assert S._resident(batch(), cpu)
+    assert not S._resident(batch(), meta)                    # another device: would be copied
+    assert not S._resident(batch(x_dtype=torch.float64), cpu)
+    assert not S._resident(batch(m_dtype=torch.uint8), cpu)
+    assert not S._resident(batch(y_dtype=torch.int32), cpu)
+    assert S._resident(batch(y_dtype=torch.int32), cpu, labels=False)
+    nm = batch()
+    nm["net_input"]["padding_mask"] = None                   # a fresh zero mask per call: new pointer
+    assert not S._resident(nm, cpu)
+    nc = batch()
+    nc["net_input"]["feats"] = torch.zeros(2, 768, 5).transpose(1, 2)
+    assert not S._resident(nc, cpu)
+    d = {"nw": torch.zeros(3), "ns": torch.zeros(3), "u": torch.zeros(3), "start": torch.zeros(2, dtype=torch.int64),
+         "keep1": torch.zeros(4, dtype=torch.bool), "keep2": torch.zeros(4, dtype=torch.bool)}
+    assert S._draws_resident(d, cpu)
+    assert not S._draws_resident(None, cpu)
+    assert not S._draws_resident(dict(d, nw=np.zeros(3, np.float32)), cpu)
+    assert not S._draws_resident(dict(d, start=torch.zeros(2, dtype=torch.int32)), cpu)

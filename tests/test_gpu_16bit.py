@@ -9,9 +9,14 @@ Two references:
   * the FP32 parity-mode kernels driven by the SAME counter RNG (rng='counter') -- the
     benchmark's configuration, including the in-kernel noise, feature mask and temporal
     mask, at the bench geometry B=64, T=300.
-Tolerance: 16-bit operands with fp32 accumulation -> embeddings/logits within 2e-2 (bf16) /
-2e-3 (fp16) of the tensor max; gradient direction cosine > 0.99 whenever the discrete DACP mask
-agrees; losses within the golden-replay bounds of test_gpu_throughput_parity.
+Tolerance: 16-bit operands with fp32 accumulation -> of the tensor max, embeddings within 1e-3
+(fp16) / 2e-2 (bf16); logits within 2e-2 (bf16) and, fp16, 7e-4 (1.5e-3 for the one-frame
+geometry B1T1, whose embedding is a single row's ReLU with nothing averaging the operand
+rounding).  Measured fp16 logits on these synthetic problems (round 5): 1.23e-3 (B1T1), 6.3e-4
+(B5T33), 3.3e-4 .. 3.7e-4 (T = 40 .. 64); fp16 rounds each operand by up to 2^-11 relative.
+north_star's 1e-4 holds on the reference's own inputs: every golden replay of
+test_gpu_throughput_parity (15 fixtures).  Gradient direction cosine > 0.99 whenever the
+discrete DACP mask agrees; losses within the golden-replay bounds of test_gpu_throughput_parity.
 """
 import os
 import subprocess
@@ -26,7 +31,14 @@ from test_gpu_parity import EDGE, _problem
 
 pytestmark = pytest.mark.gpu
 BF16_TOL = 2e-2
-ACT_TOL = {"bf16": BF16_TOL, "fp16": 2e-3}
+ACT_TOL = {"bf16": BF16_TOL, "fp16": 1e-3}      # embeddings e_*
+LOGIT_TOL = {"bf16": BF16_TOL, "fp16": 7e-4}    # logits z_*
+
+
+def _tol(prec, key, T=None):
+    if key.startswith("z_"):
+        return 1.5e-3 if (prec == "fp16" and T == 1) else LOGIT_TOL[prec]
+    return ACT_TOL[prec]
 PRECS = ["fp16", "bf16"]
 
 
@@ -39,7 +51,6 @@ def _grad_cos(g1, g2):
 @pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("geom", EDGE, ids=lambda g: "B%dT%d_Bn%dTn%d" % (g["B"], g["T"], g["Bn"], g["Tn"]))
 def test_16bit_step_edge_geometries_vs_oracle(geom, prec):
-    TOLA = ACT_TOL[prec]
     cfg = dad_oracle.make_cfg("iemocap")
     g = dict(geom)
     ragged = g.pop("ragged", True)
@@ -52,12 +63,10 @@ def test_16bit_step_edge_geometries_vs_oracle(geom, prec):
         orc.load_state(st)
         o = gh.run_step(step, inp, epoch)
         r = orc.step(inp, epoch)
-        gh.close(o["e_clean"], r["e_clean"], TOLA, "%s %s e%d e_clean" % (prec, geom, epoch))
-        gh.close(o["z_clean"], r["z_clean"], TOLA, "%s %s e%d z_clean" % (prec, geom, epoch))
-        if epoch >= 30:
-            gh.close(o["e_teacher"], r["e_teacher"], TOLA, "%s %s e_teacher" % (prec, geom))
-            gh.close(o["e_strong"], r["e_strong"], TOLA, "%s %s e_strong" % (prec, geom))
-            gh.close(o["z_strong"], r["z_strong"], TOLA, "%s %s z_strong" % (prec, geom))
+        keys = ["e_clean", "z_clean"] + (["e_teacher", "e_strong", "z_strong", "z_teacher"] if epoch >= 30 else [])
+        print("%s %s e%d: %s" % (prec, geom, epoch, {k: float("%.3g" % gh.rel(o[k], r[k])) for k in keys}))
+        for k in keys:
+            gh.close(o[k], r[k], _tol(prec, k, min(g["T"], g["Tn"])), "%s %s e%d %s" % (prec, geom, epoch, k))
         if epoch < 30 or np.array_equal(o["mask"], r["mask"]):
             assert _grad_cos(o["grads"], r["grads"]) > 0.99, (geom, epoch)
 
@@ -77,7 +86,7 @@ def test_16bit_counter_rng_matches_fp32_counter_rng(B, T, prec):
         outs.append(gh.run_step(step, inp, 60, with_draws=False))
     f, b = outs
     for k in ("e_clean", "e_teacher", "e_strong", "z_clean", "z_teacher", "z_strong"):
-        gh.close(b[k], f[k], ACT_TOL[prec], "counter %s %s B%d T%d" % (prec, k, B, T))
+        gh.close(b[k], f[k], _tol(prec, k), "counter %s %s B%d T%d" % (prec, k, B, T))
     # the discrete DACP decisions agree at this geometry (a flip would move KL / ECDA by a
     # finite step, which no precision bound covers); then every loss term is within the loss
     # bound of test_gpu_throughput_parity (the golden replays of the same mode)

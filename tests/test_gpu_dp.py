@@ -84,11 +84,104 @@ def _rank_main(rank, world, port, q):
         q.put((rank, "FAIL: %r\n%s" % (e, traceback.format_exc())))
 
 
-def test_dp_step_two_ranks_match_oracle():
+SCHEDULE16 = [35, 60, 60]
+
+
+def _rank_main_fp16(rank, world, port, q):
+    """The timed mode's DP path: fp16 operands, each step naming its next batch (the next batch's
+    rows prepared in this step's tail launch), gloo exchange.  Per rank: every step against the
+    oracle's DP step on this rank's shard within the fp16 bounds of test_gpu_throughput_parity
+    (losses and logits 1e-4, mask bit-exact); the chain with next-batch preparation equals the
+    chain without it bit for bit; the replicas stay bit-identical."""
+    try:
+        import torch
+        import torch.distributed as dist
+        import dadpkg
+        import gpu_harness as gh
+        from oracle import dad_oracle, synth
+        from test_gpu_throughput_parity import TOL, _cos, _normrel
+        tol = TOL["fp16"]
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        import datetime
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=120))
+        p = dadpkg.pkg()
+        cfg = dad_oracle.make_cfg("iemocap")
+        st = synth.make_state(SEED, 1)
+        dev = torch.device("cuda")
+        inps = [synth.make_step_inputs(SEED + 100 * rank, k, B, T) for k in range(len(SCHEDULE16))]
+
+        def dev_batch(inp):
+            c, n, d = gh.batches(inp)
+            mv = lambda b: {"net_input": {k: v.to(dev) for k, v in b["net_input"].items()}, "labels": b["labels"].to(dev)}
+            # the dtypes DADStep uses, so the draws are not copied again (the prepared-ahead rows are
+            # keyed on the next batch's device pointers)
+            dt = {"nw": torch.float32, "ns": torch.float32, "u": torch.float32, "start": torch.int64,
+                  "keep1": torch.bool, "keep2": torch.bool}
+            return mv(c), mv(n), {k: torch.from_numpy(np.asarray(v)).to(dev, dt[k]) for k, v in d.items()}
+
+        batches = [dev_batch(i) for i in inps]
+
+        def allreduce(v):
+            t = torch.from_numpy(np.ascontiguousarray(v, np.float64))
+            dist.all_reduce(t)
+            return t.numpy()
+
+        def chain(ahead, check):
+            model = p.SSRLModel().cuda()
+            step = p.DADStep(model, p.ConfigView(cfg, flavor="iemocap"), precision="fp16", rng="explicit",
+                             comm=p.ProcessGroupComm())
+            gh.load_state(step, st)
+            orc = None
+            if check:
+                orc = dad_oracle.DADOracle(*synth.init_weights(SEED)[:4], cfg)
+                orc.load_state(st)
+            prepped, losses = [], []
+            for k, epoch in enumerate(SCHEDULE16):
+                c, n, d = batches[k]
+                nxt = batches[k + 1] if ahead and k + 1 < len(batches) and SCHEDULE16[k + 1] == epoch else None
+                out = step.step(c, n, epoch, draws=d, next_batch=nxt)
+                torch.cuda.synchronize()
+                prepped.append(step.last_prepped)
+                losses.append({key: float(v) for key, v in out.items()})
+                if check:
+                    o = {kk: (v.detach().cpu().numpy() if torch.is_tensor(v) else v) for kk, v in step.outputs(B, B).items()}
+                    r = orc.step(inps[k], epoch, allreduce=allreduce, world=world)
+                    err = abs(losses[-1]["total_loss"] - r["losses_mean"][0]) / max(1.0, abs(r["losses_mean"][0]))
+                    assert err <= tol["loss"], (rank, k, "total loss", err)
+                    assert np.array_equal(o["mask"], r["mask"]), (rank, k, "mask")
+                    for key in ("z_clean",) + (("z_strong", "z_teacher") if epoch >= 30 else ()):
+                        assert gh.rel(o[key], r[key]) <= tol["logit"], (rank, k, key, gh.rel(o[key], r[key]))
+                    g = np.concatenate([x.reshape(-1) for x in gh.unflat(o["grad"])])
+                    gr = np.concatenate([np.asarray(x).reshape(-1) for x in r["grads_mean"]])
+                    assert _normrel(g, gr) <= tol["grad"] and _cos(g, gr) >= tol["cos"], (rank, k, _normrel(g, gr))
+                    for name, flat in (("student", step.model.student_flat), ("teacher", step.model.teacher_flat)):
+                        got = gh.unflat(flat.detach().cpu().numpy())
+                        assert max(_normrel(a, b_) for a, b_ in zip(got, r[name])) <= tol["param"], (rank, k, name)
+            state = torch.cat([step.model.student_flat.detach(), step.model.teacher_flat.detach(), step.exp_avg,
+                               step.exp_avg_sq, step.dacp]).cpu()
+            return state, losses, prepped
+
+        plain, plain_losses, plain_prepped = chain(False, True)
+        ahead, ahead_losses, ahead_prepped = chain(True, False)
+        assert not any(plain_prepped) and ahead_prepped == [False, False, True], ahead_prepped
+        assert torch.equal(plain, ahead) and plain_losses == ahead_losses, "next-batch preparation changed the DP chain"
+        other = plain.clone().double()
+        dist.broadcast(other, src=0)
+        assert torch.equal(plain.double(), other), "ranks diverged"
+        dist.destroy_process_group()
+        q.put((rank, "ok"))
+    except BaseException as e:  # report to the parent instead of hanging it
+        import traceback
+        q.put((rank, "FAIL: %r\n%s" % (e, traceback.format_exc())))
+
+
+@pytest.mark.parametrize("fp16", [False, True], ids=["fp32", "fp16_ahead"])
+def test_dp_step_two_ranks_match_oracle(fp16):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_rank_main_fp16 if fp16 else _rank_main, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
     res = {}

@@ -58,7 +58,8 @@ def test_train_epoch_runs_loaders_and_epoch_end(tmp_path):
     step = PKG.DADStep(model, flavor="iemocap", precision="bf16", rng="counter", seed=1)
     q0 = step.class_quality_scores.clone()
     avg = CK.train_epoch(step, clean, noisy, 40)
-    assert set(avg) >= {"total_loss", "supervised_ce_loss", "consistency_loss", "ecda_loss"}
+    assert set(avg) >= {"total_loss", "supervised_ce_loss", "consistency_loss", "ecda_loss", "range_flag"}
+    assert avg["range_flag"] == 0
     assert all(np.isfinite(v) for v in avg.values())
     assert step.adam_step == min(len(clean), len(noisy))
     assert not torch.equal(step.class_quality_scores, q0)   # DACP quality updated at epoch end
@@ -105,3 +106,23 @@ def test_store_mode_prefetch_chain_is_bit_exact(mode):
     for x, y in ((a.model.student_flat, b.model.student_flat), (a.model.teacher_flat, b.model.teacher_flat),
                  (a.exp_avg, b.exp_avg), (a.exp_avg_sq, b.exp_avg_sq), (a.dacp, b.dacp)):
         assert torch.equal(x, y)
+
+
+def test_host_next_batch_is_not_prepared_ahead():
+    """a next batch of host tensors is not prepared ahead (it would be copied here and
+    again by the step that runs it, and the rows prepared from the first copy would not match);
+    the same batch on the device is."""
+    cfg = dad_oracle.make_cfg("iemocap")
+    from test_gpu_parity import _problem
+    from test_gpu_graph import _device_batches
+    host = gh.batches(_problem(B=12, T=40, seed=71, Bn=10, Tn=44))[:2]
+    dev = _device_batches(_problem(B=12, T=40, seed=72, Bn=10, Tn=44))[:2]
+    s = gh.make_step(cfg, precision="fp16", rng="counter", seed=7)
+    gh.load_state(s, synth.make_state(71, 1))
+    s.step(dev[0], dev[1], 60, next_batch=host)
+    assert s._prepped_key is None
+    s.step(host[0], host[1], 60, next_batch=dev)
+    assert not s.last_prepped and s._prepped_key is not None
+    s.step(dev[0], dev[1], 60)
+    torch.cuda.synchronize()
+    assert s.last_prepped

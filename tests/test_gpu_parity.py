@@ -260,20 +260,24 @@ def test_train_step_shim_with_reference_loop_body():
     assert step._shadow_dirty
 
 
+@pytest.mark.parametrize("prec", ["fp32", "fp16"])
 @pytest.mark.parametrize("class_aware,B", [(True, 200), (False, 96), (True, 64), (False, 64)],
                          ids=["class_aware", "global_mmd", "class_aware_b64", "global_mmd_b64"])
-def test_large_member_sets_match_oracle(class_aware, B):
+def test_large_member_sets_match_oracle(class_aware, B, prec):
     """Large member sets: beyond the LDS-staged size (ECDA_NZ = 80 rows in csrc/tail.hip) the
     member rows and the distance matrix go through the global-memory path of dad_tail_ecda's
     class blocks, and the DACP ranks span several 512-thread rounds (B = 200 / 96, no register
     prefetch).  B = 64: the prefetch path (every row in registers at entry) with one class
-    holding every clean utterance."""
+    holding every clean utterance.  fp16 (the timed mode's operands; the tail arithmetic is fp32
+    in every mode): losses at north_star's 1e-4, the mask bit-exact, logits within test_gpu_16bit's
+    bound for short synthetic utterances (T = 6 here: little averaging of the operand rounding;
+    measured 1.9e-4), gradients within test_gpu_throughput_parity's fp16 bounds."""
     cfg = dad_oracle.make_cfg("iemocap", USE_CLASS_AWARE_MMD=class_aware)
     inp = _problem(B, 6, seed=9, snr=20.0)
     if class_aware:
         inp["yc"] = np.zeros_like(inp["yc"])          # one class holds every clean utterance
     st = synth.make_state(4, 1, tau_range=(0.0, 0.01))   # low thresholds: most noisy rows masked in
-    step = gh.make_step(cfg)
+    step = gh.make_step(cfg, precision=prec)
     orc = dad_oracle.DADOracle(*synth.init_weights(4)[:4], cfg)
     gh.load_state(step, st)
     orc.load_state(st)
@@ -281,7 +285,17 @@ def test_large_member_sets_match_oracle(class_aware, B):
     r = orc.step(inp, 60)
     assert r["ecda_loss"] != 0.0 and int(np.sum(r["mask"])) > (80 if B > 64 else 16)
     for k in ("total_loss", "supervised_ce_loss", "consistency_loss", "ecda_loss"):
-        _cmp_loss(o[k], r[k], (class_aware, k))
+        _cmp_loss(o[k], r[k], (class_aware, prec, k))
     np.testing.assert_array_equal(o["mask"], r["mask"])
-    for k, (a, b_) in enumerate(zip(o["grads"], r["grads"])):
-        gh.close_grad(a, b_, "large B grad %d" % k)
+    if prec == "fp32":
+        for k, (a, b_) in enumerate(zip(o["grads"], r["grads"])):
+            gh.close_grad(a, b_, "large B grad %d" % k)
+        return
+    from test_gpu_throughput_parity import TOL, _cos, _normrel
+    from test_gpu_16bit import LOGIT_TOL
+    for k in ("z_clean", "z_strong", "z_teacher"):   # six-frame utterances: test_gpu_16bit's synthetic bound
+        assert gh.rel(o[k], r[k]) <= LOGIT_TOL["fp16"], (class_aware, k, gh.rel(o[k], r[k]))
+    g = np.concatenate([x.reshape(-1) for x in o["grads"]])
+    gr = np.concatenate([np.asarray(x).reshape(-1) for x in r["grads"]])
+    print("fp16 large B=%d class_aware=%s: grad normrel %.3g cos %.7f" % (B, class_aware, _normrel(g, gr), _cos(g, gr)))
+    assert _normrel(g, gr) <= TOL["fp16"]["grad"] and _cos(g, gr) >= TOL["fp16"]["cos"]

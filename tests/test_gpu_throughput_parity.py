@@ -15,11 +15,13 @@ post-step parameters.
 Tolerances:
   FP16 (the timed mode): north_star's bound, 1e-4, on every loss term and on the student and
     teacher logits; fp16 keeps 11 significand bits (operands rounded by up to 2^-12 relative).
-    Measured (round 4, all 4 fixtures, all steps): losses <= 2.5e-5, logits <= 8.1e-5,
+    Measured (round 4, the 4 bench fixtures, all steps): losses <= 2.5e-5, logits <= 8.1e-5,
     embeddings <= 2.7e-4, clipped-gradient Frobenius <= 9.2e-3 (cosine 1.0; the gradient error is
     set by ReLU' decisions of pre-activations within rounding of 0, which flip whole rows),
     post-step parameters <= 1.2e-6; the DACP mask identical on every step.  The non-north-star
-    bounds are about 3x those.
+    bounds are about 3x those.  Round 5 replays every step fixture in fp16: the post-step
+    parameters of EMODB (its learning rate and few rows per step) reach 1.01e-5, so their bound
+    is 3e-5.
   BF16: 8 significand bits (2^-9).  Bounds about 3x the largest error measured on MI355X
     (round 3, all 4 fixtures, all steps: losses 1.5e-4, logits 5.4e-4, embeddings 2.3e-3,
     clipped-gradient Frobenius 2.2e-2 (cosine >= 0.99988), post-step parameters 2.1e-6).
@@ -43,7 +45,7 @@ pytestmark = pytest.mark.gpu
 
 GOLDENS = ["iemocap_b64_t300", "casia_ecda_snr0", "casia_ecda_snr5", "casia_ecda_snr10"]
 TOL = {
-    "fp16": {"loss": 1e-4, "logit": 1e-4, "emb": 1e-3, "grad": 3e-2, "cos": 0.9999, "param": 1e-5},
+    "fp16": {"loss": 1e-4, "logit": 1e-4, "emb": 1e-3, "grad": 3e-2, "cos": 0.9999, "param": 3e-5},
     "bf16": {"loss": 5e-4, "logit": 1.5e-3, "emb": 7e-3, "grad": 6e-2, "cos": 0.9995, "param": 1e-5},
 }
 BF16_LOSS_TOL = TOL["bf16"]["loss"]
@@ -77,8 +79,15 @@ def _dump_measured():
             json.dump(_MEASURED, f, indent=1, sort_keys=True)
 
 
-@pytest.mark.parametrize("prec", ["fp16", "bf16"])
-@pytest.mark.parametrize("name", GOLDENS)
+# fp16 (the timed mode) on EVERY step fixture: besides the bench geometry and configs[3], the
+# reference's other branches -- global MMD (I/utils.py:633-650), no-entropy certainty
+# (I/utils.py:414), the fixed threshold (I/train.py:417-420), EMODB's unconditional DACP
+# (E/train_emodb.py:419), mask-empty steps, Bc != Bn and T = 300 shapes -- at north_star's 1e-4.
+# bf16 (a mode, not the headline) on the four bench fixtures.
+CASES = [(n, "fp16") for n in goldens.variants()] + [(n, "bf16") for n in GOLDENS]
+
+
+@pytest.mark.parametrize("name,prec", CASES, ids=["%s-%s" % c for c in CASES])
 def test_16bit_step_matches_reference_goldens(name, prec):
     tol = TOL[prec]
     d, spec, cfg = goldens.load(name)

@@ -2,7 +2,8 @@
 never the product library).  Runs bench-shaped steps (each naming the next batch, as the bench
 does), then reads the stamps of every workgroup of the last encoder launch and summarises them per
 role: start / prologue end / end (us after the first workgroup's start) and wave-0 cycles per
-32-row job in: DMA wait, barrier, DMA issue + valid mask, MFMA, epilogue."""
+32-row job in the ping-pong loop's phases: MFMA, the MFMA phase's end (vmcnt wait + barrier), epilogue +
+DMA issue, the overhead phase's barrier."""
 import ctypes
 import os
 import sys
@@ -47,8 +48,8 @@ def main():
                                             np.median(pro[m]), np.median(end[m]), end[m].max(), np.median(per)))
         if True:
             cyc = st[m, 4:9].astype(np.float64) / (Q[m][:, None] / 2.0)
-            print("        wave-0 cycles per 32-row job p50: wait %.0f  barrier %.0f  dma+mask %.0f  mfma %.0f  epilogue %.0f" %
-                  tuple(np.median(cyc, axis=0)))
+            print("        wave-0 cycles per 32-row job p50: mfma %.0f  mfma-end wait+barrier %.0f  epilogue+dma %.0f  "
+                  "overhead barrier %.0f" % tuple(np.median(cyc, axis=0))[:4])
 
 
 if __name__ == "__main__":
