@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define DAD_ABI_VERSION 4
+#define DAD_ABI_VERSION 5
 
 /* error codes (besides hipError_t values) */
 #define DAD_OK 0
@@ -175,12 +175,14 @@ const char* dad_error_string(int code);
  * for a device of `cus` compute units and the most 32-row jobs any workgroup's range holds
  * (always <= 256, the kernel's per-workgroup table).  Diagnostics and tests. */
 int dad_encoder_ws_plan(const dad_config* cfg, int cus, int* nt, int* ns, int* max_jobs);
-/* Host-only: the 16-bit encoder's job assignment for a device of `cus` CUs (XCD sweep when it
- * applies, else the contiguous split): for every workgroup wg of the grid, jobs[4wg..4wg+3] =
- * (teacher 1/0, first job, job stride, job count); student jobs j < B*ceil(T/32) are clean slabs,
- * the rest strong slabs.  Returns the grid size (> 0) or a DAD_E_* code.  jobs holds 4*cus ints.
- * Diagnostics and tests. */
-int dad_encoder_ws_jobs(const dad_config* cfg, int cus, int* jobs);
+/* Host-only: the 16-bit encoder's job assignment for a device of `cus` CUs: for every workgroup
+ * wg of the grid, jobs[4wg..4wg+3] = (teacher 1/0, first job, job stride, job count); student jobs
+ * j < B*ceil(T/32) are clean slabs, the rest strong slabs.  `capacity` = ints available at jobs.
+ * The grid is nt + ns of dad_encoder_ws_plan: usually `cus`, more when a range would exceed the
+ * kernel's 256-job table (very long batches), so size jobs as 4 * (nt + ns).  Returns the grid
+ * size (> 0), DAD_E_ARG when 4 * grid > capacity (nothing written), or another DAD_E_* code.
+ * Diagnostics and tests.  (ABI 5: `capacity` added.) */
+int dad_encoder_ws_jobs(const dad_config* cfg, int cus, int* jobs, int capacity);
 
 /* --- fused train step ---------------------------------------------------------------
  * Replaces the body of Trainer.train_epoch's loop (I/train.py:484-492):

@@ -72,7 +72,8 @@ EXPORTS = {
     "dad_error_string": (ctypes.c_char_p, [ctypes.c_int]),
     "dad_encoder_ws_plan": (ctypes.c_int, [ctypes.POINTER(DadConfig), ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                                            ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
-    "dad_encoder_ws_jobs": (ctypes.c_int, [ctypes.POINTER(DadConfig), ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
+    "dad_encoder_ws_jobs": (ctypes.c_int, [ctypes.POINTER(DadConfig), ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                            ctypes.c_int]),
     "dad_step_compute": (ctypes.c_int, [ctypes.POINTER(DadConfig), ctypes.POINTER(DadBatch),
                                         ctypes.POINTER(DadState), ctypes.c_void_p, ctypes.c_void_p]),
     "dad_step_encode": (ctypes.c_int, [ctypes.POINTER(DadConfig), ctypes.POINTER(DadBatch),

@@ -202,14 +202,31 @@ int dad_timing_start(int every, int max_steps) {
   g_tk = Timing();
   g_tk.ev.assign((size_t)max_steps * TK_N, nullptr);
   g_tk.rec.assign((size_t)max_steps * TK_N, 0);
+  // on any failure: the events created so far are destroyed and no session is left half set up
+  auto fail = [](hipError_t e, hipStream_t s) {
+    for (hipEvent_t x : g_tk.ev)
+      if (x) (void)hipEventDestroy(x);
+    if (s) (void)hipStreamDestroy(s);
+    g_tk = Timing();
+    return (int)e;
+  };
   // timing-only events: no system-scope fence (no L2 writeback / invalidate at each record, which had
   // cost the stream ~3 us per event and slowed the kernel after it); dad_timing_stop reads them after
   // a device synchronize
-  for (auto& e : g_tk.ev) DAD_TRY(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
+  for (auto& e : g_tk.ev) {
+    const hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
+    if (r != hipSuccess) return fail(r, nullptr);
+  }
   // first use outside the timed region: a HIP event's first record sets it up (host time the
-  // first recorded steps would otherwise pay)
-  for (auto& e : g_tk.ev) DAD_TRY(hipEventRecord(e, nullptr));
-  DAD_TRY(hipDeviceSynchronize());
+  // first recorded steps would otherwise pay).  Recorded on a private non-blocking stream and
+  // synchronised there only: no other stream waits, and a stream capturing a graph is untouched.
+  hipStream_t ws = nullptr;
+  hipError_t r = hipStreamCreateWithFlags(&ws, hipStreamNonBlocking);
+  if (r != hipSuccess) return fail(r, nullptr);
+  for (auto& e : g_tk.ev)
+    if ((r = hipEventRecord(e, ws)) != hipSuccess) return fail(r, ws);
+  if ((r = hipStreamSynchronize(ws)) != hipSuccess) return fail(r, ws);
+  (void)hipStreamDestroy(ws);
   g_tk.every = every;
   g_tk.nset = max_steps;
   return DAD_OK;
@@ -273,7 +290,7 @@ int dad_encoder_ws_plan(const dad_config* cfg, int cus, int* nt, int* ns, int* m
   return DAD_OK;
 }
 
-int dad_encoder_ws_jobs(const dad_config* cfg, int cus, int* jobs) {
+int dad_encoder_ws_jobs(const dad_config* cfg, int cus, int* jobs, int capacity) {
   int rc = check_cfg(cfg);
   if (rc) return rc;
   if (cus < 2 || !jobs) return DAD_E_ARG;
@@ -282,6 +299,7 @@ int dad_encoder_ws_jobs(const dad_config* cfg, int cus, int* jobs) {
   int nt = 0, ns = 0;
   rc = wp_split(G, Bn, cus, nt, ns);
   if (rc) return rc;
+  if (capacity < 4 * (nt + ns)) return DAD_E_ARG;   // the grid outgrew the caller's table
   for (int wg = 0; wg < nt + ns; ++wg) {
     bool t = false;
     int j0 = 0, j1 = 0;

@@ -1604,7 +1604,8 @@ struct __attribute__((aligned(16))) EcdaW {
   int rowz[2 * TW_MAXB], mem[2 * TW_MAXB];
   int cnt[DAD_C];                       // masked noisy rows per class (pseudo-label)
   float pd[DAD_C][DAD_C];
-  float msp[ECDA_THREADS / 64][DAD_H];   // per-wave member-row sums (the bandwidth identity)
+  float msp[ECDA_THREADS / 64][DAD_H];   // per-wave sums of the member rows minus candidate row 0
+  double nsp[ECDA_THREADS / 64];        // per-wave sums of |member row - candidate row 0|^2
   double t3p[ECDA_THREADS / 64][3];
   float cmp[ECDA_THREADS / 64];
 };
@@ -1722,15 +1723,24 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
   };
   if (gc) {
     // squared norms of the candidate rows (a runtime loop: only the candidates are summed), and
-    // this wave's sum of its member rows (lane = 4 hidden units) for the bandwidth
+    // for the bandwidth this wave's sums over its member rows of d = z - z0 and |d|^2, z0 =
+    // candidate row 0 (lane = 4 hidden units).  Post-ReLU embeddings share a large positive mean;
+    // centred on a row of the class, the identity below sums no large cancelling terms.
     f32x4 ms = f32x4{};
+    double ns = 0.0;
+    const f32x4 z0 = *reinterpret_cast<const f32x4*>(rowp(0) + 4 * lane);
     for (int r = g; r < ncand_all; r += ECDA_NG) {
       const f32x4 v = *reinterpret_cast<const f32x4*>(rowp(r) + 4 * lane);
       const float nr = dad_wave_sum(((v[0] * v[0] + v[1] * v[1]) + v[2] * v[2]) + v[3] * v[3]);
       if (lane == 0) S.nz[r] = nr;
-      ms += S.mem[r] ? v : f32x4{};
+      if (S.mem[r]) {
+        const f32x4 d = v - z0;
+        ms += d;
+        ns += (double)dad_wave_sum(((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]) + d[3] * d[3]);
+      }
     }
     *reinterpret_cast<f32x4*>(&S.msp[g][4 * lane]) = ms;
+    if (lane == 0) S.nsp[g] = ns;
     // Gram partials: tile pair (ti, tj) over a K slice, fp32 matrix cores
     for (int item = g; item < npt * ks; item += ECDA_NG) {
       const int pr = item / ks, sl = item - pr * ks;
@@ -1813,21 +1823,17 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
     }
     cpart = dad_wave_sum(cpart);
     // detached bandwidth (I/utils.py:538-544) without the distance matrix: over the nmem member
-    // rows, sum_ij |z_i - z_j|^2 = 2 nmem sum_i |z_i|^2 - 2 |sum_i z_i|^2, from the candidates'
-    // norms and the waves' member-row sums (every wave alike, in double), so the kernel values
-    // and coefficients follow the distances in the same pass (the distance matrix no longer
-    // makes a round trip through LDS and a barrier before them)
+    // rows, with d_i = z_i - z0 for any fixed z0, sum_ij |z_i - z_j|^2 = 2 nmem sum_i |d_i|^2 -
+    // 2 |sum_i d_i|^2, from the waves' partial sums (every wave alike, combined in double), so the
+    // kernel values and coefficients follow the distances in the same pass (the distance matrix
+    // no longer makes a round trip through LDS and a barrier before them)
     f32x4 m = f32x4{};
 #pragma unroll
     for (int gg = 0; gg < ECDA_NG; ++gg) m += *reinterpret_cast<const f32x4*>(&S.msp[gg][4 * lane]);
     const double msq = dad_wave_sum_d(((double)m[0] * m[0] + (double)m[1] * m[1]) + ((double)m[2] * m[2] + (double)m[3] * m[3]));
     double nsq = 0.0;
-    for (int i0 = 0; i0 < ncand_all; i0 += 64) {
-      const int i = i0 + lane;
-      const int ic = i < ncand_all ? i : 0;
-      nsq += ((i < ncand_all) & (S.mem[ic] != 0)) ? (double)S.nz[ic] : 0.0;
-    }
-    nsq = dad_wave_sum_d(nsq);
+#pragma unroll
+    for (int gg = 0; gg < ECDA_NG; ++gg) nsq += S.nsp[gg];
     const double bws = fmax(2.0 * (double)nmem * nsq - 2.0 * msq, 0.0);
     float bw = nmem > 1 ? (float)(bws / (double)(nmem * nmem - nmem)) : 1.0f;
     bw = bw / 4.0f;

@@ -349,13 +349,10 @@ __device__ __forceinline__ bf16x8 tr_frag(const uint16_t* tile, int pitch, int r
   const int row = rowbase + 8 * (g >> 1) + q;
   const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + row * pitch + col));
   const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + (row + 4) * pitch + col));
-  bf16x8 r;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    r[e] = __builtin_bit_cast(__bf16, (short)v0[e]);
-    r[e + 4] = __builtin_bit_cast(__bf16, (short)v1[e]);
-  }
-  return r;
+  // one concatenation (a register-pair sequence), not eight element copies
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const s16x8 c = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, c);
 }
 
 // one slab in flight: group thread t holds 8 consecutive columns of row t/8 (staged to LDS

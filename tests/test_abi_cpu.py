@@ -85,9 +85,17 @@ def test_encoder_job_assignment_covers_every_slab_once(Bc, Tc, Bn, Tn, cus):
     for epoch in (0, 60):
         cfg = p.dad_config_for(p.ConfigView(flavor="iemocap"), Bc, Tc, Bn, Tn, epoch, 1,
                                precision=p._lib.PREC_FP16)
-        buf = (ctypes.c_int * (4 * max(cus, 2048)))()
-        grid = L.dad_encoder_ws_jobs(cfg, cus, buf)
-        assert grid > 0
+        nt, ns, mj = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        assert L.dad_encoder_ws_plan(cfg, cus, ctypes.byref(nt), ctypes.byref(ns), ctypes.byref(mj)) == 0
+        need = 4 * (nt.value + ns.value)
+        if need > 4 * cus:     # the grid outgrew cus: a 4*cus table is refused, nothing written
+            small = (ctypes.c_int * (4 * cus))(*([-7] * (4 * cus)))
+            assert L.dad_encoder_ws_jobs(cfg, cus, small, 4 * cus) == 1001
+            assert all(v == -7 for v in small)
+        assert L.dad_encoder_ws_jobs(cfg, cus, (ctypes.c_int * (need - 1))(), need - 1) == 1001
+        buf = (ctypes.c_int * need)()
+        grid = L.dad_encoder_ws_jobs(cfg, cus, buf, need)
+        assert grid == nt.value + ns.value > 0
         ncc, ncn = -(-Tc // 32), -(-Tn // 32)
         Jc, Js = Bc * ncc, (Bn * ncn if epoch >= 30 else 0)
         seen_t, seen_s = {}, {}

@@ -299,3 +299,36 @@ def test_large_member_sets_match_oracle(class_aware, B, prec):
     gr = np.concatenate([np.asarray(x).reshape(-1) for x in r["grads"]])
     print("fp16 large B=%d class_aware=%s: grad normrel %.3g cos %.7f" % (B, class_aware, _normrel(g, gr), _cos(g, gr)))
     assert _normrel(g, gr) <= TOL["fp16"]["grad"] and _cos(g, gr) >= TOL["fp16"]["cos"]
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp16"])
+def test_ecda_bandwidth_with_large_common_embedding_offset(prec):
+    """the detached MMD bandwidth (I/utils.py:537-544, the mean pairwise squared
+    distance) is computed from per-class partial sums, sum_ij |z_i - z_j|^2 = 2n sum|d_i|^2 -
+    2|sum d_i|^2 with d_i = z_i - z0.  With z0 = 0 that identity cancels digits when the pooled
+    embeddings share a large mean (|mean|^2 / variance); the kernel centres on a member row.  Here
+    b1 += 30 makes every hidden unit active with a common offset of ~30 and the ECDA loss and
+    gradients are held to the float64 oracle's."""
+    cfg = dad_oracle.make_cfg("iemocap")
+    inp = _problem(64, 40, seed=13, snr=20.0)
+    st = synth.make_state(13, 1, tau_range=(0.0, 0.01))     # low thresholds: ECDA members on
+    for net in ("student", "teacher"):
+        st[net] = [np.array(a, np.float32) for a in st[net]]
+        st[net][1] = st[net][1] + np.float32(30.0)
+    W1, b1, W2, b2, _ = synth.init_weights(13)
+    orc = dad_oracle.DADOracle(W1, b1, W2, b2, cfg)
+    orc.load_state(st)
+    step = gh.make_step(cfg, precision=prec)
+    gh.load_state(step, st)
+    o = gh.run_step(step, inp, 60)
+    r = orc.step(inp, 60)
+    e = np.asarray(r["e_clean"], np.float64)
+    assert e.mean() > 20.0 and r["ecda_loss"] != 0.0, (e.mean(), r["ecda_loss"])
+    tol = 1e-4
+    for k in ("ecda_loss", "total_loss"):
+        err = abs(o[k] - r[k]) / max(1.0, abs(r[k]))
+        print("%s offset-30 %s: got %.9g want %.9g rel %.3g" % (prec, k, o[k], r[k], err))
+        assert err <= tol, (prec, k, o[k], r[k], err)
+    if prec == "fp32":
+        for k, (a, b_) in enumerate(zip(o["grads"], r["grads"])):
+            gh.close_grad(a, b_, "offset-30 grad %d" % k)
