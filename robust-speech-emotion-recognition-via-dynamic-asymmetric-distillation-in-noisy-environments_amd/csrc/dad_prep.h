@@ -118,126 +118,10 @@ __device__ __forceinline__ void dad_prep_rows(const DadPrepArgs& a, int wave, in
   }
 }
 
-// Wide form: one wave per PAIR of rows of one part (clean, or noisy), so that every store is 16 B
-// per lane (the row form above stores 8 B per lane: 1.5 output rows of 16 B chunks do not divide
-// a wave).  Lane l handles output chunks c = 64 k + l (k = 0..2) of the pair: row c / 96, columns
-// 8 (c % 96) .. +7 -- two 16-B fp32 loads, one 16-B store per output part.  The counter RNG is
-// keyed by the element pair index, not by the lane, so the values are the row form's.
-template <int NOISE, bool F16, int R>
-__device__ __forceinline__ void dad_prep_pairs(const DadPrepArgs& a, int wave, int nwaves, int lane) {
-  const DadGeom& G = a.g;
-  const int NcAll = G.Bc * G.Tc;
-  const int Nc = a.clean ? NcAll : 0;
-  const int Nn = a.warmup ? 0 : G.Bn * G.Tn;
-  const int Pc = (Nc + 1) >> 1, P = Pc + ((Nn + 1) >> 1);
-  uint16_t* const oc = a.x16;
-  uint16_t* const os = a.x16 + (size_t)NcAll * DAD_D;
-  uint16_t* const ow = os + (size_t)Nn * DAD_D;
-  int rs[3], col[3];
-  uint32_t kb = 0;   // feature keep flags of the lane's 24 columns (I/utils.py:343), bit 8 k + e
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const int c = 64 * k + lane;
-    rs[k] = c >= 96 ? 1 : 0;
-    col[k] = 8 * (c - 96 * rs[k]);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) kb |= (dad_feat_keep(a.u, a.key_feat, col[k] + e, a.feat_p) != 0.0f ? 1u : 0u) << (8 * k + e);
-  }
-  for (int it = wave; it < P; it += R * nwaves) {
-    f32x4 v[R][3][2];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int item = min(it + r * nwaves, P - 1);
-      const bool noisy = item >= Pc;
-      const int Np = noisy ? Nn : Nc, T = noisy ? G.Tn : G.Tc;
-      const int row0 = 2 * (noisy ? item - Pc : item);
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const int u = min(row0 + rs[k], Np - 1);
-        const int b = u / T, t = u - b * T;
-        const float* x = (noisy ? a.xn : a.xc) + dad_src_row(a.src, noisy, b, T, t) * DAD_D + col[k];
-        v[r][k][0] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(x));
-        v[r][k][1] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(x + 4));
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int item = it + r * nwaves;
-      if (item >= P) break;
-      const bool noisy = item >= Pc;
-      const int row0 = 2 * (noisy ? item - Pc : item);
-      if (!noisy) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          const int u = row0 + rs[k];
-          const uint4 o = uint4{dad_pack2<F16>(v[r][k][0][0], v[r][k][0][1]), dad_pack2<F16>(v[r][k][0][2], v[r][k][0][3]),
-                                dad_pack2<F16>(v[r][k][1][0], v[r][k][1][1]), dad_pack2<F16>(v[r][k][1][2], v[r][k][1][3])};
-          if (u < Nc) *reinterpret_cast<uint4*>(oc + (size_t)u * DAD_D + col[k]) = o;
-        }
-        continue;
-      }
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const int un = row0 + rs[k];
-        const int b = un / G.Tn, t = un - b * G.Tn;
-        const int st = a.mask_len > 0 ? dad_prep_tstart<NOISE>(a, min(b, G.Bn - 1)) : -(1 << 30);
-        const bool tzero = t >= st && t < st + a.mask_len;      // I/utils.py:365-372 (padded Tmax)
-        float nw[8], ns[8];
-        if constexpr (NOISE) {
-          const size_t o = (size_t)min(un, Nn - 1) * DAD_D + col[k];
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const f32x4 qw = *reinterpret_cast<const f32x4*>(a.nw + o + 4 * h);
-            const f32x4 qs = *reinterpret_cast<const f32x4*>(a.ns + o + 4 * h);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) { nw[4 * h + e] = qw[e] * a.weak_std; ns[4 * h + e] = qs[e] * a.strong_std; }
-          }
-        } else {
-          const uint32_t p = ((uint32_t)un * (uint32_t)DAD_D + (uint32_t)col[k]) >> 1;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            dad_aug_noise_pair(a.key_weak, p + (uint32_t)q, a.weak_std, nw[2 * q], nw[2 * q + 1]);
-            dad_aug_noise_pair(a.key_strong, p + (uint32_t)q, a.strong_std, ns[2 * q], ns[2 * q + 1]);
-          }
-        }
-        // reference op order: x + std*N, then * feature mask, then temporal zero
-        float w[8], sv[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float x = v[r][k][e >> 2][e & 3];
-          w[e] = x + nw[e];
-          sv[e] = (x + ns[e]) * (((kb >> (8 * k + e)) & 1u) ? 1.0f : 0.0f);
-        }
-        if (un < Nn) {
-          *reinterpret_cast<uint4*>(ow + (size_t)un * DAD_D + col[k]) =
-              uint4{dad_pack2<F16>(w[0], w[1]), dad_pack2<F16>(w[2], w[3]), dad_pack2<F16>(w[4], w[5]), dad_pack2<F16>(w[6], w[7])};
-          const uint4 so = uint4{dad_pack2<F16>(sv[0], sv[1]), dad_pack2<F16>(sv[2], sv[3]), dad_pack2<F16>(sv[4], sv[5]),
-                                 dad_pack2<F16>(sv[6], sv[7])};
-          *reinterpret_cast<uint4*>(os + (size_t)un * DAD_D + col[k]) = tzero ? uint4{0u, 0u, 0u, 0u} : so;
-        }
-      }
-    }
-  }
-}
-
-#ifndef DAD_PREP_WIDE
-#define DAD_PREP_WIDE 1
-#endif
-
 // runtime dispatch on the set's precision and draw source (wave-uniform)
 template <int R>
 __device__ __forceinline__ void dad_prep_dispatch(const DadPrepArgs& a, int wave, int nwaves, int lane) {
   const bool noise = a.nw != nullptr;
-#if DAD_PREP_WIDE
-  constexpr int RW = (R + 1) / 2;   // pairs in flight: the row form's bytes in flight
-  if (a.f16) {
-    if (noise) dad_prep_pairs<1, true, RW>(a, wave, nwaves, lane);
-    else dad_prep_pairs<0, true, RW>(a, wave, nwaves, lane);
-  } else {
-    if (noise) dad_prep_pairs<1, false, RW>(a, wave, nwaves, lane);
-    else dad_prep_pairs<0, false, RW>(a, wave, nwaves, lane);
-  }
-#else
   if (a.f16) {
     if (noise) dad_prep_rows<1, true, R>(a, wave, nwaves, lane);
     else dad_prep_rows<0, true, R>(a, wave, nwaves, lane);
@@ -245,5 +129,4 @@ __device__ __forceinline__ void dad_prep_dispatch(const DadPrepArgs& a, int wave
     if (noise) dad_prep_rows<1, false, R>(a, wave, nwaves, lane);
     else dad_prep_rows<0, false, R>(a, wave, nwaves, lane);
   }
-#endif
 }

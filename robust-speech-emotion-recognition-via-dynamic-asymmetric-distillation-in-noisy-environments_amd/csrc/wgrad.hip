@@ -321,6 +321,10 @@ __global__ __launch_bounds__(DAD_WGRAD_THREADS) void dad_wgrad_f32(DadWgradArgs 
 // two per h (its largest |v| over the split's utterances maps into [2^14, 2^15): 11 significant
 // bits and no overflow or subnormals for values within 2^-28 of the largest), and row h of the
 // partial is multiplied by 2^-s_h (exact) before it is stored.
+// (The encoder's ping-pong schedule -- one group multiplies under s_setprio while the other builds
+// operands, one barrier per phase -- measured slower here in round 5: 29.5-30.1 against 23.2-23.8
+// us; a phase of 8 MFMAs is 256 cycles, and the barrier per phase cost more than the overlap won:
+// stamps per round 250 operand + 412 MFMA cycles and ~880 waiting at the two barriers.)
 // Software pipeline, one barrier per TWO rounds: round j computes slab j from LDS buffer j&3
 // while it stages slab j+2 into buffer (j+2)&3 and issues the loads of slab j+2+WGD_DEPTH,
 // all in one basic block so the staging VALU fills the MFMA gaps.  dL/de_u[h] / len_u of the
