@@ -617,7 +617,8 @@ def rooflines(ktimes, rows_c, rows_n, ms_step, precision, tail_name="dad_tail_ec
     t_roof = max(step_flops / (peak_tf * 1e12), src_bytes / (HBM_PEAK_GBS * 1e9))
     srf = {"t_roof_us": t_roof * 1e6, "t_step_us": ms_step * 1e3, "frac": t_roof / (ms_step * 1e-3),
            "flops_per_step": step_flops, "bytes_per_step": src_bytes, "mfma_peak_tflops": peak_tf}
-    tr = step_traffic([names[k] for k in ("encode", "pool", "wgrad", "reduce", "optim")] +
+    # the step's launches (dad_pool only when it runs: the wave-centric tail launch pools itself)
+    tr = step_traffic([names[k] for k in ("encode", "pool", "wgrad", "reduce", "optim") if k in ktimes] +
                       ([tail_name] if tail_name in (pmc_summary_kernels() or ()) else []))
     if tr is not None:
         srf["step_traffic_bytes"] = tr["bytes"]

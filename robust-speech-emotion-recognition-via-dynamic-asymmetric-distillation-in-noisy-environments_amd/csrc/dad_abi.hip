@@ -69,6 +69,9 @@ inline Keys keys_of(const dad_config* c) {
 }
 
 // DAD_TAIL_W=0 selects the general tail + ECDA launch for every batch (A/B runs; read once)
+#ifndef DAD_POOL_IN_TAIL
+#define DAD_POOL_IN_TAIL 1   // 0: the separate dad_pool launch also before the wave-centric tail (A/B builds)
+#endif
 bool tail_w_on() {
   static const bool on = [] { const char* e = getenv("DAD_TAIL_W"); return !(e && strcmp(e, "0") == 0); }();
   return on;
@@ -237,6 +240,7 @@ int dad_timing_kernels(unsigned mask) {
   unsigned pts = 0;
   for (int k = 0; k < DAD_TK_KERNELS; ++k)
     if ((mask >> k) & 1u) pts |= (1u << kTkPairs[k][0]) | (1u << kTkPairs[k][1]);
+  if (pts & (1u << TK_POOL)) pts |= 1u << TK_E1;   // the tail's start when pooling is fused into it
   g_tk.points = pts;
   return DAD_OK;
 }
@@ -250,7 +254,10 @@ int dad_timing_stop(double* ms_sum, int* count, int n) {
   for (int s = 0; s < g_tk.used && rc == DAD_OK; ++s) {
     const size_t b = (size_t)s * TK_N;
     for (int k = 0; k < n && k < DAD_TK_KERNELS; ++k) {
-      const int a = pairs[k][0], z = pairs[k][1];
+      int a = pairs[k][0];
+      const int z = pairs[k][1];
+      // pooling fused into the tail launch: no pool point; the tail launch runs from the encoder's end
+      if (a == TK_POOL && !g_tk.rec[b + a] && z != TK_POOL) a = TK_E1;
       if (!g_tk.rec[b + a] || !g_tk.rec[b + z]) continue;
       float ms = 0.0f;
       hipError_t e = hipEventSynchronize(g_tk.ev[b + z]);
@@ -375,6 +382,11 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   float* ecda_scratch = ws_ptr<float>(workspace, L.ecda);
   float* gzb = ws_ptr<float>(workspace, L.gzb);
   uint32_t* eflag = ws_ptr<uint32_t>(workspace, L.eflag);
+  uint32_t* pool_ready = ws_ptr<uint32_t>(workspace, L.ready);
+  // the wave-centric tail launch (B, Bn <= 64, class-aware MMD, after the warm-up) also pools the
+  // embeddings (dad_tail_ecda_w's spare blocks) instead of a separate dad_pool launch
+  const bool tail_w = !cfg->warmup && DAD_FUSED_TAIL && G.Bc <= 64 && Bn <= 64 && cfg->class_aware && tail_w_on();
+  const bool pool_in_tail = tail_w && DAD_POOL_IN_TAIL;
   const bool h16 = dad_prec16(cfg->precision);
   const bool f16 = cfg->precision == DAD_PREC_FP16;
   // 16-bit modes: this step's prepared set (parity of the step counter; the next step's set is
@@ -392,6 +404,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   ea.w1_teacher = st->teacher + DAD_OFF_W1; ea.b1_teacher = st->teacher + DAD_OFF_B1;
   ea.w1h_student = st->w1bf_student;
   ea.w1h_teacher = st->w1bf_teacher;
+  ea.pool_ready = pool_ready;
   if (explicit_rng) { ea.nw = bt->nw; ea.ns = bt->ns; ea.u = bt->u; ea.start = bt->start; }
   ea.key_weak = k.weak; ea.key_strong = k.strong; ea.key_feat = k.feat; ea.key_tstart = k.tstart;
   ea.weak_std = cfg->weak_std; ea.strong_std = cfg->strong_std; ea.feat_p = cfg->feat_p;
@@ -438,9 +451,14 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   pa.part_cnt = part_cnt; pa.cnt_tot = cnt_tot;
   pa.eflag = eflag; pa.tail_terms = st->tail + DAD_T_ECDA_TERM;
   pa.range_flag = reinterpret_cast<uint32_t*>(st->tail + DAD_T_RANGE);
-  hipLaunchKernelGGL(dad_pool, dim3(G.Bc + 2 * Bn), dim3(DAD_POOL_THREADS), 0, stream, pa);
-  DAD_TRY(hipGetLastError());
-  tk_mark(TK_POOL, stream);
+  if (pool_in_tail) {
+    pa.ready = pool_ready;   // pooled by the tail launch (zeroed by this step's encoder); no pool
+                             // timing point: the tail launch is timed from the encoder's end
+  } else {
+    hipLaunchKernelGGL(dad_pool, dim3(G.Bc + 2 * Bn), dim3(DAD_POOL_THREADS), 0, stream, pa);
+    DAD_TRY(hipGetLastError());
+    tk_mark(TK_POOL, stream);
+  }
 
   // 3. losses, DACP mask, analytic backward to dL/de and the classifier grads
   DadTailArgs ta;
@@ -458,21 +476,22 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   ca.tail_terms = st->tail + DAD_T_ECDA_TERM; ca.ge = ge_ecda; ca.scratch = ecda_scratch; ca.eflag = eflag;
   ca.sink = ws_ptr<float>(workspace, L.gflat);
   if (!cfg->warmup && DAD_FUSED_TAIL) {
-    // batches of at most 64 utterances per side, class-aware MMD: the wave-centric launch
-    if (G.Bc <= 64 && Bn <= 64 && cfg->class_aware && tail_w_on()) {
-      // + the next step's row preparation on the CUs the tail and class blocks leave idle
-      DadPrepArgs pa;
-      memset(&pa, 0, sizeof(pa));
-      int nblk = 1 + DAD_C;
+    // batches of at most 64 utterances per side, class-aware MMD: the wave-centric launch, whose
+    // spare blocks pool the embeddings (one item per wave: Bc + 2 Bn items) and then run
+    if (tail_w) {
+      // the next step's row preparation on the CUs the tail and class blocks leave idle
+      DadPrepArgs pp;
+      memset(&pp, 0, sizeof(pp));
+      int nblk = 1 + DAD_C + (pool_in_tail ? (G.Bc + 2 * Bn + DAD_TAIL_THREADS / 64 - 1) / (DAD_TAIL_THREADS / 64) : 0);
       if (can_prepare_ahead(cfg, ncfg, nbt)) {
         int cus = 0;
         const int rc = device_cus(&cus);
         if (rc) return rc;
-        pa = prep_args(ncfg, nbt, ws_ptr<uint16_t>(workspace, L.xs16 + (ncfg->counter & 1u) * L.x16set));
-        nblk = std::max(cus, 2 * (1 + DAD_C));
+        pp = prep_args(ncfg, nbt, ws_ptr<uint16_t>(workspace, L.xs16 + (ncfg->counter & 1u) * L.x16set));
+        nblk = std::max(nblk, std::max(cus, 2 * (1 + DAD_C)));
         if (prepped) *prepped = 1;
       }
-      hipLaunchKernelGGL(dad_tail_ecda_w, dim3(nblk), dim3(DAD_TAIL_THREADS), 0, stream, ta, ca, pa);
+      hipLaunchKernelGGL(dad_tail_ecda_w, dim3(nblk), dim3(DAD_TAIL_THREADS), 0, stream, ta, ca, pp, pa);
     } else
       hipLaunchKernelGGL(dad_tail_ecda, dim3(1 + DAD_C), dim3(DAD_TAIL_THREADS), 0, stream, ta, ca);
     DAD_TRY(hipGetLastError());

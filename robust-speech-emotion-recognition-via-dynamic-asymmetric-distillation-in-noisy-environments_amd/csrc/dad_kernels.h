@@ -54,6 +54,8 @@ struct DadPoolArgs {
   uint32_t* eflag;        // [Bc+Bn] ECDA row flags, zeroed here (ECDA flags the rows it writes)
   float* tail_terms;      // per-class ECDA terms + gates, zeroed here (block 0)
   uint32_t* range_flag;   // sticky: set when a pooled embedding is not finite (tail header DAD_T_RANGE)
+  uint32_t* ready;        // pooling fused into dad_tail_ecda_w: pool items done (zeroed by the
+                          // step's encoder); NULL: the separate dad_pool launch
 };
 
 struct DadEncodeArgs {
@@ -75,6 +77,7 @@ struct DadEncodeArgs {
   // the prepared 16-bit rows (dad_prep) of the clean, strong and weak branches, [B][T][768] each
   // (padded layout whatever the source mode)
   const uint16_t* x16c; const uint16_t* x16s; const uint16_t* x16w;
+  uint32_t* pool_ready;     // workgroup 0 zeroes it: the counter of the tail launch's fused pooling
 };
 
 // The weight-independent half of the 16-bit encoder (prep.hip, dad_prep.h): augmentation
@@ -182,8 +185,9 @@ __global__ void dad_pool(DadPoolArgs a);
 __global__ void dad_tail(DadTailArgs a);
 __global__ void dad_ecda(DadEcdaArgs a);
 __global__ void dad_tail_ecda(DadTailArgs ta, DadEcdaArgs ca);
-// B, Bn <= 64, class-aware; blocks > DAD_C prepare the next step's set (pa.x16 != NULL)
-__global__ void dad_tail_ecda_w(DadTailArgs ta, DadEcdaArgs ca, DadPrepArgs pa);
+// B, Bn <= 64, class-aware; blocks > DAD_C pool the step's embeddings first (pl.ready != NULL)
+// and then prepare the next step's set (pa.x16 != NULL)
+__global__ void dad_tail_ecda_w(DadTailArgs ta, DadEcdaArgs ca, DadPrepArgs pa, DadPoolArgs pl);
 __global__ void dad_wgrad_f32(DadWgradArgs a, DadReduceArgs r);   // r: the fused step's dL/de sources (gzb) or zeroed
 __global__ void dad_wgrad_direct(DadWgradArgs a, DadReduceArgs r);       // bf16 operands
 __global__ void dad_wgrad_direct_f16(DadWgradArgs a, DadReduceArgs r);   // fp16 operands

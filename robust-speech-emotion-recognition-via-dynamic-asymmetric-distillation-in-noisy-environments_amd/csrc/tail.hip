@@ -83,11 +83,27 @@ __device__ __forceinline__ double block_sum_d(double v, double* red) {
 // issued 48 dword loads per thread and joined its 4 waves through LDS twice).  Embeddings sum
 // the slab partials in slab order (I/model.py:35-36 masked mean pooling); logits
 // W2 . dropout(e) + b2 (I/model.py:54-64; the teacher classifier's dropout is off).
+//
+// The same item runs in dad_tail_ecda_w's spare workgroups (SC1 = true: the tail and class
+// blocks of that launch read the results after a counter hand-off, so every store is
+// write-through, MI355X_MICROARCH.md "Valid forms").
 static_assert(DAD_POOL_THREADS == 64 && DAD_H == 4 * 64, "dad_pool: one wave, 4 hidden units per lane");
-__global__ __launch_bounds__(DAD_POOL_THREADS) void dad_pool(DadPoolArgs a) {
-  DAD_GUARD_BLOCK(DAD_POOL_THREADS);
+
+template <bool SC1>
+__device__ __forceinline__ void pool_st4(float* p, const f32x4& v) {
+  if constexpr (SC1) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+  else *reinterpret_cast<f32x4*>(p) = v;
+}
+template <bool SC1, class T>
+__device__ __forceinline__ void pool_st1(T* p, T v) {
+  if constexpr (SC1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+
+// pool item blk (one wave, lane = 0..63): what one dad_pool workgroup does
+template <bool SC1>
+__device__ __forceinline__ void pool_item(const DadPoolArgs& a, const int blk, const int lane) {
   const DadGeom& g = a.g;
-  const int blk = blockIdx.x, lane = threadIdx.x;
   const int kind = blk < g.Bc ? 0 : (blk < g.Bc + g.Bn ? 1 : 2);   // clean, teacher (weak), student (strong)
   const int b = kind == 0 ? blk : (kind == 1 ? blk - g.Bc : blk - g.Bc - g.Bn);
   const bool noisy = kind != 0, teacher = kind == 1;
@@ -156,13 +172,14 @@ __global__ __launch_bounds__(DAD_POOL_THREADS) void dad_pool(DadPoolArgs a) {
   f32x4 e;
 #pragma unroll
   for (int k = 0; k < 4; ++k) e[k] = ssum[k] / fmaxf(len, 1.0f);
-  *reinterpret_cast<f32x4*>(a.emb + (size_t)erow * DAD_H + h0) = e;
+  pool_st4<SC1>(a.emb + (size_t)erow * DAD_H + h0, e);
   const f32x4 d = teacher ? e : e * kv;
   float zp[DAD_C];
 #pragma unroll
   for (int c = 0; c < DAD_C; ++c)
     zp[c] = dad_wave_sum(((w2[c][0] * d[0] + w2[c][1] * d[1]) + w2[c][2] * d[2]) + w2[c][3] * d[3]);
-  if (lane < DAD_C) a.logits[(size_t)erow * DAD_C + lane] = (lane == 0 ? zp[0] : (lane == 1 ? zp[1] : (lane == 2 ? zp[2] : zp[3]))) + bias;
+  if (lane < DAD_C)
+    pool_st1<SC1>(a.logits + (size_t)erow * DAD_C + lane, (lane == 0 ? zp[0] : (lane == 1 ? zp[1] : (lane == 2 ? zp[2] : zp[3]))) + bias);
   // range check: a non-finite embedding or logit sets the sticky flag.  In FP16 steps an encoder
   // operand beyond +-65504 converts to inf, which turns every pre-activation of its row into
   // +-inf or NaN: the +inf units survive the ReLU into the pooled sum.
@@ -175,13 +192,44 @@ __global__ __launch_bounds__(DAD_POOL_THREADS) void dad_pool(DadPoolArgs a) {
     // the length, and the ECDA row flag (clean b / noisy Bc + b) starts at zero: the ECDA
     // workgroups write only what they own
     const int urow = noisy ? g.Bc + b : b;
-    *reinterpret_cast<f32x4*>(a.cnt_tot + (size_t)urow * DAD_H + h0) = cnt;
+    pool_st4<SC1>(a.cnt_tot + (size_t)urow * DAD_H + h0, cnt);
     if (lane == 0) {
-      a.vlen[urow] = len;
-      a.eflag[urow] = 0u;
+      pool_st1<SC1>(a.vlen + urow, len);
+      pool_st1<SC1>(a.eflag + urow, 0u);
     }
   }
-  if (blk == 0 && lane < 2 * DAD_C) a.tail_terms[lane] = 0.0f;   // per-class ECDA terms and gates
+  if (blk == 0 && lane < 2 * DAD_C) pool_st1<SC1>(a.tail_terms + lane, 0.0f);   // per-class ECDA terms and gates
+}
+
+__global__ __launch_bounds__(DAD_POOL_THREADS) void dad_pool(DadPoolArgs a) {
+  DAD_GUARD_BLOCK(DAD_POOL_THREADS);
+  pool_item<false>(a, (int)blockIdx.x, (int)threadIdx.x);
+}
+
+// Fused pooling hand-off (dad_tail_ecda_w): each pooling wave stores its item write-through (sc1),
+// drains (s_waitcnt vmcnt(0)) and adds 1 to the counter; a tail / class block polls the counter
+// (one lane, sc1 loads), then ONE agent-scope acquire, a drain and a barrier before any of its
+// waves loads (MI355X_MICROARCH.md "Valid forms": producer sc1 stores, consumer poll + acquire).
+// The poll is bounded (~0.1 s); on timeout it sets the range flag and goes on (wrong numbers
+// instead of a hung device).
+__device__ __forceinline__ void pool_publish(uint32_t* ready, int lane) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (lane == 0) __hip_atomic_fetch_add(ready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void pool_wait(uint32_t* ready, uint32_t n, uint32_t* range_flag) {
+  if (threadIdx.x == 0) {
+    uint32_t spins = 0;
+    while (__hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < n) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1u << 22)) {
+        if (range_flag) __hip_atomic_fetch_or(range_flag, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
 }
 
 // ------------------------------------------------------------------------------ tail
@@ -2173,26 +2221,37 @@ __device__ __forceinline__ void ecda_block_w(const DadEcdaArgs& a, const DadTail
 }
 
 // block 0: the wave-centric tail; blocks 1..C: ECDA class blockIdx.x - 1.  Host contract:
-// B <= 64, Bn <= 64, class-aware MMD (dad_tail_ecda otherwise).  Blocks > C (when pa.x16 is set):
+// B <= 64, Bn <= 64, class-aware MMD (dad_tail_ecda otherwise).  Blocks > C pool the step's
+// embeddings and logits first (pl.ready set; the tail and class blocks wait for them: pool_wait),
+// which saves the separate dad_pool launch and its boundary.  Then (when pa.x16 is set):
 // the NEXT step's row preparation (dad_prep.h) on the CUs the tail and the class blocks leave
 // idle; it reads only the next batch and writes only the other prepared set, so it overlaps this
 // step's latency-bound tail and ECDA.  The tail and class blocks have the lowest block ids, so
 // they are dispatched first and never wait for a CU behind the preparation blocks.
-__global__ __launch_bounds__(TAIL_THREADS) void dad_tail_ecda_w(DadTailArgs ta, DadEcdaArgs ca, DadPrepArgs pa) {
+__global__ __launch_bounds__(TAIL_THREADS) void dad_tail_ecda_w(DadTailArgs ta, DadEcdaArgs ca, DadPrepArgs pa,
+                                                                  DadPoolArgs pl) {
   DAD_GUARD_BLOCK(TAIL_THREADS);
   __shared__ union UW {
     TailW t;
     EcdaW e;
   } u;
+  // fused pooling (pl.ready): the Bc + 2 Bn pool items (dad_pool's workgroups) on the spare
+  // blocks' waves, item i on block i mod nx, wave i / nx (one item per CU first)
+  const int nitems = pl.ready ? pl.g.Bc + 2 * pl.g.Bn : 0;
   if ((int)blockIdx.x > DAD_C) {
-    if (!pa.x16) return;
     constexpr int kWaves = TAIL_THREADS / 64;
     const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-    dad_prep_dispatch<2>(pa, ((int)blockIdx.x - 1 - DAD_C) * kWaves + w, ((int)gridDim.x - 1 - DAD_C) * kWaves,
-                         (int)threadIdx.x & 63);
+    const int nx = (int)gridDim.x - 1 - DAD_C, xb = (int)blockIdx.x - 1 - DAD_C;
+    for (int i = xb + nx * w; i < nitems; i += nx * kWaves) {
+      pool_item<true>(pl, i, (int)threadIdx.x & 63);
+      pool_publish(pl.ready, (int)threadIdx.x & 63);
+    }
+    if (!pa.x16) return;
+    dad_prep_dispatch<2>(pa, xb * kWaves + w, nx * kWaves, (int)threadIdx.x & 63);
     return;
   }
   if (ta.cfg.B > TW_MAXB || ta.cfg.Bn > TW_MAXB) return;
+  if (nitems) pool_wait(pl.ready, (uint32_t)nitems, pl.range_flag);
   if (blockIdx.x == 0) tail_block_w(ta, u.t);
   else ecda_block_w(ca, ta, (int)blockIdx.x - 1, u.e);
 }
