@@ -69,6 +69,9 @@ inline Keys keys_of(const dad_config* c) {
 }
 
 // DAD_TAIL_W=0 selects the general tail + ECDA launch for every batch (A/B runs; read once)
+#ifndef DAD_CLEAN_IN_WGRAD
+#define DAD_CLEAN_IN_WGRAD 1  // 0: the next batch's clean rows also prepared in the tail launch (A/B builds)
+#endif
 #ifndef DAD_POOL_IN_TAIL
 #define DAD_POOL_IN_TAIL 1   // 0: the separate dad_pool launch also before the wave-centric tail (A/B builds)
 #endif
@@ -475,6 +478,11 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   ca.cfg = *cfg; ca.yc = bt->yc; ca.emb = st->emb; ca.tailf = st->tail;
   ca.tail_terms = st->tail + DAD_T_ECDA_TERM; ca.ge = ge_ecda; ca.scratch = ecda_scratch; ca.eflag = eflag;
   ca.sink = ws_ptr<float>(workspace, L.gflat);
+  // next-batch preparation split (padded next batch): its noisy rows in the tail launch, its clean
+  // rows in the weight-gradient launch (dad_wgrad_direct*_cp, interleaved with the GEMM)
+  DadPrepArgs pcw;
+  memset(&pcw, 0, sizeof(pcw));
+  bool clean_in_wgrad = false;
   if (!cfg->warmup && DAD_FUSED_TAIL) {
     // batches of at most 64 utterances per side, class-aware MMD: the wave-centric launch, whose
     // spare blocks pool the embeddings (one item per wave: Bc + 2 Bn items) and then run
@@ -490,6 +498,11 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
         pp = prep_args(ncfg, nbt, ws_ptr<uint16_t>(workspace, L.xs16 + (ncfg->counter & 1u) * L.x16set));
         nblk = std::max(nblk, std::max(cus, 2 * (1 + DAD_C)));
         if (prepped) *prepped = 1;
+        if (DAD_CLEAN_IN_WGRAD && h16 && nbt->rowc == nullptr) {
+          clean_in_wgrad = true;
+          pcw = pp;        // clean rows only (dad_prep_clean_load / _store)
+          pp.clean = 0;    // noisy rows only
+        }
       }
       hipLaunchKernelGGL(dad_tail_ecda_w, dim3(nblk), dim3(DAD_TAIL_THREADS), 0, stream, ta, ca, pp, pa);
     } else
@@ -544,8 +557,13 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
     wa.ntiles = WGD_NDB * splits;
     // multiple of 8 (XCD-aware tile order) with WGD_XWG spare workgroups for the extra blocks
     const dim3 grid((wa.ntiles + WGD_XWG + 7) / 8 * 8);
-    if (f16) hipLaunchKernelGGL(dad_wgrad_direct_f16, grid, dim3(WGD_THREADS), 0, stream, wa, ra);
-    else hipLaunchKernelGGL(dad_wgrad_direct, grid, dim3(WGD_THREADS), 0, stream, wa, ra);
+    if (clean_in_wgrad) {
+      if (f16) hipLaunchKernelGGL(dad_wgrad_direct_f16_cp, grid, dim3(WGD_THREADS), 0, stream, wa, ra, pcw);
+      else hipLaunchKernelGGL(dad_wgrad_direct_cp, grid, dim3(WGD_THREADS), 0, stream, wa, ra, pcw);
+    } else {
+      if (f16) hipLaunchKernelGGL(dad_wgrad_direct_f16, grid, dim3(WGD_THREADS), 0, stream, wa, ra);
+      else hipLaunchKernelGGL(dad_wgrad_direct, grid, dim3(WGD_THREADS), 0, stream, wa, ra);
+    }
     DAD_TRY(hipGetLastError());
     tk_mark(TK_WGRAD, stream);
     hipLaunchKernelGGL(dad_reduce_w, dim3(DAD_REDUCE_BLOCKS - DAD_REDUCE_XBLK), dim3(64), 0, stream, ra);

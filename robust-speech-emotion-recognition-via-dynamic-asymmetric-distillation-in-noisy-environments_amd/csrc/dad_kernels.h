@@ -191,6 +191,9 @@ __global__ void dad_tail_ecda_w(DadTailArgs ta, DadEcdaArgs ca, DadPrepArgs pa, 
 __global__ void dad_wgrad_f32(DadWgradArgs a, DadReduceArgs r);   // r: the fused step's dL/de sources (gzb) or zeroed
 __global__ void dad_wgrad_direct(DadWgradArgs a, DadReduceArgs r);       // bf16 operands
 __global__ void dad_wgrad_direct_f16(DadWgradArgs a, DadReduceArgs r);   // fp16 operands
+// the same, also converting the NEXT step's clean rows into its prepared set (dad_prep.h, pc.clean)
+__global__ void dad_wgrad_direct_cp(DadWgradArgs a, DadReduceArgs r, DadPrepArgs pc);
+__global__ void dad_wgrad_direct_f16_cp(DadWgradArgs a, DadReduceArgs r, DadPrepArgs pc);
 __global__ void dad_reduce(DadReduceArgs a);
 __global__ void dad_reduce_w(DadReduceArgs a);
 __global__ void dad_norm(float* grad, float* normpart, float inv_world);

@@ -31,6 +31,11 @@
 #pragma once
 #include "dad_kernels.h"
 
+// (plain stores: non-temporal stores of the prepared rows measured slower in round 5 -- encoder
+// 27.9-28.2 -> 29.2-29.6 us, the tail launch unchanged -- because the encoder then reads them from
+// HBM instead of the Infinity Cache)
+__device__ __forceinline__ void dad_prep_st(char* p, uint2 v) { *reinterpret_cast<uint2*>(p) = v; }
+
 template <int NOISE>
 __device__ __forceinline__ int dad_prep_tstart(const DadPrepArgs& a, int b) {
   if (NOISE) return (int)a.start[b];
@@ -74,8 +79,7 @@ __device__ __forceinline__ void dad_prep_rows(const DadPrepArgs& a, int wave, in
         char* o = reinterpret_cast<char*>(oc + (size_t)u * DAD_D + 4 * lane);
 #pragma unroll
         for (int k = 0; k < 3; ++k)
-          *reinterpret_cast<uint2*>(o + 512 * k) =
-              uint2{dad_pack2<F16>(v[r][k][0], v[r][k][1]), dad_pack2<F16>(v[r][k][2], v[r][k][3])};
+          dad_prep_st(o + 512 * k, uint2{dad_pack2<F16>(v[r][k][0], v[r][k][1]), dad_pack2<F16>(v[r][k][2], v[r][k][3])});
         continue;
       }
       const int un = u - Nc;
@@ -110,9 +114,9 @@ __device__ __forceinline__ void dad_prep_rows(const DadPrepArgs& a, int wave, in
           w[e] = v[r][k][e] + nw[e];
           s[e] = (v[r][k][e] + ns[e]) * kp[k][e];
         }
-        *reinterpret_cast<uint2*>(o_w + 512 * k) = uint2{dad_pack2<F16>(w[0], w[1]), dad_pack2<F16>(w[2], w[3])};
+        dad_prep_st(o_w + 512 * k, uint2{dad_pack2<F16>(w[0], w[1]), dad_pack2<F16>(w[2], w[3])});
         const uint2 so = uint2{dad_pack2<F16>(s[0], s[1]), dad_pack2<F16>(s[2], s[3])};
-        *reinterpret_cast<uint2*>(o_s + 512 * k) = tzero ? uint2{0u, 0u} : so;
+        dad_prep_st(o_s + 512 * k, tzero ? uint2{0u, 0u} : so);
       }
     }
   }
@@ -129,4 +133,29 @@ __device__ __forceinline__ void dad_prep_dispatch(const DadPrepArgs& a, int wave
     if (noise) dad_prep_rows<1, false, R>(a, wave, nwaves, lane);
     else dad_prep_rows<0, false, R>(a, wave, nwaves, lane);
   }
+}
+
+// One CLEAN row of a prepared set in two halves, for callers that interleave it with other work
+// (the weight-gradient launch, dad_wgrad_direct: its loads go out in one round, the conversion and
+// stores a few rounds later): row u of [Bc*Tc] (clamped for the load, not stored past the end);
+// lane l owns columns 256k + 4l .. +3 as in dad_prep_rows (no RNG on the clean rows).  Padded
+// batches only (a.src.rowc == NULL): source row u is row u of xc, with no table lookup (a dependent
+// load there would drain the caller's loads in flight).
+__device__ __forceinline__ void dad_prep_clean_load(const DadPrepArgs& a, int u, int lane, f32x4 (&v)[3]) {
+  const int uc = min(u, a.g.Bc * a.g.Tc - 1);
+  const float* x = a.xc + (size_t)uc * DAD_D + 4 * lane;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) v[k] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(x + 256 * k));
+}
+// (a row past the end was loaded as the last row and is stored there again: the same bytes, so the
+// stores need no condition -- a conditional memory operation inside the caller's pipelined loop
+// would make hipcc drain the loads in flight where the paths merge)
+// F16: the set's precision (a.f16; the caller's compile-time copy, so no branch sits between stores)
+template <bool F16>
+__device__ __forceinline__ void dad_prep_clean_store(const DadPrepArgs& a, int u, int lane, const f32x4 (&v)[3]) {
+  const int uc = min(u, a.g.Bc * a.g.Tc - 1);
+  char* o = reinterpret_cast<char*>(a.x16 + (size_t)uc * DAD_D + 4 * lane);
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+    dad_prep_st(o + 512 * k, uint2{dad_pack2<F16>(v[k][0], v[k][1]), dad_pack2<F16>(v[k][2], v[k][3])});
 }

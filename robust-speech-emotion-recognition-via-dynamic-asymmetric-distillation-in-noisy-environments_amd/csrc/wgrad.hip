@@ -14,6 +14,7 @@
 
 #include "dad_common.h"
 #include "dad_kernels.h"
+#include "dad_prep.h"
 #include "dad_probe.h"
 
 namespace {
@@ -513,9 +514,15 @@ __device__ __forceinline__ int wgd_f16_exp(float max_abs) {
 // per two rounds (eight buffers and a barrier every four rounds measured neutral, round 3)
 constexpr int WGD_NBUF = 4;
 // one 256 h x WGD_DB d tile over slabs [s0, s1): fp32 partial
-template <bool F16>
+// CP: this launch also converts the NEXT step's clean rows into its prepared set (pc, when the
+// step names its next batch): wave gw of GW takes rows gw, gw + GW, ...; two rows' loads go out in
+// the first round of each block of NB rounds and are converted and stored at the start of the next
+// block (an HBM miss under this load takes about as long as NB rounds); the rows left after the
+// loop follow it.
+template <bool F16, bool CP>
 __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceArgs& ra, int s0, int s1, int dbase,
-                                         float* outf, uint16_t* Xt, const uint4* lut, uint16_t* gs, float* red) {
+                                         float* outf, uint16_t* Xt, const uint4* lut, uint16_t* gs, float* red,
+                                         const DadPrepArgs& pc, int gw, int GW) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane((tid >> 6) & 3);
   const int grp = __builtin_amdgcn_readfirstlane(tid >> 8);
@@ -674,16 +681,50 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
     // the final MFMAs.  Both groups run the same rounds, so the barriers match.
     round(0, 0, false, mine > 0, SD < mine, false);
     int j = 1;
+    int prow = gw;        // CP: this wave's next clean row of the next step
+    f32x4 pv[2][3];
+    bool pending = false; // CP: rows prow - 2 GW, prow - GW loaded, not yet stored
     for (; j + NB - 1 + SD < cntmin; j += NB) {   // every round stages slab j + k + SD < cntmin
 #pragma unroll
-      for (int k = 0; k < NB; ++k) round(j + k, (k + 1) % NB, true, true, true, (k + 1) % SD == SD - 1);
+      for (int k = 0; k < NB; ++k) {
+        if constexpr (CP) {
+          if (k == 0) {
+            // the rows loaded one block (NB rounds) ago, then this block's two
+            if (pending) {
+              dad_prep_clean_store<F16>(pc, prow - 2 * GW, lane, pv[0]);
+              dad_prep_clean_store<F16>(pc, prow - GW, lane, pv[1]);
+            }
+            dad_prep_clean_load(pc, prow, lane, pv[0]);
+            dad_prep_clean_load(pc, prow + GW, lane, pv[1]);
+            prow += 2 * GW;
+            pending = true;
+          }
+        }
+        round(j + k, (k + 1) % NB, true, true, true, (k + 1) % SD == SD - 1);
+      }
     }
 #pragma unroll
     for (int k = 0; k < NB + SD + 1; ++k)   // nround - j <= NB + SD
       if (j + k < nround)
         round(j + k, (k + 1) % NB, j + k - 1 < mine, j + k < mine, j + k + SD < mine, (k + 1) % SD == SD - 1);
     if (nround - 1 < mine) wgd_mma<F16>(F, acc);
+    if constexpr (CP) {
+      if (pending) {
+        dad_prep_clean_store<F16>(pc, prow - 2 * GW, lane, pv[0]);
+        dad_prep_clean_store<F16>(pc, prow - GW, lane, pv[1]);
+      }
+      for (; prow < pc.g.Bc * pc.g.Tc; prow += GW) {   // the rows the loop left
+        dad_prep_clean_load(pc, prow, lane, pv[0]);
+        dad_prep_clean_store<F16>(pc, prow, lane, pv[0]);
+      }
+    }
     t2 = WGD_CLK();
+  } else if constexpr (CP) {
+    for (int prow = gw; prow < pc.g.Bc * pc.g.Tc; prow += GW) {
+      f32x4 pv[3];
+      dad_prep_clean_load(pc, prow, lane, pv);
+      dad_prep_clean_store<F16>(pc, prow, lane, pv);
+    }
   }
   const int kh = lane >> 5;
   if constexpr (WGD_GROUPS == 2) {
@@ -750,8 +791,8 @@ struct __attribute__((aligned(16))) WgdSmem {
 
 __device__ double extra_block(const DadReduceArgs& a, int e, int tid, float (*xs)[16][6]);
 
-template <bool F16>
-__device__ __forceinline__ void wgrad_direct_body(const DadWgradArgs& a, const DadReduceArgs& ra) {
+template <bool F16, bool CP>
+__device__ __forceinline__ void wgrad_direct_body(const DadWgradArgs& a, const DadReduceArgs& ra, const DadPrepArgs& pc) {
   __shared__ WgdSmem S;
   __shared__ __attribute__((aligned(16))) uint16_t gs[WGD_MAXU * DAD_H];
   uint16_t* Xt = S.a.xt;
@@ -789,16 +830,26 @@ __device__ __forceinline__ void wgrad_direct_body(const DadWgradArgs& a, const D
   const int per = (total + a.splits - 1) / a.splits;
   const int s0 = split * per, s1 = min(total, s0 + per);
   wgd_lut(S.lut);   // (the tile's first barrier orders it before the first read)
-  wgd_tile<F16>(a, ra, s0, s1, dblk * WGD_DB, a.wpart + (size_t)split * DAD_H * DAD_D, Xt, S.lut, gs, S.a.red);
+  wgd_tile<F16, CP>(a, ra, s0, s1, dblk * WGD_DB, a.wpart + (size_t)split * DAD_H * DAD_D, Xt, S.lut, gs, S.a.red, pc,
+                    tile * (WGD_THREADS / 64) + (int)(threadIdx.x >> 6), a.ntiles * (WGD_THREADS / 64));
 }
 
 __global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct(DadWgradArgs a, DadReduceArgs ra) {
   DAD_GUARD_BLOCK(WGD_THREADS);
-  wgrad_direct_body<false>(a, ra);
+  wgrad_direct_body<false, false>(a, ra, DadPrepArgs{});
 }
 __global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct_f16(DadWgradArgs a, DadReduceArgs ra) {
   DAD_GUARD_BLOCK(WGD_THREADS);
-  wgrad_direct_body<true>(a, ra);
+  wgrad_direct_body<true, false>(a, ra, DadPrepArgs{});
+}
+__global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct_cp(DadWgradArgs a, DadReduceArgs ra, DadPrepArgs pc) {
+  DAD_GUARD_BLOCK(WGD_THREADS);
+  wgrad_direct_body<false, true>(a, ra, pc);
+}
+__global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct_f16_cp(DadWgradArgs a, DadReduceArgs ra,
+                                                                         DadPrepArgs pc) {
+  DAD_GUARD_BLOCK(WGD_THREADS);
+  wgrad_direct_body<true, true>(a, ra, pc);
 }
 
 // ---------------------------------------------------------------- reduce + squared norms
