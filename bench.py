@@ -429,11 +429,11 @@ TIMED_KERNELS = ["encode"]
 
 
 def timed_kernels(precision, ahead):
-    """The kernel the timed region records events around: the line's dominant launch -- the tail
-    launch when it also prepares the next step's rows (16-bit with next-batch preparation: the
-    longest launch of the step), else the encoder.  The other kernels' times come from the
-    separate eager pass after the timed region."""
-    return ["tail"] if precision != "fp32" and ahead else TIMED_KERNELS
+    """The kernels the timed region records events around: with next-batch preparation (16-bit)
+    the three long launches (encoder; tail launch with the noisy-row preparation; weight gradient
+    with the clean-row conversion, the longest), else the encoder.  The other kernels' times come
+    from the separate eager pass after the timed region."""
+    return ["wgrad", "tail", "encode"] if precision != "fp32" and ahead else TIMED_KERNELS
 
 
 def capture_steps(step, data, epoch, split=None, ahead=False):
@@ -593,27 +593,45 @@ def rooflines(ktimes, rows_c, rows_n, ms_step, precision, tail_name="dad_tail_ec
     wg_flops = 2 * 768 * 256 * (rows_c + rows_n)
     step_flops = 2 * 768 * 256 * (2 * rows_c + 3 * rows_n)
     names = dict(KNAMES[precision], tail=tail_name)
+    if h16 and prepped_ahead:   # the weight gradient that also converts the next batch's clean rows
+        names["wgrad"] = WGRAD_KERNEL[precision][1] + "_cp"
     kern = {}
     for k, (m, n) in sorted(ktimes.items()):
         kern[names.get(k, k)] = {"avg_ms": m, "timed_launches": n}
     if "encode" not in ktimes:
         return None, None, kern
     enc = ktimes["encode"][0]
-    wkey, wname = WGRAD_KERNEL[precision]
+    wkey, wname = "wgrad", names["wgrad"]
     wg = ktimes.get(wkey, (float("nan"), 0))[0]
     ekn = ENC_KERNEL[precision]
     enc_rf = _roof(ekn, enc, enc_bytes, enc_flops, peak_tf)
     enc_rf["timed_launches"] = ktimes["encode"][1]
-    rf = enc_rf
-    if h16 and prepped_ahead and "tail" in ktimes and ktimes["tail"][0] > enc:
-        # the dominant launch is the tail launch carrying the next batch's row preparation: an
-        # HBM stream (the tail and ECDA blocks on 5 CUs run inside it)
-        rf = _roof(tail_name, ktimes["tail"][0], src_bytes, 0.0, peak_tf, bound="hbm",
-                   bytes_moved=src_bytes + prep_bytes,
-                   note="tail + ECDA blocks and the next batch's row preparation (dad_prep) in one launch; "
-                        "algorithmic bytes (SURVEY.md §8(d)) = one step's fp32 features read once; bytes_moved "
-                        "adds the 16-bit prepared rows the design writes")
-        rf["timed_launches"] = ktimes["tail"][1]
+    launch_rf = {"encode": enc_rf}
+    if h16 and prepped_ahead:
+        # the next batch's preparation rides in two launches (padded batches): the tail launch
+        # prepares its noisy rows, the weight gradient converts its clean rows
+        nsrc, csrc = int(rows_n * 768 * 4), int(rows_c * 768 * 4)
+        if "tail" in ktimes:
+            launch_rf["tail"] = _roof(
+                tail_name, ktimes["tail"][0], nsrc, 0.0, peak_tf, bound="hbm",
+                bytes_moved=nsrc + int(2 * rows_n * 768 * 2),
+                note="pooling, tail + ECDA blocks and the next batch's noisy-row preparation in one launch; "
+                     "algorithmic bytes (SURVEY.md §8(d)) = the noisy fp32 features read once; bytes_moved adds "
+                     "their strong and weak 16-bit rows written")
+            launch_rf["tail"]["timed_launches"] = ktimes["tail"][1]
+        if wkey in ktimes:
+            launch_rf["wgrad"] = _roof(
+                wname, wg, csrc, wg_flops, peak_tf,
+                bytes_moved=int((rows_c + rows_n) * 768 * 2) + csrc + int(rows_c * 768 * 2),
+                note="dW1 split-K GEMM and the next batch's clean-row conversion in one launch; algorithmic "
+                     "work = dW1's FLOPs and the clean fp32 features read once; bytes_moved adds the prepared "
+                     "clean + strong rows the GEMM reads and the clean 16-bit rows written (not the split-K "
+                     "partials)")
+            launch_rf["wgrad"]["timed_launches"] = ktimes[wkey][1]
+    # `roofline`: the launch that takes longest
+    dom = max(launch_rf, key=lambda k: launch_rf[k]["avg_launch_ms"])
+    rf = dict(launch_rf[dom])
+    rf["dominant_of"] = {k: round(v["avg_launch_ms"] * 1e3, 2) for k, v in launch_rf.items()}
     t_roof = max(step_flops / (peak_tf * 1e12), src_bytes / (HBM_PEAK_GBS * 1e9))
     srf = {"t_roof_us": t_roof * 1e6, "t_step_us": ms_step * 1e3, "frac": t_roof / (ms_step * 1e-3),
            "flops_per_step": step_flops, "bytes_per_step": src_bytes, "mfma_peak_tflops": peak_tf}
@@ -641,6 +659,7 @@ def rooflines(ktimes, rows_c, rows_n, ms_step, precision, tail_name="dad_tail_ec
             mf[kn]["pmc_stale"] = pk["stale"]
     kern["mfma_util"] = mf
     kern["encoder_roofline"] = enc_rf
+    kern["launch_rooflines"] = launch_rf
     return rf, srf, kern
 
 
@@ -983,12 +1002,12 @@ def main():
     elif args.flavor == "iemocap":
         workload = ("IEMOCAP DAD train step (configs[%d]): batch=64/GPU, T=300x768 synthetic emotion2vec-shaped "
                     "features, post-warm-up epoch %d (CE+KL+ECDA active), counter-RNG augmentation (16-bit modes: prepared for "
-                    "each next step inside the tail launch)"
+                    "each next step inside the tail launch (noisy rows) and the weight-gradient launch (clean rows))"
                     % (1 if world == 1 else 2, args.epoch))
     else:
         workload = ("%s DAD train step%s: batch=%d/GPU, T=%dx768 synthetic features, noisy branch at SNR %g dB, "
                     "post-warm-up epoch %d, counter-RNG augmentation (16-bit modes: prepared for each next step inside the "
-                    "tail launch)"
+                    "tail and weight-gradient launches)"
                     % (args.flavor.upper(), " (configs[3]: DACP+ECDA forced on; SCL is 0 in the reference)"
                        if args.force_ecda else "", B, T, args.snr, args.epoch))
     # per-kernel table: the separate pass, with the timed region's encoder entry
@@ -1001,8 +1020,10 @@ def main():
         src = "encoder: stream events around the encoder graph of every %d-th replayed step" % len(graphs)
     else:
         tk = timed_kernels(args.precision, not args.mixed and not args.no_ahead)[0]
-        src = "%s: HIP events around it in the timed region (every %d-th step)" % (
-            {"tail": "tail launch (the dominant launch)", "encode": "encoder"}[tk], event_every(args.steps))
+        tks = timed_kernels(args.precision, not args.mixed and not args.no_ahead)
+        src = "%s: HIP events around them in the timed region (every %d-th step)" % (
+            ", ".join({"wgrad": "weight gradient (+ clean-row conversion)", "tail": "tail launch (+ pooling, noisy-row "
+                       "preparation)", "encode": "encoder"}[k] for k in tks), event_every(args.steps))
     kern["source"] = ("%s; the other kernels: a separate eager pass of %d steps after it (events at every "
                       "boundary of every 2nd step)" % (src, args.kernel_steps))
     line = {
