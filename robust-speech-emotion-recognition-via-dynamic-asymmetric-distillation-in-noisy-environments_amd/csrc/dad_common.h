@@ -382,7 +382,7 @@ static inline DadWs dad_ws_layout(const DadGeom& g, int splits, int precision) {
   w.xs16 = off;     off = dad_align(off + 2 * w.x16set);
   w.w1h = off;      off = dad_align(off + 2 * (size_t)DAD_H * DAD_D);
   w.gflat = off;    off = dad_align(off + sizeof(float) * DAD_GRAD_FLOATS);
-  w.ready = off;    off = dad_align(off + sizeof(uint32_t));
+  w.ready = off;    off = dad_align(off + 128 * 8);   // DAD_POOL_SHARDS counters, 128 B apart
   w.bytes = off;
   return w;
 }

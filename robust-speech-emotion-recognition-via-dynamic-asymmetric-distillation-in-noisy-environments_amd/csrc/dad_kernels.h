@@ -40,6 +40,8 @@
 #define DAD_GUARD_BLOCK(n) \
   if (blockDim.x != (n) || blockDim.y != 1 || blockDim.z != 1) return
 
+#define DAD_POOL_SHARDS 8   // fused-pooling arrival counters, one per XCD (128 B apart)
+
 struct DadPoolArgs {
   DadGeom g;
   int warmup;
@@ -54,8 +56,9 @@ struct DadPoolArgs {
   uint32_t* eflag;        // [Bc+Bn] ECDA row flags, zeroed here (ECDA flags the rows it writes)
   float* tail_terms;      // per-class ECDA terms + gates, zeroed here (block 0)
   uint32_t* range_flag;   // sticky: set when a pooled embedding is not finite (tail header DAD_T_RANGE)
-  uint32_t* ready;        // pooling fused into dad_tail_ecda_w: pool items done (zeroed by the
-                          // step's encoder); NULL: the separate dad_pool launch
+  uint32_t* ready;        // pooling fused into dad_tail_ecda_w: pool items done, DAD_POOL_SHARDS
+                          // counters 128 B apart (zeroed by the step's encoder); NULL: the
+                          // separate dad_pool launch
 };
 
 struct DadEncodeArgs {

@@ -212,21 +212,29 @@ __global__ __launch_bounds__(DAD_POOL_THREADS) void dad_pool(DadPoolArgs a) {
 // waves loads (MI355X_MICROARCH.md "Valid forms": producer sc1 stores, consumer poll + acquire).
 // The poll is bounded (~0.1 s); on timeout it sets the range flag and goes on (wrong numbers
 // instead of a hung device).
+// The counter is sharded per XCD (DAD_POOL_SHARDS words, each on a 128-B line of its own: the
+// arrivals of one XCD serialise on one line only) and a poll sums the shards.
 __device__ __forceinline__ void pool_publish(uint32_t* ready, int lane) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (lane == 0) __hip_atomic_fetch_add(ready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == 0) {
+    const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & (DAD_POOL_SHARDS - 1);   // HW_REG_XCC_ID
+    __hip_atomic_fetch_add(ready + 32 * xcc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 __device__ __forceinline__ void pool_wait(uint32_t* ready, uint32_t n, uint32_t* range_flag) {
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
     uint32_t spins = 0;
-    while (__hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < n) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1u << 22)) {
-        if (range_flag) __hip_atomic_fetch_or(range_flag, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+      const uint32_t v = lane < DAD_POOL_SHARDS ? __hip_atomic_load(ready + 32 * lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+      if ((uint32_t)dad_wave_sum((float)v) >= n) break;   // (exact: at most a few hundred arrivals)
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 23)) {
+        if (range_flag && lane == 0) __hip_atomic_fetch_or(range_flag, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (lane == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
@@ -2248,9 +2256,13 @@ __global__ __launch_bounds__(TAIL_THREADS) void dad_tail_ecda_w(DadTailArgs ta, 
     }
     if (!pa.x16) return;
     dad_prep_dispatch<2>(pa, xb * kWaves + w, nx * kWaves, (int)threadIdx.x & 63);
+#ifdef DAD_PROBE_STAMPS
+    if (threadIdx.x == 0) atomicMax(&ecda_stamps[DAD_C * ECDA_SLOTS + 15], (unsigned long long)DAD_PROBE_WALL());
+#endif
     return;
   }
   if (ta.cfg.B > TW_MAXB || ta.cfg.Bn > TW_MAXB) return;
+  if (blockIdx.x == 0) TAIL_STAMP(14);   // launch entry (slot 15: the last preparation block's end)
   if (nitems) pool_wait(pl.ready, (uint32_t)nitems, pl.range_flag);
   if (blockIdx.x == 0) tail_block_w(ta, u.t);
   else ecda_block_w(ca, ta, (int)blockIdx.x - 1, u.e);

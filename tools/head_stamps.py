@@ -27,7 +27,10 @@ def main():
     raw = []
     for r in range(reps):   # the last step of a 4-step burst, reps times
         for i in range(4):
-            step.step(data[i % 2][0], data[i % 2][1], 60)
+            # STAMP_AHEAD=1: each step names the next batch (the bench's shape: the tail launch also
+            # prepares the next batch's noisy rows)
+            nxt = data[(i + 1) % 2] if os.environ.get("STAMP_AHEAD") == "1" else None
+            step.step(data[i % 2][0], data[i % 2][1], 60, next_batch=nxt)
         torch.cuda.synchronize()
         ebuf = (ctypes.c_ulonglong * (4 * S + 16))()
         assert L.dad_probe_read_ecda_stamps(ebuf, len(ebuf)) == 0
@@ -42,6 +45,11 @@ def main():
     T = 4 * S
     tn = ["end", "ce", "probs", "dacp", "kl", "outputs", "clsbwd"]
     print("median of %d steps" % raw.shape[0])
+    if on(T + 14):
+        ends = [rel(c * S + 8) for c in range(4) if on(c * S + 8)]
+        print("launch entry %.2f (tail start 0 = after the pooling wait) | ECDA last class end %.2f | "
+              "last preparation block end %s us" % (rel(T + 14), max(ends) if ends else float("nan"),
+                                                    ("%.2f" % rel(T + 15)) if on(T + 15) else "-"))
     print("tail start 0 | " + "  ".join("%s %.2f" % (tn[k - 1], rel(T + k)) for k in range(1, 8) if on(T + k)))
     if on(T + 13) and on(T + 12):
         ghz = np.median((raw[:, T + 13] - raw[:, T + 12]) / ((raw[:, T + 1] - raw[:, T]) * 10.0))
