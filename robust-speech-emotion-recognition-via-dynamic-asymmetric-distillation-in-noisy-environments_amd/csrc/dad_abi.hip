@@ -482,7 +482,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   // rows in the weight-gradient launch (dad_wgrad_direct*_cp, interleaved with the GEMM)
   DadPrepArgs pcw;
   memset(&pcw, 0, sizeof(pcw));
-  bool clean_in_wgrad = false;
+  bool clean_in_wgrad = false, clean_store = false;
   if (!cfg->warmup && DAD_FUSED_TAIL) {
     // batches of at most 64 utterances per side, class-aware MMD: the wave-centric launch, whose
     // spare blocks pool the embeddings (one item per wave: Bc + 2 Bn items) and then run
@@ -498,8 +498,9 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
         pp = prep_args(ncfg, nbt, ws_ptr<uint16_t>(workspace, L.xs16 + (ncfg->counter & 1u) * L.x16set));
         nblk = std::max(nblk, std::max(cus, 2 * (1 + DAD_C)));
         if (prepped) *prepped = 1;
-        if (DAD_CLEAN_IN_WGRAD && h16 && nbt->rowc == nullptr) {
+        if (DAD_CLEAN_IN_WGRAD && h16 && (nbt->rowc == nullptr || ncfg->B <= 64)) {
           clean_in_wgrad = true;
+          clean_store = nbt->rowc != nullptr;   // store batch: rows through its utterance table
           pcw = pp;        // clean rows only (dad_prep_clean_load / _store)
           pp.clean = 0;    // noisy rows only
         }
@@ -557,7 +558,10 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
     wa.ntiles = WGD_NDB * splits;
     // multiple of 8 (XCD-aware tile order) with WGD_XWG spare workgroups for the extra blocks
     const dim3 grid((wa.ntiles + WGD_XWG + 7) / 8 * 8);
-    if (clean_in_wgrad) {
+    if (clean_in_wgrad && clean_store) {
+      if (f16) hipLaunchKernelGGL(dad_wgrad_direct_f16_cps, grid, dim3(WGD_THREADS), 0, stream, wa, ra, pcw);
+      else hipLaunchKernelGGL(dad_wgrad_direct_cps, grid, dim3(WGD_THREADS), 0, stream, wa, ra, pcw);
+    } else if (clean_in_wgrad) {
       if (f16) hipLaunchKernelGGL(dad_wgrad_direct_f16_cp, grid, dim3(WGD_THREADS), 0, stream, wa, ra, pcw);
       else hipLaunchKernelGGL(dad_wgrad_direct_cp, grid, dim3(WGD_THREADS), 0, stream, wa, ra, pcw);
     } else {

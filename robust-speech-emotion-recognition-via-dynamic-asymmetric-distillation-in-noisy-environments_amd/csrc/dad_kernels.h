@@ -197,6 +197,9 @@ __global__ void dad_wgrad_direct_f16(DadWgradArgs a, DadReduceArgs r);   // fp16
 // the same, also converting the NEXT step's clean rows into its prepared set (dad_prep.h, pc.clean)
 __global__ void dad_wgrad_direct_cp(DadWgradArgs a, DadReduceArgs r, DadPrepArgs pc);
 __global__ void dad_wgrad_direct_f16_cp(DadWgradArgs a, DadReduceArgs r, DadPrepArgs pc);
+// store-batch variants (the next batch's clean rows gathered from a FeatureStore, Bc <= 64)
+__global__ void dad_wgrad_direct_cps(DadWgradArgs a, DadReduceArgs r, DadPrepArgs pc);
+__global__ void dad_wgrad_direct_f16_cps(DadWgradArgs a, DadReduceArgs r, DadPrepArgs pc);
 __global__ void dad_reduce(DadReduceArgs a);
 __global__ void dad_reduce_w(DadReduceArgs a);
 __global__ void dad_norm(float* grad, float* normpart, float inv_world);

@@ -31,10 +31,24 @@
 #pragma once
 #include "dad_kernels.h"
 
-// (plain stores: non-temporal stores of the prepared rows measured slower in round 5 -- encoder
-// 27.9-28.2 -> 29.2-29.6 us, the tail launch unchanged -- because the encoder then reads them from
-// HBM instead of the Infinity Cache)
-__device__ __forceinline__ void dad_prep_st(char* p, uint2 v) { *reinterpret_cast<uint2*>(p) = v; }
+// Stores of the prepared rows.  WT (dad_prep_rows, the noisy rows in the tail launch and the
+// standalone dad_prep): write-through (sc1), so the line leaves the XCD's L2 with the store and the
+// launch does not end with megabytes of dirty rows for the kernel-end writeback (MI355X_MICROARCH.md
+// "boundary": + dirty bytes / 6 TB/s).  A/B on one box, 3 rounds: tail launch 29.2 -> 28.0-28.6 us,
+// step 100.4-101.2 -> 99.7-100.2 us.  Inline asm: an atomic store (__hip_atomic_store) made hipcc
+// wait for the memory operations in flight around every store.  Not write-through (measured, round 5):
+//  - the clean rows converted inside the weight gradient (dad_prep_clean_store): 34 -> 110 us, since
+//    every later vmcnt wait of the GEMM's pipeline then waits for the stores' round trip to memory;
+//  - the weight gradient's split-K partials: step +0.8 us (tail launch of the next step +1 us);
+//  - 16-B stores (lane pairs swapping 8-B pieces by DPP, 2 instead of 3 stores per row): tail
+//    launch +0.4 us;
+//  - non-temporal stores: encoder 27.9-28.2 -> 29.2-29.6 us (it then reads the rows from HBM
+//    instead of the Infinity Cache), tail launch unchanged.
+template <bool WT>
+__device__ __forceinline__ void dad_prep_st(char* p, uint2 v) {
+  if constexpr (WT) asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(v));
+  else *reinterpret_cast<uint2*>(p) = v;
+}
 
 template <int NOISE>
 __device__ __forceinline__ int dad_prep_tstart(const DadPrepArgs& a, int b) {
@@ -79,7 +93,7 @@ __device__ __forceinline__ void dad_prep_rows(const DadPrepArgs& a, int wave, in
         char* o = reinterpret_cast<char*>(oc + (size_t)u * DAD_D + 4 * lane);
 #pragma unroll
         for (int k = 0; k < 3; ++k)
-          dad_prep_st(o + 512 * k, uint2{dad_pack2<F16>(v[r][k][0], v[r][k][1]), dad_pack2<F16>(v[r][k][2], v[r][k][3])});
+          dad_prep_st<true>(o + 512 * k, uint2{dad_pack2<F16>(v[r][k][0], v[r][k][1]), dad_pack2<F16>(v[r][k][2], v[r][k][3])});
         continue;
       }
       const int un = u - Nc;
@@ -114,9 +128,9 @@ __device__ __forceinline__ void dad_prep_rows(const DadPrepArgs& a, int wave, in
           w[e] = v[r][k][e] + nw[e];
           s[e] = (v[r][k][e] + ns[e]) * kp[k][e];
         }
-        dad_prep_st(o_w + 512 * k, uint2{dad_pack2<F16>(w[0], w[1]), dad_pack2<F16>(w[2], w[3])});
+        dad_prep_st<true>(o_w + 512 * k, uint2{dad_pack2<F16>(w[0], w[1]), dad_pack2<F16>(w[2], w[3])});
         const uint2 so = uint2{dad_pack2<F16>(s[0], s[1]), dad_pack2<F16>(s[2], s[3])};
-        dad_prep_st(o_s + 512 * k, tzero ? uint2{0u, 0u} : so);
+        dad_prep_st<true>(o_s + 512 * k, tzero ? uint2{0u, 0u} : so);
       }
     }
   }
@@ -139,11 +153,42 @@ __device__ __forceinline__ void dad_prep_dispatch(const DadPrepArgs& a, int wave
 // (the weight-gradient launch, dad_wgrad_direct: its loads go out in one round, the conversion and
 // stores a few rounds later): row u of [Bc*Tc] (clamped for the load, not stored past the end);
 // lane l owns columns 256k + 4l .. +3 as in dad_prep_rows (no RNG on the clean rows).  Padded
-// batches only (a.src.rowc == NULL): source row u is row u of xc, with no table lookup (a dependent
-// load there would drain the caller's loads in flight).
-__device__ __forceinline__ void dad_prep_clean_load(const DadPrepArgs& a, int u, int lane, f32x4 (&v)[3]) {
+// batches: source row u is row u of xc; store batches (STORE, Bc <= 64): the row through the
+// utterance table held in registers (StoreRowsW) -- no table lookup in memory (a dependent load
+// there would drain the caller's loads in flight).
+// Store batches (a.src.rowc set, Bc <= 64): StoreRowsW holds each utterance's store row base and
+// length in lane b (loaded once, before the caller's loop), so the source row is a wave-uniform
+// readlane, not a dependent global load.
+struct StoreRowsW {
+  uint32_t lo, hi;   // lane b: rowc[b] (int64) halves
+  int len;           // lane b: lenc[b]
+  uint32_t tmag;     // fast division by Tc: floor(2^32 / Tc) + 1 (0 for Tc = 1)
+};
+__device__ __forceinline__ StoreRowsW dad_store_rows_w(const DadPrepArgs& a, int lane) {
+  StoreRowsW r;
+  const int b = min(lane, a.g.Bc - 1);
+  const int64_t base = a.src.rowc[b];
+  r.lo = (uint32_t)base;
+  r.hi = (uint32_t)((uint64_t)base >> 32);
+  r.len = a.src.lenc[b];
+  r.tmag = a.g.Tc > 1 ? 0xffffffffu / (uint32_t)a.g.Tc + 1u : 0u;
+  return r;
+}
+template <bool STORE>
+__device__ __forceinline__ size_t dad_clean_src_row(const DadPrepArgs& a, int uc, const StoreRowsW& sr) {
+  if constexpr (!STORE) return (size_t)uc;
+  const int b = sr.tmag ? (int)__umulhi((uint32_t)uc, sr.tmag) : uc;   // uniform (uc is)
+  const int t = uc - b * a.g.Tc;
+  const uint64_t base = (uint64_t)__builtin_amdgcn_readlane(sr.lo, b) |
+                        ((uint64_t)__builtin_amdgcn_readlane(sr.hi, b) << 32);
+  const int len = __builtin_amdgcn_readlane(sr.len, b);
+  return (size_t)(base + (uint64_t)min(t, max(len, 1) - 1));   // dad_src_row's rule
+}
+template <bool STORE = false>
+__device__ __forceinline__ void dad_prep_clean_load(const DadPrepArgs& a, int u, int lane, f32x4 (&v)[3],
+                                                    const StoreRowsW& sr = StoreRowsW{}) {
   const int uc = min(u, a.g.Bc * a.g.Tc - 1);
-  const float* x = a.xc + (size_t)uc * DAD_D + 4 * lane;
+  const float* x = a.xc + dad_clean_src_row<STORE>(a, uc, sr) * DAD_D + 4 * lane;
 #pragma unroll
   for (int k = 0; k < 3; ++k) v[k] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(x + 256 * k));
 }
@@ -157,5 +202,5 @@ __device__ __forceinline__ void dad_prep_clean_store(const DadPrepArgs& a, int u
   char* o = reinterpret_cast<char*>(a.x16 + (size_t)uc * DAD_D + 4 * lane);
 #pragma unroll
   for (int k = 0; k < 3; ++k)
-    dad_prep_st(o + 512 * k, uint2{dad_pack2<F16>(v[k][0], v[k][1]), dad_pack2<F16>(v[k][2], v[k][3])});
+    dad_prep_st<false>(o + 512 * k, uint2{dad_pack2<F16>(v[k][0], v[k][1]), dad_pack2<F16>(v[k][2], v[k][3])});
 }

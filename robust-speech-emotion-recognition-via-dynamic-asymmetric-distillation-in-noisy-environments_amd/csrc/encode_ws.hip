@@ -426,6 +426,13 @@ __device__ __forceinline__ void wp_loop_pp(const Ctx& C, const JobMap jm, const 
   }
   if (!grp) lds_barrier();                           // group 0: phase 2 nj idle
   for (int k = 0; DAD_PROBE_ON && k < 4; ++k) WS_STAMP(4 + k, ph[k]);
+  // every wave's phase sums (stamps build): [2560 + 40 wg + 5 w] = MFMA, MFMA-end, overhead work,
+  // overhead barrier, group | SIMD << 8
+  if (DAD_PROBE_ON && lane == 0 && blockIdx.x < 256) {
+    for (int k = 0; k < 4; ++k) DAD_PROBE_SET(ws_stamps, 2560 + 40 * blockIdx.x + 5 * w + k, ph[k]);
+    DAD_PROBE_SET(ws_stamps, 2560 + 40 * blockIdx.x + 5 * w + 4,
+                  grp | ((__builtin_amdgcn_s_getreg((1 << 11) | (4 << 6) | 4) & 3u) << 8));
+  }
 }
 
 // Roles (dad_wp_job_range): teacher workgroups run the weak slabs with the teacher's W1, student

@@ -518,8 +518,9 @@ constexpr int WGD_NBUF = 4;
 // step names its next batch): wave gw of GW takes rows gw, gw + GW, ...; two rows' loads go out in
 // the first round of each block of NB rounds and are converted and stored at the start of the next
 // block (an HBM miss under this load takes about as long as NB rounds); the rows left after the
-// loop follow it.
-template <bool F16, bool CP>
+// loop follow it.  CP = 1: padded next batch; CP = 2: store batch (Bc <= 64), source rows through
+// the utterance table held in registers (StoreRowsW).
+template <bool F16, int CP>
 __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceArgs& ra, int s0, int s1, int dbase,
                                          float* outf, uint16_t* Xt, const uint4* lut, uint16_t* gs, float* red,
                                          const DadPrepArgs& pc, int gw, int GW) {
@@ -682,6 +683,7 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
     round(0, 0, false, mine > 0, SD < mine, false);
     int j = 1;
     int prow = gw;        // CP: this wave's next clean row of the next step
+    const StoreRowsW srw = CP == 2 ? dad_store_rows_w(pc, lane) : StoreRowsW{};
     f32x4 pv[2][3];
     bool pending = false; // CP: rows prow - 2 GW, prow - GW loaded, not yet stored
     for (; j + NB - 1 + SD < cntmin; j += NB) {   // every round stages slab j + k + SD < cntmin
@@ -694,8 +696,8 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
               dad_prep_clean_store<F16>(pc, prow - 2 * GW, lane, pv[0]);
               dad_prep_clean_store<F16>(pc, prow - GW, lane, pv[1]);
             }
-            dad_prep_clean_load(pc, prow, lane, pv[0]);
-            dad_prep_clean_load(pc, prow + GW, lane, pv[1]);
+            dad_prep_clean_load<CP == 2>(pc, prow, lane, pv[0], srw);
+            dad_prep_clean_load<CP == 2>(pc, prow + GW, lane, pv[1], srw);
             prow += 2 * GW;
             pending = true;
           }
@@ -714,15 +716,16 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
         dad_prep_clean_store<F16>(pc, prow - GW, lane, pv[1]);
       }
       for (; prow < pc.g.Bc * pc.g.Tc; prow += GW) {   // the rows the loop left
-        dad_prep_clean_load(pc, prow, lane, pv[0]);
+        dad_prep_clean_load<CP == 2>(pc, prow, lane, pv[0], srw);
         dad_prep_clean_store<F16>(pc, prow, lane, pv[0]);
       }
     }
     t2 = WGD_CLK();
-  } else if constexpr (CP) {
+  } else if constexpr (CP != 0) {
+    const StoreRowsW srw = CP == 2 ? dad_store_rows_w(pc, lane) : StoreRowsW{};
     for (int prow = gw; prow < pc.g.Bc * pc.g.Tc; prow += GW) {
       f32x4 pv[3];
-      dad_prep_clean_load(pc, prow, lane, pv);
+      dad_prep_clean_load<CP == 2>(pc, prow, lane, pv, srw);
       dad_prep_clean_store<F16>(pc, prow, lane, pv);
     }
   }
@@ -791,7 +794,7 @@ struct __attribute__((aligned(16))) WgdSmem {
 
 __device__ double extra_block(const DadReduceArgs& a, int e, int tid, float (*xs)[16][6]);
 
-template <bool F16, bool CP>
+template <bool F16, int CP>
 __device__ __forceinline__ void wgrad_direct_body(const DadWgradArgs& a, const DadReduceArgs& ra, const DadPrepArgs& pc) {
   __shared__ WgdSmem S;
   __shared__ __attribute__((aligned(16))) uint16_t gs[WGD_MAXU * DAD_H];
@@ -836,20 +839,29 @@ __device__ __forceinline__ void wgrad_direct_body(const DadWgradArgs& a, const D
 
 __global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct(DadWgradArgs a, DadReduceArgs ra) {
   DAD_GUARD_BLOCK(WGD_THREADS);
-  wgrad_direct_body<false, false>(a, ra, DadPrepArgs{});
+  wgrad_direct_body<false, 0>(a, ra, DadPrepArgs{});
 }
 __global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct_f16(DadWgradArgs a, DadReduceArgs ra) {
   DAD_GUARD_BLOCK(WGD_THREADS);
-  wgrad_direct_body<true, false>(a, ra, DadPrepArgs{});
+  wgrad_direct_body<true, 0>(a, ra, DadPrepArgs{});
 }
 __global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct_cp(DadWgradArgs a, DadReduceArgs ra, DadPrepArgs pc) {
   DAD_GUARD_BLOCK(WGD_THREADS);
-  wgrad_direct_body<false, true>(a, ra, pc);
+  wgrad_direct_body<false, 1>(a, ra, pc);
 }
 __global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct_f16_cp(DadWgradArgs a, DadReduceArgs ra,
                                                                          DadPrepArgs pc) {
   DAD_GUARD_BLOCK(WGD_THREADS);
-  wgrad_direct_body<true, true>(a, ra, pc);
+  wgrad_direct_body<true, 1>(a, ra, pc);
+}
+__global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct_cps(DadWgradArgs a, DadReduceArgs ra, DadPrepArgs pc) {
+  DAD_GUARD_BLOCK(WGD_THREADS);
+  wgrad_direct_body<false, 2>(a, ra, pc);
+}
+__global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct_f16_cps(DadWgradArgs a, DadReduceArgs ra,
+                                                                          DadPrepArgs pc) {
+  DAD_GUARD_BLOCK(WGD_THREADS);
+  wgrad_direct_body<true, 2>(a, ra, pc);
 }
 
 // ---------------------------------------------------------------- reduce + squared norms

@@ -168,7 +168,8 @@ def _step_outputs(step, clean, noisy, epoch, draws, Bc, Bn):
     return out
 
 
-@pytest.mark.parametrize("precision,rng", [("fp32", "explicit"), ("bf16", "explicit"), ("bf16", "counter")])
+@pytest.mark.parametrize("precision,rng", [("fp32", "explicit"), ("bf16", "explicit"), ("bf16", "counter"),
+                                           ("fp16", "explicit"), ("fp16", "counter")])
 def test_store_mode_step_equals_padded_step(precision, rng):
     """Store mode (the encoder gathers rows straight from the FeatureStore, no padded copy)
     computes exactly what the padded batch computes: same losses, logits, embeddings, updated
@@ -203,9 +204,11 @@ def test_store_mode_step_equals_padded_step(precision, rng):
         np.testing.assert_array_equal(b[k], a[k], err_msg=k)
 
 
-def test_device_batches_drive_the_step(tmp_path):
+@pytest.mark.parametrize("precision", ["bf16", "fp16"])
+def test_device_batches_drive_the_step(tmp_path, precision):
     """The loaders' batches go straight into DADStep (the reference loop body); fused loaders
-    (store mode) give the same training trajectory as collating loaders."""
+    (store mode) give the same training trajectory as collating loaders (bf16 and the timed fp16
+    mode)."""
     do.write_synthetic_split(str(tmp_path), 31, n_utt=80, max_len=25, flavor="iemocap")
     res = []
     for fused in (False, True):
@@ -214,7 +217,7 @@ def test_device_batches_drive_the_step(tmp_path):
         clean.fused = noisy.fused = fused
         torch.manual_seed(1)
         model = PKG.SSRLModel().cuda()
-        step = PKG.DADStep(model, flavor="iemocap", precision="bf16", rng="counter", seed=2)
+        step = PKG.DADStep(model, flavor="iemocap", precision=precision, rng="counter", seed=2)
         torch.manual_seed(0)
         ci, ni = iter(clean), iter(noisy)
         for _ in range(3):

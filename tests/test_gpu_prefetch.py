@@ -6,6 +6,7 @@ prepare the NEXT batch's rows on the CUs its tail launch leaves idle.  A chain o
 rotating device-resident batches that names each next batch must equal the same chain without it
 bit for bit (same RNG streams, same bytes, same GEMMs); the later steps must really have skipped
 their own preparation; a step whose batch is not the one named falls back to preparing itself."""
+import numpy as np
 import pytest
 import torch
 
@@ -66,3 +67,44 @@ def test_prefetch_refused_for_other_geometry():
     step.step(b[0], b[1], 60)
     torch.cuda.synchronize()
     assert not step.last_prepped
+
+
+@pytest.mark.parametrize("precision", ["fp16", "bf16"])
+def test_prefetch_store_batches(precision):
+    """Store-mode batches (rows gathered from a ragged FeatureStore, no padded copy) prepared ahead:
+    the next batch's clean rows are converted inside the weight-gradient launch through the
+    utterance table (dad_wgrad_direct*_cps), its noisy rows in the tail launch.  The chain equals
+    the plain store chain and the padded (collated) chain bit for bit."""
+    import dadpkg
+    PKG = dadpkg.pkg()
+    D = PKG.data
+    cfg = dad_oracle.make_cfg("iemocap")
+    rs = np.random.RandomState(52)
+    n_utt = 96
+    sizes = rs.randint(6, 41, size=n_utt)
+    sizes[:4] = 40                                   # every batch below holds one 40-frame utterance
+    feats = (rs.standard_normal((int(sizes.sum()), 768)) * 0.5).astype("float32")
+    offsets = np.concatenate([[0], np.cumsum(sizes)[:-1]])
+    store = D.FeatureStore(feats, sizes, offsets, rs.randint(0, 4, size=n_utt))
+    picks = []
+    for i in range(3):
+        ic = np.concatenate([[i], 4 + rs.choice(n_utt - 4, 15, replace=False)])
+        inn = np.concatenate([[3], 4 + rs.choice(n_utt - 4, 11, replace=False)])
+        picks.append((ic, inn))
+    st = synth.make_state(52, 1)
+    runs = {}
+    for mode in ("padded", "store"):
+        mk = store.collate if mode == "padded" else store.batch_index
+        batches = [(mk(ic, T=40), mk(inn, T=40, with_labels=False)) for ic, inn in picks]
+        if mode == "store":
+            assert isinstance(batches[0][0]["net_input"]["feats"], D.StoreFeats)
+        for ahead in (False, True):
+            runs[(mode, ahead)] = _chain(cfg, precision, batches, st, ahead=ahead)
+    _, _, prepped = runs[("store", True)]
+    assert prepped == [False] + [True] * (K - 1), prepped
+    want, want_losses, _ = runs[("padded", False)]
+    for key in (("store", False), ("store", True), ("padded", True)):
+        got, got_losses, _ = runs[key]
+        for name, a, b in zip(("student", "teacher", "exp_avg", "exp_avg_sq", "dacp", "grad"), got, want):
+            assert torch.equal(a, b), "%s: %s differs (max %.3g)" % (key, name, float((a - b).abs().max()))
+        assert got_losses == want_losses, key

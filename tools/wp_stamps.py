@@ -30,9 +30,12 @@ def main():
     torch.cuda.synchronize()
     L = PKG.lib()
     n = 256
-    buf = (ctypes.c_ulonglong * (10 * n))()
-    assert L.dad_probe_read_ws_stamps(buf, 10 * n) == 0
-    st = np.frombuffer(buf, dtype=np.uint64).reshape(n, 10).astype(np.int64)
+    buf = (ctypes.c_ulonglong * (10 * n + 40 * n))()
+    assert L.dad_probe_read_ws_stamps(buf, 10 * n + 40 * n) == 0
+    allst = np.frombuffer(buf, dtype=np.uint64).astype(np.int64)
+    st = allst[:10 * n].reshape(n, 10)
+    pw = allst[10 * n:].reshape(n, 8, 5)          # per wave: 4 phase sums, group | SIMD << 8
+    st_all = st
     st = st[st[:, 0] > 0]
     t0 = st[:, 0].min()
     start, pro, end = (st[:, 0] - t0) / 100.0, (st[:, 1] - t0) / 100.0, (st[:, 2] - t0) / 100.0
@@ -50,6 +53,23 @@ def main():
             cyc = st[m, 4:9].astype(np.float64) / (Q[m][:, None] / 2.0)
             print("        wave-0 cycles per 32-row job p50: mfma %.0f  mfma-end wait+barrier %.0f  epilogue+dma %.0f  "
                   "overhead barrier %.0f" % tuple(np.median(cyc, axis=0))[:4])
+            # every wave, by group: per-job cycles (p50 over workgroups of this role)
+            sel = np.nonzero(st_all[:, 0] > 0)[0][m]
+            for g in (0, 1):
+                rows = []
+                for wg in sel:
+                    jobs = (st_all[wg, 3] & 0xffff) / 2.0
+                    for w in range(8):
+                        if (pw[wg, w, 4] & 0xff) == g and jobs > 0:
+                            rows.append(pw[wg, w, :4] / jobs)
+                if rows:
+                    rows = np.array(rows, dtype=np.float64)
+                    print("        group %d (%d waves) cycles per job p50: mfma %.0f  mfma-end %.0f  overhead work %.0f  "
+                          "overhead barrier %.0f | mfma p90 %.0f max %.0f" % ((g, len(rows)) + tuple(np.median(rows, axis=0))
+                                                                        + (np.percentile(rows[:, 0], 90), rows[:, 0].max())))
+            simd = [(pw[wg, w, 4] >> 8) & 3 for wg in sel[:1] for w in range(8)]
+            grp = [pw[wg, w, 4] & 0xff for wg in sel[:1] for w in range(8)]
+            print("        first workgroup: SIMD per wave %s, group per wave %s" % (simd, grp))
 
 
 if __name__ == "__main__":
