@@ -345,18 +345,31 @@ __device__ __forceinline__ void dad_glds16x6(const char* base, uint32_t tab, uin
 template <bool TEACHER, bool F16>
 __device__ __forceinline__ void wp_loop_pp(const Ctx& C, const JobMap jm, const int nj, const int w, const int lane,
                                            char* smem, const uint32_t sbase, const bf16x8* W, const float* bias,
-                                           const uint32_t* vb, const DadEncodeArgs& a, const int grp) {
+                                           uint32_t* vb, const DadEncodeArgs& a, const int grp) {
   using S = Shape<8>;
   constexpr int NP = 6;                  // 1-KB DMA pieces per wave per job (48 per job)
   bf16x8 wf[S::NT][kKS];
   float bh[S::NT];
   const int hw = S::HW * w;
+  // W1 into the registers (48 KB per wave: 393 KB per CU, at the ~70 GB/s a CU reads from L2 the
+  // longest part of the prologue), and a use of every fragment, so the compiler's waits for them
+  // sit in the prologue and not at the first MFMA inside the loop
+  auto load_w1 = [&]() {
 #pragma unroll
-  for (int t = 0; t < S::NT; ++t)
+    for (int t = 0; t < S::NT; ++t)
 #pragma unroll
-    for (int ks = 0; ks < kKS; ++ks) wf[t][ks] = W[(size_t)(((hw >> 4) + t) * kKS + ks) * 64 + lane];
+      for (int ks = 0; ks < kKS; ++ks) wf[t][ks] = W[(size_t)(((hw >> 4) + t) * kKS + ks) * 64 + lane];
 #pragma unroll
-  for (int t = 0; t < S::NT; ++t) bh[t] = bias[hw + 16 * t + (lane & 15)];
+    for (int t = 0; t < S::NT; ++t) bh[t] = bias[hw + 16 * t + (lane & 15)];
+  };
+  auto w1_resident = [&]() {
+#pragma unroll
+    for (int t = 0; t < S::NT; ++t) {
+#pragma unroll
+      for (int ks = 0; ks < kKS; ++ks) asm volatile("" ::"v"(wf[t][ks]));
+      asm volatile("" ::"v"(bh[t]));
+    }
+  };
   // Per-lane source offsets of the wave's pieces relative to the slab's first row: piece p = 6w + i
   // of a stage lands at LDS byte 1024 (p % 24) + 16 lane of tile p / 24, i.e. row r, slot k of the
   // XOR-swizzled tile, and loads source chunk k ^ r of row 16 (p / 24) + r.  Job-independent: kept
@@ -380,11 +393,32 @@ __device__ __forceinline__ void wp_loop_pp(const Ctx& C, const JobMap jm, const 
                  sbase + (uint32_t)(s * 2 * kTile) + 1024u * NP * (uint32_t)w);
   };
   unsigned long long ph[4] = {0, 0, 0, 0};
+  // Prologue.  Every wave issues its pieces of jobs 0 and 1; group 0 (which multiplies in phase 0)
+  // loads its W1 now, group 1 only after the first barrier, while group 0 multiplies job 0: the
+  // CU's inbound bytes before phase 0 are jobs 0-1 + half of W1 instead of all of it (stamps: W1
+  // and both jobs resident 7.6 us after the launch's start, the loop ~18.5 us).
   dma(0, 0);
   if (nj > 1) dma(1, 1);
+  if (!grp) load_w1();
+  // valid bits of every job (bit r = row r of the 32-row slab is a frame of the utterance)
+  for (int p = w * 64 + lane; p < nj * DAD_SLAB; p += 64 * 8) {
+    const Job J = job_of(C, TEACHER, jm(p / DAD_SLAB));
+    const int t = J.c * DAD_SLAB + (p & (DAD_SLAB - 1));
+    const uint8_t* pad = J.kind == KIND_CLEAN ? C.mc : C.mn;
+    const bool v = t < J.T && pad[J.row0 + t] == 0;
+    const uint64_t bal = __ballot(v);
+    if ((lane & 31) == 0) vb[p / DAD_SLAB] = (uint32_t)(bal >> (lane & 32));
+  }
   wait_vm<0>();
-  lds_barrier();
-  if (grp) lds_barrier();                            // group 1: phase 0 idle
+  if (!grp) w1_resident();
+  lds_barrier();                                     // jobs 0 and 1 landed, valid bits visible
+  WS_STAMP(8, DAD_PROBE_WALL());                     // (group 0's W1 resident)
+  if (grp) {                                         // group 1: phase 0 (idle) loads its W1
+    load_w1();
+    wait_vm<0>();
+    w1_resident();
+    lds_barrier();
+  }
   int s_cur = 0;
   for (int j = 0; j < nj; ++j) {
     // MFMA phase of job j
@@ -459,16 +493,7 @@ __device__ __forceinline__ void encode_wp_body(const DadEncodeArgs& a, char* sme
   // ping-pong group: 1 for the second wave on this wave's SIMD (hardware SIMD id, HW_ID[5:4])
   int* simd = reinterpret_cast<int*>(smem + kOffSimd);
   if (lane == 0) simd[w] = (int)((__builtin_amdgcn_s_getreg((1 << 11) | (4 << 6) | 4)) & 3u);
-  for (int p = tid; p < nj * DAD_SLAB; p += 64 * WAVES) {
-    const Job J = job_of(C, teacher, jm(p / DAD_SLAB));
-    const int t = J.c * DAD_SLAB + (p & (DAD_SLAB - 1));
-    const uint8_t* pad = J.kind == KIND_CLEAN ? C.mc : C.mn;
-    const bool v = t < J.T && pad[J.row0 + t] == 0;
-    const uint64_t bal = __ballot(v);
-    if ((lane & 31) == 0) vb[p / DAD_SLAB] = (uint32_t)(bal >> (lane & 32));
-  }
-  __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): the pad loads retired (no DMA in flight yet)
-  lds_barrier();                        // vb, simd visible
+  lds_barrier();                        // simd visible (the valid bits follow in wp_loop_pp's prologue)
   int grp = 0;
   for (int v = 0; v < w; ++v) grp += simd[v] == simd[w];
   grp &= 1;

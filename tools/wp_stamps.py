@@ -46,9 +46,13 @@ def main():
         if not m.any():
             continue
         per = (end[m] - pro[m]) / Q[m]
-        print("%-7s n=%3d Q p50 %d  start p50/max %.1f/%.1f  prologue-end p50 %.1f  end p50/max %.1f/%.1f us  "
-              "loop us/sub-slab p50 %.3f" % (name, m.sum(), np.median(Q[m]), np.median(start[m]), start[m].max(),
-                                            np.median(pro[m]), np.median(end[m]), end[m].max(), np.median(per)))
+        w1 = (st[:, 8] - t0) / 100.0
+        print("%-7s n=%3d Q p50 %d  start p50/max %.1f/%.1f  prologue-end p50 %.1f  W1+2 jobs landed p50/max %.1f/%.1f  "
+              "end p50/max %.1f/%.1f us  loop us/sub-slab p50 %.3f"
+              % (name, m.sum(), np.median(Q[m]), np.median(start[m]), start[m].max(), np.median(pro[m]),
+                 np.median(w1[m]), w1[m].max(), np.median(end[m]), end[m].max(), np.median(per)))
+        ends = np.sort(end[m])
+        print("        end percentiles p10/p50/p90/max %.1f/%.1f/%.1f/%.1f us" % tuple(np.percentile(ends, [10, 50, 90, 100])))
         if True:
             cyc = st[m, 4:9].astype(np.float64) / (Q[m][:, None] / 2.0)
             print("        wave-0 cycles per 32-row job p50: mfma %.0f  mfma-end wait+barrier %.0f  epilogue+dma %.0f  "
