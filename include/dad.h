@@ -272,6 +272,14 @@ int dad_collate(const void* store, int store_dtype, const int64_t* offsets, cons
 int dad_collate_index(const int64_t* offsets, const int32_t* sizes, int64_t n_samples, const int64_t* index,
                       int B, int T, int64_t* row_out, int32_t* len_out, uint8_t* pad,
                       const int64_t* labels_in, int64_t* labels_out, void* stream);
+/* dad_collate_index for every batch of an epoch in one launch (the store-mode loader's epoch start):
+ * n samples in batch order, sample i of a batch padded to T_i = pad_T[i] (its batch's T) with its
+ * pad row at pad + pad_off[i] (T_i bytes); row_out / len_out / labels_out [n].  Per sample the same
+ * values dad_collate_index writes. */
+int dad_collate_index_epoch(const int64_t* offsets, const int32_t* sizes, int64_t n_samples, const int64_t* index,
+                            int64_t n, const int64_t* pad_off, const int64_t* pad_T, int64_t* row_out,
+                            int32_t* len_out, uint8_t* pad, const int64_t* labels_in, int64_t* labels_out,
+                            void* stream);
 
 /* --- eval path ------------------------------------------------
  * SSRLModel.predict's classifier in eval mode (I/model.py:225-245) on embeddings e [B][256]

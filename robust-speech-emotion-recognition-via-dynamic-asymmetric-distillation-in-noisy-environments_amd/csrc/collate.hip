@@ -143,6 +143,25 @@ __global__ __launch_bounds__(256) void dad_collate_index_kernel(DadCollateArgs a
   }
 }
 
+// one block per sample of the epoch (samples in batch order): its pad row at pad_off[i], T = pad_T[i]
+__global__ __launch_bounds__(256) void dad_collate_index_epoch_kernel(DadCollateArgs a, long n, const int64_t* pad_off,
+                                                                     const int64_t* pad_T, int64_t* row_out,
+                                                                     int32_t* len_out) {
+  const long i = blockIdx.x;
+  if (i >= n) return;
+  const long s = a.index[i];
+  const bool ok = s >= 0 && s < a.n_samples;
+  const int size = ok ? a.sizes[s] : 0;
+  const long T = pad_T[i];
+  uint8_t* pad = a.pad + pad_off[i];
+  for (long t = threadIdx.x; t < T; t += 256) pad[t] = t < size ? 0 : 1;
+  if (threadIdx.x == 0) {
+    row_out[i] = size > 0 ? a.offsets[s] : 0;
+    len_out[i] = size;
+    if (a.labels_out) a.labels_out[i] = ok ? a.labels_in[s] : -1;
+  }
+}
+
 int dad_collate_grid(long B, long T) {
   const long per = (long)kWaves * kRowsPerWave;
   return (int)((B * T + per - 1) / per);
@@ -178,6 +197,23 @@ extern "C" int dad_collate_index(const int64_t* offsets, const int32_t* sizes, i
   const long n = (long)B * T;
   hipLaunchKernelGGL(dad_collate_index_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, a,
                      row_out, len_out);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? DAD_OK : (int)e;
+}
+
+extern "C" int dad_collate_index_epoch(const int64_t* offsets, const int32_t* sizes, int64_t n_samples,
+                                       const int64_t* index, int64_t n, const int64_t* pad_off, const int64_t* pad_T,
+                                       int64_t* row_out, int32_t* len_out, uint8_t* pad, const int64_t* labels_in,
+                                       int64_t* labels_out, void* stream) {
+  if (!offsets || !sizes || !index || !pad_off || !pad_T || !row_out || !len_out || !pad) return DAD_E_ARG;
+  if ((labels_in == nullptr) != (labels_out == nullptr)) return DAD_E_ARG;
+  if (n <= 0 || n > (1L << 31) || n_samples <= 0) return DAD_E_SHAPE;
+  DadCollateArgs a;
+  memset(&a, 0, sizeof(a));
+  a.offsets = offsets; a.sizes = sizes; a.n_samples = (long)n_samples; a.index = index;
+  a.pad = pad; a.labels_in = labels_in; a.labels_out = labels_out;
+  hipLaunchKernelGGL(dad_collate_index_epoch_kernel, dim3((unsigned)n), dim3(256), 0, (hipStream_t)stream, a, (long)n,
+                     pad_off, pad_T, row_out, len_out);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? DAD_OK : (int)e;
 }

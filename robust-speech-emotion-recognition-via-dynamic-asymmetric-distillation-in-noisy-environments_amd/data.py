@@ -226,6 +226,7 @@ class DeviceLoader:
         self.batch_size = batch_size
         self.style = style
         self.with_labels = with_labels and store.labels is not None
+        self._pinned = self._pin_ev = None      # _upload's pinned staging buffer
         self._index_loader = torch.utils.data.DataLoader(range(len(store)), batch_size=batch_size, shuffle=shuffle,
                                                          generator=generator, drop_last=drop_last,
                                                          collate_fn=_identity, num_workers=0)
@@ -235,6 +236,26 @@ class DeviceLoader:
 
     def __iter__(self):
         return _DeviceLoaderIter(self)
+
+    def _upload(self, host, dev):
+        """int64 array -> a new device tensor, asynchronously through this loader's pinned buffer
+        (allocated once: pinning per epoch called the host allocator each time; an event keeps the
+        buffer from being refilled before the previous copy has read it)."""
+        t = torch.from_numpy(np.ascontiguousarray(host, dtype=np.int64))
+        if dev.type != "cuda":
+            return t.to(dev)
+        if self._pinned is None or self._pinned.numel() < t.numel():
+            self._pinned = torch.empty(max(t.numel(), 1), dtype=torch.int64).pin_memory()
+            self._pin_ev = None
+        if self._pin_ev is not None:
+            self._pin_ev.synchronize()
+        buf = self._pinned[:t.numel()]
+        buf.copy_(t)
+        out = torch.empty(t.numel(), dtype=torch.int64, device=dev)
+        out.copy_(buf, non_blocking=True)
+        self._pin_ev = torch.cuda.Event()
+        self._pin_ev.record(torch.cuda.current_stream(dev))
+        return out
 
 
 def _identity(batch):
@@ -279,6 +300,7 @@ class _DeviceLoaderIter:
         self._it = iter(loader._index_loader)     # the reference's iter(): same global-RNG draw
         self._batches = None
         self._k = 0
+        self._rows = None           # store mode: the epoch's rows / lengths / masks / labels (_epoch_index)
 
     def __iter__(self):
         return self
@@ -291,21 +313,65 @@ class _DeviceLoaderIter:
             if self._batches is None:
                 self._batches = [np.asarray(b, dtype=np.int64) for b in self._it]
             flat = np.concatenate(self._batches) if self._batches else np.zeros(0, np.int64)
-            # one upload per epoch, from pinned memory and asynchronous: a pageable copy would
-            # wait for every step already queued on the stream (a pipeline drain per epoch)
-            host = torch.from_numpy(flat)
             dev = torch.device(L.store.device)
-            self._index_d = (host.pin_memory() if dev.type == "cuda" else host).to(dev, non_blocking=True)
-            self._starts = np.concatenate([[0], np.cumsum([len(b) for b in self._batches])])
+            sizes = [len(b) for b in self._batches]
+            self._starts = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
             self._T = [int(L.store.sizes[b].max()) if len(b) else 0 for b in self._batches]
+            n = len(flat)
+            epoch = L.fused and dev.type == "cuda" and n > 0 and min(self._T) > 0
+            if epoch:   # store mode: the epoch's per-sample pad offsets and T go up with the index
+                if flat.min() < 0 or flat.max() >= len(L.store):
+                    raise IndexError("sample index out of range [0, %d)" % len(L.store))
+                Tk = np.asarray(self._T, np.int64)
+                bs = np.asarray(sizes, np.int64)
+                self._pad_off = np.concatenate([[0], np.cumsum(bs * Tk)]).astype(np.int64)
+                host = np.concatenate([flat, np.repeat(self._pad_off[:-1], bs) + (np.arange(n) - np.repeat(
+                    self._starts[:-1], bs)) * np.repeat(Tk, bs), np.repeat(Tk, bs)])
+            else:
+                host = flat
+            # one upload per epoch, asynchronous, from the loader's pinned buffer (a pageable copy
+            # waits for every step already queued on the stream: a pipeline drain per epoch)
+            up = L._upload(host, dev)
+            self._index_d = up[:n]
+            if epoch:
+                self._epoch_index(up)
         if self._k >= len(self._batches):
             raise StopIteration
         k = self._k
         self._k += 1
         b = self._batches[k]
+        s0, s1 = self._starts[k], self._starts[k + 1]
+        if self._rows is not None:   # store mode: this batch's views of the epoch's index tensors
+            T = self._T[k]
+            p0 = self._pad_off[k]
+            pad = self._pad[p0:p0 + (s1 - s0) * T].view(s1 - s0, T)
+            idx_d = self._index_d[s0:s1]
+            feats = StoreFeats(L.store, b, idx_d, self._rows[s0:s1], self._lens[s0:s1], T)
+            return FeatureStore._pack(idx_d, feats, pad, None if self._lab is None else self._lab[s0:s1], L.style)
         fn = L.store.batch_index if L.fused else L.store.collate
-        return fn(b, index_d=self._index_d[self._starts[k]:self._starts[k + 1]], T=self._T[k], style=L.style,
-                  with_labels=L.with_labels)
+        return fn(b, index_d=self._index_d[s0:s1], T=self._T[k], style=L.style, with_labels=L.with_labels)
+
+    def _epoch_index(self, up):
+        """Store mode: what FeatureStore.batch_index writes per batch (store rows, lengths, padding
+        mask at the batch's own T, labels), for every batch of the epoch at its first next(), in one
+        launch (dad_collate_index_epoch) into epoch-sized buffers the batches are views of.  Per batch
+        that replaces four device allocations and a library call on the host (~35 us, two loaders per
+        train step, which kept the store-fed step host-bound) with a few tensor views."""
+        L = self.loader
+        st = L.store
+        dev = torch.device(st.device)
+        n = int(self._starts[-1])
+        self._rows = torch.empty(n, dtype=torch.int64, device=dev)
+        self._lens = torch.empty(n, dtype=torch.int32, device=dev)
+        self._pad = torch.empty(int(self._pad_off[-1]), dtype=torch.bool, device=dev)
+        self._lab = None
+        if L.with_labels and st.labels_d is not None:
+            self._lab = torch.empty(n, dtype=torch.int64, device=dev)
+        _lib.check(_lib.lib().dad_collate_index_epoch(
+            _lib.ptr(st.offsets_d), _lib.ptr(st.sizes_d), len(st), _lib.ptr(up[:n]), n, _lib.ptr(up[n:2 * n]),
+            _lib.ptr(up[2 * n:]), _lib.ptr(self._rows), _lib.ptr(self._lens), _lib.ptr(self._pad),
+            _lib.ptr(st.labels_d if self._lab is not None else None), _lib.ptr(self._lab),
+            torch.cuda.current_stream(dev).cuda_stream), "dad_collate_index_epoch")
 
 
 # ------------------------------------------------------------------- reference file formats

@@ -31,12 +31,21 @@ def _dev_batch(batch, device, labels=True):
     feats = ni["feats"]
     rows = lens = None
     if isinstance(feats, StoreFeats):
-        if feats.store.feats.dtype == torch.float32 and feats.store.feats.device == device:
-            x, rows, lens = feats.store.feats, feats.rows, feats.lens
+        sf = feats.store.feats
+        if sf.dtype == torch.float32 and sf.device == device:
+            x, rows, lens = sf, feats.rows, feats.lens
         else:                      # the encoders read f32 rows: other stores are widened by dad_collate
             x = feats.materialize().to(device)
-        pad = ni["padding_mask"].to(device=device).contiguous().view(torch.uint8)
-        y = batch["labels"].to(device=device, dtype=torch.int64).contiguous() if labels else None
+        pm = ni["padding_mask"]
+        # (the loaders' own tensors need no conversion: skip the no-op .to()/.contiguous() dispatches)
+        if not (pm.dtype == torch.bool and pm.device == device and pm.is_contiguous()):
+            pm = pm.to(device=device, dtype=torch.bool).contiguous()
+        pad = pm.view(torch.uint8)
+        y = None
+        if labels:
+            y = batch["labels"]
+            if not (y.dtype == torch.int64 and y.device == device and y.is_contiguous()):
+                y = y.to(device=device, dtype=torch.int64).contiguous()
         return x, pad, y, rows, lens
     x = feats.to(device=device, dtype=torch.float32, non_blocking=True).contiguous()
     pm = ni.get("padding_mask")

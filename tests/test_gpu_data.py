@@ -227,3 +227,36 @@ def test_device_batches_drive_the_step(tmp_path, precision):
         res.append((np.array([float(v) for v in losses.values()]), model.student_flat.detach().cpu().numpy()))
     np.testing.assert_array_equal(res[0][0], res[1][0])
     np.testing.assert_array_equal(res[0][1], res[1][1])
+
+
+@pytest.mark.parametrize("with_labels,style", [(True, "iemocap"), (False, "casia")])
+def test_fused_loader_epoch_views_equal_batch_index(with_labels, style):
+    """Store-mode loaders prepare an epoch's rows, lengths, masks and labels at its first next() and
+    hand out views (data._DeviceLoaderIter._epoch_index): every batch of two epochs (ragged last
+    batch, batch-dependent T) equals FeatureStore.batch_index on the same indices."""
+    rs = np.random.RandomState(44)
+    sizes = rs.randint(1, 41, size=37)
+    feats = rs.standard_normal((int(sizes.sum()), 768)).astype(np.float32)
+    offsets = np.concatenate([[0], np.cumsum(sizes)[:-1]])
+    st = D.FeatureStore(feats, sizes, offsets, rs.randint(0, 4, size=37))
+    g = torch.Generator()
+    g.manual_seed(5)
+    L = D.DeviceLoader(st, batch_size=8, shuffle=True, generator=g, style=style, with_labels=with_labels, fused=True)
+    for _ in range(2):
+        n = 0
+        for batch in L:
+            f = batch["net_input"]["feats"]
+            assert isinstance(f, D.StoreFeats)
+            want = st.batch_index(f.index, style=style, with_labels=with_labels)
+            wf = want["net_input"]["feats"]
+            assert f.shape == wf.shape
+            for a, b in ((f.rows, wf.rows), (f.lens, wf.lens), (f.index_d, wf.index_d),
+                         (batch["net_input"]["padding_mask"], want["net_input"]["padding_mask"])):
+                assert a.dtype == b.dtype and torch.equal(a, b)
+            assert set(batch) == set(want)
+            if "labels" in want and want["labels"] is not None:
+                assert torch.equal(batch["labels"], want["labels"])
+            if "id" in want:
+                assert torch.equal(batch["id"], want["id"])
+            n += len(f.index)
+        assert n == 37

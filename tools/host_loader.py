@@ -70,8 +70,9 @@ def main():
             pr.disable()
             torch.cuda.synchronize()
             s = io.StringIO()
-            pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(18)
-            print(s.getvalue()[-3500:])
+            st = pstats.Stats(pr, stream=s)
+            st.strip_dirs().sort_stats("tottime").print_stats(25)
+            print(s.getvalue()[-6000:])
             break
 
 
