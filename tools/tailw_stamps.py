@@ -27,8 +27,9 @@ def main():
     reps = int(os.environ.get("STAMP_REPS", "15"))
     raw = []
     for r in range(reps):   # the last step of a 4-step burst, reps times
-        for i in range(4):
-            step.step(data[i % 2][0], data[i % 2][1], 60)
+        for i in range(4):   # (STAMP_AHEAD=1, the default: each step names the next, as the bench does)
+            nxt = data[(i + 1) % 2] if os.environ.get("STAMP_AHEAD", "1") == "1" else None
+            step.step(data[i % 2][0], data[i % 2][1], 60, next_batch=nxt)
         torch.cuda.synchronize()
         ebuf = (ctypes.c_ulonglong * (4 * S + 16))()
         assert L.dad_probe_read_ecda_stamps(ebuf, len(ebuf)) == 0
@@ -39,6 +40,11 @@ def main():
     rel = np.median((raw - t0) / 100.0, axis=0)
     on = np.all(raw > 0, axis=0)
     print("median of %d steps; us after the tail block's start" % raw.shape[0])
+    if on[T0 + 14]:
+        ends = [rel[c * S + 8] for c in range(4) if on[c * S + 8]]
+        print("launch entry %.2f  tail block start 0  tail end %.2f  class ends %s  last preparation block end %s"
+              % (rel[T0 + 14], rel[T0 + 1], " ".join("%.2f" % e for e in ends),
+                 ("%.2f" % rel[T0 + 15]) if on[T0 + 15] else "-"))
     print("tail: " + "  ".join("%s %.2f" % (n, rel[T0 + k]) for k, n in ((4, "mask"), (2, "ce-wave"), (7, "certainty"), (8, "ranks"), (9, "quantile"),
                                                                           (10, "bcast"), (4, "dacp-wave"), (5, "kl"),
                                                                           (6, "w1-done"), (1, "end")) if on[T0 + k]))
