@@ -314,19 +314,22 @@ class _DeviceLoaderIter:
                 self._batches = [np.asarray(b, dtype=np.int64) for b in self._it]
             flat = np.concatenate(self._batches) if self._batches else np.zeros(0, np.int64)
             dev = torch.device(L.store.device)
-            sizes = [len(b) for b in self._batches]
+            sizes = np.fromiter((len(b) for b in self._batches), np.int64, len(self._batches))
             self._starts = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
-            self._T = [int(L.store.sizes[b].max()) if len(b) else 0 for b in self._batches]
             n = len(flat)
+            # each batch's T = its longest sample (one reduceat over the epoch, empty batches 0)
+            Tk = np.zeros(len(sizes), np.int64)
+            if n:
+                ne = sizes > 0
+                Tk[ne] = np.maximum.reduceat(np.asarray(L.store.sizes)[flat], self._starts[:-1][ne])
+            self._T = Tk.tolist()
             epoch = L.fused and dev.type == "cuda" and n > 0 and min(self._T) > 0
             if epoch:   # store mode: the epoch's per-sample pad offsets and T go up with the index
                 if flat.min() < 0 or flat.max() >= len(L.store):
                     raise IndexError("sample index out of range [0, %d)" % len(L.store))
-                Tk = np.asarray(self._T, np.int64)
-                bs = np.asarray(sizes, np.int64)
-                self._pad_off = np.concatenate([[0], np.cumsum(bs * Tk)]).astype(np.int64)
-                host = np.concatenate([flat, np.repeat(self._pad_off[:-1], bs) + (np.arange(n) - np.repeat(
-                    self._starts[:-1], bs)) * np.repeat(Tk, bs), np.repeat(Tk, bs)])
+                self._pad_off = np.concatenate([[0], np.cumsum(sizes * Tk)]).astype(np.int64)
+                Ts = np.repeat(Tk, sizes)            # each sample's T; its pad row follows the previous row's
+                host = np.concatenate([flat, np.concatenate([[0], np.cumsum(Ts)[:-1]]), Ts])
             else:
                 host = flat
             # one upload per epoch, asynchronous, from the loader's pinned buffer (a pageable copy
