@@ -28,17 +28,27 @@ def main():
     store = PKG.data.FeatureStore(torch.randn(n_utt * T, 768, device=dev, generator=g), np.full(n_utt, T),
                                   np.arange(n_utt) * T, np.arange(n_utt) % 4, device=dev)
     resident = bench.make_batches(P, 8, B, T, seed=17, device=dev)
+    # the same store's utterances collated once into 8 resident padded batch pairs (store content,
+    # padded addressing)
+    rs = np.random.RandomState(5)
+    collated = []
+    for k in range(8):
+        c = store.collate(rs.choice(n_utt, B, replace=False))
+        nz = store.collate(rs.choice(n_utt, B, replace=False), with_labels=False)
+        collated.append((c, nz))
 
     def epochs(loader):
         while True:
             yield from loader
 
-    for mode in ("resident", "store", "resident", "store"):
+    for mode in ("resident", "store", "collated", "resident", "store", "collated", "store"):
         if mode == "store":
             ci = epochs(PKG.data.DeviceLoader(store, batch_size=B, shuffle=True, fused=True))
             ni = epochs(PKG.data.DeviceLoader(store.subset(np.arange(n_utt), with_labels=False), batch_size=B,
                                               shuffle=True, fused=True))
             src = lambda k: (next(ci), next(ni))  # noqa: E731
+        elif mode == "collated":
+            src = lambda k: collated[k % len(collated)]  # noqa: E731
         else:
             src = lambda k: resident[k % len(resident)][:2]  # noqa: E731
         nxt = [src(0)]
