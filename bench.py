@@ -218,19 +218,36 @@ def cpu_baseline(B, T, steps, epoch, seconds=CPU_BASELINE_SECONDS):
     return out
 
 
-def data_path_bench(step, B, T, epoch, dev, n_utt=1024, reps=40, steps=20):
+def synthetic_store(P, n_utt, T, dev, seed, noisy, snr_db=5.0):
+    """FeatureStore of n_utt full-length utterances drawn as make_batches draws its rows (label
+    y = i mod 4; clean: P[y] + 0.5 N, noisy: P[(y+1) mod 4] + sig N with make_batches' per-utterance
+    sig), so steps fed from it see the headline's data: the ECDA member sets, and with them the tail
+    launch's time, depend on the features (pure N(0, 1) features made the tail launch 8 us longer)."""
+    g = torch.Generator(device=dev).manual_seed(seed)
+    Pd = P.to(dev)
+    y = torch.arange(n_utt, device=dev) % 4
+    feats = torch.empty(n_utt * T, 768, device=dev)
+    for i0 in range(0, n_utt, 64):
+        i1 = min(n_utt, i0 + 64)
+        yy = y[i0:i1]
+        if noisy:
+            sig = (0.5 + 10 ** (-snr_db / 20)) * (0.5 + 2.0 * torch.rand(i1 - i0, 1, 1, generator=g, device=dev))
+            x = Pd[(yy + 1) % 4][:, None, :] + sig * torch.randn(i1 - i0, T, 768, generator=g, device=dev)
+        else:
+            x = Pd[yy][:, None, :] + 0.5 * torch.randn(i1 - i0, T, 768, generator=g, device=dev)
+        feats[i0 * T:i1 * T] = x.reshape(-1, 768)
+    return PKG.data.FeatureStore(feats, np.full(n_utt, T, np.int64), np.arange(n_utt, dtype=np.int64) * T,
+                                 np.arange(n_utt, dtype=np.int64) % 4, device=dev)
+
+
+def data_path_bench(step, B, T, epoch, dev, P, n_utt=1024, reps=40, steps=20):
     """The device-resident data path (csrc/collate.hip): dad_collate of
     a [B, T] batch from a FeatureStore of n_utt full-length utterances (n_utt*T*3 KB in HBM,
     well past the caches), timed with HIP events on the launch stream; then the train step fed
-    by two DeviceLoaders over the store (clean + noisy collated every step, inside the clock)."""
-    g = torch.Generator(device=dev)
-    g.manual_seed(3)
-    feats = torch.randn(n_utt * T, 768, device=dev, generator=g)
-    sizes = np.full(n_utt, T, np.int64)
-    offsets = np.arange(n_utt, dtype=np.int64) * T
-    labels = np.arange(n_utt, dtype=np.int64) % 4
-    store = PKG.data.FeatureStore(feats, sizes, offsets, labels, device=dev)
-    del feats
+    by DeviceLoaders over a clean and a noisy store of the headline's synthetic distribution
+    (synthetic_store; clean + noisy collated every step, inside the clock)."""
+    store = synthetic_store(P, n_utt, T, dev, seed=3, noisy=False)
+    nstore = synthetic_store(P, n_utt, T, dev, seed=4, noisy=True)
     idx = [np.random.RandomState(k).choice(n_utt, B, replace=False) for k in range(reps)]
     idx_d = [torch.from_numpy(i).to(dev) for i in idx]
     for k in range(3):
@@ -252,7 +269,7 @@ def data_path_bench(step, B, T, epoch, dev, n_utt=1024, reps=40, steps=20):
         # the step with both batches drawn from device loaders inside the timed region:
         # collated (dad_collate copies [B, T, 768]) or fused (store mode: the encoder gathers)
         clean = PKG.data.DeviceLoader(store, batch_size=B, shuffle=True, fused=fused)
-        noisy = PKG.data.DeviceLoader(store.subset(np.arange(n_utt), with_labels=False), batch_size=B,
+        noisy = PKG.data.DeviceLoader(nstore.subset(np.arange(n_utt), with_labels=False), batch_size=B,
                                       shuffle=True, fused=fused)
         ci, ni = epochs(clean), epochs(noisy)
         # batches drawn one ahead, each step naming the next (checkpoint.train_epoch's loop): the
@@ -275,8 +292,9 @@ def data_path_bench(step, B, T, epoch, dev, n_utt=1024, reps=40, steps=20):
     collated, fused = fed(False), fed(True)
     collated["note"] = "clean + noisy batch collated (copied) per step"
     fused["note"] = "store mode: rows gathered by the encoder's LDS-DMA, no padded copy"
-    return {"kernel": "dad_collate_kernel", "store": "%d utterances x %d frames x 768 f32 (%.2f GB) resident in HBM"
-            % (n_utt, T, n_utt * T * 3072 / 1e9), "collate_ms": ms, "algorithmic_bytes_per_launch": nbytes,
+    return {"kernel": "dad_collate_kernel", "store": "two stores (clean, noisy) of %d utterances x %d frames x 768 f32 "
+            "(%.2f GB each) resident in HBM, the headline batches' synthetic distribution" % (n_utt, T, n_utt * T * 3072 / 1e9),
+            "collate_ms": ms, "algorithmic_bytes_per_launch": nbytes,
             "achieved_gbs": nbytes / (ms * 1e-3) / 1e9, "peak_gbs": HBM_PEAK_GBS,
             "frac": nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
             "step_with_device_collate": collated, "step_with_store_gather": fused}
@@ -892,7 +910,7 @@ def main():
                 if args.precision == "fp16" and args.bf16_steps > 0:
                     bf16 = side_mode(model, view, data, B, T, args, "bf16", args.bf16_steps)
             if not args.no_data_path:
-                data_path = data_path_bench(step, B, T, args.epoch, dev)
+                data_path = data_path_bench(step, B, T, args.epoch, dev, P)
             restore(model, step, snap0)
             del snap0
         run(args.warmup)

@@ -23,10 +23,15 @@ def main():
     view = PKG.ConfigView(None, flavor="iemocap")
     step = PKG.DADStep(model, view, precision="fp16", rng="counter", seed=1000)
     B, T, n_utt, epoch = 64, 300, 1024, 60
-    g = torch.Generator(device=dev)
-    g.manual_seed(3)
-    store = PKG.data.FeatureStore(torch.randn(n_utt * T, 768, device=dev, generator=g), np.full(n_utt, T),
-                                  np.arange(n_utt) * T, np.arange(n_utt) % 4, device=dev)
+    # clean and noisy stores of the headline batches' distribution (STORE_RANDN=1: N(0, 1) features)
+    if os.environ.get("STORE_RANDN") == "1":
+        g = torch.Generator(device=dev)
+        g.manual_seed(3)
+        store = nstore = PKG.data.FeatureStore(torch.randn(n_utt * T, 768, device=dev, generator=g), np.full(n_utt, T),
+                                               np.arange(n_utt) * T, np.arange(n_utt) % 4, device=dev)
+    else:
+        store = bench.synthetic_store(P, n_utt, T, dev, seed=3, noisy=False)
+        nstore = bench.synthetic_store(P, n_utt, T, dev, seed=4, noisy=True)
     resident = bench.make_batches(P, 8, B, T, seed=17, device=dev)
     # the same store's utterances collated once into 8 resident padded batch pairs (store content,
     # padded addressing)
@@ -34,17 +39,17 @@ def main():
     collated = []
     for k in range(8):
         c = store.collate(rs.choice(n_utt, B, replace=False))
-        nz = store.collate(rs.choice(n_utt, B, replace=False), with_labels=False)
+        nz = nstore.collate(rs.choice(n_utt, B, replace=False), with_labels=False)
         collated.append((c, nz))
 
     def epochs(loader):
         while True:
             yield from loader
 
-    for mode in ("resident", "store", "collated", "resident", "store", "collated", "store"):
+    for mode in ("resident", "store", "collated", "resident", "store", "collated"):
         if mode == "store":
             ci = epochs(PKG.data.DeviceLoader(store, batch_size=B, shuffle=True, fused=True))
-            ni = epochs(PKG.data.DeviceLoader(store.subset(np.arange(n_utt), with_labels=False), batch_size=B,
+            ni = epochs(PKG.data.DeviceLoader(nstore.subset(np.arange(n_utt), with_labels=False), batch_size=B,
                                               shuffle=True, fused=True))
             src = lambda k: (next(ci), next(ni))  # noqa: E731
         elif mode == "collated":
