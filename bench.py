@@ -68,13 +68,18 @@ def init_model_weights(model, seed, margin=5.0):
     return P.float()
 
 
-def make_batches(P, n, B, T, seed, device, snr_db=5.0):
-    """n (clean, noisy) batch pairs, all frames valid (BASELINE.md §3 inputs)."""
+def make_batches(P, n, B, T, seed, device, snr_db=5.0, random_labels=False):
+    """n (clean, noisy) batch pairs, all frames valid (BASELINE.md §3 inputs).  Labels: B/4 of each
+    class (the default), or drawn uniformly (random_labels: class sizes as a random batch from a
+    balanced corpus has them)."""
     g = torch.Generator(device=device).manual_seed(seed)
     Pd = P.to(device)
     out = []
     for i in range(n):
-        yc = (torch.arange(B, device=device) + i) % 4
+        if random_labels:
+            yc = torch.randint(0, 4, (B,), generator=g, device=device)
+        else:
+            yc = (torch.arange(B, device=device) + i) % 4
         yn = (yc + 1) % 4
         xc = Pd[yc][:, None, :] + 0.5 * torch.randn(B, T, 768, generator=g, device=device)
         sig = (0.5 + 10 ** (-snr_db / 20)) * (0.5 + 2.0 * torch.rand(B, 1, 1, generator=g, device=device))

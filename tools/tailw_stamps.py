@@ -21,7 +21,8 @@ def main():
     model = PKG.SSRLModel().cuda()
     P = bench.init_model_weights(model, seed=0)
     step = PKG.DADStep(model, flavor="iemocap", precision=os.environ.get("STAMP_PREC", "fp16"), rng="counter", seed=1)
-    data = bench.make_batches(P, 2, B, T, seed=17, device=torch.device("cuda"))
+    data = bench.make_batches(P, 2, B, T, seed=int(os.environ.get("STAMP_SEED", "17")), device=torch.device("cuda"),
+                              random_labels=os.environ.get("STAMP_RANDLAB") == "1")
     S = 32  # slots per ECDA class (tail.hip ECDA_SLOTS)
     L = PKG.lib()
     reps = int(os.environ.get("STAMP_REPS", "15"))
