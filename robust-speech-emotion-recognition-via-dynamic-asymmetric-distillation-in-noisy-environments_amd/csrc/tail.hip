@@ -1684,14 +1684,17 @@ __device__ __forceinline__ void ew_pair_inv(int pr, int nt, int& ti, int& tj) {
 // (the phase was bound by issuing the 32 KB of stores, not by the MFMA chain).
 #define EW_TP 40
 static_assert(ECDA_NG * 32 * EW_TP <= sizeof(EcdaW::b) / sizeof(float), "ew_member_grads: a 32 x EW_TP tile per wave in S.b");
-template <int NP, class RG>
+// NK: the 8-candidate blocks of the (Csym Z) chain, ceil(ncand_all / 8) (the coefficients and rows
+// past the candidates are zero, so the blocks they fill add nothing): a 33-candidate class runs 5
+// blocks of its 64-row tiling's 8
+template <int NP, int NK, class RG>
 __device__ __forceinline__ void ew_member_grads(EcdaW& S, const float* db, int dp, int c, int ncs, int ncand_all,
                                                 float mmd_scale, float comp_scale, float* ge_c, float* ge_s,
                                                 float* sink, const RG& repg_at) {
+  static_assert(NK >= 1 && NK <= NP / 8, "ew_member_grads: NK 8-candidate blocks of NP");
   const int tid = threadIdx.x, lane = tid & 63;
   const int g = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int kh = lane >> 5, l32 = lane & 31;
-  constexpr int NK = NP / 8;
   for (int item = g; item < (NP / 32) * (DAD_H / 32); item += ECDA_NG) {
     const int ti = item >> 3, tc = item & 7;
     const int d = 32 * tc + l32;
@@ -2013,8 +2016,15 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
     // member grads 2 sum_j Csym_ij (z_i - z_j) = 2 (rs_i z_i - (Csym Z)_i): (Csym Z) on the
     // matrix cores, 32 candidates x 32 hidden units per item
     if constexpr (!WIDE) {
-      if (npad == 32) ew_member_grads<32>(S, db, dp, c, ncs, ncand_all, mmd_scale, comp_scale, ge_c, ge_s, a.sink, repg_at);
-      else ew_member_grads<64>(S, db, dp, c, ncs, ncand_all, mmd_scale, comp_scale, ge_c, ge_s, a.sink, repg_at);
+      if (npad == 32) {
+        ew_member_grads<32, 4>(S, db, dp, c, ncs, ncand_all, mmd_scale, comp_scale, ge_c, ge_s, a.sink, repg_at);
+      } else {
+        const int nk = (ncand_all + 7) >> 3;   // 5 .. 8 (33 .. 64 candidates)
+        if (nk <= 5) ew_member_grads<64, 5>(S, db, dp, c, ncs, ncand_all, mmd_scale, comp_scale, ge_c, ge_s, a.sink, repg_at);
+        else if (nk == 6) ew_member_grads<64, 6>(S, db, dp, c, ncs, ncand_all, mmd_scale, comp_scale, ge_c, ge_s, a.sink, repg_at);
+        else if (nk == 7) ew_member_grads<64, 7>(S, db, dp, c, ncs, ncand_all, mmd_scale, comp_scale, ge_c, ge_s, a.sink, repg_at);
+        else ew_member_grads<64, 8>(S, db, dp, c, ncs, ncand_all, mmd_scale, comp_scale, ge_c, ge_s, a.sink, repg_at);
+      }
     }
     for (int item = g; WIDE && item < nt * (DAD_H / 32); item += ECDA_NG) {
       const int ti = item >> 3, tc = item & 7;
