@@ -1909,8 +1909,8 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
     const float wi = S.wz[ic];
     const bool si = ei < ncs;
     const float css = 2.0f / Wss, ctt = 2.0f / Wtt, cst = -2.0f / Wst;
-    for (int e = 0; e < ept; ++e) {
-      const int i = ei, j = ej0 + e;
+    auto coef = [&](const int j) {
+      const int i = ei;
       // G_ij read at (min, max) in the upper-triangle tiles: D is symmetric bit for bit
       const int lo = i < j ? i : j, hi = i < j ? j : i;
       const int pr = ew_pair(lo >> 5, hi >> 5, nt);
@@ -1940,6 +1940,20 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
       v = i == j ? 0.0f : v;
       db[i * dp + j] = v;
       rsp += v;
+    };
+    if (!WIDE && npad == 64) {
+      // the 64-row tiling: thread column jt + tpr e, only the columns the member-gradient chain
+      // reads (8 ceil(ncand / 8), ew_member_grads' NK blocks), so a 40-candidate class runs 5 of
+      // the 8 elements per thread; rows past the candidates get their zeros without the kernel math
+      const int jt = ej0 / ept, kz = (ncand_all + 7) & ~7;
+      for (int e = 0; e < ept; ++e) {
+        const int j = jt + tpr * e;
+        if (j >= kz) break;
+        if (ei < ncand_all) coef(j);
+        else db[ei * dp + j] = 0.0f;
+      }
+    } else {
+      for (int e = 0; e < ept; ++e) coef(ej0 + e);
     }
     ECDA_CYC(22);
     // row sums of the coefficients: the tpr threads of a row are adjacent lanes
