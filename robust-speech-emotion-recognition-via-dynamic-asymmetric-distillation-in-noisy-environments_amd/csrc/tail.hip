@@ -1800,12 +1800,30 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
     }
     *reinterpret_cast<f32x4*>(&S.msp[g][4 * lane]) = ms;
     if (lane == 0) S.nsp[g] = ns;
-    // Gram partials: tile pair (ti, tj) over a K slice, fp32 matrix cores
-    for (int item = g; item < npt * ks; item += ECDA_NG) {
-      const int pr = item / ks, sl = item - pr * ks;
+    // Gram partials: tile pair (ti, tj) over a K slice, fp32 matrix cores.  The 64-row tiling
+    // (3 pairs) cuts pairs (0,0) and (0,1) into 4 slices and (1,1) into 2: 10 items in the 10
+    // partial slots, dealt so that the waves w and w + 4 (one SIMD's pair) hold 6 slices' MFMAs
+    // each (3 x 64 or 128 + 64 of K) instead of two 128-K items on two SIMDs and one on the others
+    for (int item = g; item < (npt == 3 ? 10 : npt * ks); item += ECDA_NG) {
+      int pr, sl, nsl;
+      if (npt == 3) {
+        // item -> pair (2 bits) | slice (2 bits): 0:(0,2) 1:(1,1) 2:(2,0) 3:(2,1) 4:(0,3) 5:(1,2)
+        // 6:(0,0) 7:(0,1) 8:(1,0) 9:(1,3)
+        constexpr uint64_t kDeal = 0x2ull | (0x5ull << 4) | (0x8ull << 8) | (0x9ull << 12) | (0x3ull << 16) |
+                                   (0x6ull << 20) | (0x0ull << 24) | (0x1ull << 28) | (0x4ull << 32) | (0x7ull << 36);
+        const int v = (int)((kDeal >> (4 * item)) & 15u);
+        pr = v >> 2;
+        sl = v & 3;
+        nsl = pr < 2 ? 4 : 2;
+      } else {
+        pr = item / ks;
+        sl = item - pr * ks;
+        nsl = ks;
+      }
+      const int slot = npt == 3 ? (pr < 2 ? 4 * pr : 8) + sl : item;
       int ti, tj;
       ew_pair_inv(pr, nt, ti, tj);
-      const int kw = DAD_H / ks, k0 = sl * kw;
+      const int kw = DAD_H / nsl, k0 = sl * kw;
       const int ia = 32 * ti + l32, ib = 32 * tj + l32;
       // MFMA step e of a k-block of 8 takes k-index k + 4 kh + e on both operands (any k order
       // sums the same dot products): each lane reads 4 consecutive floats per operand
@@ -1821,7 +1839,7 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
         for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[e], bv[e], acc, 0, 0, 0);
       }
 #pragma unroll
-      for (int r = 0; r < 16; ++r) S.b.gp[item][dad_acc_row(r, kh) * EW_GP + l32] = acc[r];
+      for (int r = 0; r < 16; ++r) S.b.gp[slot][dad_acc_row(r, kh) * EW_GP + l32] = acc[r];
     }
   }
   // centroids of every class over its masked noisy rows, partials combined in wave order
@@ -1915,7 +1933,8 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
       const int lo = i < j ? i : j, hi = i < j ? j : i;
       const int pr = ew_pair(lo >> 5, hi >> 5, nt);
       float gsum = 0.0f;
-      for (int s2 = 0; s2 < ks; ++s2) gsum += S.b.gp[pr * ks + s2][(lo & 31) * EW_GP + (hi & 31)];
+      const int sb = npt == 3 ? (pr < 2 ? 4 * pr : 8) : pr * ks, sn = npt == 3 ? (pr < 2 ? 4 : 2) : ks;
+      for (int s2 = 0; s2 < sn; ++s2) gsum += S.b.gp[sb + s2][(lo & 31) * EW_GP + (hi & 31)];
       const bool ok = (i < ncand_all) & (j < ncand_all) & (i != j);
       const float d = ok ? fmaxf((S.nz[lo] + S.nz[hi]) - 2.0f * gsum, 0.0f) : 0.0f;
       const int jc = j < ncand_all ? j : 0;
