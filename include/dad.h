@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define DAD_ABI_VERSION 5
+#define DAD_ABI_VERSION 6
 
 /* error codes (besides hipError_t values) */
 #define DAD_OK 0
@@ -70,9 +70,14 @@ extern "C" {
 #define DAD_T_ECDA_GATE 28    /* [4] */
 #define DAD_T_KL_ON 32
 #define DAD_T_ECDA_ON 33
-#define DAD_T_RANGE 34        /* u32 bits: nonzero once a step's pooled embedding or logit was not finite (FP16:
-                                 an encoder operand beyond +-65504; any mode: non-finite features); sticky: only
-                                 the caller clears it (the buffer starts zero-filled) */
+#define DAD_T_RANGE 34        /* u32 bits, sticky (only the caller clears them; the buffer starts zero-filled):
+                                 DAD_RANGE_NONFINITE: a step's pooled embedding or logit was not finite (FP16: an
+                                 encoder operand beyond +-65504; any mode: non-finite features);
+                                 DAD_RANGE_POOL_TIMEOUT: a tail / class block gave up waiting for the tail
+                                 launch's fused pooling (~0.2 s); that step's update was skipped (its total loss
+                                 is NaN).  dad_step_apply skips the update of any step whose total loss is not finite. */
+#define DAD_RANGE_NONFINITE 1u
+#define DAD_RANGE_POOL_TIMEOUT 2u
 #define DAD_T_TAU_HAT 40      /* [4] batch quantile thresholds */
 /* after the header (noisy batch, Bn rows): score[Bn], pred[Bn] (as float), mask[Bn], q[Bn][4] */
 #define DAD_TAIL_FLOATS(Bn) (DAD_TAIL_HDR + (Bn) * (3 + DAD_NUM_CLASSES))
@@ -167,6 +172,9 @@ typedef struct dad_state {
 } dad_state;
 
 /* --- sizing ------------------------------------------------------------------------ */
+/* DAD_ABI_VERSION the library was built with (ABI 6): a binding compares it with the header's
+ * value when it loads the library, so a stale build fails at load instead of at a call. */
+int dad_abi_version(void);
 size_t dad_param_count(void);
 /* Step workspace bytes for cfg's geometry and precision (no initialisation needed). */
 int dad_workspace_bytes(const dad_config* cfg, size_t* bytes);

@@ -10,6 +10,7 @@ from . import _build
 
 c_float_p = ctypes.POINTER(ctypes.c_float)
 
+DAD_ABI_VERSION = 6        # dad.h DAD_ABI_VERSION this binding mirrors
 DAD_NPARAM = 256 * 768 + 256 + 4 * 256 + 4
 DAD_GRAD_EXTRA = 16
 DAD_GRAD_FLOATS = DAD_NPARAM + DAD_GRAD_EXTRA
@@ -24,6 +25,7 @@ RNG_EXPLICIT, RNG_COUNTER = 0, 1
 T_TOTAL, T_CE, T_KL, T_ECDA, T_SCL, T_MSUM, T_CLIPNORM, T_CLIPCOEF = range(8)
 T_W, T_TAU_BEFORE, T_TAU_AFTER, T_FLOORED, T_ECDA_TERM, T_ECDA_GATE = 8, 12, 16, 20, 24, 28
 T_KL_ON, T_ECDA_ON, T_RANGE, T_TAU_HAT = 32, 33, 34, 40
+RANGE_NONFINITE, RANGE_POOL_TIMEOUT = 1, 2   # bits of the T_RANGE word (dad.h DAD_RANGE_*)
 
 
 def tail_floats(bn):
@@ -67,6 +69,7 @@ class DadState(ctypes.Structure):
 
 # exported symbols (must match include/dad.h); tests check every one is present
 EXPORTS = {
+    "dad_abi_version": (ctypes.c_int, []),
     "dad_param_count": (ctypes.c_size_t, []),
     "dad_workspace_bytes": (ctypes.c_int, [ctypes.POINTER(DadConfig), ctypes.POINTER(ctypes.c_size_t)]),
     "dad_error_string": (ctypes.c_char_p, [ctypes.c_int]),
@@ -161,10 +164,16 @@ def lib():
         raise DadError("libdad_hip.so not built (%s); run __graft_entry__.build() or "
                        "python -m <pkg>._build" % path)
     L = ctypes.CDLL(path)
+    if not hasattr(L, "dad_abi_version"):
+        raise DadError("%s predates ABI 6 (no dad_abi_version): rebuild it (__graft_entry__.build())" % path)
     for name, (res, args) in EXPORTS.items():
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
+    ver = L.dad_abi_version()
+    if ver != DAD_ABI_VERSION:
+        raise DadError("%s was built for ABI %d, this binding needs ABI %d: rebuild it (__graft_entry__.build())"
+                       % (path, ver, DAD_ABI_VERSION))
     _LIB = L
     return L
 

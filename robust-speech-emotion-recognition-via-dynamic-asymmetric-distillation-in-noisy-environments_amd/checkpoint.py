@@ -151,15 +151,21 @@ def train_epoch(step, clean_loader, noisy_loader, epoch, lr=None):
         step.epoch_end()
     if tot is None:
         return {}
-    # the FP16 range flag (dad.h DAD_T_RANGE) rides in the epoch's one device->host read: an
-    # encoder operand beyond +-65504 makes that step's update non-finite, which the reference's
-    # fp32 path cannot do; it is reported (and cleared) instead of silently training on
+    # the range flag (dad.h DAD_T_RANGE, every batch shape's word) rides in the epoch's one
+    # device->host read.  An encoder operand beyond +-65504 (FP16) or non-finite features make a
+    # step's loss non-finite, which the reference's fp32 path cannot do: reported, and that step's
+    # update skipped when its total loss is NaN.  A pooling hand-off timeout is a device fault, not
+    # a data property: its steps' updates were skipped, and train_epoch raises.
     flag = step.range_flag(clear=True).float().reshape(1)
     vals = torch.cat([tot / n, flag]).cpu().tolist()
     out = dict(zip(sorted(losses), vals[:-1]))
-    if vals[-1] != 0.0:
+    bits = int(vals[-1])
+    out["range_flag"] = bits
+    if bits & _lib.RANGE_POOL_TIMEOUT:
+        raise RuntimeError("train_epoch(epoch=%d): the tail launch's pooling hand-off timed out in at least one "
+                           "step (range flag %d); those steps' updates were skipped" % (epoch, bits))
+    if bits & _lib.RANGE_NONFINITE:
         warnings.warn("train_epoch(epoch=%d): non-finite embeddings or logits in this epoch (fp16 operand "
-                      "range exceeded or non-finite features); the parameters are no longer finite" % epoch,
-                      RuntimeWarning)
-    out["range_flag"] = int(vals[-1] != 0.0)
+                      "range exceeded or non-finite features); steps with a non-finite total loss were not applied"
+                      % epoch, RuntimeWarning)
     return out

@@ -275,6 +275,7 @@ int dad_timing_stop(double* ms_sum, int* count, int n) {
   return rc;
 }
 
+int dad_abi_version(void) { return DAD_ABI_VERSION; }
 size_t dad_param_count(void) { return DAD_NPARAM; }
 
 const char* dad_error_string(int code) {
@@ -543,6 +544,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
   ra.key_drop1 = k.drop1; ra.key_drop2 = k.drop2; ra.p_drop = cfg->p_drop; ra.drop_scale = cfg->drop_scale;
   ra.ge = ge; ra.vlen = vlen; ra.cnt_tot = cnt_tot; ra.tailf = st->tail;
   ra.grad = st->grad; ra.normpart = normpart;
+  ra.pool_abort = pool_in_tail ? pool_ready + DAD_POOL_ABORT : nullptr;
   ra.splits = splits; ra.wpart = wa.wpart;
   if (!h16) {
     // FP32: one tile = (split, 128 columns); then every reduce block (dW1 sums and the

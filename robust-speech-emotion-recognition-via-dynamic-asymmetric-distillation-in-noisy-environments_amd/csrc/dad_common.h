@@ -336,7 +336,8 @@ struct DadWs {
   size_t x16set;     // bytes per prepared set
   size_t w1h;        // f16/bf16 [H][D]             modular encoder ops: 16-bit copy of W1
   size_t gflat;      // f32 [DAD_GRAD_FLOATS]       modular encoder backward: scratch grad vector
-  size_t ready;      // u32                        fused pooling counter of dad_tail_ecda_w
+  size_t ready;      // u32                        fused pooling counter of dad_tail_ecda_w (DAD_POOL_SHARDS lines),
+                     //                            then the step's pooling-timeout word (DAD_POOL_ABORT)
   size_t bytes;
   int splits;
 };
@@ -382,7 +383,7 @@ static inline DadWs dad_ws_layout(const DadGeom& g, int splits, int precision) {
   w.xs16 = off;     off = dad_align(off + 2 * w.x16set);
   w.w1h = off;      off = dad_align(off + 2 * (size_t)DAD_H * DAD_D);
   w.gflat = off;    off = dad_align(off + sizeof(float) * DAD_GRAD_FLOATS);
-  w.ready = off;    off = dad_align(off + 128 * 8);   // DAD_POOL_SHARDS counters, 128 B apart
+  w.ready = off;    off = dad_align(off + 128 * 9);   // DAD_POOL_SHARDS counters, 128 B apart, + the abort word
   w.bytes = off;
   return w;
 }

@@ -41,6 +41,10 @@
   if (blockDim.x != (n) || blockDim.y != 1 || blockDim.z != 1) return
 
 #define DAD_POOL_SHARDS 8   // fused-pooling arrival counters, one per XCD (128 B apart)
+// the word after them (ready + 32 * DAD_POOL_SHARDS): 1 when a tail / class block of this step gave up
+// waiting for the pooling (pool_wait); zeroed with the counters by the step's encoder.  The weight
+// gradient's loss-total block then writes a NaN total loss, and dad_optim skips the update.
+#define DAD_POOL_ABORT (32 * DAD_POOL_SHARDS)
 
 struct DadPoolArgs {
   DadGeom g;
@@ -158,6 +162,7 @@ struct DadReduceArgs {
   float p_drop, drop_scale;
   const float* tailf;
   float* grad; float* normpart;
+  const uint32_t* pool_abort;   // fused pooling: this step's abort word (DAD_POOL_ABORT), else NULL
 };
 
 struct DadOptimArgs {

@@ -213,7 +213,7 @@ __device__ __forceinline__ void encode_f32_slab(const DadEncodeArgs& a, const fl
 __global__ __launch_bounds__(DAD_ENC_F32_THREADS) void dad_encode_f32(DadEncodeArgs a) {
   DAD_GUARD_BLOCK(DAD_ENC_F32_THREADS);
   if (blockIdx.x == 0 && threadIdx.x == 0 && a.pool_ready)   // the tail launch's fused pooling counter
-    for (int k = 0; k < DAD_POOL_SHARDS; ++k) __hip_atomic_store(a.pool_ready + 32 * k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int k = 0; k <= DAD_POOL_SHARDS; ++k) __hip_atomic_store(a.pool_ready + 32 * k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // the strong augmentation's feature keep flags (I/utils.py:343), once per workgroup
   __shared__ __attribute__((aligned(16))) float fk[DAD_D];
   for (int d = threadIdx.x; d < DAD_D; d += DAD_ENC_F32_THREADS) fk[d] = dad_feat_keep(a.u, a.key_feat, d, a.feat_p);

@@ -485,7 +485,7 @@ __device__ __forceinline__ void encode_wp_body(const DadEncodeArgs& a, char* sme
   WS_STAMP(0, DAD_PROBE_WALL());
   WS_STAMP(3, ((unsigned long long)(teacher ? 0 : 1) << 16) | (unsigned long long)(2 * nj));
   if (blockIdx.x == 0 && tid == 0 && a.pool_ready)   // (the tail launch that counts into it follows this one)
-    for (int k = 0; k < DAD_POOL_SHARDS; ++k) __hip_atomic_store(a.pool_ready + 32 * k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int k = 0; k <= DAD_POOL_SHARDS; ++k) __hip_atomic_store(a.pool_ready + 32 * k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (nj <= 0) return;
   const uint32_t sbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
   // valid bits of every job (bit r = row r of the 32-row slab is a frame of the utterance)

@@ -207,6 +207,12 @@ __global__ __launch_bounds__(DAD_OPTIM_THREADS) void dad_optim(DadOptimArgs a) {
     if (a.losses_out)
       for (int k = 0; k < 4; ++k) a.losses_out[k] = ex[12 + k];
   }
+  // a non-finite total loss (NaN from a pooling timeout in the tail launch, DAD_POOL_ABORT; or an
+  // FP16 operand overflow / non-finite inputs) leaves this step's parameters, moments, teacher,
+  // shadows and DACP state untouched; the losses and the clip fields above still report it (the
+  // reference would write NaN into all of them)
+  const float total = a.grad[DAD_NPARAM + 12];
+  if (!(fabsf(total) <= 3.402823466e38f)) return;
   if (blockIdx.x == 0) dacp_commit(cfg, a.grad, a.dacp, tid);
   const bool f16 = cfg.precision == DAD_PREC_FP16;
   if (vec)

@@ -210,8 +210,10 @@ __global__ __launch_bounds__(DAD_POOL_THREADS) void dad_pool(DadPoolArgs a) {
 // drains (s_waitcnt vmcnt(0)) and adds 1 to the counter; a tail / class block polls the counter
 // (one lane, sc1 loads), then ONE agent-scope acquire, a drain and a barrier before any of its
 // waves loads (MI355X_MICROARCH.md "Valid forms": producer sc1 stores, consumer poll + acquire).
-// The poll is bounded (~0.1 s); on timeout it sets the range flag and goes on (wrong numbers
-// instead of a hung device).
+// The poll is bounded (~0.2 s); on timeout it sets bit 1 of the range flag and the step's abort
+// word and goes on (no hung device): the block then computes on partly pooled rows, but the
+// weight gradient's loss-total block turns the total loss into NaN and dad_optim leaves the
+// parameters, moments, teacher and DACP state of that step untouched.
 // The counter is sharded per XCD (DAD_POOL_SHARDS words, each on a 128-B line of its own: the
 // arrivals of one XCD serialise on one line only) and a poll sums the shards.
 __device__ __forceinline__ void pool_publish(uint32_t* ready, int lane) {
@@ -230,7 +232,10 @@ __device__ __forceinline__ void pool_wait(uint32_t* ready, uint32_t n, uint32_t*
       if ((uint32_t)dad_wave_sum((float)v) >= n) break;   // (exact: at most a few hundred arrivals)
       __builtin_amdgcn_s_sleep(1);
       if (++spins > (1u << 23)) {
-        if (range_flag && lane == 0) __hip_atomic_fetch_or(range_flag, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) {   // bit 1 of the sticky flag, and this step's abort word: no update (dad_optim)
+          if (range_flag) __hip_atomic_fetch_or(range_flag, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(ready + DAD_POOL_ABORT, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         break;
       }
     }
@@ -1687,6 +1692,11 @@ static_assert(ECDA_NG * 32 * EW_TP <= sizeof(EcdaW::b) / sizeof(float), "ew_memb
 // NK: the 8-candidate blocks of the (Csym Z) chain, ceil(ncand_all / 8) (the coefficients and rows
 // past the candidates are zero, so the blocks they fill add nothing): a 33-candidate class runs 5
 // blocks of its 64-row tiling's 8
+// 64-row tiling: the 8-candidate column blocks of the coefficient matrix that the member-gradient
+// chain reads (ew_member_grads<64, NK> reads columns [0, 8 NK) of db) and that the coefficient pass
+// therefore writes: ONE helper for both, so the pass never leaves a read column stale
+__device__ __forceinline__ int ew_nk64(int ncand_all) { return max((ncand_all + 7) >> 3, 5); }
+
 template <int NP, int NK, class RG>
 __device__ __forceinline__ void ew_member_grads(EcdaW& S, const float* db, int dp, int c, int ncs, int ncand_all,
                                                 float mmd_scale, float comp_scale, float* ge_c, float* ge_s,
@@ -1964,7 +1974,7 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
       // the 64-row tiling: thread column jt + tpr e, only the columns the member-gradient chain
       // reads (8 ceil(ncand / 8), ew_member_grads' NK blocks), so a 40-candidate class runs 5 of
       // the 8 elements per thread; rows past the candidates get their zeros without the kernel math
-      const int jt = ej0 / ept, kz = (ncand_all + 7) & ~7;
+      const int jt = ej0 / ept, kz = 8 * ew_nk64(ncand_all);   // = ew_member_grads' 8 NK columns
       for (int e = 0; e < ept; ++e) {
         const int j = jt + tpr * e;
         if (j >= kz) break;
@@ -2052,7 +2062,7 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
       if (npad == 32) {
         ew_member_grads<32, 4>(S, db, dp, c, ncs, ncand_all, mmd_scale, comp_scale, ge_c, ge_s, a.sink, repg_at);
       } else {
-        const int nk = (ncand_all + 7) >> 3;   // 5 .. 8 (33 .. 64 candidates)
+        const int nk = ew_nk64(ncand_all);   // 5 .. 8 (33 .. 64 candidates): the columns the pass wrote
         if (nk <= 5) ew_member_grads<64, 5>(S, db, dp, c, ncs, ncand_all, mmd_scale, comp_scale, ge_c, ge_s, a.sink, repg_at);
         else if (nk == 6) ew_member_grads<64, 6>(S, db, dp, c, ncs, ncand_all, mmd_scale, comp_scale, ge_c, ge_s, a.sink, repg_at);
         else if (nk == 7) ew_member_grads<64, 7>(S, db, dp, c, ncs, ncand_all, mmd_scale, comp_scale, ge_c, ge_s, a.sink, repg_at);

@@ -454,14 +454,34 @@ class DADStep:
         return out
 
     def range_flag(self, clear=False):
-        """Device u32 scalar, nonzero once a step with the current batch shapes produced a non-finite
-        pooled embedding or logit (dad.h DAD_T_RANGE: in FP16 an encoder operand beyond +-65504;
-        in any mode non-finite features).  Sticky; `clear=True` resets it after reading."""
-        t = self._last["tail"]
-        v = t[_lib.T_RANGE:_lib.T_RANGE + 1].view(torch.int32).clone()[0]
+        """Device int32 scalar: the OR of the sticky range words (dad.h DAD_T_RANGE) of every batch
+        shape this step has run (each (Bc, Bn) shape has its own tail buffer, so a ragged last batch
+        does not hide a flag raised by the full-size batches).  Bits (`decode_range_flag`):
+        RANGE_NONFINITE (1): a pooled embedding or logit was not finite (FP16: an encoder operand
+        beyond +-65504; any mode: non-finite features); RANGE_POOL_TIMEOUT (2): the tail launch's
+        fused pooling hand-off timed out and that step's update was skipped.  (Any step whose total
+        loss is not finite leaves the parameters and state untouched.)  FP16/BF16: the encoder's
+        ReLU works on the float bits (max(bits, 0)), so a NaN pre-activation with the sign bit set
+        is dropped, not propagated as torch's ReLU would: NaN features can go unflagged there,
+        while +-inf (an operand beyond the 16-bit range) is flagged.  `clear=True` resets every word after
+        reading."""
+        words = [b["tail"][_lib.T_RANGE:_lib.T_RANGE + 1].view(torch.int32) for b in self._bufs.values()]
+        if not words:
+            return torch.zeros((), dtype=torch.int32, device=self.device)
+        v = words[0].clone()
+        for w in words[1:]:
+            v = torch.bitwise_or(v, w)
         if clear:
-            t[_lib.T_RANGE:_lib.T_RANGE + 1].zero_()
-        return v
+            for w in words:
+                w.zero_()
+        return v[0]
+
+    @staticmethod
+    def decode_range_flag(v):
+        """Names of the bits set in a range_flag() value."""
+        v = int(v)
+        return [n for n, b in (("nonfinite", _lib.RANGE_NONFINITE), ("pool_timeout", _lib.RANGE_POOL_TIMEOUT))
+                if v & b]
 
     def outputs(self, Bc=None, Bn=None):
         """Per-step intermediates (device tensors) of the last step, for inspection/tests."""

@@ -139,3 +139,17 @@ def test_no_oracle_import_in_product():
                 txt = open(os.path.join(dp, f)).read()
                 assert "oracle" not in re.findall(r"(?:import|from)\s+(oracle)\b", txt), f
                 assert "/root/reference" not in txt, f
+
+
+def test_abi_version_checked_at_load(monkeypatch):
+    """the library reports the ABI it was built for and the binding refuses a stale build
+    at load (here: a binding that expects another version)."""
+    p = dadpkg.pkg()
+    L = p.lib()
+    assert L.dad_abi_version() == p._lib.DAD_ABI_VERSION
+    hdr = open(HEADER).read()
+    assert "#define DAD_ABI_VERSION %d" % p._lib.DAD_ABI_VERSION in hdr
+    monkeypatch.setattr(p._lib, "_LIB", None)
+    monkeypatch.setattr(p._lib, "DAD_ABI_VERSION", p._lib.DAD_ABI_VERSION + 1)
+    with pytest.raises(p._lib.DadError, match="rebuild"):
+        p._lib.lib()

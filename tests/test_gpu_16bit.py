@@ -134,6 +134,52 @@ def test_fp16_range_flag():
     torch.cuda.synchronize()
 
 
+def test_range_flag_covers_every_batch_shape():
+    """each (Bc, Bn) shape has its own tail buffer; range_flag() ORs the words of all
+    of them, so a flag raised by a full-size batch is seen (and cleared) after a ragged last batch
+    of another shape ran."""
+    cfg = dad_oracle.make_cfg("iemocap")
+    step = gh.make_step(cfg, precision="fp16", rng="counter", seed=2)
+    gh.load_state(step, synth.make_state(21, 1))
+    full = _problem(B=8, T=40, seed=21, ragged=True)
+    big = dict(full)
+    big["xc"] = full["xc"].copy()
+    big["xc"][1, 3, 17] = 1.0e5                            # beyond the fp16 range: this shape's word
+    gh.run_step(step, big, 60, with_draws=False)
+    last = _problem(B=5, T=40, seed=22, ragged=True, Bn=3)  # the epoch's ragged last batch: another word
+    gh.load_state(step, synth.make_state(21, 1))
+    gh.run_step(step, last, 60, with_draws=False)
+    v = int(step.range_flag(clear=True))
+    assert v & 1 and step.decode_range_flag(v) == ["nonfinite"]
+    assert int(step.range_flag()) == 0                     # every shape's word cleared
+    gh.run_step(step, full, 60, with_draws=False)
+    assert int(step.range_flag()) == 0
+
+
+def test_nonfinite_total_loss_skips_the_update():
+    """A step whose total loss is not finite (an FP16 operand overflow here; the tail launch's pooling
+    timeout writes a NaN total on purpose) leaves the parameters, moments, teacher and DACP state
+    untouched (dad_optim), and the next finite step trains as before."""
+    import torch
+    cfg = dad_oracle.make_cfg("iemocap")
+    inp = _problem(B=8, T=40, seed=31, ragged=True)
+    step = gh.make_step(cfg, precision="fp16", rng="counter", seed=4)
+    gh.load_state(step, synth.make_state(31, 1))
+    before = [t.detach().clone() for t in (step.model.student_flat, step.model.teacher_flat, step.exp_avg,
+                                            step.exp_avg_sq, step.dacp)]
+    bad = dict(inp)
+    bad["xc"] = inp["xc"].copy()
+    bad["xc"][0, 0, 5] = 1.0e5                             # beyond the fp16 range in a clean frame
+    o = gh.run_step(step, bad, 60, with_draws=False)
+    assert not np.isfinite(o["total_loss"])
+    after = (step.model.student_flat, step.model.teacher_flat, step.exp_avg, step.exp_avg_sq, step.dacp)
+    for b, a in zip(before, after):
+        assert torch.equal(b, a)
+    assert int(step.range_flag(clear=True)) & 1
+    o = gh.run_step(step, inp, 60, with_draws=False)
+    assert np.isfinite(o["total_loss"]) and all(np.all(np.isfinite(p)) for p in o["student"])
+
+
 def test_general_tail_kernel_switch_matches_wave_centric():
     """DAD_TAIL_W=0 (read once per process) selects the general tail + ECDA launch for every batch;
     in a subprocess it reproduces the wave-centric launch's losses, mask and gradient on a

@@ -34,6 +34,10 @@ def main():
     print("workgroups %d; cycles: prologue %.0f loop %.0f epilogue %.0f" % (len(e), m[0], m[1], m[2]))
     print("prologue: to slab loads %.0f, dL/de table %.0f, first staging %.0f, barrier %.0f" % (m[3], m[6], m[7], m[0] - m[3] - m[6] - m[7]))
     print("per round (n=%.1f): compute+stage+load %.0f barrier %.0f" % (m[8], m[4] / m[8], m[5] / m[8]))
+    tot = e[:, 0] + e[:, 1] + e[:, 2]
+    print("total cycles per workgroup: p50 %.0f p90 %.0f max %.0f; loop p50 %.0f max %.0f; epilogue max %.0f"
+          % (np.percentile(tot, 50), np.percentile(tot, 90), tot.max(), np.percentile(e[:, 1], 50), e[:, 1].max(),
+             e[:, 2].max()))
 
 
 if __name__ == "__main__":
