@@ -828,6 +828,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--fp32-steps", type=int, default=24, help="also time the FP32 parity mode (N=1)")
     ap.add_argument("--bf16-steps", type=int, default=48, help="also time the BF16 mode (N=1, fp16 runs)")
+    ap.add_argument("--randlab-steps", type=int, default=48,
+                    help="also time the step on batches with random class sizes (labels drawn uniformly, as a "
+                         "random batch of a balanced corpus has them; N=1)")
     ap.add_argument("--kernel-steps", type=int, default=32,
                     help="steps of the per-kernel timing pass after the timed region (0: none)")
     ap.add_argument("--no-data-path", action="store_true", help="skip the device collate measurement (N=1)")
@@ -905,7 +908,7 @@ def main():
         # warm-up's prepared rows and caches in place.  (The driver's --steps 20 --warmup 5 line had
         # measured the clock ramp: 137 -> 130 -> 124 us per step over consecutive 20-step segments,
         # round 2.)  The parity block runs after the timed region, from the state it started in.
-        parity = fp32 = bf16 = data_path = None
+        parity = fp32 = bf16 = data_path = randlab = None
         side = rank == 0 and world == 1
         if side:
             snap0 = snapshot(model, step)
@@ -914,6 +917,14 @@ def main():
                     fp32 = side_mode(model, view, data, B, T, args, "fp32", args.fp32_steps)
                 if args.precision == "fp16" and args.bf16_steps > 0:
                     bf16 = side_mode(model, view, data, B, T, args, "bf16", args.bf16_steps)
+            if args.randlab_steps > 0:
+                # the headline batches hold exactly B/4 utterances per class; a trainer's random batches
+                # have Binomial(B, 1/4) class sizes, and classes of more than 32 ECDA candidates take the
+                # 64-row tiling of the tail launch's class blocks
+                rdata = make_batches(P, N_BATCHES, B, T, seed=29, device=dev, snr_db=args.snr, random_labels=True)
+                randlab = side_mode(model, view, rdata, B, T, args, args.precision, args.randlab_steps)
+                randlab["data"] = "synthetic, labels drawn uniformly per utterance (random class sizes)"
+                del rdata
             if not args.no_data_path:
                 data_path = data_path_bench(step, B, T, args.epoch, dev, P)
             restore(model, step, snap0)
@@ -1002,7 +1013,7 @@ def main():
         total_utts = B * world * args.steps
         rows_per_step = 2 * B * T
     if args.mixed:
-        parity = fp32 = bf16 = data_path = None
+        parity = fp32 = bf16 = data_path = randlab = None
         losses = {k: float(v) for k, v in step.losses().items()}
         nbc = step._last_shape
         msum = float(step.outputs(*nbc)["msum"])
@@ -1073,6 +1084,8 @@ def main():
         line["fp32_mode"] = fp32
     if bf16 is not None:
         line["bf16_mode"] = bf16
+    if randlab is not None:
+        line["random_labels"] = randlab
     if data_path is not None:
         line["data_path"] = data_path
     if world == 1 and not args.no_cpu_baseline:

@@ -369,9 +369,6 @@ struct WgdSlab {
   int ul, nvalid;
 };
 
-#ifndef WGD_V2
-#define WGD_V2 1
-#endif
 // Loop-invariant lane offsets and buffer resources of one tile (WGD_V2): every per-slab address of
 // the loop is then a scalar (SGPR) base plus one of these, so the loads, the LDS staging and the
 // table reads cost no vector instructions for their addresses (the loop is bound by vector issue).
@@ -406,34 +403,13 @@ __device__ __forceinline__ WgdTable wgd_table(const DadGeom& g, int s, int u0) {
   return t;
 }
 
-// group slab j (wave-uniform, clamped by the caller): x rows (clamped into the slab's valid
-// rows) and this lane's two row masks; uniform base pointers + loop-invariant lane offsets
-__device__ __forceinline__ void wgd_load(const DadWgradArgs& a, const WgdTable& tab, int j, int sfirst, int dbase,
-                                         int wv, WgdSlab& r) {
-  const int tid = threadIdx.x & 255;
-  const int row0 = __builtin_amdgcn_readlane(tab.row0, j);
-  const int info = __builtin_amdgcn_readlane(tab.info, j);
-  r.nvalid = info & 255;
-  r.ul = info >> 8;
-  const int row = min(tid >> 3, r.nvalid - 1);
-  const uint16_t* xb = a.xs16 + (size_t)row0 * DAD_D + dbase;
-  const uint32_t* mb = a.bits + (size_t)(sfirst + WGD_GROUPS * j) * DAD_H;
-  r.x = *reinterpret_cast<const u32x4*>(xb + row * DAD_D + (tid & 7) * 8);
-  // masks of h = 32 (2 wv + m) + lane % 32 (both 32-lane halves load the same words)
-#pragma unroll
-  for (int m = 0; m < 2; ++m) r.mw[m] = mb[(2 * wv + m) * 32 + (tid & 31)];
-}
 
-#if WGD_V2
 // group slab j: its x rows through a buffer resource of the slab's 32 rows (SGPR base: rows past the
 // clean + strong parts read 0, rows past the utterance are the next utterance's prepared rows; both
 // are finite and meet mask bits 0, so no clamp runs per slab) and this lane's two row masks
 // (buffer loads at the slab's scalar offset)
-__device__ __forceinline__ void wgd_load2(const DadWgradArgs& a, const WgdTable& tab, int j, int sfirst,
+__device__ __forceinline__ void wgd_load(const DadWgradArgs& a, const WgdTable& tab, int j, int sfirst,
                                           const WgdLane& ln, WgdSlab& r) {
-#ifdef WGD_DIAG_HOT
-  j = 0;   // diagnostic build only (wrong results): every load re-reads the group's first slab (L2-hot)
-#endif
   const int row0 = __builtin_amdgcn_readlane(tab.row0, j);
   const int info = __builtin_amdgcn_readlane(tab.info, j);
   r.ul = info >> 8;
@@ -447,7 +423,6 @@ __device__ __forceinline__ void wgd_load2(const DadWgradArgs& a, const WgdTable&
   r.mw[0] = __builtin_amdgcn_raw_buffer_load_b32(rb, ln.moff, soff, 0);
   r.mw[1] = __builtin_amdgcn_raw_buffer_load_b32(rb, ln.moff + 128, soff, 0);
 }
-#endif
 
 __device__ __forceinline__ void wgd_stage(const WgdSlab& r, uint16_t* Xt) {
   const int tid = threadIdx.x & 255;
@@ -464,24 +439,16 @@ __device__ __forceinline__ void wgd_stage(const WgdSlab& r, uint16_t* Xt) {
 // LDS cycles were bank conflicts).  One bitfield extract and one 16-B LDS read per fragment.
 constexpr int WGD_LUT_SLOTS = 16;
 constexpr int WGD_LUT = 256 * WGD_LUT_SLOTS;
-__device__ __forceinline__ uint4 wgd_amask(uint32_t mask, const uint4* lut, int ks) {
-  const int lane = threadIdx.x & 63;
-  const uint32_t byte = __builtin_amdgcn_ubfe(mask, 16 * ks + 8 * (lane >> 5), 8);
-  return lut[byte * WGD_LUT_SLOTS + (lane & (WGD_LUT_SLOTS - 1))];
-}
-
-#if WGD_V2
 // WGD_V2 table: lut[b][s] holds v_perm SELECTORS instead of halfword masks: dword p of the A fragment
 // is v_perm(g, g, sel) with sel taking bytes 0, 1 of g (the 16-bit dL/de_u[h] / len_u) into the
 // halfword of each set bit (row 2p: bits 0-15, row 2p + 1: bits 16-31) and the zero byte (0x0c)
 // into the others.  One v_perm per dword replaces the AND with a g | g << 16 pair, and the
 // table address is one v_perm too: byte (2 ks + lane / 32) of the mask word into bits 8-15, the
 // lane's slot offset into bits 0-7 (lsel).
-__device__ __forceinline__ uint4 wgd_amask2(uint32_t mask, const uint4* lut, uint32_t lsel, uint32_t slot) {
+__device__ __forceinline__ uint4 wgd_amask(uint32_t mask, const uint4* lut, uint32_t lsel, uint32_t slot) {
   const uint32_t off = __builtin_amdgcn_perm(mask, slot, lsel);   // (mask byte << 8) | (lane & 15) * 16
   return *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(lut) + off);
 }
-#endif
 
 // one slab's operands for one wave: A (G) fragments a[ks][m], B (x) fragments b[ks][n]
 struct WgdFrag {
@@ -498,25 +465,6 @@ struct WgdRaw {
 };
 
 __device__ __forceinline__ WgdRaw wgd_read(const uint16_t* Xt, const uint32_t (&mk)[2], const uint4* lut,
-                                           const uint16_t* gs, int ul, int wv) {
-  WgdRaw w;
-  const int i = threadIdx.x & 31;
-#pragma unroll
-  for (int m = 0; m < 2; ++m) w.gp[m] = gs[ul * DAD_H + (2 * wv + m) * 32 + i];
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-#pragma unroll
-    for (int n = 0; n < 2; ++n) {
-      w.b[ks][n] = tr_frag(Xt, WGD_XP, 16 * ks, 32 * n);
-    }
-#pragma unroll
-    for (int m = 0; m < 2; ++m) w.am[ks][m] = wgd_amask(mk[m], lut, ks);
-  }
-  return w;
-}
-
-#if WGD_V2
-__device__ __forceinline__ WgdRaw wgd_read2(const uint16_t* Xt, const uint32_t (&mk)[2], const uint4* lut,
                                             const uint16_t* gs, int ul, const WgdLane& ln) {
   WgdRaw w;
   const uint16_t* gl = reinterpret_cast<const uint16_t*>(reinterpret_cast<const char*>(gs) + ln.gsoff) + ul * DAD_H;
@@ -527,11 +475,11 @@ __device__ __forceinline__ WgdRaw wgd_read2(const uint16_t* Xt, const uint32_t (
 #pragma unroll
     for (int n = 0; n < 2; ++n) w.b[ks][n] = tr_frag(Xt, WGD_XP, 16 * ks, 32 * n);
 #pragma unroll
-    for (int m = 0; m < 2; ++m) w.am[ks][m] = wgd_amask2(mk[m], lut, ln.lsel[ks], ln.slot);
+    for (int m = 0; m < 2; ++m) w.am[ks][m] = wgd_amask(mk[m], lut, ln.lsel[ks], ln.slot);
   }
   return w;
 }
-__device__ __forceinline__ WgdFrag wgd_finish2(const WgdRaw& w) {
+__device__ __forceinline__ WgdFrag wgd_finish(const WgdRaw& w) {
   WgdFrag f;
 #pragma unroll
   for (int m = 0; m < 2; ++m)
@@ -542,25 +490,6 @@ __device__ __forceinline__ WgdFrag wgd_finish2(const WgdRaw& w) {
       f.a[ks][m] = __builtin_bit_cast(bf16x8, uint4{__builtin_amdgcn_perm(g, g, s.x), __builtin_amdgcn_perm(g, g, s.y),
                                                     __builtin_amdgcn_perm(g, g, s.z), __builtin_amdgcn_perm(g, g, s.w)});
     }
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-    for (int n = 0; n < 2; ++n) f.b[ks][n] = w.b[ks][n];
-  return f;
-}
-#endif
-
-__device__ __forceinline__ WgdFrag wgd_finish(const WgdRaw& w) {
-  WgdFrag f;
-#pragma unroll
-  for (int m = 0; m < 2; ++m) {
-    const uint32_t gpair = w.gp[m] | (w.gp[m] << 16);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const uint4 am = w.am[ks][m];
-      f.a[ks][m] = __builtin_bit_cast(bf16x8, uint4{am.x & gpair, am.y & gpair, am.z & gpair, am.w & gpair});
-    }
-  }
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -599,7 +528,6 @@ __device__ __forceinline__ int wgd_f16_exp(float max_abs) {
 
 }  // namespace
 
-#if WGD_V2
 // dad_prep_clean_load / _store with the row's address in SGPRs (u is wave-uniform): a buffer
 // resource per row, the lane's column offset a loop-invariant register, the three 16-B / 8-B
 // pieces at immediate offsets; non-temporal loads as in dad_prep_clean_load
@@ -624,12 +552,6 @@ __device__ __forceinline__ void wgd_cp_store(const DadPrepArgs& a, int u, uint32
     __builtin_amdgcn_raw_buffer_store_b64(u32x2{dad_pack2<F16>(v[k][0], v[k][1]), dad_pack2<F16>(v[k][2], v[k][3])}, r,
                                           soff + 512 * k, 0, 0);
 }
-#define WGD_CP_LOAD(pc, u, lane, v, srw) wgd_cp_load<CP == 2>(pc, u, cploff, v, srw)
-#define WGD_CP_STORE(pc, u, lane, v) wgd_cp_store<F16>(pc, u, cpsoff, v)
-#else
-#define WGD_CP_LOAD(pc, u, lane, v, srw) dad_prep_clean_load<CP == 2>(pc, u, lane, v, srw)
-#define WGD_CP_STORE(pc, u, lane, v) dad_prep_clean_store<F16>(pc, u, lane, v)
-#endif
 
 // x-tile LDS buffers per slab group: a slab is staged two rounds before it is read, one barrier
 // per two rounds (eight buffers and a barrier every four rounds measured neutral, round 3)
@@ -655,9 +577,7 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
 #pragma unroll
     for (int n = 0; n < 2; ++n) acc[m][n] = f32x16{};
   float unscale = 1.0f;   // FP16: 2^-s_h of row h = 64 wv + lane
-#if WGD_V2
   const uint32_t cploff = (uint32_t)lane * 16u, cpsoff = (uint32_t)lane * 8u;   // CP: a row's lane columns
-#endif
   for (int k = 0; DAD_PROBE_ON && k < 10; ++k)
     if (tid == 0 && blockIdx.x < 512) DAD_PROBE_SET(wgd_stamps, blockIdx.x * 10 + k, 0);
   const unsigned long long t0 = WGD_CLK();
@@ -700,7 +620,6 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
     }
     const int sfirst = s0 + grp;
     const WgdTable tab = wgd_table(g, min(sfirst + WGD_GROUPS * lane, s1 - 1), u0);
-#if WGD_V2
     WgdLane ln;
     {
       const int t = tid & 255;
@@ -712,20 +631,12 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
       ln.gsoff = (uint32_t)(((2 * wv) * 32 + (lane & 31)) * 2);
       ln.nrows = g.Bc * g.Tc + (a.warmup ? 0 : g.Bn * g.Tn);
     }
-#define WGD_LOAD(j, r) wgd_load2(a, tab, j, sfirst, ln, r)
-#define WGD_READ(xt, mk, ul) wgd_read2(xt, mk, lut, gs, ul, ln)
-#define WGD_FINISH(R) wgd_finish2(R)
-#else
-#define WGD_LOAD(j, r) wgd_load(a, tab, j, sfirst, dbase, wv, r)
-#define WGD_READ(xt, mk, ul) wgd_read(xt, mk, lut, gs, ul, wv)
-#define WGD_FINISH(R) wgd_finish(R)
-#endif
     const int jlast = max(mine - 1, 0);
     WgdSlab r[WGD_DEPTH];
     // loads are unconditional (slab index clamped at the group's last slab): conditional
     // loads make the compiler merge the paths' pending counts into a vmcnt(0) drain
 #pragma unroll
-    for (int k = 0; k < WGD_DEPTH; ++k) WGD_LOAD(min(k, jlast), r[k]);
+    for (int k = 0; k < WGD_DEPTH; ++k) wgd_load(a, tab, min(k, jlast), sfirst, ln, r[k]);
     const unsigned long long ta = WGD_CLK();
     // the table: the first batch's values stay in registers (v0); FP16 takes the row's largest
     // |v| first (a second pass recomputes later batches), then writes the scaled values
@@ -788,7 +699,7 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
       mwq[q][1] = r[q].mw[1];
     }
 #pragma unroll
-    for (int q = 0; q < SD; ++q) WGD_LOAD(min(WGD_DEPTH + q, jlast), r[q]);
+    for (int q = 0; q < SD; ++q) wgd_load(a, tab, min(WGD_DEPTH + q, jlast), sfirst, ln, r[q]);
     const unsigned long long tc = WGD_CLK();
     __syncthreads();
     t1 = WGD_CLK();
@@ -804,16 +715,16 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
       const unsigned long long c0 = WGD_CLK();
       const int nk = (k + SD) % WGD_DEPTH;
       WgdRaw R;
-      if (comp) R = WGD_READ(Xg + (k % NB) * (DAD_SLAB * WGD_XP), mwq[k % SD], ulq[k % SD]);
+      if (comp) R = wgd_read(Xg + (k % NB) * (DAD_SLAB * WGD_XP), mwq[k % SD], lut, gs, ulq[k % SD], ln);
       __builtin_amdgcn_sched_barrier(0);   // reads first, their latency under the MFMAs
       if (prev) wgd_mma<F16>(F, acc);
       if (stage) wgd_stage(r[nk], Xg + ((k + SD) % NB) * (DAD_SLAB * WGD_XP));
       ulq[k % SD] = r[nk].ul;
       mwq[k % SD][0] = r[nk].mw[0];
       mwq[k % SD][1] = r[nk].mw[1];
-      WGD_LOAD(min(jr + SD + WGD_DEPTH, jlast), r[nk]);
+      wgd_load(a, tab, min(jr + SD + WGD_DEPTH, jlast), sfirst, ln, r[nk]);
       __builtin_amdgcn_sched_barrier(0);
-      if (comp) F = WGD_FINISH(R);
+      if (comp) F = wgd_finish(R);
       const unsigned long long c1 = WGD_CLK();
       if (bar) __syncthreads();
       WGD_ACC(4, c1 - c0); WGD_ACC(5, WGD_CLK() - c1); WGD_ACC(8, 1);
@@ -830,18 +741,25 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
     const StoreRowsW srw = CP == 2 ? dad_store_rows_w(pc, lane) : StoreRowsW{};
     f32x4 pv[2][3];
     bool pending = false; // CP: rows prow - 2 GW, prow - GW loaded, not yet stored
+    f32x4 po[2][3];       // CP two blocks ahead: rows prow - 4 GW, prow - 3 GW (loaded two blocks ago)
+    bool pend2 = false;
     for (; j + NB - 1 + SD < cntmin; j += NB) {   // every round stages slab j + k + SD < cntmin
 #pragma unroll
       for (int k = 0; k < NB; ++k) {
         if constexpr (CP) {
           if (k == 0) {
-            // the rows loaded one block (NB rounds) ago, then this block's two
-            if (pending) {
-              WGD_CP_STORE(pc, prow - 2 * GW, lane, pv[0]);
-              WGD_CP_STORE(pc, prow - GW, lane, pv[1]);
+            // the rows loaded two blocks (2 NB rounds) ago, then this block's two
+            if (pend2) {
+              wgd_cp_store<F16>(pc, prow - 4 * GW, cpsoff, po[0]);
+              wgd_cp_store<F16>(pc, prow - 3 * GW, cpsoff, po[1]);
             }
-            WGD_CP_LOAD(pc, prow, lane, pv[0], srw);
-            WGD_CP_LOAD(pc, prow + GW, lane, pv[1], srw);
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+#pragma unroll
+              for (int e = 0; e < 3; ++e) po[q][e] = pv[q][e];
+            pend2 = pending;
+            wgd_cp_load<CP == 2>(pc, prow, cploff, pv[0], srw);
+            wgd_cp_load<CP == 2>(pc, prow + GW, cploff, pv[1], srw);
             prow += 2 * GW;
             pending = true;
           }
@@ -855,13 +773,17 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
         round(j + k, (k + 1) % NB, j + k - 1 < mine, j + k < mine, j + k + SD < mine, (k + 1) % SD == SD - 1);
     if (nround - 1 < mine) wgd_mma<F16>(F, acc);
     if constexpr (CP) {
+      if (pend2) {
+        wgd_cp_store<F16>(pc, prow - 4 * GW, cpsoff, po[0]);
+        wgd_cp_store<F16>(pc, prow - 3 * GW, cpsoff, po[1]);
+      }
       if (pending) {
-        WGD_CP_STORE(pc, prow - 2 * GW, lane, pv[0]);
-        WGD_CP_STORE(pc, prow - GW, lane, pv[1]);
+        wgd_cp_store<F16>(pc, prow - 2 * GW, cpsoff, pv[0]);
+        wgd_cp_store<F16>(pc, prow - GW, cpsoff, pv[1]);
       }
       for (; prow < pc.g.Bc * pc.g.Tc; prow += GW) {   // the rows the loop left
-        WGD_CP_LOAD(pc, prow, lane, pv[0], srw);
-        WGD_CP_STORE(pc, prow, lane, pv[0]);
+        wgd_cp_load<CP == 2>(pc, prow, cploff, pv[0], srw);
+        wgd_cp_store<F16>(pc, prow, cpsoff, pv[0]);
       }
     }
     t2 = WGD_CLK();
@@ -869,8 +791,8 @@ __device__ __forceinline__ void wgd_tile(const DadWgradArgs& a, const DadReduceA
     const StoreRowsW srw = CP == 2 ? dad_store_rows_w(pc, lane) : StoreRowsW{};
     for (int prow = gw; prow < pc.g.Bc * pc.g.Tc; prow += GW) {
       f32x4 pv[3];
-      WGD_CP_LOAD(pc, prow, lane, pv, srw);
-      WGD_CP_STORE(pc, prow, lane, pv);
+      wgd_cp_load<CP == 2>(pc, prow, cploff, pv, srw);
+      wgd_cp_store<F16>(pc, prow, cpsoff, pv);
     }
   }
   const int kh = lane >> 5;
@@ -917,12 +839,7 @@ __device__ __forceinline__ void wgd_lut(uint4* lut) {
     uint32_t e[4];
 #pragma unroll
     for (int p = 0; p < 4; ++p)
-#if WGD_V2
       e[p] = (((t >> (2 * p)) & 1) ? 0x00000100u : 0x00000c0cu) | (((t >> (2 * p + 1)) & 1) ? 0x01000000u : 0x0c0c0000u);
-#else
-      e[p] = ((uint32_t)__builtin_amdgcn_sbfe(t, 2 * p, 1) & 0x0000ffffu) |
-             ((uint32_t)__builtin_amdgcn_sbfe(t, 2 * p + 1, 1) & 0xffff0000u);
-#endif
     lut[i] = uint4{e[0], e[1], e[2], e[3]};
   }
 }
@@ -943,347 +860,12 @@ struct __attribute__((aligned(16))) WgdSmem {
 
 __device__ double extra_block(const DadReduceArgs& a, int e, int tid, float (*xs)[16][6]);
 
-#ifndef WGD_T3
-#define WGD_T3 0
-#endif
-#if WGD_T3
-// ---------------------------------------------------------------- 128 h x 128 d tiles (WGD_T3)
-// The same split-K GEMM with the workgroup tile reshaped from 256 h x 64 d to 128 h x 128 d (still 12
-// tiles per split, so the same 21 splits and partial bytes): wave w of a group owns 32 h x all 128 d
-// (4 n tiles), so each A fragment -- the expensive operand, rebuilt from the ReLU' bits by a table
-// read and four v_perm -- feeds 4 MFMAs instead of 2, and each split's G is expanded by 6 column
-// blocks instead of 12.  The x tile doubles (32 rows x 128 d, two 16-B pieces per thread per slab).
-constexpr int W3_HB = 128, W3_DB = 128;
-constexpr int W3_NDB = DAD_D / W3_DB;   // column blocks per h block
-constexpr int W3_XP = 160;              // x tile pitch in halves: 320 B, rows 64 B apart mod 256 (tr reads)
-static_assert(W3_NDB * (DAD_H / W3_HB) == WGD_NDB, "dad_wgrad_direct: 12 tiles per split either way");
-static_assert(WGD_GROUPS == 2, "dad_wgrad_direct (128 x 128 tiles): two slab groups");
-
-struct W3Slab {
-  u32x4 x0, x1;   // this thread's 2 x 16 B of x: columns 8 (t & 7) and 64 + 8 (t & 7) of row t >> 3
-  uint32_t mw;    // the ReLU' row mask of this lane's hidden unit
-  int ul;         // the slab's utterance slot
-};
-struct W3Lane {
-  uint32_t xoff, moff, lsel[2], slot, gsoff;
-  int nrows;
-};
-__device__ __forceinline__ void w3_load(const DadWgradArgs& a, const WgdTable& tab, int j, int sfirst, const W3Lane& ln,
-                                        W3Slab& r) {
-  const int row0 = __builtin_amdgcn_readlane(tab.row0, j);
-  const int info = __builtin_amdgcn_readlane(tab.info, j);
-  r.ul = info >> 8;
-  const int n = min(__builtin_amdgcn_readfirstlane(ln.nrows) - row0, DAD_SLAB);
-  const auto rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.xs16 + (size_t)row0 * DAD_D), (short)0,
-                                                    n * DAD_D * 2, 0x00020000);
-  r.x0 = __builtin_amdgcn_raw_buffer_load_b128(rx, ln.xoff, 0, 0);
-  r.x1 = __builtin_amdgcn_raw_buffer_load_b128(rx, ln.xoff + 128, 0, 0);
-  const auto rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(a.bits), (short)0, -1, 0x00020000);
-  r.mw = __builtin_amdgcn_raw_buffer_load_b32(rb, ln.moff, (sfirst + WGD_GROUPS * j) * DAD_H * 4, 0);
-}
-__device__ __forceinline__ void w3_stage(const W3Slab& r, uint16_t* Xt) {
-  const int t = threadIdx.x & 255;
-  uint16_t* p = Xt + (t >> 3) * W3_XP + (t & 7) * 8;   // 8 lanes of a row: 128 contiguous bytes per store
-  *reinterpret_cast<u32x4*>(p) = r.x0;
-  *reinterpret_cast<u32x4*>(p + 64) = r.x1;
-}
-struct W3Raw {
-  bf16x8 b[2][4];
-  uint4 am[2];
-  uint32_t gp;
-};
-struct W3Frag {
-  bf16x8 a[2], b[2][4];
-};
-__device__ __forceinline__ W3Raw w3_read(const uint16_t* Xt, uint32_t mk, const uint4* lut, const uint16_t* gs, int ul,
-                                         const W3Lane& ln) {
-  W3Raw w;
-  w.gp = reinterpret_cast<const uint16_t*>(reinterpret_cast<const char*>(gs) + ln.gsoff)[ul * W3_HB];
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-#pragma unroll
-    for (int n = 0; n < 4; ++n) w.b[ks][n] = tr_frag(Xt, W3_XP, 16 * ks, 32 * n);
-    w.am[ks] = wgd_amask2(mk, lut, ln.lsel[ks], ln.slot);
-  }
-  return w;
-}
-__device__ __forceinline__ W3Frag w3_finish(const W3Raw& w) {
-  W3Frag f;
-  const uint32_t g = w.gp;
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    const uint4 s = w.am[ks];
-    f.a[ks] = __builtin_bit_cast(bf16x8, uint4{__builtin_amdgcn_perm(g, g, s.x), __builtin_amdgcn_perm(g, g, s.y),
-                                               __builtin_amdgcn_perm(g, g, s.z), __builtin_amdgcn_perm(g, g, s.w)});
-#pragma unroll
-    for (int n = 0; n < 4; ++n) f.b[ks][n] = w.b[ks][n];
-  }
-  return f;
-}
-template <bool F16>
-__device__ __forceinline__ void w3_mma(const W3Frag& f, f32x16 (&acc)[4]) {
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      if constexpr (F16)
-        acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, f.a[ks]),
-                                                        __builtin_bit_cast(f16x8, f.b[ks][n]), acc[n], 0, 0, 0);
-      else
-        acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[ks], f.b[ks][n], acc[n], 0, 0, 0);
-    }
-}
-
-// LDS of a 128 x 128 workgroup: the table at offset 0 (a table read needs no base add), the x tiles
-// (2 groups x 4 buffers x 32 rows x 320 B; the end-of-tile exchange and the per-h unscale reuse
-// them, the F16 max exchange of the prologue uses group 1's buffer 2), the dL/de table [64 utt][128 h]
-constexpr int W3_XT = WGD_GROUPS * 4 * DAD_SLAB * W3_XP;   // halves
-struct __attribute__((aligned(16))) W3Smem {
-  uint4 lut[WGD_LUT];
-  union {
-    uint16_t xt[W3_XT];
-    float red[W3_XT / 2];
-  } a;
-  uint16_t gs[WGD_MAXU * W3_HB];
-};
-static_assert(sizeof(W3Smem) <= 163840, "dad_wgrad_direct (128 x 128): 160 KB of LDS");
-static_assert(2 * 4 * 2 * 16 * 64 + W3_HB <= W3_XT / 2, "exchange + unscale fit the x tiles");
-
-template <bool F16, int CP>
-__device__ __forceinline__ void w3_tile(const DadWgradArgs& a, const DadReduceArgs& ra, int s0, int s1, int h0, int d0,
-                                        float* outf, W3Smem& S, const DadPrepArgs& pc, int gw, int GW) {
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane((tid >> 6) & 3);
-  const int grp = __builtin_amdgcn_readfirstlane(tid >> 8);
-  const DadGeom& g = a.g;
-  uint16_t* Xt = S.a.xt;
-  const uint4* lut = S.lut;
-  uint16_t* gs = S.gs;
-  f32x16 acc[4];
-#pragma unroll
-  for (int n = 0; n < 4; ++n) acc[n] = f32x16{};
-  float unscale = 1.0f;   // FP16: 2^-s_h of h = h0 + (tid & 127) (every quarter of the workgroup holds it)
-  const uint32_t cploff = (uint32_t)lane * 16u, cpsoff = (uint32_t)lane * 8u;   // CP: a row's lane columns
-  for (int k = 0; DAD_PROBE_ON && k < 10; ++k)
-    if (tid == 0 && blockIdx.x < 512) DAD_PROBE_SET(wgd_stamps, blockIdx.x * 10 + k, 0);
-  const unsigned long long t0 = WGD_CLK();
-  unsigned long long t1 = t0, t2 = t0;
-  if (s0 < s1) {
-    const int n = s1 - s0;
-    const int nround = (n + WGD_GROUPS - 1) / WGD_GROUPS;
-    const int mine = (n - grp + WGD_GROUPS - 1) / WGD_GROUPS;
-    const int cntmin = n / WGD_GROUPS;
-    const int u0 = wgd_utt(g, s0), nu = wgd_utt(g, s1 - 1) - u0 + 1;
-    uint16_t* Xg = Xt + grp * (4 * DAD_SLAB * W3_XP);
-    // dL/de_u[h] / max(1, len_u) of the split's utterances for the tile's 128 hidden units: thread
-    // (quarter q = tid / 128, hl = tid % 128) evaluates utterance slots 2q, 2q + 1 of each batch of 8
-    // (fused_ge1, as wgd_tile) and writes them as 16-bit; FP16: the per-h largest |v| over the split
-    // is combined over the 4 quarters through LDS (one barrier), then fp16(v * 2^s_h) as in wgd_tile
-    constexpr int KG = 2;
-    const int q = tid >> 7, hl = tid & (W3_HB - 1), hh = h0 + hl;
-    auto slot = [&](int k) { return q * KG + k; };
-    float w2[4], ec0[KG], vl0[KG];
-    f32x4 gz0[KG];
-    uint32_t ef0[KG];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) w2[c] = ra.student[DAD_OFF_W2 + c * DAD_H + hh];
-#pragma unroll
-    for (int k = 0; k < KG; ++k) {
-      const int u = u0 + min(slot(k), nu - 1);
-      ec0[k] = ra.ge_ecda[(size_t)u * DAD_H + hh];
-      gz0[k] = *reinterpret_cast<const f32x4*>(ra.gzb + (size_t)u * DAD_C);
-      ef0[k] = ra.eflag[u];
-      vl0[k] = ra.vlen[u];
-    }
-    const int sfirst = s0 + grp;
-    const WgdTable tab = wgd_table(g, min(sfirst + WGD_GROUPS * lane, s1 - 1), u0);
-    W3Lane ln;
-    {
-      const int t = tid & 255;
-      ln.xoff = (uint32_t)(((t >> 3) * DAD_D + d0 + (t & 7) * 8) * 2);
-      ln.moff = (uint32_t)((h0 + 32 * wv + (lane & 31)) * 4);
-      ln.slot = (uint32_t)(lane & (WGD_LUT_SLOTS - 1)) << 4;
-      ln.lsel[0] = 0x0c0c0000u | ((4u + (uint32_t)(lane >> 5)) << 8);
-      ln.lsel[1] = 0x0c0c0000u | ((6u + (uint32_t)(lane >> 5)) << 8);
-      ln.gsoff = (uint32_t)((32 * wv + (lane & 31)) * 2);
-      ln.nrows = g.Bc * g.Tc + (a.warmup ? 0 : g.Bn * g.Tn);
-    }
-    const int jlast = max(mine - 1, 0);
-    W3Slab r[WGD_DEPTH];
-#pragma unroll
-    for (int k = 0; k < WGD_DEPTH; ++k) w3_load(a, tab, min(k, jlast), sfirst, ln, r[k]);
-    const unsigned long long ta = WGD_CLK();
-    auto ge_table = [&](auto ex_tag) {
-      constexpr bool EX = decltype(ex_tag)::value;
-      auto batch = [&](int ul0, float (&v)[KG]) {
-#pragma unroll
-        for (int k = 0; k < KG; ++k) {
-          const int u = u0 + min(ul0 + slot(k), nu - 1);
-          v[k] = ul0 == 0 ? fused_ge1_v<EX>(ra, g.Bc, u, hh, w2, gz0[k], ef0[k], ec0[k]) / fmaxf(vl0[k], 1.0f)
-                          : fused_ge1<EX>(ra, g.Bc, u, hh, w2) / fmaxf(ra.vlen[u], 1.0f);
-        }
-      };
-      auto put = [&](int ul0, const float (&v)[KG], float scale) {
-#pragma unroll
-        for (int k = 0; k < KG; ++k) {
-          const int uk = ul0 + slot(k);
-          if (uk < nu) gs[uk * W3_HB + hl] = dad_half_bits(F16 ? v[k] * scale : v[k], F16);
-        }
-      };
-      float v0[KG];
-      batch(0, v0);
-      float scale = 1.0f;
-      if constexpr (F16) {
-        float mx = 0.0f;
-#pragma unroll
-        for (int k = 0; k < KG; ++k) mx = fmaxf(mx, slot(k) < nu ? fabsf(v0[k]) : 0.0f);
-        for (int ul0 = 8; ul0 < nu; ul0 += 8) {
-          float v[KG];
-          batch(ul0, v);
-#pragma unroll
-          for (int k = 0; k < KG; ++k) mx = fmaxf(mx, ul0 + slot(k) < nu ? fabsf(v[k]) : 0.0f);
-        }
-        float* mxs = reinterpret_cast<float*>(Xt + (4 + 2) * DAD_SLAB * W3_XP);   // group 1's buffer 2
-        mxs[q * W3_HB + hl] = mx;
-        __syncthreads();
-        mx = fmaxf(fmaxf(mxs[hl], mxs[W3_HB + hl]), fmaxf(mxs[2 * W3_HB + hl], mxs[3 * W3_HB + hl]));
-        const int s = wgd_f16_exp(mx);
-        scale = __builtin_ldexpf(1.0f, s);
-        unscale = __builtin_ldexpf(1.0f, -s);
-      }
-      put(0, v0, scale);
-      for (int ul0 = 8; ul0 < nu; ul0 += 8) {
-        float v[KG];
-        batch(ul0, v);
-        put(ul0, v, scale);
-      }
-    };
-    if (ra.keep1) ge_table(std::true_type{});
-    else ge_table(std::false_type{});
-    const unsigned long long tb = WGD_CLK();
-    constexpr int NB = 4, SD = 2;
-    int ulq[SD];
-    uint32_t mwq[SD];
-#pragma unroll
-    for (int qq = 0; qq < SD; ++qq) {
-      if (mine > qq) w3_stage(r[qq], Xg + qq * (DAD_SLAB * W3_XP));
-      ulq[qq] = r[qq].ul;
-      mwq[qq] = r[qq].mw;
-    }
-#pragma unroll
-    for (int qq = 0; qq < SD; ++qq) w3_load(a, tab, min(WGD_DEPTH + qq, jlast), sfirst, ln, r[qq]);
-    const unsigned long long tc = WGD_CLK();
-    __syncthreads();
-    t1 = WGD_CLK();
-    WGD_ACC(3, ta - t0); WGD_ACC(6, tb - ta); WGD_ACC(7, tc - tb); (void)ta; (void)tb; (void)tc;
-    W3Frag F;
-    auto round = [&](int jr, int k, bool prev, bool comp, bool stage, bool bar) {
-      const unsigned long long c0 = WGD_CLK();
-      const int nk = (k + SD) % WGD_DEPTH;
-      W3Raw R;
-      if (comp) R = w3_read(Xg + (k % NB) * (DAD_SLAB * W3_XP), mwq[k % SD], lut, gs, ulq[k % SD], ln);
-      __builtin_amdgcn_sched_barrier(0);
-      if (prev) w3_mma<F16>(F, acc);
-      if (stage) w3_stage(r[nk], Xg + ((k + SD) % NB) * (DAD_SLAB * W3_XP));
-      ulq[k % SD] = r[nk].ul;
-      mwq[k % SD] = r[nk].mw;
-      w3_load(a, tab, min(jr + SD + WGD_DEPTH, jlast), sfirst, ln, r[nk]);
-      __builtin_amdgcn_sched_barrier(0);
-      if (comp) F = w3_finish(R);
-      const unsigned long long c1 = WGD_CLK();
-      if (bar) __syncthreads();
-      WGD_ACC(4, c1 - c0); WGD_ACC(5, WGD_CLK() - c1); WGD_ACC(8, 1);
-      (void)c0; (void)c1;
-    };
-    round(0, 0, false, mine > 0, SD < mine, false);
-    int j = 1;
-    int prow = gw;
-    const StoreRowsW srw = CP == 2 ? dad_store_rows_w(pc, lane) : StoreRowsW{};
-    f32x4 pv[2][3];
-    bool pending = false;
-    for (; j + NB - 1 + SD < cntmin; j += NB) {
-#pragma unroll
-      for (int k = 0; k < NB; ++k) {
-        if constexpr (CP) {
-          if (k == 0) {
-            if (pending) {
-              wgd_cp_store<F16>(pc, prow - 2 * GW, cpsoff, pv[0]);
-              wgd_cp_store<F16>(pc, prow - GW, cpsoff, pv[1]);
-            }
-            wgd_cp_load<CP == 2>(pc, prow, cploff, pv[0], srw);
-            wgd_cp_load<CP == 2>(pc, prow + GW, cploff, pv[1], srw);
-            prow += 2 * GW;
-            pending = true;
-          }
-        }
-        round(j + k, (k + 1) % NB, true, true, true, (k + 1) % SD == SD - 1);
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < NB + SD + 1; ++k)
-      if (j + k < nround)
-        round(j + k, (k + 1) % NB, j + k - 1 < mine, j + k < mine, j + k + SD < mine, (k + 1) % SD == SD - 1);
-    if (nround - 1 < mine) w3_mma<F16>(F, acc);
-    if constexpr (CP) {
-      if (pending) {
-        wgd_cp_store<F16>(pc, prow - 2 * GW, cpsoff, pv[0]);
-        wgd_cp_store<F16>(pc, prow - GW, cpsoff, pv[1]);
-      }
-      for (; prow < pc.g.Bc * pc.g.Tc; prow += GW) {
-        wgd_cp_load<CP == 2>(pc, prow, cploff, pv[0], srw);
-        wgd_cp_store<F16>(pc, prow, cpsoff, pv[0]);
-      }
-    }
-    t2 = WGD_CLK();
-  } else if constexpr (CP != 0) {
-    const StoreRowsW srw = CP == 2 ? dad_store_rows_w(pc, lane) : StoreRowsW{};
-    for (int prow = gw; prow < pc.g.Bc * pc.g.Tc; prow += GW) {
-      f32x4 pv[3];
-      wgd_cp_load<CP == 2>(pc, prow, cploff, pv, srw);
-      wgd_cp_store<F16>(pc, prow, cpsoff, pv);
-    }
-  }
-  // the two groups' partials of the same 32 h x 128 d: group g finishes n tiles 2g, 2g + 1
-  const int kh = lane >> 5;
-  float* red = S.a.red;
-  float* us = red + 2 * 4 * 2 * 16 * 64;   // [128] 2^-s_h (after the exchange slots)
-  // (acc indexed by compile-time n only: a runtime index would put the accumulators in scratch)
-  auto finish = [&](auto gtag) {
-    constexpr int G = decltype(gtag)::value;
-    __syncthreads();   // the x tiles are free
-#pragma unroll
-    for (int nn = 0; nn < 2; ++nn)
-#pragma unroll
-      for (int rr = 0; rr < 16; ++rr) red[(((G * 4 + wv) * 2 + nn) * 16 + rr) * 64 + lane] = acc[2 * (1 - G) + nn][rr];
-    if (tid < W3_HB) us[tid] = unscale;
-    __syncthreads();
-#pragma unroll
-    for (int nn = 0; nn < 2; ++nn)
-#pragma unroll
-      for (int rr = 0; rr < 16; ++rr) {
-        const int hl = 32 * wv + dad_acc_row(rr, kh);
-        const int d = 32 * (2 * G + nn) + (lane & 31);
-        const float v = acc[2 * G + nn][rr] + red[((((1 - G) * 4 + wv) * 2 + nn) * 16 + rr) * 64 + lane];
-        outf[(size_t)(h0 + hl) * DAD_D + d0 + d] = F16 ? v * us[hl] : v;
-      }
-    __syncthreads();
-  };
-  if (grp == 0) finish(std::integral_constant<int, 0>{});
-  else finish(std::integral_constant<int, 1>{});
-  WGD_ACC(0, t1 - t0); WGD_ACC(1, t2 - t1); WGD_ACC(2, WGD_CLK() - t2);
-  (void)t0; (void)t1; (void)t2;
-}
-#endif
 
 template <bool F16, int CP>
 __device__ __forceinline__ void wgrad_direct_body(const DadWgradArgs& a, const DadReduceArgs& ra, const DadPrepArgs& pc) {
-#if WGD_T3
-  __shared__ W3Smem S;
-#else
   __shared__ WgdSmem S;
   __shared__ __attribute__((aligned(16))) uint16_t gs[WGD_MAXU * DAD_H];
   uint16_t* Xt = S.a.xt;
-#endif
   // XCD-aware tile order (grid is a multiple of 8; workgroups go round-robin over the 8
   // XCDs): each XCD takes a consecutive run of tiles, so the column blocks of one split,
   // which read the same ReLU' row masks, share an L2
@@ -1319,15 +901,8 @@ __device__ __forceinline__ void wgrad_direct_body(const DadWgradArgs& a, const D
   const int s0 = split * per, s1 = min(total, s0 + per);
   wgd_lut(S.lut);   // (the tile's first barrier orders it before the first read)
   const int gw = __builtin_amdgcn_readfirstlane(tile * (WGD_THREADS / 64) + (int)(threadIdx.x >> 6));
-#if WGD_T3
-  // tile (split, sub): h block sub / W3_NDB, column block sub % W3_NDB (a split's 12 tiles share an XCD)
-  const int hb = dblk / W3_NDB, db = dblk - hb * W3_NDB;
-  w3_tile<F16, CP>(a, ra, s0, s1, hb * W3_HB, db * W3_DB, a.wpart + (size_t)split * DAD_H * DAD_D, S, pc, gw,
-                   a.ntiles * (WGD_THREADS / 64));
-#else
   wgd_tile<F16, CP>(a, ra, s0, s1, dblk * WGD_DB, a.wpart + (size_t)split * DAD_H * DAD_D, Xt, S.lut, gs, S.a.red, pc,
                     gw, a.ntiles * (WGD_THREADS / 64));
-#endif
 }
 
 __global__ __launch_bounds__(WGD_THREADS, 1) void dad_wgrad_direct(DadWgradArgs a, DadReduceArgs ra) {

@@ -16,7 +16,7 @@ PROF_ARGS="--kernel-steps 0 --no-data-path --no-parity --launch eager" bash tool
 sed -n '/Kernel durations/,/Step period/p' gpurun_out/prof_report.md | grep -E "dad_|Step period"
 cd /tmp
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --kernel-include-regex "dad_(encode|wgrad)" --output-format csv \
-  -d "$R/gpurun_out/qpmc" -o run -- python "$R/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --no-parity --fp32-steps 0 --bf16-steps 0 --no-data-path --launch eager \
+  -d "$R/gpurun_out/qpmc" -o run -- python "$R/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --no-parity --fp32-steps 0 --bf16-steps 0 --randlab-steps 0 --no-data-path --launch eager \
   > "$R/gpurun_out/qpmc.log" 2>&1 || exit 1
 cd "$R"
 python tools/pmc_brief.py gpurun_out/qpmc/run_counter_collection.csv || true

@@ -8,6 +8,9 @@
 //   2 agpr   as 0 with the accumulators in AGPRs
 //   3 asm3   as 0, three k-steps ahead
 //   4 nowait as 0 without the waits (timing only: the MFMAs read fragments still in flight)
+//   5 half   VERDICT r05 item 4's layout: each wave holds HALF the hidden units (one 16-h tile, 96
+//            VGPRs of B), so every A fragment read feeds one MFMA instead of two: 24 k-steps x 2
+//            MFMAs per job (the same FLOP per CU takes twice the jobs); cycles are reported per MFMA
 //   hipcc --offload-arch=gfx950 -O3 tools/pp_mfma_bench.hip -o tools/bin/pp_mfma_bench
 #include <hip/hip_runtime.h>
 
@@ -56,6 +59,19 @@ __device__ __forceinline__ void kstep(f16x8 (&xa)[PF + 1][2], const uint32_t (&a
   }
 }
 
+template <int K, int PF>
+__device__ __forceinline__ void kstep_half(f16x8 (&xa)[PF + 1][2], const uint32_t (&addr)[4], const f16x8 (&w)[2][KS],
+                                           f32x4 (&acc)[2][2]) {
+  if constexpr (K < KS) {
+    rdk<K + PF, PF>(xa, addr);
+    constexpr int younger = (K + PF < KS ? PF : KS - 1 - K);
+    wt<2 * younger>(xa[K % (PF + 1)][0], xa[K % (PF + 1)][1]);
+    mfma<false>(acc[0][0], xa[K % (PF + 1)][0], w[0][K]);
+    mfma<false>(acc[1][0], xa[K % (PF + 1)][1], w[0][K]);
+    kstep_half<K + 1, PF>(xa, addr, w, acc);
+  }
+}
+
 template <int MODE>
 __global__ __launch_bounds__(256, 1) void chain(float* out, unsigned long long* cyc) {
   __shared__ __attribute__((aligned(16))) char lds[100 * 1024];
@@ -95,7 +111,8 @@ __global__ __launch_bounds__(256, 1) void chain(float* out, unsigned long long* 
         rd<256 * 0>(xa[k][0], addr[k & 3] + 256 * (k >> 2));
         rd<TILE>(xa[k][1], addr[k & 3] + 256 * (k >> 2));
       }
-      kstep<0, PF, MODE == 2, MODE != 4>(xa, addr, w, acc);
+      if constexpr (MODE == 5) kstep_half<0, PF>(xa, addr, w, acc);
+      else kstep<0, PF, MODE == 2, MODE != 4>(xa, addr, w, acc);
     }
   }
   asm volatile("s_nop 7\n\ts_nop 7" ::"v"(acc[0][0]));
@@ -128,8 +145,9 @@ void run(const char* name, float* out, unsigned long long* cyc, int nwg) {
   for (int i = 0; i < nwg * 4; ++i) sum += (double)h[i];
   const double per_job = sum / (nwg * 4) / ITER;
   const double us_job = ms * 1e3 / REP / ITER;
+  const double nm = MODE == 5 ? 48.0 : 96.0;   // MFMAs per job per wave
   printf("%-7s cycles/job/wave %7.0f  (%.1f per MFMA)  us/job %.3f  implied clock %.2f GHz\n", name, per_job,
-         per_job / 96.0, us_job, per_job / us_job / 1e3);
+         per_job / nm, us_job, per_job / us_job / 1e3);
 }
 
 int main() {
@@ -143,6 +161,7 @@ int main() {
   run<2>("agpr", out, cyc, nwg);
   run<3>("asm3", out, cyc, nwg);
   run<4>("nowait", out, cyc, nwg);
+  run<5>("half", out, cyc, nwg);
   run<0>("asm", out, cyc, nwg);
   return 0;
 }

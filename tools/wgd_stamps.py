@@ -21,8 +21,10 @@ def main():
     P = bench.init_model_weights(model, seed=0)
     step = PKG.DADStep(model, flavor="iemocap", precision=os.environ.get("STAMP_PREC", "fp16"), rng="counter", seed=1)
     data = bench.make_batches(P, 2, B, T, seed=17, device=torch.device("cuda"))
+    ahead = os.environ.get("STAMP_AHEAD", "0") == "1"   # 1: each step names the next (dad_wgrad_direct*_cp)
     for i in range(6):
-        step.step(data[i % 2][0], data[i % 2][1], 60)
+        nxt = (data[(i + 1) % 2][0], data[(i + 1) % 2][1]) if ahead else None
+        step.step(data[i % 2][0], data[i % 2][1], 60, next_batch=nxt)
     torch.cuda.synchronize()
     L = PKG.lib()
     n = 256
