@@ -837,6 +837,9 @@ def main():
     ap.add_argument("--no-parity", action="store_true", help="skip the 16-bit-vs-fp32 parity block (N=1)")
     ap.add_argument("--no-ahead", action="store_true",
                     help="16-bit modes: every step prepares its own rows (no next-batch preparation in the tail launch)")
+    ap.add_argument("--prep-under-exchange", default="auto", choices=["auto", "on", "off"],
+                    help="16-bit modes: the next batch's noisy rows on a side stream from the end of the backward "
+                         "(under the all-reduce; the default at N > 1) instead of in the tail launch (the default at N = 1)")
     ap.add_argument("--launch", default="eager", choices=["graph", "eager"],
                     help="timed steps as eager launches (default) or hipGraph replays (one graph per resident batch; "
                          "measured no faster on this ROCm, DESIGN.md §5)")
@@ -887,7 +890,9 @@ def main():
         view = step.view
     else:
         view = flavor_view(args)
-        step = PKG.DADStep(model, view, precision=args.precision, rng="counter", seed=1000 + rank, comm=comm)
+        step = PKG.DADStep(model, view, precision=args.precision, rng="counter", seed=1000 + rank, comm=comm,
+                           prep_under_exchange=None if args.prep_under_exchange == "auto"
+                           else args.prep_under_exchange == "on")
         data = make_batches(P, N_BATCHES, B, T, seed=17 + rank, device=dev, snr_db=args.snr)
         torch.cuda.synchronize()
 
@@ -1071,7 +1076,9 @@ def main():
         "config": {"workload": workload, "flavor": "mixed" if args.mixed else args.flavor, "snr_db": args.snr,
                    "global_batch": B * world, "per_gpu_batch": B, "seq_len": T, "feature_dim": 768,
                    "parallelism": "dp%d" % world},
-        "comm": {"transport": args.comm if world > 1 else None, "ranks_seen": ranks_seen},
+        "comm": {"transport": args.comm if world > 1 else None, "ranks_seen": ranks_seen,
+                 "next_noisy_rows": "side stream under the exchange" if getattr(step, "prep_under_exchange", False)
+                 else "tail launch"},
         "launch": launch if not args.mixed else "eager",
         "roofline": rf, "step_roofline": srf, "kernels": kern,
         "losses_last_step": losses, "mask_sum_last_step": msum, "ecda_on_last_step": ecda_on,

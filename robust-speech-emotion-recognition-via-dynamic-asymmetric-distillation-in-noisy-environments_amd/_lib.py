@@ -20,6 +20,7 @@ DAD_MAX_BATCH = 1024
 PREC_FP32, PREC_BF16, PREC_FP16 = 0, 1, 2
 DRAW_WEAK, DRAW_STRONG, DRAW_FEAT_KEEP, DRAW_TSTART, DRAW_KEEP1, DRAW_KEEP2 = range(1, 7)
 RNG_EXPLICIT, RNG_COUNTER = 0, 1
+PREP_CLEAN, PREP_NOISY = 1, 2     # dad.h DAD_PREP_* (dad_step_backward_ahead_split / dad_step_prepare_rows)
 
 # tail header slots (dad.h DAD_T_*)
 T_TOTAL, T_CE, T_KL, T_ECDA, T_SCL, T_MSUM, T_CLIPNORM, T_CLIPCOEF = range(8)
@@ -87,6 +88,12 @@ EXPORTS = {
                                                ctypes.POINTER(DadState), ctypes.c_void_p, ctypes.c_void_p,
                                                ctypes.POINTER(DadConfig), ctypes.POINTER(DadBatch),
                                                ctypes.POINTER(ctypes.c_int)]),
+    "dad_step_backward_ahead_split": (ctypes.c_int, [ctypes.POINTER(DadConfig), ctypes.POINTER(DadBatch),
+                                                     ctypes.POINTER(DadState), ctypes.c_void_p, ctypes.c_void_p,
+                                                     ctypes.POINTER(DadConfig), ctypes.POINTER(DadBatch),
+                                                     ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+    "dad_step_prepare_rows": (ctypes.c_int, [ctypes.POINTER(DadConfig), ctypes.POINTER(DadBatch), ctypes.c_void_p,
+                                             ctypes.c_void_p, ctypes.c_int]),
     "dad_step_apply": (ctypes.c_int, [ctypes.POINTER(DadConfig), ctypes.POINTER(DadState),
                                       ctypes.c_void_p, ctypes.c_void_p]),
     "dad_step": (ctypes.c_int, [ctypes.POINTER(DadConfig), ctypes.POINTER(DadBatch), ctypes.POINTER(DadState),

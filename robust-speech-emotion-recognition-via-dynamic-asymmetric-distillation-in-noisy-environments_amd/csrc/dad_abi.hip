@@ -350,10 +350,14 @@ static bool can_prepare_ahead(const dad_config* cfg, const dad_config* ncfg, con
   return true;
 }
 
+// pending != nullptr (dad_step_backward_ahead_split): the tail launch prepares none of the next
+// batch's rows; the weight gradient still converts its clean rows where it can, and *pending names
+// the parts (DAD_PREP_*) the caller prepares with dad_step_prepare_rows
 static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const dad_state* st, void* workspace,
                                void* stream_, bool do_encode, bool do_backward, const dad_config* ncfg = nullptr,
-                               const dad_batch* nbt = nullptr, int* prepped = nullptr) {
+                               const dad_batch* nbt = nullptr, int* prepped = nullptr, int* pending = nullptr) {
   if (prepped) *prepped = 0;
+  if (pending) *pending = 0;
   int rc = check_cfg(cfg);
   if (rc) return rc;
   if (!bt || !st || !workspace) return DAD_E_ARG;
@@ -497,13 +501,17 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
         const int rc = device_cus(&cus);
         if (rc) return rc;
         pp = prep_args(ncfg, nbt, ws_ptr<uint16_t>(workspace, L.xs16 + (ncfg->counter & 1u) * L.x16set));
-        nblk = std::max(nblk, std::max(cus, 2 * (1 + DAD_C)));
+        if (!pending) nblk = std::max(nblk, std::max(cus, 2 * (1 + DAD_C)));
         if (prepped) *prepped = 1;
         if (DAD_CLEAN_IN_WGRAD && h16 && (nbt->rowc == nullptr || ncfg->B <= 64)) {
           clean_in_wgrad = true;
           clean_store = nbt->rowc != nullptr;   // store batch: rows through its utterance table
           pcw = pp;        // clean rows only (dad_prep_clean_load / _store)
           pp.clean = 0;    // noisy rows only
+        }
+        if (pending) {     // the caller prepares the rest (under the DP exchange): the tail launch none
+          *pending = DAD_PREP_NOISY | (clean_in_wgrad ? 0 : DAD_PREP_CLEAN);
+          memset(&pp, 0, sizeof(pp));
         }
       }
       hipLaunchKernelGGL(dad_tail_ecda_w, dim3(nblk), dim3(DAD_TAIL_THREADS), 0, stream, ta, ca, pp, pa);
@@ -599,6 +607,32 @@ int dad_step_backward(const dad_config* cfg, const dad_batch* bt, const dad_stat
 int dad_step_backward_ahead(const dad_config* cfg, const dad_batch* bt, const dad_state* st, void* workspace,
                             void* stream, const dad_config* next_cfg, const dad_batch* next_batch, int* prepped) {
   return step_compute_phases(cfg, bt, st, workspace, stream, false, true, next_cfg, next_batch, prepped);
+}
+
+int dad_step_backward_ahead_split(const dad_config* cfg, const dad_batch* bt, const dad_state* st, void* workspace,
+                                  void* stream, const dad_config* next_cfg, const dad_batch* next_batch, int* prepped,
+                                  int* pending) {
+  if (!pending) return DAD_E_ARG;
+  return step_compute_phases(cfg, bt, st, workspace, stream, false, true, next_cfg, next_batch, prepped, pending);
+}
+
+int dad_step_prepare_rows(const dad_config* cfg, const dad_batch* bt, void* workspace, void* stream, int parts) {
+  const int rc = check_cfg(cfg);
+  if (rc) return rc;
+  if (!bt || !workspace || (parts & ~(DAD_PREP_CLEAN | DAD_PREP_NOISY)) != 0) return DAD_E_ARG;
+  if (!dad_prec16(cfg->precision)) return DAD_E_UNSUPPORTED;
+  if (parts == 0) return DAD_OK;
+  if ((parts & DAD_PREP_CLEAN) && !bt->xc) return DAD_E_ARG;
+  const bool noisy = (parts & DAD_PREP_NOISY) && !cfg->warmup;
+  if (noisy && (!bt->xn || (cfg->rng_mode == DAD_RNG_EXPLICIT && (!bt->nw || !bt->ns || !bt->u || !bt->start))))
+    return DAD_E_ARG;
+  if ((bt->rowc == nullptr) != (bt->lenc == nullptr) || (bt->rown == nullptr) != (bt->lenn == nullptr)) return DAD_E_ARG;
+  const DadWs L = dad_ws_layout(geom_of(cfg), max_splits_of(cfg), cfg->precision);
+  DadPrepArgs p = prep_args(cfg, bt, ws_ptr<uint16_t>(workspace, L.xs16 + (cfg->counter & 1u) * L.x16set));
+  p.clean = (parts & DAD_PREP_CLEAN) ? 1 : 0;
+  if (!p.clean && !noisy) return DAD_OK;
+  if (!noisy) p.warmup = 1;   // (dad_prep_rows: no noisy rows in a warm-up set)
+  return launch_prep(p, (hipStream_t)stream);
 }
 
 int dad_step_apply(const dad_config* cfg, const dad_state* st, void* workspace, void* stream_) {

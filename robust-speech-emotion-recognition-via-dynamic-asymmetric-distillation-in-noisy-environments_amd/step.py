@@ -132,10 +132,14 @@ class DADStep:
         rng: 'counter' (in-kernel counter-based RNG) or 'explicit' (draws passed to step()).
         seed: counter-RNG seed.
         comm: optional `dist.DPComm` for data-parallel gradient averaging.
+        prep_under_exchange: 16-bit steps that name their next batch: prepare its noisy rows on a
+            second stream while the gradient all-reduce runs (dad_step_backward_ahead_split), instead
+            of on the tail launch's spare blocks.  Default: on when `comm` spans more than one rank
+            (at one rank there is no exchange to hide it under).  Results are bit-identical.
     """
 
     def __init__(self, model, cfg=None, flavor=None, precision="fp32", rng="counter", seed=0, comm=None,
-                 anchors=None, splits=0):
+                 anchors=None, splits=0, prep_under_exchange=None):
         self.model = model
         self.view = cfg if isinstance(cfg, ConfigView) else ConfigView(cfg, flavor=flavor)
         self.device = model.student_flat.device
@@ -169,6 +173,11 @@ class DADStep:
         self.last_prepped = False
         self._next_keep = None
         self._shadow_dirty = False
+        if prep_under_exchange is None:
+            prep_under_exchange = comm is not None and comm.world > 1
+        self.prep_under_exchange = bool(prep_under_exchange)
+        self._side = None            # the side stream of the preparation under the exchange
+        self._prep_event = None      # recorded after it: the next step's encoder waits for it
         self.refresh_shadow()
 
     # ----------------------------------------------------------------------------- state
@@ -388,6 +397,7 @@ class DADStep:
         pk, self._prepped_key = self._prepped_key, None
         cfg.prepped = 1 if (pk is not None and pk == self._prep_key(cfg, bt)) else 0
         self.last_prepped = bool(cfg.prepped)   # diagnostics: this step's rows came from the last tail launch
+        self._join_side()                   # the rows prepared on the side stream under the last exchange
         ws = self._workspace(cfg)
         stream = self._stream()
         L = _lib.lib()
@@ -402,21 +412,49 @@ class DADStep:
                                                    counter=next_counter)
         else:
             ncfg = None
+        pending = ctypes.c_int(0)
         if ncfg is not None:
             done = ctypes.c_int(0)
-            _lib.check(L.dad_step_backward_ahead(cfg, bt, st, _lib.ptr(ws), stream, ncfg, nbt, ctypes.byref(done)),
-                       "dad_step_backward_ahead")
+            if self.prep_under_exchange:
+                _lib.check(L.dad_step_backward_ahead_split(cfg, bt, st, _lib.ptr(ws), stream, ncfg, nbt,
+                                                           ctypes.byref(done), ctypes.byref(pending)),
+                           "dad_step_backward_ahead_split")
+            else:
+                _lib.check(L.dad_step_backward_ahead(cfg, bt, st, _lib.ptr(ws), stream, ncfg, nbt, ctypes.byref(done)),
+                           "dad_step_backward_ahead")
             if done.value:
                 self._prepped_key = self._prep_key(ncfg, nbt)
                 self._next_keep = nkeep          # the preparation reads these until it has run
         else:
             _lib.check(L.dad_step_backward(cfg, bt, st, _lib.ptr(ws), stream), "dad_step_backward")
+        if pending.value:
+            # the next batch's remaining rows on the side stream, from the end of the backward on:
+            # under the all-reduce (and the optimizer), on CUs the exchange leaves idle
+            main = torch.cuda.current_stream(self.device)
+            if self._side is None:
+                self._side = torch.cuda.Stream(self.device)
+            ev = torch.cuda.Event()
+            ev.record(main)
+            self._side.wait_event(ev)
+            _lib.check(L.dad_step_prepare_rows(ncfg, nbt, _lib.ptr(ws), self._side.cuda_stream, pending.value),
+                       "dad_step_prepare_rows")
+            self._prep_event = torch.cuda.Event()
+            self._prep_event.record(self._side)
         if self.comm is not None and self.comm.world > 1:
             self.comm.allreduce_grad(st, stream, grad=self.grad)
+        if torch.cuda.is_current_stream_capturing():
+            self._join_side()               # a captured graph must join its side stream itself
         _lib.check(L.dad_step_apply(cfg, st, _lib.ptr(ws), stream), "dad_step_apply")
         self.adam_step += 1
         self.global_step += 1
         return self.losses()
+
+    def _join_side(self):
+        """The current stream waits for the preparation issued on the side stream (if any): before
+        anything reads or reallocates the workspace."""
+        if self._prep_event is not None:
+            torch.cuda.current_stream(self.device).wait_event(self._prep_event)
+            self._prep_event = None
 
     def train_step(self, clean_batch, noisy_batch, epoch, draws=None):
         """Trainer.train_step (I/train.py:397-471) with an autograd-compatible total_loss.
@@ -430,6 +468,7 @@ class DADStep:
         if self.comm is not None and self.comm.world > 1:
             raise RuntimeError("train_step is the single-process shim; use step() with a DPComm")
         self.refresh_shadow()        # the caller's optimizer/EMA changed the fp32 params
+        self._join_side()
         self._prepped_key = None     # (this step prepares its own rows into the workspace)
         cfg, bt, st = self._prepare(clean_batch, noisy_batch, epoch, None, draws)
         ws = self._workspace(cfg)

@@ -19,8 +19,9 @@ pytestmark = pytest.mark.gpu
 K = 7
 
 
-def _chain(cfg, precision, batches, st, ahead, wrong_at=None):
+def _chain(cfg, precision, batches, st, ahead, wrong_at=None, split=False):
     step = gh.make_step(cfg, precision=precision, rng="counter", seed=5)
+    step.prep_under_exchange = split    # (the DP step's default: noisy rows on a side stream)
     gh.load_state(step, st)
     losses, prepped = [], []
     for k in range(K):
@@ -108,3 +109,60 @@ def test_prefetch_store_batches(precision):
         for name, a, b in zip(("student", "teacher", "exp_avg", "exp_avg_sq", "dacp", "grad"), got, want):
             assert torch.equal(a, b), "%s: %s differs (max %.3g)" % (key, name, float((a - b).abs().max()))
         assert got_losses == want_losses, key
+
+
+@pytest.mark.parametrize("precision,B,T", [("fp16", 16, 40), ("fp16", 64, 300)])
+def test_prefetch_under_exchange_equals_plain_chain(precision, B, T):
+    """The data-parallel layout (DADStep.prep_under_exchange, C ABI dad_step_backward_ahead_split +
+    dad_step_prepare_rows): the tail launch prepares none of the next batch's rows, the weight
+    gradient converts its clean rows and the noisy rows are prepared on a second stream from the
+    end of the backward on (under the all-reduce at N > 1; here on one GPU without one), the next
+    step's encoder waiting on its event.  The chain equals the plain chain bit for bit, with the
+    same steps skipping their own preparation as the tail-launch layout."""
+    cfg = dad_oracle.make_cfg("iemocap")
+    Bn, Tn = (12, 50) if B == 16 else (B, T)
+    batches = [_device_batches(_problem(B=B, T=T, seed=61 + i, Bn=Bn, Tn=Tn))[:2] for i in range(3)]
+    st = synth.make_state(61, 1)
+    want, want_losses, _ = _chain(cfg, precision, batches, st, ahead=False)
+    got, got_losses, prepped = _chain(cfg, precision, batches, st, ahead=True, wrong_at=3, split=True)
+    assert prepped == [False, True, True, True, False, True, True], prepped
+    for name, a, b in zip(("student", "teacher", "exp_avg", "exp_avg_sq", "dacp", "grad"), got, want):
+        assert torch.equal(a, b), "%s differs (max %.3g)" % (name, float((a - b).abs().max()))
+    assert got_losses == want_losses
+
+
+def test_prepare_rows_matches_step_preparation():
+    """dad_step_prepare_rows writes exactly the prepared set a step's own preparation writes: a step
+    run after it with cfg.prepped = 1 (rows taken from the set) equals the same step preparing its
+    rows itself, bit for bit."""
+    import ctypes
+    import dadpkg
+    PKG = dadpkg.pkg()
+    L = PKG._lib.lib()
+    cfg = dad_oracle.make_cfg("iemocap")
+    c, n = _device_batches(_problem(B=16, T=40, seed=71, Bn=12, Tn=50))[:2]
+    st = synth.make_state(71, 1)
+    res = []
+    for external in (False, True):
+        step = gh.make_step(cfg, precision="fp16", rng="counter", seed=5)
+        gh.load_state(step, st)
+        if external:
+            dcfg, bt, keep = step._batch_structs(c, n, 60, None, None)
+            ws = step._workspace(dcfg)
+            rc = L.dad_step_prepare_rows(dcfg, bt, PKG._lib.ptr(ws), step._stream(),
+                                         PKG._lib.PREP_CLEAN | PKG._lib.PREP_NOISY)
+            assert rc == 0
+            step._prepped_key = step._prep_key(dcfg, bt)      # as if the previous step had prepared it
+        out = step.step(c, n, 60)
+        assert step.last_prepped == external
+        torch.cuda.synchronize()
+        res.append((_state(step), {k: float(v) for k, v in out.items()}))
+    for name, a, b in zip(("student", "teacher", "exp_avg", "exp_avg_sq", "dacp", "grad"), res[1][0], res[0][0]):
+        assert torch.equal(a, b), name
+    assert res[0][1] == res[1][1]
+    # FP32 has no prepared rows; bad part masks are refused
+    dcfg, bt, _ = step._batch_structs(c, n, 60, None, None)
+    ws = step._workspace(dcfg)
+    assert L.dad_step_prepare_rows(dcfg, bt, PKG._lib.ptr(ws), step._stream(), 4) == 1001
+    dcfg.precision = PKG._lib.PREC_FP32
+    assert L.dad_step_prepare_rows(dcfg, bt, PKG._lib.ptr(ws), step._stream(), 3) == 1004
