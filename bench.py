@@ -837,9 +837,13 @@ def main():
     ap.add_argument("--no-parity", action="store_true", help="skip the 16-bit-vs-fp32 parity block (N=1)")
     ap.add_argument("--no-ahead", action="store_true",
                     help="16-bit modes: every step prepares its own rows (no next-batch preparation in the tail launch)")
-    ap.add_argument("--prep-under-exchange", default="auto", choices=["auto", "on", "off"],
-                    help="16-bit modes: the next batch's noisy rows on a side stream from the end of the backward "
-                         "(under the all-reduce; the default at N > 1) instead of in the tail launch (the default at N = 1)")
+    ap.add_argument("--prep-under-exchange", default="auto", choices=["auto", "off", "clean", "noisy", "all"],
+                    help="16-bit modes: which of the next batch's rows are prepared on a side stream from the end of "
+                         "the backward (under the all-reduce) instead of inside the step's launches; auto = off (measured "
+                         "slower at exchange windows of 0-20 us, DESIGN.md section 5)")
+    ap.add_argument("--exchange-us", type=float, default=0.0,
+                    help="N = 1 only: a spin of about this many microseconds after the backward, standing in for a DP "
+                         "step's all-reduce window (measures the --prep-under-exchange layouts on one GPU)")
     ap.add_argument("--launch", default="eager", choices=["graph", "eager"],
                     help="timed steps as eager launches (default) or hipGraph replays (one graph per resident batch; "
                          "measured no faster on this ROCm, DESIGN.md §5)")
@@ -891,12 +895,22 @@ def main():
     else:
         view = flavor_view(args)
         step = PKG.DADStep(model, view, precision=args.precision, rng="counter", seed=1000 + rank, comm=comm,
-                           prep_under_exchange=None if args.prep_under_exchange == "auto"
-                           else args.prep_under_exchange == "on")
+                           prep_under_exchange={"auto": None, "off": 0, "clean": 1, "noisy": 2,
+                                                "all": 3}[args.prep_under_exchange])
         data = make_batches(P, N_BATCHES, B, T, seed=17 + rank, device=dev, snr_db=args.snr)
         torch.cuda.synchronize()
 
         pos = [0]
+        spin = None
+        if args.exchange_us > 0 and world == 1:
+            # torch.cuda._sleep spins for a number of GPU clock cycles: calibrated here against events
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            torch.cuda._sleep(1000000)
+            e1.record()
+            torch.cuda.synchronize()
+            cyc = int(args.exchange_us * 1e6 / (e0.elapsed_time(e1) * 1e3))
+            spin = lambda: torch.cuda._sleep(cyc)
 
         def run(n):
             # each step names the next resident batch: its augmentation + 16-bit conversion run in
@@ -905,7 +919,8 @@ def main():
                 i = pos[0]
                 pos[0] += 1
                 c, nb = data[i % len(data)]
-                step.step(c, nb, args.epoch, next_batch=None if args.no_ahead else data[(i + 1) % len(data)])
+                step.step(c, nb, args.epoch, next_batch=None if args.no_ahead else data[(i + 1) % len(data)],
+                          after_backward=spin)
 
         # The side legs of the line (the FP32 mode, the BF16 mode, the data path) run first, from the
         # initial state, which is restored after them; then the W warm-up steps, right before the
@@ -1077,8 +1092,9 @@ def main():
                    "global_batch": B * world, "per_gpu_batch": B, "seq_len": T, "feature_dim": 768,
                    "parallelism": "dp%d" % world},
         "comm": {"transport": args.comm if world > 1 else None, "ranks_seen": ranks_seen,
-                 "next_noisy_rows": "side stream under the exchange" if getattr(step, "prep_under_exchange", False)
-                 else "tail launch"},
+                 "next_rows_under_exchange": {0: "none", 1: "clean", 2: "noisy", 3: "clean+noisy"}[
+                     step._defer_parts() if hasattr(step, "_defer_parts") else 0],
+                 "exchange_standin_us": args.exchange_us if world == 1 else None},
         "launch": launch if not args.mixed else "eager",
         "roofline": rf, "step_roofline": srf, "kernels": kern,
         "losses_last_step": losses, "mask_sum_last_step": msum, "ecda_on_last_step": ecda_on,

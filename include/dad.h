@@ -220,18 +220,19 @@ int dad_step_backward(const dad_config* cfg, const dad_batch* batch, const dad_s
 int dad_step_backward_ahead(const dad_config* cfg, const dad_batch* batch, const dad_state* st,
                             void* workspace, void* stream, const dad_config* next_cfg,
                             const dad_batch* next_batch, int* prepped);
-/* dad_step_backward_ahead with the next batch's rows left (partly) to the caller, for the data-parallel
- * step (ABI 6): the tail launch prepares none of them (it then ends with its tail and class blocks), the
- * weight gradient still converts the clean rows where it can (padded next batches, or store batches of
- * at most 64 utterances), and *pending = the DAD_PREP_* parts the caller must prepare with
+/* dad_step_backward_ahead with parts of the next batch's rows left to the caller, for the data-parallel
+ * step (ABI 6): `defer` (DAD_PREP_CLEAN and/or DAD_PREP_NOISY) names the parts this step's launches skip
+ * (deferred clean rows: the weight gradient runs as the plain GEMM; deferred noisy rows: the tail launch
+ * ends with its tail and class blocks); *pending = the parts the caller must prepare with
  * dad_step_prepare_rows(next_cfg, next_batch, workspace, any stream, *pending) before the next step's
  * dad_step_encode (order the streams with events).  A DP caller issues it on a second stream under the
- * gradient all-reduce, where the CUs would idle.  *prepped as for dad_step_backward_ahead. */
+ * gradient all-reduce, where the CUs would idle.  *prepped as for dad_step_backward_ahead (*pending = 0
+ * when *prepped = 0). */
 #define DAD_PREP_CLEAN 1
 #define DAD_PREP_NOISY 2
 int dad_step_backward_ahead_split(const dad_config* cfg, const dad_batch* batch, const dad_state* st,
                                   void* workspace, void* stream, const dad_config* next_cfg,
-                                  const dad_batch* next_batch, int* prepped, int* pending);
+                                  const dad_batch* next_batch, int defer, int* prepped, int* pending);
 /* FP16/BF16: the augmentation and 16-bit conversion of (cfg, batch)'s rows (parts: DAD_PREP_CLEAN and/or
  * DAD_PREP_NOISY) into the workspace's prepared set of cfg->counter's parity -- the set the step with this
  * cfg reads (dad_prep; the draws of cfg's counter).  DAD_E_UNSUPPORTED in FP32. */

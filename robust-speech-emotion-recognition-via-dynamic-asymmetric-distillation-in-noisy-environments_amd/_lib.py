@@ -90,7 +90,7 @@ EXPORTS = {
                                                ctypes.POINTER(ctypes.c_int)]),
     "dad_step_backward_ahead_split": (ctypes.c_int, [ctypes.POINTER(DadConfig), ctypes.POINTER(DadBatch),
                                                      ctypes.POINTER(DadState), ctypes.c_void_p, ctypes.c_void_p,
-                                                     ctypes.POINTER(DadConfig), ctypes.POINTER(DadBatch),
+                                                     ctypes.POINTER(DadConfig), ctypes.POINTER(DadBatch), ctypes.c_int,
                                                      ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     "dad_step_prepare_rows": (ctypes.c_int, [ctypes.POINTER(DadConfig), ctypes.POINTER(DadBatch), ctypes.c_void_p,
                                              ctypes.c_void_p, ctypes.c_int]),

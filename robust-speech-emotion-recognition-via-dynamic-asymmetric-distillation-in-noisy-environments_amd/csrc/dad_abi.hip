@@ -350,12 +350,12 @@ static bool can_prepare_ahead(const dad_config* cfg, const dad_config* ncfg, con
   return true;
 }
 
-// pending != nullptr (dad_step_backward_ahead_split): the tail launch prepares none of the next
-// batch's rows; the weight gradient still converts its clean rows where it can, and *pending names
-// the parts (DAD_PREP_*) the caller prepares with dad_step_prepare_rows
+// defer (dad_step_backward_ahead_split): the DAD_PREP_* parts of the next batch's rows this step's
+// launches leave to the caller (dad_step_prepare_rows); *pending = the parts actually left
 static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const dad_state* st, void* workspace,
                                void* stream_, bool do_encode, bool do_backward, const dad_config* ncfg = nullptr,
-                               const dad_batch* nbt = nullptr, int* prepped = nullptr, int* pending = nullptr) {
+                               const dad_batch* nbt = nullptr, int* prepped = nullptr, int defer = 0,
+                               int* pending = nullptr) {
   if (prepped) *prepped = 0;
   if (pending) *pending = 0;
   int rc = check_cfg(cfg);
@@ -501,18 +501,21 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
         const int rc = device_cus(&cus);
         if (rc) return rc;
         pp = prep_args(ncfg, nbt, ws_ptr<uint16_t>(workspace, L.xs16 + (ncfg->counter & 1u) * L.x16set));
-        if (!pending) nblk = std::max(nblk, std::max(cus, 2 * (1 + DAD_C)));
         if (prepped) *prepped = 1;
-        if (DAD_CLEAN_IN_WGRAD && h16 && (nbt->rowc == nullptr || ncfg->B <= 64)) {
+        if (!(defer & DAD_PREP_CLEAN) && DAD_CLEAN_IN_WGRAD && h16 && (nbt->rowc == nullptr || ncfg->B <= 64)) {
           clean_in_wgrad = true;
           clean_store = nbt->rowc != nullptr;   // store batch: rows through its utterance table
           pcw = pp;        // clean rows only (dad_prep_clean_load / _store)
           pp.clean = 0;    // noisy rows only
         }
-        if (pending) {     // the caller prepares the rest (under the DP exchange): the tail launch none
-          *pending = DAD_PREP_NOISY | (clean_in_wgrad ? 0 : DAD_PREP_CLEAN);
-          memset(&pp, 0, sizeof(pp));
-        }
+        if (defer & DAD_PREP_CLEAN) pp.clean = 0;   // the caller's (under the DP exchange)
+        const bool noisy_here = !(defer & DAD_PREP_NOISY);
+        if (pending) *pending = defer & (DAD_PREP_CLEAN | DAD_PREP_NOISY);
+        if (!noisy_here && !pp.clean) memset(&pp, 0, sizeof(pp));   // nothing left for the tail launch
+        // spare blocks for whatever the tail launch prepares (noisy rows, and clean ones when the weight
+        // gradient cannot take them)
+        if (pp.x16) nblk = std::max(nblk, std::max(cus, 2 * (1 + DAD_C)));
+        if (pp.x16 && !noisy_here) pp.warmup = 1;   // (dad_prep_rows: clean rows only)
       }
       hipLaunchKernelGGL(dad_tail_ecda_w, dim3(nblk), dim3(DAD_TAIL_THREADS), 0, stream, ta, ca, pp, pa);
     } else
@@ -610,10 +613,11 @@ int dad_step_backward_ahead(const dad_config* cfg, const dad_batch* bt, const da
 }
 
 int dad_step_backward_ahead_split(const dad_config* cfg, const dad_batch* bt, const dad_state* st, void* workspace,
-                                  void* stream, const dad_config* next_cfg, const dad_batch* next_batch, int* prepped,
-                                  int* pending) {
-  if (!pending) return DAD_E_ARG;
-  return step_compute_phases(cfg, bt, st, workspace, stream, false, true, next_cfg, next_batch, prepped, pending);
+                                  void* stream, const dad_config* next_cfg, const dad_batch* next_batch, int defer,
+                                  int* prepped, int* pending) {
+  if (!pending || (defer & ~(DAD_PREP_CLEAN | DAD_PREP_NOISY)) != 0) return DAD_E_ARG;
+  return step_compute_phases(cfg, bt, st, workspace, stream, false, true, next_cfg, next_batch, prepped, defer,
+                             pending);
 }
 
 int dad_step_prepare_rows(const dad_config* cfg, const dad_batch* bt, void* workspace, void* stream, int parts) {

@@ -132,10 +132,15 @@ class DADStep:
         rng: 'counter' (in-kernel counter-based RNG) or 'explicit' (draws passed to step()).
         seed: counter-RNG seed.
         comm: optional `dist.DPComm` for data-parallel gradient averaging.
-        prep_under_exchange: 16-bit steps that name their next batch: prepare its noisy rows on a
-            second stream while the gradient all-reduce runs (dad_step_backward_ahead_split), instead
-            of on the tail launch's spare blocks.  Default: on when `comm` spans more than one rank
-            (at one rank there is no exchange to hide it under).  Results are bit-identical.
+        prep_under_exchange: 16-bit steps that name their next batch: which of its rows are prepared
+            on a second stream from the end of the backward on, i.e. under the gradient all-reduce
+            (dad_step_backward_ahead_split), instead of inside this step's launches: 0 / False (none,
+            the default), True (= the clean rows: the weight gradient then runs as the plain GEMM), or a
+            mask of _lib.PREP_CLEAN / PREP_NOISY.  Results are bit-identical either way.  Measured on
+            one MI355X with a spin standing in for the exchange window (bench.py --exchange-us, DESIGN
+            section 5): the side-stream layouts cost 21-40 us per step against the in-launch layout at
+            windows of 0-20 us (the two cross-stream hops and the standalone preparation are exposed),
+            so nothing is moved by default at any N; the option is for longer exchange windows.
     """
 
     def __init__(self, model, cfg=None, flavor=None, precision="fp32", rng="counter", seed=0, comm=None,
@@ -173,9 +178,7 @@ class DADStep:
         self.last_prepped = False
         self._next_keep = None
         self._shadow_dirty = False
-        if prep_under_exchange is None:
-            prep_under_exchange = comm is not None and comm.world > 1
-        self.prep_under_exchange = bool(prep_under_exchange)
+        self.prep_under_exchange = 0 if prep_under_exchange is None else prep_under_exchange
         self._side = None            # the side stream of the preparation under the exchange
         self._prep_event = None      # recorded after it: the next step's encoder waits for it
         self.refresh_shadow()
@@ -374,7 +377,7 @@ class DADStep:
         return True
 
     def step(self, clean_batch, noisy_batch, epoch, lr=None, draws=None, after_encode=None, next_batch=None,
-             next_counter=None):
+             next_counter=None, after_backward=None):
         """One full training step; returns the reference's loss dict as 0-d device tensors.
 
         after_encode: optional callable run on the host between the encoder launch and the rest
@@ -387,6 +390,9 @@ class DADStep:
         labels and, with explicit draws, the draws in DADStep's dtypes, all on the step's device);
         a host batch is ignored here and copied once, by the step that runs it.  The named
         batch's device tensors must keep their contents until that step.
+        after_backward: optional callable run on the host after the backward and the gradient
+            exchange are enqueued, before the update (bench.py enqueues a timed spin there to stand in
+            for the all-reduce window of a DP step on one GPU).
         next_counter: the next step's RNG step counter (default this step's + 1).  Graph replays
         that cycle a fixed set of captured steps pass the first captured step's counter from the
         last one (bench.capture_steps), so the cycle stays consistent.
@@ -415,8 +421,9 @@ class DADStep:
         pending = ctypes.c_int(0)
         if ncfg is not None:
             done = ctypes.c_int(0)
-            if self.prep_under_exchange:
-                _lib.check(L.dad_step_backward_ahead_split(cfg, bt, st, _lib.ptr(ws), stream, ncfg, nbt,
+            defer = self._defer_parts()
+            if defer:
+                _lib.check(L.dad_step_backward_ahead_split(cfg, bt, st, _lib.ptr(ws), stream, ncfg, nbt, defer,
                                                            ctypes.byref(done), ctypes.byref(pending)),
                            "dad_step_backward_ahead_split")
             else:
@@ -442,12 +449,21 @@ class DADStep:
             self._prep_event.record(self._side)
         if self.comm is not None and self.comm.world > 1:
             self.comm.allreduce_grad(st, stream, grad=self.grad)
+        if after_backward is not None:
+            after_backward()                # (bench.py: a stand-in for the exchange window at N = 1)
         if torch.cuda.is_current_stream_capturing():
             self._join_side()               # a captured graph must join its side stream itself
         _lib.check(L.dad_step_apply(cfg, st, _lib.ptr(ws), stream), "dad_step_apply")
         self.adam_step += 1
         self.global_step += 1
         return self.losses()
+
+    def _defer_parts(self):
+        """prep_under_exchange as a DAD_PREP_* mask (True: the clean rows)."""
+        v = self.prep_under_exchange
+        if v is True:
+            return _lib.PREP_CLEAN
+        return int(v or 0)
 
     def _join_side(self):
         """The current stream waits for the preparation issued on the side stream (if any): before

@@ -88,9 +88,9 @@ SCHEDULE16 = [35, 60, 60]
 
 
 def _rank_main_fp16(rank, world, port, q):
-    """The timed mode's DP path: fp16 operands, each step naming its next batch (its noisy rows prepared
-    on a side stream under the exchange, DADStep.prep_under_exchange; and, as at N = 1, in this step's
-    tail launch), gloo exchange.  Per rank: every step against the
+    """The timed mode's DP path: fp16 operands, each step naming its next batch (its rows prepared inside
+    this step's launches, the default; and its clean rows, or all of them, on a side stream under the
+    exchange, DADStep.prep_under_exchange), gloo exchange.  Per rank: every step against the
     oracle's DP step on this rank's shard within the fp16 bounds of test_gpu_throughput_parity
     (losses 1e-4, mask bit-exact; logits within test_gpu_16bit's bound for short synthetic rows); the chain with next-batch preparation equals the
     chain without it bit for bit; the replicas stay bit-identical."""
@@ -129,7 +129,7 @@ def _rank_main_fp16(rank, world, port, q):
             dist.all_reduce(t)
             return t.numpy()
 
-        def chain(ahead, check, split=True):
+        def chain(ahead, check, split=0):
             model = p.SSRLModel().cuda()
             step = p.DADStep(model, p.ConfigView(cfg, flavor="iemocap"), precision="fp16", rng="explicit",
                              comm=p.ProcessGroupComm(), prep_under_exchange=split)
@@ -167,13 +167,14 @@ def _rank_main_fp16(rank, world, port, q):
             return state, losses, prepped
 
         plain, plain_losses, plain_prepped = chain(False, True)
-        # the DP default: the next batch's noisy rows on a side stream under the exchange
+        # the next batch's rows inside this step's launches (the default at every N)
         ahead, ahead_losses, ahead_prepped = chain(True, False)
         assert not any(plain_prepped) and ahead_prepped == [False, False, True], ahead_prepped
         assert torch.equal(plain, ahead) and plain_losses == ahead_losses, "next-batch preparation changed the DP chain"
-        # the N = 1 layout (noisy rows in the tail launch) with the exchange
-        tl, tl_losses, tl_prepped = chain(True, False, split=False)
-        assert tl_prepped == [False, False, True] and torch.equal(plain, tl) and plain_losses == tl_losses
+        # the clean rows, and all of the next batch's rows, on a side stream under the exchange
+        for split in (1, 3):
+            tl, tl_losses, tl_prepped = chain(True, False, split=split)
+            assert tl_prepped == [False, False, True] and torch.equal(plain, tl) and plain_losses == tl_losses, split
         other = plain.clone().double()
         dist.broadcast(other, src=0)
         assert torch.equal(plain.double(), other), "ranks diverged"
@@ -218,5 +219,5 @@ def test_bench_spawns_ranks_gloo():
     assert line["n_gpus"] == 2
     assert line["config"]["parallelism"] == "dp2"
     assert line["config"]["global_batch"] == 128
-    assert line["comm"] == {"transport": "gloo", "ranks_seen": 2}
+    assert line["comm"]["transport"] == "gloo" and line["comm"]["ranks_seen"] == 2
     assert line["value"] > 0 and line["ecda_on_last_step"] == 1.0

@@ -111,20 +111,21 @@ def test_prefetch_store_batches(precision):
         assert got_losses == want_losses, key
 
 
-@pytest.mark.parametrize("precision,B,T", [("fp16", 16, 40), ("fp16", 64, 300)])
-def test_prefetch_under_exchange_equals_plain_chain(precision, B, T):
+@pytest.mark.parametrize("precision,B,T,parts", [("fp16", 16, 40, 1), ("fp16", 16, 40, 2), ("fp16", 16, 40, 3),
+                                                 ("fp16", 64, 300, 1), ("bf16", 64, 300, 3)])
+def test_prefetch_under_exchange_equals_plain_chain(precision, B, T, parts):
     """The data-parallel layout (DADStep.prep_under_exchange, C ABI dad_step_backward_ahead_split +
-    dad_step_prepare_rows): the tail launch prepares none of the next batch's rows, the weight
-    gradient converts its clean rows and the noisy rows are prepared on a second stream from the
-    end of the backward on (under the all-reduce at N > 1; here on one GPU without one), the next
-    step's encoder waiting on its event.  The chain equals the plain chain bit for bit, with the
+    dad_step_prepare_rows): the deferred parts of the next batch's rows (1 clean: the weight gradient
+    runs without its conversion; 2 noisy: the tail launch without its preparation; 3 both) are
+    prepared on a second stream from the end of the backward on (under the all-reduce at N > 1; here
+    on one GPU without one), the next step's encoder waiting on its event.  The chain equals the plain chain bit for bit, with the
     same steps skipping their own preparation as the tail-launch layout."""
     cfg = dad_oracle.make_cfg("iemocap")
     Bn, Tn = (12, 50) if B == 16 else (B, T)
     batches = [_device_batches(_problem(B=B, T=T, seed=61 + i, Bn=Bn, Tn=Tn))[:2] for i in range(3)]
     st = synth.make_state(61, 1)
     want, want_losses, _ = _chain(cfg, precision, batches, st, ahead=False)
-    got, got_losses, prepped = _chain(cfg, precision, batches, st, ahead=True, wrong_at=3, split=True)
+    got, got_losses, prepped = _chain(cfg, precision, batches, st, ahead=True, wrong_at=3, split=parts)
     assert prepped == [False, True, True, True, False, True, True], prepped
     for name, a, b in zip(("student", "teacher", "exp_avg", "exp_avg_sq", "dacp", "grad"), got, want):
         assert torch.equal(a, b), "%s differs (max %.3g)" % (name, float((a - b).abs().max()))
