@@ -2203,10 +2203,14 @@ __device__ __forceinline__ void ecda_block_w(const DadEcdaArgs& a, const DadTail
   const bool rep_on = nvalid > 1 && cnc > 0 && rep_coef != 0.0f;
   ECDA_CYC(13);
   if (!gc && !rep_on) return;
-  // candidates: clean rows of label c (members when gated), then noisy rows of pseudo-label c
-  // (members when masked in); positions by ballot prefix counts, every wave alike
+  // candidates: clean rows of label c (members when gated), then the noisy rows of pseudo-label c
+  // that the mask takes in (I/utils.py:573-576, the reference's target set); positions by ballot
+  // prefix counts, every wave alike.  Noisy rows of pseudo-label c left out by the mask take no part
+  // in any term (kernel pairs, bandwidth, centroids, gradients), so they are not staged: a teacher
+  // that sends most of the noisy batch to one class with half of it masked out no longer pushes
+  // that class past 64 candidates into the wide path
   const bool ccand = gc && y == c;
-  const bool ncand = lane < Bn && M.p == c;
+  const bool ncand = lane < Bn && M.p == c && M.m;
   const uint64_t bc = __ballot(ccand), bn = __ballot(ncand);
   const int ncs = gc ? ccc : 0;
   const int ncand_all = ncs + (int)__popcll(bn);
@@ -2243,7 +2247,7 @@ __device__ __forceinline__ void ecda_block_w(const DadEcdaArgs& a, const DadTail
   if (g == 0) {
     if (lane < DAD_C) S.cnt[lane] = sel4i(cn, lane);
     if (ccand) { S.rowz[posc] = lane; S.wz[posc] = 1.0f; S.mem[posc] = 1; }
-    if (ncand) { S.rowz[posn] = lane; S.wz[posn] = M.s; S.mem[posn] = M.m ? 1 : 0; }
+    if (ncand) { S.rowz[posn] = lane; S.wz[posn] = M.s; S.mem[posn] = 1; }
   }
   ECDA_CYC(16);
   {
@@ -2269,7 +2273,7 @@ __device__ __forceinline__ void ecda_block_w(const DadEcdaArgs& a, const DadTail
   }
   ECDA_CYC(17);
   // weight sum of the noisy members (I/utils.py:552-557), in every wave
-  const double wsum_t = dad_wave_sum_d((ncand && M.m) ? (double)M.s : 0.0);
+  const double wsum_t = dad_wave_sum_d(ncand ? (double)M.s : 0.0);
   (void)cc;
   ECDA_CYC(18);
   ECDA_STAMP(2);

@@ -184,7 +184,7 @@ class FeatureStore:
 
     @staticmethod
     def _pack(index_d, feats, pad, lab, style):
-        net_input = {"feats": feats, "padding_mask": pad.view(torch.bool)}
+        net_input = {"feats": feats, "padding_mask": pad if pad.dtype == torch.bool else pad.view(torch.bool)}
         if style == "casia":           # C/dataload_casia_noisy.py:93-106: no 'id'; 'labels' only when labeled
             return {"net_input": net_input, **({"labels": lab} if lab is not None else {})}
         return {"id": index_d, "net_input": net_input, "labels": lab}
@@ -345,12 +345,9 @@ class _DeviceLoaderIter:
         b = self._batches[k]
         s0, s1 = self._starts[k], self._starts[k + 1]
         if self._rows is not None:   # store mode: this batch's views of the epoch's index tensors
-            T = self._T[k]
-            p0 = self._pad_off[k]
-            pad = self._pad[p0:p0 + (s1 - s0) * T].view(s1 - s0, T)
-            idx_d = self._index_d[s0:s1]
-            feats = StoreFeats(L.store, b, idx_d, self._rows[s0:s1], self._lens[s0:s1], T)
-            return FeatureStore._pack(idx_d, feats, pad, None if self._lab is None else self._lab[s0:s1], L.style)
+            idx_d, rows, lens, pad, lab = self._views[k]
+            feats = StoreFeats(L.store, b, idx_d, rows, lens, self._T[k])
+            return FeatureStore._pack(idx_d, feats, pad, lab, L.style)
         fn = L.store.batch_index if L.fused else L.store.collate
         return fn(b, index_d=self._index_d[s0:s1], T=self._T[k], style=L.style, with_labels=L.with_labels)
 
@@ -375,6 +372,15 @@ class _DeviceLoaderIter:
             _lib.ptr(up[2 * n:]), _lib.ptr(self._rows), _lib.ptr(self._lens), _lib.ptr(self._pad),
             _lib.ptr(st.labels_d if self._lab is not None else None), _lib.ptr(self._lab),
             torch.cuda.current_stream(dev).cuda_stream), "dad_collate_index_epoch")
+        # every batch's views, made here by one split per buffer (C++: well under a microsecond per view)
+        # instead of per next() (five Python slicings and a reshape, ~30 us per batch: with two loaders per
+        # train step that was half of the store-fed step's host time, which bounded it)
+        sizes = [int(x) for x in np.diff(self._starts)]
+        nb = len(sizes)
+        sp = lambda t: t.split(sizes) if t is not None else [None] * nb
+        pads = [c.view(sz, T) for c, sz, T in zip(self._pad.split([s * T for s, T in zip(sizes, self._T)]), sizes,
+                                                   self._T)]
+        self._views = list(zip(sp(self._index_d), sp(self._rows), sp(self._lens), pads, sp(self._lab)))
 
 
 # ------------------------------------------------------------------- reference file formats

@@ -9,6 +9,7 @@ import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
@@ -62,6 +63,15 @@ def main():
         print("%-8s host %6.1f us/step (loaders %5.1f)  wall %6.1f us/step  prepped %s" %
               ("store" if fused else "collate", (t1 - t0) / n * 1e6, tl / n * 1e6, (t2 - t0) / n * 1e6,
                step.last_prepped), flush=True)
+        if fused and os.environ.get("DAD_LIB_VARIANT") == "stamps":
+            import tailw_stamps   # the last steps' tail-launch timelines, and the losses and range flag
+            raw = []
+            for _ in range(8):
+                one()
+                torch.cuda.synchronize()
+                raw.append(tailw_stamps.read_stamps())
+            tailw_stamps.report(np.stack(raw))
+            print("losses", step.losses(), "range flag", step.decode_range_flag(step.range_flag()))
         if fused:
             pr = cProfile.Profile()
             pr.enable()

@@ -26,20 +26,54 @@ def main():
     S = 32  # slots per ECDA class (tail.hip ECDA_SLOTS)
     L = PKG.lib()
     reps = int(os.environ.get("STAMP_REPS", "15"))
+    sleep = int(os.environ.get("STAMP_SLEEP", "0"))     # spin cycles queued ahead of each burst (0: none)
+    store_fed = os.environ.get("STAMP_STORE") == "1"    # batches from store-mode loaders (tools/host_loader.py)
+    if store_fed:
+        n_utt = 1024
+        g = torch.Generator(device="cuda")
+        g.manual_seed(3)
+        st = PKG.data.FeatureStore(torch.randn(n_utt * T, 768, device="cuda", generator=g), np.full(n_utt, T),
+                                   np.arange(n_utt) * T, np.arange(n_utt) % 4, device=torch.device("cuda"))
+
+        def epochs(loader):
+            while True:
+                yield from loader
+        ci = epochs(PKG.data.DeviceLoader(st, batch_size=B, shuffle=True, fused=True))
+        ni = epochs(PKG.data.DeviceLoader(st.subset(np.arange(n_utt), with_labels=False), batch_size=B, shuffle=True,
+                                          fused=True))
+        nxt = [(next(ci), next(ni))]
     raw = []
     for r in range(reps):   # the last step of a 4-step burst, reps times
+        if sleep:
+            torch.cuda._sleep(sleep)
         for i in range(4):   # (STAMP_AHEAD=1, the default: each step names the next, as the bench does)
+            if store_fed:
+                cur, nxt[0] = nxt[0], (next(ci), next(ni))
+                step.step(cur[0], cur[1], 60, next_batch=nxt[0])
+                continue
             nxt = data[(i + 1) % 2] if os.environ.get("STAMP_AHEAD", "1") == "1" else None
             step.step(data[i % 2][0], data[i % 2][1], 60, next_batch=nxt)
         torch.cuda.synchronize()
         ebuf = (ctypes.c_ulonglong * (4 * S + 16))()
         assert L.dad_probe_read_ecda_stamps(ebuf, len(ebuf)) == 0
         raw.append(np.frombuffer(ebuf, dtype=np.uint64).astype(np.int64))
-    raw = np.stack(raw[2:] if reps > 4 else raw)
+    report(np.stack(raw[2:] if reps > 4 else raw))
+
+
+def read_stamps():
+    """The last tail launch's stamps (stamps build only)."""
+    ebuf = (ctypes.c_ulonglong * (4 * 32 + 16))()
+    assert PKG.lib().dad_probe_read_ecda_stamps(ebuf, len(ebuf)) == 0
+    return np.frombuffer(ebuf, dtype=np.uint64).astype(np.int64)
+
+
+def report(raw):
+    S = 32
     T0 = 4 * S
     t0 = raw[:, T0:T0 + 1]
-    rel = np.median((raw - t0) / 100.0, axis=0)
-    on = np.all(raw > 0, axis=0)
+    rel = np.nanmedian(np.where(raw > 0, (raw - t0) / 100.0, np.nan), axis=0)
+    on = np.mean(raw > 0, axis=0) > 0.5
+    print("class blocks stamped in %s of %d steps" % ([int(np.sum(raw[:, c * S] > 0)) for c in range(4)], raw.shape[0]))
     print("median of %d steps; us after the tail block's start" % raw.shape[0])
     if on[T0 + 14]:
         ends = [rel[c * S + 8] for c in range(4) if on[c * S + 8]]
