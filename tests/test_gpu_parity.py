@@ -302,6 +302,40 @@ def test_large_member_sets_match_oracle(class_aware, B, prec):
 
 
 @pytest.mark.parametrize("prec", ["fp32", "fp16"])
+@pytest.mark.parametrize("counts", [(40, 8, 8, 8), (30, 30, 2, 2)], ids=["one_split", "two_split"])
+def test_split_class_blocks_match_oracle(counts, prec):
+    """Classes of 33..64 ECDA members (clean rows of the label + masked noisy rows of the
+    pseudo-label): dad_tail_ecda_w splits each over two class blocks (rows 0..31 / 32..63, the
+    second block's share of the loss term folded in by the loss total).  Losses at 1e-4, mask
+    bit-exact, gradients as the other parity tests (fp32: gh.close_grad; fp16: the throughput
+    bounds); the test checks that the geometry does produce such a class."""
+    cfg = dad_oracle.make_cfg("iemocap")
+    inp = _problem(64, 6, seed=21, snr=20.0)
+    inp["yc"] = np.repeat(np.arange(4), counts).astype(inp["yc"].dtype)
+    st = synth.make_state(21, 1, tau_range=(0.0, 0.01))     # low thresholds: most noisy rows masked in
+    step = gh.make_step(cfg, precision=prec)
+    orc = dad_oracle.DADOracle(*synth.init_weights(21)[:4], cfg)
+    gh.load_state(step, st)
+    orc.load_state(st)
+    o = gh.run_step(step, inp, 60)
+    r = orc.step(inp, 60)
+    m = np.asarray(r["mask"]) > 0
+    members = [int(np.sum(inp["yc"] == c)) + int(np.sum((np.asarray(r["pred"]) == c) & m)) for c in range(4)]
+    assert any(32 < n <= 64 for n in members), members
+    for k in ("total_loss", "supervised_ce_loss", "consistency_loss", "ecda_loss"):
+        _cmp_loss(o[k], r[k], (counts, prec, k))
+    np.testing.assert_array_equal(o["mask"], r["mask"])
+    if prec == "fp32":
+        for k, (a, b_) in enumerate(zip(o["grads"], r["grads"])):
+            gh.close_grad(a, b_, "split class grad %d" % k)
+        return
+    from test_gpu_throughput_parity import TOL, _cos, _normrel
+    g = np.concatenate([x.reshape(-1) for x in o["grads"]])
+    gr = np.concatenate([np.asarray(x).reshape(-1) for x in r["grads"]])
+    assert _normrel(g, gr) <= TOL["fp16"]["grad"] and _cos(g, gr) >= TOL["fp16"]["cos"], members
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp16"])
 def test_ecda_bandwidth_with_large_common_embedding_offset(prec):
     """the detached MMD bandwidth (I/utils.py:537-544, the mean pairwise squared
     distance) is computed from per-class partial sums, sum_ij |z_i - z_j|^2 = 2n sum|d_i|^2 -

@@ -11,6 +11,7 @@ for r in $(seq 1 ${AB_ROUNDS:-2}); do
       --steps ${AB_STEPS:-400} ${BENCH_ARGS:-} > gpurun_out/ab/$v.$r.log 2>&1 || { echo "FAIL $v"; tail -5 gpurun_out/ab/$v.$r.log; exit 1; }
     python -c "
 import json; d=json.loads([l for l in open('gpurun_out/ab/$v.$r.log') if l.startswith('{')][-1])
-print('$v r$r', 'ms %.4f' % d['ms_per_step'], {k: round(v['avg_ms'] * 1e3, 1) for k, v in d['kernels'].items() if 'avg_ms' in v})"
+print('$v r$r', 'ms %.4f' % d['ms_per_step'], {k: round(v['avg_ms'] * 1e3, 1) for k, v in d['kernels'].items() if 'avg_ms' in v},
+      'randlab ms %.4f' % d['random_labels']['ms_per_step'] if 'random_labels' in d else '')"
   done
 done

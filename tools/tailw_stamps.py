@@ -14,6 +14,7 @@ os.environ.setdefault("DAD_LIB_VARIANT", "stamps")
 import bench  # noqa: E402
 
 PKG = bench.PKG
+NB = 8   # class blocks of dad_tail_ecda_w (tail.hip TW_CB): block k = class k % 4, part k // 4
 
 
 def main():
@@ -54,7 +55,7 @@ def main():
             nxt = data[(i + 1) % 2] if os.environ.get("STAMP_AHEAD", "1") == "1" else None
             step.step(data[i % 2][0], data[i % 2][1], 60, next_batch=nxt)
         torch.cuda.synchronize()
-        ebuf = (ctypes.c_ulonglong * (4 * S + 16))()
+        ebuf = (ctypes.c_ulonglong * (NB * S + 16))()
         assert L.dad_probe_read_ecda_stamps(ebuf, len(ebuf)) == 0
         raw.append(np.frombuffer(ebuf, dtype=np.uint64).astype(np.int64))
     report(np.stack(raw[2:] if reps > 4 else raw))
@@ -62,21 +63,21 @@ def main():
 
 def read_stamps():
     """The last tail launch's stamps (stamps build only)."""
-    ebuf = (ctypes.c_ulonglong * (4 * 32 + 16))()
+    ebuf = (ctypes.c_ulonglong * (NB * 32 + 16))()
     assert PKG.lib().dad_probe_read_ecda_stamps(ebuf, len(ebuf)) == 0
     return np.frombuffer(ebuf, dtype=np.uint64).astype(np.int64)
 
 
 def report(raw):
     S = 32
-    T0 = 4 * S
+    T0 = NB * S
     t0 = raw[:, T0:T0 + 1]
     rel = np.nanmedian(np.where(raw > 0, (raw - t0) / 100.0, np.nan), axis=0)
     on = np.mean(raw > 0, axis=0) > 0.5
-    print("class blocks stamped in %s of %d steps" % ([int(np.sum(raw[:, c * S] > 0)) for c in range(4)], raw.shape[0]))
+    print("class blocks stamped in %s of %d steps" % ([int(np.sum(raw[:, c * S] > 0)) for c in range(NB)], raw.shape[0]))
     print("median of %d steps; us after the tail block's start" % raw.shape[0])
     if on[T0 + 14]:
-        ends = [rel[c * S + 8] for c in range(4) if on[c * S + 8]]
+        ends = [rel[c * S + 8] for c in range(NB) if on[c * S + 8]]
         print("launch entry %.2f  tail block start 0  tail end %.2f  class ends %s  last preparation block end %s"
               % (rel[T0 + 14], rel[T0 + 1], " ".join("%.2f" % e for e in ends),
                  ("%.2f" % rel[T0 + 15]) if on[T0 + 15] else "-"))
@@ -88,20 +89,24 @@ def report(raw):
         print("  tail block clock: %.2f GHz" % ghz)
     cyc = [(19, 13, "gates"), (13, 14, "stores+norm-math"), (14, 15, "norm-sums"), (15, 16, "zero+tables"),
            (16, 17, "centroid-partials"), (17, 18, "wsum")]
-    for c in range(4):
+    for c in range(NB):
         o = c * S
         if all(on[o + a] and on[o + b] for a, b, _ in cyc):
             print("ecda class %d staging cycles: %s" % (c, "  ".join(
                 "%s %d" % (n, int(np.median(raw[:, o + b] - raw[:, o + a]))) for a, b, n in cyc)))
     cyc2 = [(6, 20, "cent-dist"), (20, 21, "comp+bw"), (21, 22, "pairs"), (22, 23, "sums"), (23, 24, "b3+terms"),
             (24, 25, "mg-reads+mfma"), (25, 26, "mg-stage"), (26, 27, "mg-stores"), (27, 28, "flags")]
-    for c in range(4):
+    for c in range(NB):
         o = c * S
+        if not on[o + 20]:
+            continue
         print("ecda class %d coef/grad cycles: %s" % (c, "  ".join(
             "%s %d" % (n, int(np.median(raw[:, o + b] - raw[:, o + a]))) for a, b, n in cyc2 if on[o + a] and on[o + b])))
     names = ["start", "dacp", "staged", "b1", "gram+cent", "b2", "b3", "b4", "end", "rows-landed", "", "", "cand-stored"]
-    for c in range(4):
+    for c in range(NB):
         o = c * S
+        if not on[o]:
+            continue
         print("ecda class %d (cand %d, clean %d): %s" % (c, raw[-1, o + 10], raw[-1, o + 11], "  ".join(
             "%s %.2f" % (names[k], rel[o + k]) for k in (0, 1, 9, 12, 2, 3, 4, 5, 6, 7, 8) if on[o + k])))
 
