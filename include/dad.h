@@ -79,9 +79,6 @@ extern "C" {
 #define DAD_RANGE_NONFINITE 1u
 #define DAD_RANGE_POOL_TIMEOUT 2u
 #define DAD_T_TAU_HAT 40      /* [4] batch quantile thresholds */
-#define DAD_T_ECDA_TERM_HI 44 /* [4] scratch: the second class block's share of a 33..64-candidate class's term
-                                 (dad_tail_ecda_w); the weight gradient's loss total folds it into
-                                 DAD_T_ECDA_TERM and zeroes it */
 /* after the header (noisy batch, Bn rows): score[Bn], pred[Bn] (as float), mask[Bn], q[Bn][4] */
 #define DAD_TAIL_FLOATS(Bn) (DAD_TAIL_HDR + (Bn) * (3 + DAD_NUM_CLASSES))
 

@@ -495,7 +495,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
       // the next step's row preparation on the CUs the tail and class blocks leave idle
       DadPrepArgs pp;
       memset(&pp, 0, sizeof(pp));
-      int nblk = 1 + 2 * DAD_C + (pool_in_tail ? (G.Bc + 2 * Bn + DAD_TAIL_THREADS / 64 - 1) / (DAD_TAIL_THREADS / 64) : 0);
+      int nblk = 1 + DAD_C + (pool_in_tail ? (G.Bc + 2 * Bn + DAD_TAIL_THREADS / 64 - 1) / (DAD_TAIL_THREADS / 64) : 0);
       if (can_prepare_ahead(cfg, ncfg, nbt)) {
         int cus = 0;
         const int rc = device_cus(&cus);
@@ -514,7 +514,7 @@ static int step_compute_phases(const dad_config* cfg, const dad_batch* bt, const
         if (!noisy_here && !pp.clean) memset(&pp, 0, sizeof(pp));   // nothing left for the tail launch
         // spare blocks for whatever the tail launch prepares (noisy rows, and clean ones when the weight
         // gradient cannot take them)
-        if (pp.x16) nblk = std::max(nblk, std::max(cus, 2 * (1 + 2 * DAD_C)));
+        if (pp.x16) nblk = std::max(nblk, std::max(cus, 2 * (1 + DAD_C)));
         if (pp.x16 && !noisy_here) pp.warmup = 1;   // (dad_prep_rows: clean rows only)
       }
       hipLaunchKernelGGL(dad_tail_ecda_w, dim3(nblk), dim3(DAD_TAIL_THREADS), 0, stream, ta, ca, pp, pa);

@@ -160,7 +160,7 @@ struct DadReduceArgs {
   const uint8_t* keep1; const uint8_t* keep2;
   uint32_t key_drop1, key_drop2;
   float p_drop, drop_scale;
-  float* tailf;           // read: the loss terms; written: the folded ECDA class terms (DAD_T_ECDA_TERM_HI)
+  const float* tailf;
   float* grad; float* normpart;
   const uint32_t* pool_abort;   // fused pooling: this step's abort word (DAD_POOL_ABORT), else NULL
 };

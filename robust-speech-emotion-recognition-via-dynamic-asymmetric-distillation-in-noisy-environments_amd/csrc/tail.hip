@@ -20,37 +20,32 @@
 #include "dad_prep.h"
 #include "dad_probe.h"
 
-// class blocks of dad_tail_ecda_w: two per class (rows 0..31 and 32..63 of a class of 33..64
-// candidates; the second one leaves at once for smaller or wide classes)
-#define TW_CB (2 * DAD_C)
-// ECDA per-class-block phase wall clocks (100 MHz) of the stamps build (dad_probe.h): 32 slots per
-// class block (dad_tail_ecda_w: TW_CB of them; dad_tail_ecda / dad_ecda: DAD_C), then the tail
-// block's phases
+// ECDA per-class phase wall clocks (100 MHz) of the stamps build (dad_probe.h): 16 slots per
+// class, then the tail block's phases
 #define ECDA_SLOTS 32
-DAD_PROBE_BUFFER(ecda_stamps, TW_CB * ECDA_SLOTS + 16)
-#define ECDA_SLOT0 ((gridDim.x > DAD_C ? blockIdx.x - 1 : blockIdx.x) * ECDA_SLOTS)
+DAD_PROBE_BUFFER(ecda_stamps, DAD_C * ECDA_SLOTS + 16)
 #define ECDA_STAMP(k) \
-  if (threadIdx.x == 0) DAD_PROBE_SET(ecda_stamps, ECDA_SLOT0 + (k), DAD_PROBE_WALL())
+  if (threadIdx.x == 0) DAD_PROBE_SET(ecda_stamps, (gridDim.x > DAD_C ? blockIdx.x - 1 : blockIdx.x) * ECDA_SLOTS + (k), DAD_PROBE_WALL())
 // shader-clock stamp of wave 0 (cycle-level sub-phases of the stamps build), pinned in place
 #define ECDA_CYC(k)                                                                          \
   do {                                                                                       \
     __builtin_amdgcn_sched_barrier(0);                                                       \
     if (threadIdx.x == 0)                                                                    \
-      DAD_PROBE_SET(ecda_stamps, ECDA_SLOT0 + (k), DAD_PROBE_CLK());                  \
+      DAD_PROBE_SET(ecda_stamps, (gridDim.x > DAD_C ? blockIdx.x - 1 : blockIdx.x) * ECDA_SLOTS + (k), DAD_PROBE_CLK()); \
     __builtin_amdgcn_sched_barrier(0);                                                       \
   } while (0)
-#define ECDA_STAMP_SIZES(n, ns) \
-  do { DAD_PROBE_SET(ecda_stamps, ECDA_SLOT0 + 10, (n)); DAD_PROBE_SET(ecda_stamps, ECDA_SLOT0 + 11, (ns)); } while (0)
+#define ECDA_STAMP_SIZES(c, n, ns) \
+  do { DAD_PROBE_SET(ecda_stamps, (c) * ECDA_SLOTS + 10, (n)); DAD_PROBE_SET(ecda_stamps, (c) * ECDA_SLOTS + 11, (ns)); } while (0)
 #define TAIL_STAMP(k) \
-  if (threadIdx.x == 0) DAD_PROBE_SET(ecda_stamps, TW_CB * ECDA_SLOTS + (k), DAD_PROBE_WALL())
+  if (threadIdx.x == 0) DAD_PROBE_SET(ecda_stamps, DAD_C * ECDA_SLOTS + (k), DAD_PROBE_WALL())
 // shader-clock cycles at the tail block's start / end (slots 12 / 13): with the wall-clock
 // stamps 0 / 1 they give the clock the block ran at
 #define TAIL_CYCLES(k) \
-  if (threadIdx.x == 0) DAD_PROBE_SET(ecda_stamps, TW_CB * ECDA_SLOTS + (k), DAD_PROBE_CLK())
+  if (threadIdx.x == 0) DAD_PROBE_SET(ecda_stamps, DAD_C * ECDA_SLOTS + (k), DAD_PROBE_CLK())
 
 // stamp from wave 1's first lane (the tail block's DACP / KL wave)
 #define TAIL_STAMP_W1(k) \
-  if (threadIdx.x == 64 && blockIdx.x == 0) DAD_PROBE_SET(ecda_stamps, TW_CB * ECDA_SLOTS + (k), DAD_PROBE_WALL())
+  if (threadIdx.x == 64 && blockIdx.x == 0) DAD_PROBE_SET(ecda_stamps, DAD_C * ECDA_SLOTS + (k), DAD_PROBE_WALL())
 
 #define TAIL_THREADS DAD_TAIL_THREADS
 
@@ -203,9 +198,7 @@ __device__ __forceinline__ void pool_item(const DadPoolArgs& a, const int blk, c
       pool_st1<SC1>(a.eflag + urow, 0u);
     }
   }
-  constexpr int kHi = DAD_T_ECDA_TERM_HI - DAD_T_ECDA_TERM;
-  if (blk == 0 && (lane < 2 * DAD_C || (lane >= kHi && lane < kHi + DAD_C)))
-    pool_st1<SC1>(a.tail_terms + lane, 0.0f);   // per-class ECDA terms, gates and second-block shares
+  if (blk == 0 && lane < 2 * DAD_C) pool_st1<SC1>(a.tail_terms + lane, 0.0f);   // per-class ECDA terms and gates
 }
 
 __global__ __launch_bounds__(DAD_POOL_THREADS) void dad_pool(DadPoolArgs a) {
@@ -1306,7 +1299,7 @@ __device__ __forceinline__ void ecda_block(const DadEcdaArgs& a, const int c, Ec
   const float comp = ecda_block_sum_f(S, cpart) / (float)nt;
   if (tid == 0) {
     a.tail_terms[c] = att_c * (mmd + cfg.ecda_gamma * comp + cfg.ecda_delta * rep);
-    ECDA_STAMP_SIZES(n, ns);
+    ECDA_STAMP_SIZES(c, n, ns);
     a.tail_terms[DAD_T_ECDA_GATE - DAD_T_ECDA_TERM + c] = 1.0f;
   }
 }
@@ -1704,20 +1697,18 @@ static_assert(ECDA_NG * 32 * EW_TP <= sizeof(EcdaW::b) / sizeof(float), "ew_memb
 // therefore writes: ONE helper for both, so the pass never leaves a read column stale
 __device__ __forceinline__ int ew_nk64(int ncand_all) { return max((ncand_all + 7) >> 3, 5); }
 
-// Row tiles [ti0, ti0 + NT) of the NP padded candidates; db holds the coefficient rows from row
-// tile ti0 on (the two-block split of a 33..64-candidate class: one row tile per block).
-template <int NP, int NK, int NT, class RG>
-__device__ __forceinline__ void ew_member_grads(EcdaW& S, const float* db, int dp, int ti0, int c, int ncs,
-                                                int ncand_all, float mmd_scale, float comp_scale, float* ge_c,
-                                                float* ge_s, float* sink, const RG& repg_at) {
+template <int NP, int NK, class RG>
+__device__ __forceinline__ void ew_member_grads(EcdaW& S, const float* db, int dp, int c, int ncs, int ncand_all,
+                                                float mmd_scale, float comp_scale, float* ge_c, float* ge_s,
+                                                float* sink, const RG& repg_at) {
   static_assert(NK >= 1 && NK <= NP / 8, "ew_member_grads: NK 8-candidate blocks of NP");
   const int tid = threadIdx.x, lane = tid & 63;
   const int g = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int kh = lane >> 5, l32 = lane & 31;
-  for (int item = g; item < NT * (DAD_H / 32); item += ECDA_NG) {
-    const int ti = ti0 + (item >> 3), tc = item & 7;
+  for (int item = g; item < (NP / 32) * (DAD_H / 32); item += ECDA_NG) {
+    const int ti = item >> 3, tc = item & 7;
     const int d = 32 * tc + l32;
-    const float* ra = &db[(32 * (ti - ti0) + l32) * dp + 4 * kh];
+    const float* ra = &db[(32 * ti + l32) * dp + 4 * kh];
     f32x4 av[NK];
     float bv[NK][4];
 #pragma unroll
@@ -1769,14 +1760,8 @@ __device__ __forceinline__ void ew_member_grads(EcdaW& S, const float* db, int d
 
 // The class work after the candidates are known.  WIDE = more than 64 candidates: rows are read
 // from the embedding buffer (global, through the candidate -> row table) instead of LDS.
-// 33..64 candidates (the "split" tiling): two blocks per class, block hb taking candidate rows
-// 32 hb .. 32 hb + 31 -- its Gram tiles (hb, 0) and (hb, 1), the coefficients and row sums of its
-// rows, the member gradients of its rows (K over all candidates), and its rows' share of the kernel
-// sums (the loss term: hb 0 in DAD_T_ECDA_TERM + c with the compactness and repulsion, hb 1 in
-// DAD_T_ECDA_TERM_HI + c, added by the weight gradient's loss-total block).  One block held all
-// of it before: 25 us of chain for a 33-candidate class against 18 for 32 (stamps, round 6).
 template <bool WIDE>
-__device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, const int hb, EcdaW& S, const WaveMask& M,
+__device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, EcdaW& S, const WaveMask& M,
                                              const f32x4 (&ps)[ECDA_PRE_U], const int prd,
                                              const int ncls, const int nvalid, const int npairs, const bool gc,
                                              const bool rep_on, const float rep_coef, const float att_c, const int ncs,
@@ -1789,10 +1774,9 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
   const float* emb_c = a.emb;
   const float* emb_s = a.emb + (size_t)(B + Bn) * DAD_H;
   const int npad = ncand_all <= 32 ? 32 : (ncand_all <= 64 ? 64 : 128);
-  const bool split = !WIDE && npad == 64;         // this block: row tile hb of the two
   const int nt = npad / 32;                       // 32-row tiles
-  const int npt = nt * (nt + 1) / 2;              // upper-triangle tile pairs: 1 or 10 (split: 2 of row tile hb)
-  const int ks = npt == 1 ? 8 : (split ? 4 : 1);  // K splits per pair
+  const int npt = nt * (nt + 1) / 2;              // upper-triangle tile pairs: 1, 3 or 10
+  const int ks = npt == 1 ? 8 : (npt == 3 ? 2 : 1);   // K splits per pair
   float* db = WIDE ? S.a.dbw : S.c.dbn;
   const int dp = WIDE ? EW_CPW : EW_CP;
   const int cnc = S.cnt[c];
@@ -1826,24 +1810,29 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
     }
     *reinterpret_cast<f32x4*>(&S.msp[g][4 * lane]) = ms;
     if (lane == 0) S.nsp[g] = ns;
-    // Gram partials: tile pair (ti, tj) over a K slice, fp32 matrix cores, one item per slot.
-    // 32 candidates: the one tile in 8 slices; split: tiles (hb, 0) and (hb, 1) in 4 slices each
-    // (the tile (1, 0) of block 1 is the transpose of block 0's (0, 1) bit for bit: the same
-    // products in the same order); wide: the 10 upper-triangle tiles whole
-    for (int item = g; item < (split ? 8 : npt * ks); item += ECDA_NG) {
-      int ti, tj, sl, nsl;
-      if (split) {
-        ti = hb;
-        tj = item >> 2;
-        sl = item & 3;
-        nsl = 4;
+    // Gram partials: tile pair (ti, tj) over a K slice, fp32 matrix cores.  The 64-row tiling
+    // (3 pairs) cuts pairs (0,0) and (0,1) into 4 slices and (1,1) into 2: 10 items in the 10
+    // partial slots, dealt so that the waves w and w + 4 (one SIMD's pair) hold 6 slices' MFMAs
+    // each (3 x 64 or 128 + 64 of K) instead of two 128-K items on two SIMDs and one on the others
+    for (int item = g; item < (npt == 3 ? 10 : npt * ks); item += ECDA_NG) {
+      int pr, sl, nsl;
+      if (npt == 3) {
+        // item -> pair (2 bits) | slice (2 bits): 0:(0,2) 1:(1,1) 2:(2,0) 3:(2,1) 4:(0,3) 5:(1,2)
+        // 6:(0,0) 7:(0,1) 8:(1,0) 9:(1,3)
+        constexpr uint64_t kDeal = 0x2ull | (0x5ull << 4) | (0x8ull << 8) | (0x9ull << 12) | (0x3ull << 16) |
+                                   (0x6ull << 20) | (0x0ull << 24) | (0x1ull << 28) | (0x4ull << 32) | (0x7ull << 36);
+        const int v = (int)((kDeal >> (4 * item)) & 15u);
+        pr = v >> 2;
+        sl = v & 3;
+        nsl = pr < 2 ? 4 : 2;
       } else {
-        const int pr = item / ks;
+        pr = item / ks;
         sl = item - pr * ks;
         nsl = ks;
-        ew_pair_inv(pr, nt, ti, tj);
       }
-      const int slot = item;
+      const int slot = npt == 3 ? (pr < 2 ? 4 * pr : 8) + sl : item;
+      int ti, tj;
+      ew_pair_inv(pr, nt, ti, tj);
       const int kw = DAD_H / nsl, k0 = sl * kw;
       const int ia = 32 * ti + l32, ib = 32 * tj + l32;
       // MFMA step e of a k-block of 8 takes k-index k + 4 kh + e on both operands (any k order
@@ -1876,13 +1865,10 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
   __syncthreads();   // ---------------------------------------------------------------- 2
   ECDA_STAMP(5);
   ECDA_CYC(6);
-  // element ownership of the coefficient matrix: row ei, columns ej0 .. ej0 + ept - 1 (32
-  // candidates, wide); split: this block's 32 rows, row ei = 32 hb + tid / 16, columns
-  // tid % 16 + 16 e
-  const int ept = split ? 4 : npad * npad / ECDA_THREADS;     // 2, 4 or 32
-  const int tpr = split ? 16 : npad / ept;                    // threads per row: 16 or 4
-  const int ei = (split ? 32 * hb : 0) + tid / tpr, ej0 = (tid % tpr) * ept;
-  const int eil = split ? ei - 32 * hb : ei;                  // its row of db
+  // element ownership of the [npad x npad] matrices: row ei, columns ej0 .. ej0 + ept - 1
+  const int ept = npad * npad / ECDA_THREADS;     // 2, 8 or 32
+  const int tpr = npad / ept;                     // threads per row: 16, 8 or 4
+  const int ei = tid / tpr, ej0 = (tid - ei * tpr) * ept;
   // centroid distances (I/utils.py:582-595): 32 threads per (p, q) pair, pair-symmetric order
   {
     const int pair = tid / 32, t32 = tid & 31;
@@ -1953,18 +1939,12 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
     const float css = 2.0f / Wss, ctt = 2.0f / Wtt, cst = -2.0f / Wst;
     auto coef = [&](const int j) {
       const int i = ei;
-      // G_ij read at (min, max) in the upper-triangle tiles (split: at (i, j) in this block's
-      // tiles, the transpose of the other block's bit for bit): D is symmetric bit for bit
+      // G_ij read at (min, max) in the upper-triangle tiles: D is symmetric bit for bit
       const int lo = i < j ? i : j, hi = i < j ? j : i;
+      const int pr = ew_pair(lo >> 5, hi >> 5, nt);
       float gsum = 0.0f;
-      if (split) {
-        const float* gq = &S.b.gp[4 * (j >> 5)][(i & 31) * EW_GP + (j & 31)];
-#pragma unroll
-        for (int s2 = 0; s2 < 4; ++s2) gsum += gq[s2 * (32 * EW_GP)];
-      } else {
-        const int pr = ew_pair(lo >> 5, hi >> 5, nt);
-        for (int s2 = 0; s2 < ks; ++s2) gsum += S.b.gp[pr * ks + s2][(lo & 31) * EW_GP + (hi & 31)];
-      }
+      const int sb = npt == 3 ? (pr < 2 ? 4 * pr : 8) : pr * ks, sn = npt == 3 ? (pr < 2 ? 4 : 2) : ks;
+      for (int s2 = 0; s2 < sn; ++s2) gsum += S.b.gp[sb + s2][(lo & 31) * EW_GP + (hi & 31)];
       const bool ok = (i < ncand_all) & (j < ncand_all) & (i != j);
       const float d = ok ? fmaxf((S.nz[lo] + S.nz[hi]) - 2.0f * gsum, 0.0f) : 0.0f;
       const int jc = j < ncand_all ? j : 0;
@@ -1987,28 +1967,26 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
       const float vss = css * dK, vtt = (ctt * ww) * dK, vst = (cst * wj) * dK, vts = (cst * wi) * dK;
       float v = ss ? vss : (tt ? vtt : (st ? vst : (ts ? vts : 0.0f)));
       v = i == j ? 0.0f : v;
-      db[eil * dp + j] = v;
+      db[i * dp + j] = v;
       rsp += v;
     };
-    if (split) {
-      // thread column jt + 16 e, only the columns the member-gradient chain reads (8 ceil(ncand /
-      // 8), ew_member_grads' NK blocks), so a 40-candidate class runs 3 of the 4 elements per
-      // thread; rows past the candidates get their zeros without the kernel math
+    if (!WIDE && npad == 64) {
+      // the 64-row tiling: thread column jt + tpr e, only the columns the member-gradient chain
+      // reads (8 ceil(ncand / 8), ew_member_grads' NK blocks), so a 40-candidate class runs 5 of
+      // the 8 elements per thread; rows past the candidates get their zeros without the kernel math
       const int jt = ej0 / ept, kz = 8 * ew_nk64(ncand_all);   // = ew_member_grads' 8 NK columns
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int j = jt + 16 * e;
-        if (j < kz) {
-          if (ei < ncand_all) coef(j);
-          else db[eil * dp + j] = 0.0f;
-        }
+      for (int e = 0; e < ept; ++e) {
+        const int j = jt + tpr * e;
+        if (j >= kz) break;
+        if (ei < ncand_all) coef(j);
+        else db[ei * dp + j] = 0.0f;
       }
     } else {
       for (int e = 0; e < ept; ++e) coef(ej0 + e);
     }
     ECDA_CYC(22);
     // row sums of the coefficients: the tpr threads of a row are adjacent lanes
-    rsp = tpr == 16 ? dpp_seg_sum<16>(rsp) : dpp_seg_sum<4>(rsp);
+    rsp = tpr == 16 ? dpp_seg_sum<16>(rsp) : (tpr == 8 ? dpp_seg_sum<8>(rsp) : dpp_seg_sum<4>(rsp));
     if ((tid & (tpr - 1)) == tpr - 1) S.rs[ei] = rsp;
 #pragma unroll
     for (int k = 0; k < 3; ++k) t3[k] = dad_wave_sum_d(t3[k]);
@@ -2065,18 +2043,16 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
       t3[1] += S.t3p[gg][1];
       t3[2] += S.t3p[gg][2];
     }
-    // t_ss, t_tt, t_st as the reference forms them in float32 (I/utils.py:558-563); split: this
-    // block's rows' share (the mmd is linear in the sums)
+    // t_ss, t_tt, t_st as the reference forms them in float32 (I/utils.py:558-563)
     const float mmd = (float)t3[0] / Wss + (float)t3[1] / Wtt - 2.0f * ((float)t3[2] / Wst);
     float csum = 0.0f;
 #pragma unroll
     for (int gg = 0; gg < ECDA_NG; ++gg) csum += S.cmp[gg];
     const float comp = csum / (float)cnc;
-    if (tid == 0 && hb == 0) {
+    if (tid == 0) {
       a.tail_terms[c] = att_c * (mmd + cfg.ecda_gamma * comp + cfg.ecda_delta * rep);
       a.tail_terms[DAD_T_ECDA_GATE - DAD_T_ECDA_TERM + c] = 1.0f;
     }
-    if (tid == 0 && hb != 0) a.tail_terms[DAD_T_ECDA_TERM_HI - DAD_T_ECDA_TERM + c] = att_c * mmd;
     ECDA_CYC(24);
     const float mmd_scale = wscale * att_c;
     const float comp_scale = wscale * att_c * cfg.ecda_gamma * (2.0f / (float)cnc);
@@ -2084,13 +2060,13 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
     // matrix cores, 32 candidates x 32 hidden units per item
     if constexpr (!WIDE) {
       if (npad == 32) {
-        ew_member_grads<32, 4, 1>(S, db, dp, 0, c, ncs, ncand_all, mmd_scale, comp_scale, ge_c, ge_s, a.sink, repg_at);
-      } else {   // split: this block's row tile
+        ew_member_grads<32, 4>(S, db, dp, c, ncs, ncand_all, mmd_scale, comp_scale, ge_c, ge_s, a.sink, repg_at);
+      } else {
         const int nk = ew_nk64(ncand_all);   // 5 .. 8 (33 .. 64 candidates): the columns the pass wrote
-        if (nk <= 5) ew_member_grads<64, 5, 1>(S, db, dp, hb, c, ncs, ncand_all, mmd_scale, comp_scale, ge_c, ge_s, a.sink, repg_at);
-        else if (nk == 6) ew_member_grads<64, 6, 1>(S, db, dp, hb, c, ncs, ncand_all, mmd_scale, comp_scale, ge_c, ge_s, a.sink, repg_at);
-        else if (nk == 7) ew_member_grads<64, 7, 1>(S, db, dp, hb, c, ncs, ncand_all, mmd_scale, comp_scale, ge_c, ge_s, a.sink, repg_at);
-        else ew_member_grads<64, 8, 1>(S, db, dp, hb, c, ncs, ncand_all, mmd_scale, comp_scale, ge_c, ge_s, a.sink, repg_at);
+        if (nk <= 5) ew_member_grads<64, 5>(S, db, dp, c, ncs, ncand_all, mmd_scale, comp_scale, ge_c, ge_s, a.sink, repg_at);
+        else if (nk == 6) ew_member_grads<64, 6>(S, db, dp, c, ncs, ncand_all, mmd_scale, comp_scale, ge_c, ge_s, a.sink, repg_at);
+        else if (nk == 7) ew_member_grads<64, 7>(S, db, dp, c, ncs, ncand_all, mmd_scale, comp_scale, ge_c, ge_s, a.sink, repg_at);
+        else ew_member_grads<64, 8>(S, db, dp, c, ncs, ncand_all, mmd_scale, comp_scale, ge_c, ge_s, a.sink, repg_at);
       }
     }
     for (int item = g; WIDE && item < nt * (DAD_H / 32); item += ECDA_NG) {
@@ -2135,13 +2111,11 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
   for (int i = tid; i < ncand_all; i += ECDA_THREADS)
     if (S.mem[i]) a.eflag[i < ncs ? S.rowz[i] : B + S.rowz[i]] = 1u;
   ECDA_STAMP(8);
-  if (tid == 0) ECDA_STAMP_SIZES(ncand_all, ncs);
+  if (tid == 0) ECDA_STAMP_SIZES(c, ncand_all, ncs);
 }
 
-// One ECDA class (I/utils.py:565-632, class-aware) for B, Bn <= 64; hb = 1: the class's second
-// block, which works only for a class of 33..64 candidates (ecda_class_w's split tiling).
-__device__ __forceinline__ void ecda_block_w(const DadEcdaArgs& a, const DadTailArgs& ta, const int c, const int hb,
-                                             EcdaW& S) {
+// One ECDA class (I/utils.py:565-632, class-aware) for B, Bn <= 64.
+__device__ __forceinline__ void ecda_block_w(const DadEcdaArgs& a, const DadTailArgs& ta, const int c, EcdaW& S) {
   const dad_config& cfg = a.cfg;
   const int B = cfg.B, Bn = cfg.Bn;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -2241,7 +2215,6 @@ __device__ __forceinline__ void ecda_block_w(const DadEcdaArgs& a, const DadTail
   const int ncs = gc ? ccc : 0;
   const int ncand_all = ncs + (int)__popcll(bn);
   const bool wide = ncand_all > TW_MAXB;
-  if (hb != 0 && (!gc || ncand_all <= 32 || wide)) return;   // (uniform: before any barrier)
   const uint64_t below = (1ull << lane) - 1ull;
   const int posc = (int)__popcll(bc & below);
   const int posn = ncs + (int)__popcll(bn & below);
@@ -2307,14 +2280,13 @@ __device__ __forceinline__ void ecda_block_w(const DadEcdaArgs& a, const DadTail
   __syncthreads();   // ---------------------------------------------------------------- 1
   ECDA_STAMP(3);
   if (wide)
-    ecda_class_w<true>(a, c, hb, S, M, ps, prd, ncls, nvalid, npairs, gc, rep_on, rep_coef, att_c, ncs, ncand_all, wsum_t);
+    ecda_class_w<true>(a, c, S, M, ps, prd, ncls, nvalid, npairs, gc, rep_on, rep_coef, att_c, ncs, ncand_all, wsum_t);
   else
-    ecda_class_w<false>(a, c, hb, S, M, ps, prd, ncls, nvalid, npairs, gc, rep_on, rep_coef, att_c, ncs, ncand_all, wsum_t);
+    ecda_class_w<false>(a, c, S, M, ps, prd, ncls, nvalid, npairs, gc, rep_on, rep_coef, att_c, ncs, ncand_all, wsum_t);
 }
 
-// block 0: the wave-centric tail; blocks 1..2C: ECDA class (blockIdx.x - 1) % C, part (blockIdx.x -
-// 1) / C (ecda_block_w's hb).  Host contract: B <= 64, Bn <= 64, class-aware MMD (dad_tail_ecda
-// otherwise).  Blocks > 2C pool the step's
+// block 0: the wave-centric tail; blocks 1..C: ECDA class blockIdx.x - 1.  Host contract:
+// B <= 64, Bn <= 64, class-aware MMD (dad_tail_ecda otherwise).  Blocks > C pool the step's
 // embeddings and logits first (pl.ready set; the tail and class blocks wait for them: pool_wait),
 // which saves the separate dad_pool launch and its boundary.  Then (when pa.x16 is set):
 // the NEXT step's row preparation (dad_prep.h) on the CUs the tail and the class blocks leave
@@ -2331,10 +2303,10 @@ __global__ __launch_bounds__(TAIL_THREADS) void dad_tail_ecda_w(DadTailArgs ta, 
   // fused pooling (pl.ready): the Bc + 2 Bn pool items (dad_pool's workgroups) on the spare
   // blocks' waves, item i on block i mod nx, wave i / nx (one item per CU first)
   const int nitems = pl.ready ? pl.g.Bc + 2 * pl.g.Bn : 0;
-  if ((int)blockIdx.x > TW_CB) {
+  if ((int)blockIdx.x > DAD_C) {
     constexpr int kWaves = TAIL_THREADS / 64;
     const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-    const int nx = (int)gridDim.x - 1 - TW_CB, xb = (int)blockIdx.x - 1 - TW_CB;
+    const int nx = (int)gridDim.x - 1 - DAD_C, xb = (int)blockIdx.x - 1 - DAD_C;
     for (int i = xb + nx * w; i < nitems; i += nx * kWaves) {
       pool_item<true>(pl, i, (int)threadIdx.x & 63);
       pool_publish(pl.ready, (int)threadIdx.x & 63);
@@ -2342,7 +2314,7 @@ __global__ __launch_bounds__(TAIL_THREADS) void dad_tail_ecda_w(DadTailArgs ta, 
     if (!pa.x16) return;
     dad_prep_dispatch<2>(pa, xb * kWaves + w, nx * kWaves, (int)threadIdx.x & 63);
 #ifdef DAD_PROBE_STAMPS
-    if (threadIdx.x == 0) atomicMax(&ecda_stamps[TW_CB * ECDA_SLOTS + 15], (unsigned long long)DAD_PROBE_WALL());
+    if (threadIdx.x == 0) atomicMax(&ecda_stamps[DAD_C * ECDA_SLOTS + 15], (unsigned long long)DAD_PROBE_WALL());
 #endif
     return;
   }
@@ -2350,7 +2322,7 @@ __global__ __launch_bounds__(TAIL_THREADS) void dad_tail_ecda_w(DadTailArgs ta, 
   if (blockIdx.x == 0) TAIL_STAMP(14);   // launch entry (slot 15: the last preparation block's end)
   if (nitems) pool_wait(pl.ready, (uint32_t)nitems, pl.range_flag);
   if (blockIdx.x == 0) tail_block_w(ta, u.t);
-  else ecda_block_w(ca, ta, ((int)blockIdx.x - 1) % DAD_C, ((int)blockIdx.x - 1) / DAD_C, u.e);
+  else ecda_block_w(ca, ta, (int)blockIdx.x - 1, u.e);
 }
 
 // ------------------------------------------------------------- helper-type drop-ins

@@ -1014,18 +1014,9 @@ __device__ double extra_block_t(const DadReduceArgs& a, int e, int tid, float (*
     sq += (double)gb * gb;
   }
   if (e == 0 && a.tailf && tid == 128) {
-    float* tf = a.tailf;
-    // a class split over two blocks of the tail launch (33..64 candidates) left its second
-    // block's share in DAD_T_ECDA_TERM_HI: folded into the class's term here (and zeroed, so a
-    // second pass over the same step adds nothing); + 0 for every other class
-    float t[DAD_C];
-#pragma unroll
-    for (int k = 0; k < DAD_C; ++k) {
-      t[k] = tf[DAD_T_ECDA_TERM + k] + tf[DAD_T_ECDA_TERM_HI + k];
-      tf[DAD_T_ECDA_TERM + k] = t[k];
-      tf[DAD_T_ECDA_TERM_HI + k] = 0.0f;
-    }
-    const float ecda_l = ((t[0] + t[1]) + t[2]) + t[3];
+    const float* tf = a.tailf;
+    const float ecda_l = ((tf[DAD_T_ECDA_TERM] + tf[DAD_T_ECDA_TERM + 1]) + tf[DAD_T_ECDA_TERM + 2]) +
+                         tf[DAD_T_ECDA_TERM + 3];
     const float ce = tf[DAD_T_CE], kl = tf[DAD_T_KL];
     float* ex = a.grad + DAD_NPARAM;
     // a pooling timeout in the tail launch (DAD_POOL_ABORT): NaN total, so dad_optim (on every DP

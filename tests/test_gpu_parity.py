@@ -302,17 +302,23 @@ def test_large_member_sets_match_oracle(class_aware, B, prec):
 
 
 @pytest.mark.parametrize("prec", ["fp32", "fp16"])
-@pytest.mark.parametrize("counts", [(40, 8, 8, 8), (30, 30, 2, 2)], ids=["one_split", "two_split"])
-def test_split_class_blocks_match_oracle(counts, prec):
+@pytest.mark.parametrize("counts,tau", [((40, 8, 8, 8), None), ((30, 30, 2, 2), None), ((20, 16, 14, 14), (0.0, 1.0, 1.0, 1.0))],
+                         ids=["one_large", "two_large", "idle_others"])
+def test_large_class_tiling_matches_oracle(counts, tau, prec):
     """Classes of 33..64 ECDA members (clean rows of the label + masked noisy rows of the
-    pseudo-label): dad_tail_ecda_w splits each over two class blocks (rows 0..31 / 32..63, the
-    second block's share of the loss term folded in by the loss total).  Losses at 1e-4, mask
-    bit-exact, gradients as the other parity tests (fp32: gh.close_grad; fp16: the throughput
-    bounds); the test checks that the geometry does produce such a class."""
+    pseudo-label): dad_tail_ecda_w's 64-row tiling of a class block (3 Gram tile pairs, the
+    coefficient columns of ceil(n / 8) 8-candidate blocks).  one_split / two_split: one or two
+    such classes next to classes with work; idle_others: thresholds mask in only class 0's noisy
+    rows (36 members), so classes 1..3 have neither ECDA nor repulsion work (the geometry of a
+    collapsed teacher).  Losses at 1e-4, mask bit-exact, gradients as the other parity tests
+    (fp32: gh.close_grad; fp16: the throughput bounds); the test checks that the geometry does
+    produce such a class."""
     cfg = dad_oracle.make_cfg("iemocap")
     inp = _problem(64, 6, seed=21, snr=20.0)
     inp["yc"] = np.repeat(np.arange(4), counts).astype(inp["yc"].dtype)
     st = synth.make_state(21, 1, tau_range=(0.0, 0.01))     # low thresholds: most noisy rows masked in
+    if tau is not None:
+        st["tau"] = np.asarray(tau, np.float32)
     step = gh.make_step(cfg, precision=prec)
     orc = dad_oracle.DADOracle(*synth.init_weights(21)[:4], cfg)
     gh.load_state(step, st)
@@ -322,6 +328,8 @@ def test_split_class_blocks_match_oracle(counts, prec):
     m = np.asarray(r["mask"]) > 0
     members = [int(np.sum(inp["yc"] == c)) + int(np.sum((np.asarray(r["pred"]) == c) & m)) for c in range(4)]
     assert any(32 < n <= 64 for n in members), members
+    if tau is not None:   # one class with work, the others idle
+        assert [int(np.sum((np.asarray(r["pred"]) == c) & m)) for c in range(1, 4)] == [0, 0, 0], members
     for k in ("total_loss", "supervised_ce_loss", "consistency_loss", "ecda_loss"):
         _cmp_loss(o[k], r[k], (counts, prec, k))
     np.testing.assert_array_equal(o["mask"], r["mask"])

@@ -32,17 +32,17 @@ def main():
             nxt = data[(i + 1) % 2] if os.environ.get("STAMP_AHEAD") == "1" else None
             step.step(data[i % 2][0], data[i % 2][1], 60, next_batch=nxt)
         torch.cuda.synchronize()
-        ebuf = (ctypes.c_ulonglong * (8 * S + 16))()
+        ebuf = (ctypes.c_ulonglong * (4 * S + 16))()
         assert L.dad_probe_read_ecda_stamps(ebuf, len(ebuf)) == 0
         raw.append(np.frombuffer(ebuf, dtype=np.uint64).astype(np.int64))
     raw = np.stack(raw[2:] if reps > 4 else raw)
-    t0 = raw[:, 8 * S:8 * S + 1]   # (tail.hip: TW_CB = 8 class-block slot groups, then the tail's)
+    t0 = raw[:, 4 * S:4 * S + 1]
     relm = np.median((raw - t0) / 100.0, axis=0)        # us after the tail block's start, median
     setm = np.all(raw > 0, axis=0)
     last = raw[-1]
     on = lambda k: bool(setm[k])
     rel = lambda k: relm[k]
-    T = 8 * S
+    T = 4 * S
     tn = ["end", "ce", "probs", "dacp", "kl", "outputs", "clsbwd"]
     print("median of %d steps" % raw.shape[0])
     if on(T + 14):

@@ -14,7 +14,7 @@ os.environ.setdefault("DAD_LIB_VARIANT", "stamps")
 import bench  # noqa: E402
 
 PKG = bench.PKG
-NB = 8   # class blocks of dad_tail_ecda_w (tail.hip TW_CB): block k = class k % 4, part k // 4
+NB = 4   # class blocks of dad_tail_ecda_w (tail.hip TW_CB)
 
 
 def main():
