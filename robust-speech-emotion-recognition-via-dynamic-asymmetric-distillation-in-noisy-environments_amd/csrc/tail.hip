@@ -1967,22 +1967,28 @@ __device__ __forceinline__ void ecda_class_w(const DadEcdaArgs& a, const int c, 
       const float vss = css * dK, vtt = (ctt * ww) * dK, vst = (cst * wj) * dK, vts = (cst * wi) * dK;
       float v = ss ? vss : (tt ? vtt : (st ? vst : (ts ? vts : 0.0f)));
       v = i == j ? 0.0f : v;
-      db[i * dp + j] = v;
       rsp += v;
+      return v;
     };
+    // 64-row tiling: the thread's 8 elements unrolled, their stores after the last one (a store
+    // to db inside the loop kept the next element's LDS reads behind it: pairs 9.7k -> 8.9k
+    // cycles for a 38-41 member class; the 32-row case, 2 elements, measured no better so)
     if (!WIDE && npad == 64) {
       // the 64-row tiling: thread column jt + tpr e, only the columns the member-gradient chain
       // reads (8 ceil(ncand / 8), ew_member_grads' NK blocks), so a 40-candidate class runs 5 of
       // the 8 elements per thread; rows past the candidates get their zeros without the kernel math
       const int jt = ej0 / ept, kz = 8 * ew_nk64(ncand_all);   // = ew_member_grads' 8 NK columns
-      for (int e = 0; e < ept; ++e) {
-        const int j = jt + tpr * e;
-        if (j >= kz) break;
-        if (ei < ncand_all) coef(j);
-        else db[ei * dp + j] = 0.0f;
+      float v8[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int j = jt + 8 * e;
+        v8[e] = (j < kz && ei < ncand_all) ? coef(j) : 0.0f;
       }
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (jt + 8 * e < kz) db[ei * dp + jt + 8 * e] = v8[e];
     } else {
-      for (int e = 0; e < ept; ++e) coef(ej0 + e);
+      for (int e = 0; e < ept; ++e) db[ei * dp + ej0 + e] = coef(ej0 + e);
     }
     ECDA_CYC(22);
     // row sums of the coefficients: the tpr threads of a row are adjacent lanes
