@@ -24,6 +24,8 @@
 // class, then the tail block's phases
 #define ECDA_SLOTS 32
 DAD_PROBE_BUFFER(ecda_stamps, DAD_C * ECDA_SLOTS + 16)
+// dad_tail_ecda_w's preparation waves (spare block xb < 256, wave w): [start, end] wall clocks
+DAD_PROBE_BUFFER(prep_stamps, 256 * 8 * 2)
 #define ECDA_STAMP(k) \
   if (threadIdx.x == 0) DAD_PROBE_SET(ecda_stamps, (gridDim.x > DAD_C ? blockIdx.x - 1 : blockIdx.x) * ECDA_SLOTS + (k), DAD_PROBE_WALL())
 // shader-clock stamp of wave 0 (cycle-level sub-phases of the stamps build), pinned in place
@@ -2318,9 +2320,13 @@ __global__ __launch_bounds__(TAIL_THREADS) void dad_tail_ecda_w(DadTailArgs ta, 
       pool_publish(pl.ready, (int)threadIdx.x & 63);
     }
     if (!pa.x16) return;
+#ifdef DAD_PROBE_STAMPS
+    if ((threadIdx.x & 63) == 0 && xb < 256) prep_stamps[2 * (xb * kWaves + w)] = DAD_PROBE_WALL();
+#endif
     dad_prep_dispatch<2>(pa, xb * kWaves + w, nx * kWaves, (int)threadIdx.x & 63);
 #ifdef DAD_PROBE_STAMPS
     if (threadIdx.x == 0) atomicMax(&ecda_stamps[DAD_C * ECDA_SLOTS + 15], (unsigned long long)DAD_PROBE_WALL());
+    if ((threadIdx.x & 63) == 0 && xb < 256) prep_stamps[2 * (xb * kWaves + w) + 1] = DAD_PROBE_WALL();
 #endif
     return;
   }

@@ -58,6 +58,7 @@ def main():
         ebuf = (ctypes.c_ulonglong * (NB * S + 16))()
         assert L.dad_probe_read_ecda_stamps(ebuf, len(ebuf)) == 0
         raw.append(np.frombuffer(ebuf, dtype=np.uint64).astype(np.int64))
+    report_prep(read_prep_stamps(), raw[-1][NB * S])
     report(np.stack(raw[2:] if reps > 4 else raw))
 
 
@@ -66,6 +67,38 @@ def read_stamps():
     ebuf = (ctypes.c_ulonglong * (NB * 32 + 16))()
     assert PKG.lib().dad_probe_read_ecda_stamps(ebuf, len(ebuf)) == 0
     return np.frombuffer(ebuf, dtype=np.uint64).astype(np.int64)
+
+
+def read_prep_stamps():
+    """Per preparation wave (spare block xb, wave w -> index 8 xb + w): [start, end] wall clocks."""
+    buf = (ctypes.c_ulonglong * (256 * 8 * 2))()
+    assert PKG.lib().dad_probe_read_prep_stamps(buf, len(buf)) == 0
+    return np.frombuffer(buf, dtype=np.uint64).astype(np.int64).reshape(256 * 8, 2)
+
+
+def report_prep(ps, t0, nitems=192):
+    """Preparation waves' start / end (us after the tail block's start), the waves that ran a
+    pooling item first (block i mod nx, wave 0 for the first nx items) against the others."""
+    ok = ps[:, 1] > 0
+    idx = np.arange(len(ps))
+    pool = ok & (idx % 8 == 0) & (idx // 8 < nitems)
+    rest = ok & ~pool
+    for name, m in (("pool waves", pool), ("other waves", rest)):
+        if m.any():
+            st, en = (ps[m, 0] - t0) / 100.0, (ps[m, 1] - t0) / 100.0
+            print("prep %-11s n %4d  start med %.2f max %.2f  end med %.2f p90 %.2f max %.2f" % (
+                name, m.sum(), np.median(st), st.max(), np.median(en), np.percentile(en, 90), en.max()))
+    en = (ps[:, 1] - t0) / 100.0
+    xcd = (idx // 8 + 1 + 4) % 8          # block id = xb + 1 + C, dispatched round-robin over the 8 XCDs
+    print("prep end by XCD (median / max): " + "  ".join(
+        "%d: %.1f/%.1f" % (x, np.median(en[ok & (xcd == x)]), en[ok & (xcd == x)].max()) for x in range(8)))
+    print("prep end by wave slot (median / max): " + "  ".join(
+        "%d: %.1f/%.1f" % (w, np.median(en[ok & (idx % 8 == w)]), en[ok & (idx % 8 == w)].max()) for w in range(8)))
+    dur = (ps[:, 1] - ps[:, 0]) / 100.0
+    print("prep duration (us): med %.2f p10 %.2f p90 %.2f max %.2f" % (
+        np.median(dur[ok]), np.percentile(dur[ok], 10), np.percentile(dur[ok], 90), dur[ok].max()))
+    late = ok & (en > np.percentile(en[ok], 95))
+    print("latest 5%% waves by block: %s" % sorted(set((idx[late] // 8).tolist()))[:40])
 
 
 def report(raw):
