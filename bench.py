@@ -440,7 +440,8 @@ def run_mixed(args, model, dev, rank, world, dist, comm):
 
 
 def event_every(steps):
-    return max(1, min(EVENT_EVERY, steps // 4))
+    # (a 20-step region records 2 steps, not 4: each recorded step puts its events on the stream)
+    return max(1, min(EVENT_EVERY, steps // 2))
 
 
 # The timed region records events around one kernel only (the roofline kernel, timed_kernels):
@@ -844,10 +845,13 @@ def main():
     ap.add_argument("--exchange-us", type=float, default=0.0,
                     help="N = 1 only: a spin of about this many microseconds after the backward, standing in for a DP "
                          "step's all-reduce window (measures the --prep-under-exchange layouts on one GPU)")
+    ap.add_argument("--settle-ms", type=float, default=50.0,
+                    help="untimed headline steps (about this many ms of GPU time) right before the warm-up")
     ap.add_argument("--launch", default="eager", choices=["graph", "eager"],
                     help="timed steps as eager launches (default) or hipGraph replays (one graph per resident batch; "
                          "measured no faster on this ROCm, DESIGN.md §5)")
     args = ap.parse_args()
+    settle_steps = 0
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
@@ -949,17 +953,34 @@ def main():
                 data_path = data_path_bench(step, B, T, args.epoch, dev, P)
             restore(model, step, snap0)
             del snap0
-        run(args.warmup)
-        torch.cuda.synchronize()
-        snap = snapshot(model, step)          # the state the first timed step starts from
-        # every EVENT_EVERY-th timed step records hip events at its kernel boundaries (created
-        # here, outside the timed region; the region only records them)
         launch = args.launch
         if launch == "graph" and isinstance(comm, PKG.ProcessGroupComm):
             launch = "eager (the gloo all-reduce runs on the host: not capturable)"
         graphs = None
         timer = None
         enc_events = []
+        if launch != "graph":
+            # every EVENT_EVERY-th timed step records hip events at its kernel boundaries.  The
+            # events are created here, BEFORE the warm-up (milliseconds of host time: created
+            # between the warm-up and the clock they had idled the GPU right before the timed
+            # region, and a short region then started on lowered clocks), and the timer is reset
+            # after the warm-up, so only timed steps are counted
+            timer = PKG._lib.KernelTimer(event_every(args.steps), args.steps // event_every(args.steps) + 1,
+                                         kernels=timed_kernels(args.precision, not args.no_ahead))
+        if args.settle_ms > 0:
+            # clock settling: untimed steps of the headline, enqueued back to back for about
+            # settle_ms of GPU time right before the warm-up (the side legs above leave the GPU idle
+            # between their pieces: a 20-step region after them ran 4-6 % above the steady rate,
+            # tools/gpu_region_ab.sh, and a GPU idle for 2 s needs ~100 steps to settle,
+            # tools/region_segments.py).  Not part of W or of the timed region; in the line as
+            # settle_steps.
+            settle_steps = max(1, int(args.settle_ms / 0.1))
+            run(settle_steps)
+        else:
+            settle_steps = 0
+        run(args.warmup)
+        torch.cuda.synchronize()
+        snap = snapshot(model, step)          # the state the first timed step starts from
         if launch == "graph":
             # the capture advances the host's step counters by len(data): the timed replays are
             # steps warmup .. warmup+7 of the same run, cycled; the encoder of the last batch's
@@ -981,11 +1002,14 @@ def main():
                     e0.record()
                     e1.record()
                 torch.cuda.synchronize()
-        if graphs is None:
-            # one event set per recorded step only (each set is 8 events created up front: sized
-            # for every step, a 200-step region had created 1,608 events right before its clock)
+        if graphs is None and timer is None:
+            # (graph capture failed: eager after all) one event set per recorded step only (each
+            # set is 8 events created up front: sized for every step, a 200-step region had created
+            # 1,608 events right before its clock)
             timer = PKG._lib.KernelTimer(event_every(args.steps), args.steps // event_every(args.steps) + 1,
                                          kernels=timed_kernels(args.precision, not args.no_ahead))
+        if timer is not None:
+            timer.reset()                     # (host only: the warm-up's steps are not counted)
 
         def timed(n):
             if graphs is None:
@@ -1082,7 +1106,8 @@ def main():
                       "boundary of every 2nd step)" % (src, args.kernel_steps))
     line = {
         "metric": METRIC, "value": value, "unit": "utterances/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
+        "warmup": args.warmup, "settle_steps": settle_steps, "ms_per_step": ms, "higher_is_better": True,
+        "scaling": "weak",
         "vs_baseline": None, "dtype": args.precision, "data": "synthetic",
         "dtype_note": {"fp16": "encoder and weight-gradient GEMMs on fp16 operands (11-bit significand), fp32 "
                                "accumulation; everything else fp32 (the mode that meets north_star's 1e-4)",

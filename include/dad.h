@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define DAD_ABI_VERSION 6
+#define DAD_ABI_VERSION 7
 
 /* error codes (besides hipError_t values) */
 #define DAD_OK 0
@@ -172,7 +172,7 @@ typedef struct dad_state {
 } dad_state;
 
 /* --- sizing ------------------------------------------------------------------------ */
-/* DAD_ABI_VERSION the library was built with (ABI 6): a binding compares it with the header's
+/* DAD_ABI_VERSION the library was built with (ABI 7; 6 lacked dad_timing_reset): a binding compares it with the header's
  * value when it loads the library, so a stale build fails at load instead of at a call. */
 int dad_abi_version(void);
 size_t dad_param_count(void);
@@ -397,6 +397,11 @@ int dad_timing_start(int every, int max_steps);
  * whose bit (1 << DAD_TK_*) is set (default: all).  Each recorded event costs the stream a few
  * microseconds, so a timed region that needs one kernel's duration records only its two. */
 int dad_timing_kernels(unsigned mask);
+/* dad_timing_reset (ABI 7): forget the steps counted and recorded so far in the active session (its
+ * events stay created); the next step is the session's step 0.  A timed region can then follow its
+ * warm-up with no gap: dad_timing_start's event set-up (milliseconds of host time with the GPU idle)
+ * runs before the warm-up, the reset between them. */
+int dad_timing_reset(void);
 int dad_timing_stop(double* ms_sum, int* count, int n);
 
 /* --- data-parallel gradient exchange (RCCL over xGMI) ------------------------------ */

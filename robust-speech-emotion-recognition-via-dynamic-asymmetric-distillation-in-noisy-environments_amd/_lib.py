@@ -10,7 +10,7 @@ from . import _build
 
 c_float_p = ctypes.POINTER(ctypes.c_float)
 
-DAD_ABI_VERSION = 6        # dad.h DAD_ABI_VERSION this binding mirrors
+DAD_ABI_VERSION = 7        # dad.h DAD_ABI_VERSION this binding mirrors
 DAD_NPARAM = 256 * 768 + 256 + 4 * 256 + 4
 DAD_GRAD_EXTRA = 16
 DAD_GRAD_FLOATS = DAD_NPARAM + DAD_GRAD_EXTRA
@@ -141,6 +141,7 @@ EXPORTS = {
                                      ctypes.c_void_p, ctypes.c_void_p]),
     "dad_timing_start": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     "dad_timing_kernels": (ctypes.c_int, [ctypes.c_uint]),
+    "dad_timing_reset": (ctypes.c_int, []),
     "dad_timing_stop": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
     "dad_comm_unique_id_bytes": (ctypes.c_int, []),
     "dad_comm_get_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
@@ -210,6 +211,10 @@ class KernelTimer:
                 mask |= 1 << TK_NAMES.index(k)
             check(lib().dad_timing_kernels(mask), "dad_timing_kernels")
         self.active = True
+
+    def reset(self):
+        """dad_timing_reset: the steps so far (a warm-up) are not counted; the events stay created."""
+        check(lib().dad_timing_reset(), "dad_timing_reset")
 
     def stop(self):
         n = len(TK_NAMES)

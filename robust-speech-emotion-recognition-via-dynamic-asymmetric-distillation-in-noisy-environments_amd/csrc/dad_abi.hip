@@ -200,6 +200,16 @@ void tk_end() {
 
 extern "C" {
 
+int dad_timing_reset(void) {
+  std::lock_guard<std::mutex> lk(g_tk_mu);
+  if (g_tk.nset <= 0) return DAD_E_ARG;   // no active session
+  g_tk.calls = 0;
+  g_tk.used = 0;
+  g_tk.cur = -1;
+  std::fill(g_tk.rec.begin(), g_tk.rec.end(), (uint8_t)0);
+  return DAD_OK;
+}
+
 int dad_timing_start(int every, int max_steps) {
   std::lock_guard<std::mutex> lk(g_tk_mu);
   if (every < 1 || max_steps < 1) return DAD_E_ARG;
