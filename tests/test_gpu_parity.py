@@ -301,18 +301,30 @@ def test_large_member_sets_match_oracle(class_aware, B, prec):
     assert _normrel(g, gr) <= TOL["fp16"]["grad"] and _cos(g, gr) >= TOL["fp16"]["cos"]
 
 
+LARGE_CLASS_CASES = {
+    # clean label counts, DACP thresholds (None: synth's low ones), what the geometry must show
+    "one_large": ((40, 8, 8, 8), None, "large"),
+    "two_large": ((30, 30, 2, 2), None, "large"),
+    "idle_others": ((20, 16, 14, 14), (0.0, 1.0, 1.0, 1.0), "large,idle"),
+    "partial_mask": ((20, 16, 14, 14), (0.82, 0.0, 0.0, 0.0), "partial"),
+    "partial_mask_large": ((40, 8, 8, 8), (0.82, 0.0, 0.0, 0.0), "large,partial"),
+}
+
+
 @pytest.mark.parametrize("prec", ["fp32", "fp16"])
-@pytest.mark.parametrize("counts,tau", [((40, 8, 8, 8), None), ((30, 30, 2, 2), None), ((20, 16, 14, 14), (0.0, 1.0, 1.0, 1.0))],
-                         ids=["one_large", "two_large", "idle_others"])
-def test_large_class_tiling_matches_oracle(counts, tau, prec):
-    """Classes of 33..64 ECDA members (clean rows of the label + masked noisy rows of the
+@pytest.mark.parametrize("case", sorted(LARGE_CLASS_CASES))
+def test_large_class_tiling_matches_oracle(case, prec):
+    """ECDA classes of 33..64 members (clean rows of the label + masked noisy rows of the
     pseudo-label): dad_tail_ecda_w's 64-row tiling of a class block (3 Gram tile pairs, the
-    coefficient columns of ceil(n / 8) 8-candidate blocks).  one_split / two_split: one or two
+    coefficient columns of ceil(n / 8) 8-candidate blocks).  one_large / two_large: one or two
     such classes next to classes with work; idle_others: thresholds mask in only class 0's noisy
     rows (36 members), so classes 1..3 have neither ECDA nor repulsion work (the geometry of a
-    collapsed teacher).  Losses at 1e-4, mask bit-exact, gradients as the other parity tests
-    (fp32: gh.close_grad; fp16: the throughput bounds); the test checks that the geometry does
-    produce such a class."""
+    collapsed teacher).  partial_mask(_large): class 0's threshold leaves 6 of its 16 noisy rows of
+    pseudo-label 0 out of the mask; they are not members (I/utils.py:573-576) and the class blocks
+    no longer stage them (round 6: they had sized the tiling, up to the wide path).  Losses at 1e-4,
+    mask bit-exact, gradients as the other parity tests (fp32: gh.close_grad; fp16: the throughput
+    bounds); the test checks that the geometry does produce what the case names."""
+    counts, tau, expect = LARGE_CLASS_CASES[case]
     cfg = dad_oracle.make_cfg("iemocap")
     inp = _problem(64, 6, seed=21, snr=20.0)
     inp["yc"] = np.repeat(np.arange(4), counts).astype(inp["yc"].dtype)
@@ -326,16 +338,20 @@ def test_large_class_tiling_matches_oracle(counts, tau, prec):
     o = gh.run_step(step, inp, 60)
     r = orc.step(inp, 60)
     m = np.asarray(r["mask"]) > 0
-    members = [int(np.sum(inp["yc"] == c)) + int(np.sum((np.asarray(r["pred"]) == c) & m)) for c in range(4)]
-    assert any(32 < n <= 64 for n in members), members
-    if tau is not None:   # one class with work, the others idle
-        assert [int(np.sum((np.asarray(r["pred"]) == c) & m)) for c in range(1, 4)] == [0, 0, 0], members
+    pred = np.asarray(r["pred"])
+    members = [int(np.sum(inp["yc"] == c)) + int(np.sum((pred == c) & m)) for c in range(4)]
+    if "large" in expect:
+        assert any(32 < n <= 64 for n in members), members
+    if "idle" in expect:   # one class with work, the others idle
+        assert [int(np.sum((pred == c) & m)) for c in range(1, 4)] == [0, 0, 0], members
+    if "partial" in expect:
+        assert 0 < int(np.sum((pred == 0) & ~m)) < int(np.sum(pred == 0)), members
     for k in ("total_loss", "supervised_ce_loss", "consistency_loss", "ecda_loss"):
-        _cmp_loss(o[k], r[k], (counts, prec, k))
+        _cmp_loss(o[k], r[k], (case, prec, k))
     np.testing.assert_array_equal(o["mask"], r["mask"])
     if prec == "fp32":
         for k, (a, b_) in enumerate(zip(o["grads"], r["grads"])):
-            gh.close_grad(a, b_, "split class grad %d" % k)
+            gh.close_grad(a, b_, "large class grad %d" % k)
         return
     from test_gpu_throughput_parity import TOL, _cos, _normrel
     g = np.concatenate([x.reshape(-1) for x in o["grads"]])
