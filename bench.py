@@ -926,33 +926,13 @@ def main():
                 step.step(c, nb, args.epoch, next_batch=None if args.no_ahead else data[(i + 1) % len(data)],
                           after_backward=spin)
 
-        # The side legs of the line (the FP32 mode, the BF16 mode, the data path) run first, from the
-        # initial state, which is restored after them; then the W warm-up steps, right before the
-        # timed region: it starts on a GPU that has been busy for ~100 ms (steady clocks) with the
-        # warm-up's prepared rows and caches in place.  (The driver's --steps 20 --warmup 5 line had
-        # measured the clock ramp: 137 -> 130 -> 124 us per step over consecutive 20-step segments,
-        # round 2.)  The parity block runs after the timed region, from the state it started in.
+        # Order: the clock-settling run (--settle-ms), the W warm-up steps right before the timed
+        # region (it starts on a GPU that has been busy for ~50 ms, with the warm-up's prepared rows
+        # and caches in place; round 2 had measured the clock ramp of a cold start: 137 -> 130 -> 124
+        # us per step over consecutive 20-step segments), the timed region, then the per-kernel pass,
+        # the parity block (from the state the region started in) and the side legs.
         parity = fp32 = bf16 = data_path = randlab = None
         side = rank == 0 and world == 1
-        if side:
-            snap0 = snapshot(model, step)
-            if args.precision != "fp32":
-                if args.fp32_steps > 0:
-                    fp32 = side_mode(model, view, data, B, T, args, "fp32", args.fp32_steps)
-                if args.precision == "fp16" and args.bf16_steps > 0:
-                    bf16 = side_mode(model, view, data, B, T, args, "bf16", args.bf16_steps)
-            if args.randlab_steps > 0:
-                # the headline batches hold exactly B/4 utterances per class; a trainer's random batches
-                # have Binomial(B, 1/4) class sizes, and classes of more than 32 ECDA candidates take the
-                # 64-row tiling of the tail launch's class blocks (DESIGN.md §6, §11)
-                rdata = make_batches(P, N_BATCHES, B, T, seed=29, device=dev, snr_db=args.snr, random_labels=True)
-                randlab = side_mode(model, view, rdata, B, T, args, args.precision, args.randlab_steps)
-                randlab["data"] = "synthetic, labels drawn uniformly per utterance (random class sizes)"
-                del rdata
-            if not args.no_data_path:
-                data_path = data_path_bench(step, B, T, args.epoch, dev, P)
-            restore(model, step, snap0)
-            del snap0
         launch = args.launch
         if launch == "graph" and isinstance(comm, PKG.ProcessGroupComm):
             launch = "eager (the gloo all-reduce runs on the host: not capturable)"
@@ -1053,6 +1033,28 @@ def main():
         if side and args.precision != "fp32" and not args.no_parity:
             parity = parity_block(model, step, view, snap, data[args.warmup % len(data)], args.epoch,
                                   args.precision)
+        if side:
+            # The side legs (the FP32 / BF16 modes, random labels, the data path) run after the timed
+            # region, from the weights it left: run before it, from the initial weights, every kernel
+            # read 1-3 us slower on the same batches (tools/data_effect.py: the encoder 30.4-31.6 against
+            # 28.7 us after 500 steps, the weight gradient 34.5-35.6 against 33.4; the chip's clock
+            # follows the operands), which the random-label leg then showed as the labels' cost
+            # (0.1148 against 0.0976 ms; from trained weights 0.1026 against 0.1005).
+            if args.precision != "fp32":
+                if args.fp32_steps > 0:
+                    fp32 = side_mode(model, view, data, B, T, args, "fp32", args.fp32_steps)
+                if args.precision == "fp16" and args.bf16_steps > 0:
+                    bf16 = side_mode(model, view, data, B, T, args, "bf16", args.bf16_steps)
+            if args.randlab_steps > 0:
+                # the headline batches hold exactly B/4 utterances per class; a trainer's random batches
+                # have Binomial(B, 1/4) class sizes, and classes of more than 32 ECDA members take the
+                # 64-row tiling of the tail launch's class blocks (DESIGN.md §6, §11)
+                rdata = make_batches(P, N_BATCHES, B, T, seed=29, device=dev, snr_db=args.snr, random_labels=True)
+                randlab = side_mode(model, view, rdata, B, T, args, args.precision, args.randlab_steps)
+                randlab["data"] = "synthetic, labels drawn uniformly per utterance (random class sizes)"
+                del rdata
+            if not args.no_data_path:
+                data_path = data_path_bench(step, B, T, args.epoch, dev, P)
         timed_steps = args.steps
         total_utts = B * world * args.steps
         rows_per_step = 2 * B * T
