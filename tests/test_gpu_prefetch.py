@@ -167,3 +167,31 @@ def test_prepare_rows_matches_step_preparation():
     assert L.dad_step_prepare_rows(dcfg, bt, PKG._lib.ptr(ws), step._stream(), 4) == 1001
     dcfg.precision = PKG._lib.PREC_FP32
     assert L.dad_step_prepare_rows(dcfg, bt, PKG._lib.ptr(ws), step._stream(), 3) == 1004
+
+
+def test_timing_reset_counts_only_later_steps():
+    """dad_timing_reset (ABI 7, bench.py's warm-up): the steps before the reset are not counted and
+    the session's events stay usable: every step timed (every = 1), 3 steps, reset, 2 steps -> the
+    encoder's count is 2 and its mean a positive duration; a reset with no session is refused."""
+    import dadpkg
+    L = dadpkg.pkg()._lib
+    cfg = dad_oracle.make_cfg("iemocap")
+    st = synth.make_state(3, 1, tau_range=(0.0, 0.01))
+    batches = [_device_batches(_problem(B=16, T=40, seed=41 + i))[:2] for i in range(2)]
+    step = gh.make_step(cfg, precision="fp16", rng="counter", seed=5)
+    gh.load_state(step, st)
+    timer = L.KernelTimer(1, 8)
+    try:
+        for k in range(3):
+            step.step(*batches[k % len(batches)], 60)
+        torch.cuda.synchronize()
+        timer.reset()
+        for k in range(2):
+            step.step(*batches[k % len(batches)], 60)
+        torch.cuda.synchronize()
+    finally:
+        res = timer.stop()
+    ms, n = res["encode"]
+    assert n == 2 and ms > 0.0, res
+    with pytest.raises(L.DadError):
+        L.KernelTimer.reset(timer)   # (stopped: no active session)
