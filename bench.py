@@ -7,6 +7,9 @@ augmentation, CE + masked KL + class-aware ECDA/MMD, DACP mask, analytic backwar
 global-norm clip + Adam + teacher EMA (+ one RCCL all-reduce of the grads for N > 1).
 Post-warm-up epoch 60 (full loss weights) with a confident synthetic teacher, so the KL and
 ECDA terms are active.  Inputs are resident in HBM before timing.
+Order of a run: ~50 ms of untimed headline steps to settle the clocks (--settle-ms, `settle_steps` in
+the line), the W warm-up steps, the K timed steps, a per-kernel pass, the parity block, then the side
+legs (FP32 / BF16 modes, random labels, data path) and the CPU baseline.
 
     python bench.py [--gpus N --steps K --warmup W --precision fp16|bf16|fp32]
     torchrun --nproc-per-node N bench.py --gpus N ...          (one process per GPU)
@@ -36,7 +39,7 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BF16_PEAK_TFLOPS = 2500.0      # dense bf16 / fp16 MFMA (the same rate for both)
 PEAK_TFLOPS = {"fp16": BF16_PEAK_TFLOPS, "bf16": BF16_PEAK_TFLOPS}
 FP32_PEAK_TFLOPS = 157.3       # f32 MFMA == f32 vector rate
-# every 8th timed step (every steps/4-th in short runs) records hip events (DAD_BENCH_EVENT_EVERY
+# every 8th timed step (every steps/2-th in short runs) records hip events (DAD_BENCH_EVENT_EVERY
 # overrides, for measuring what the events themselves cost)
 EVENT_EVERY = int(os.environ.get("DAD_BENCH_EVENT_EVERY", "8"))
                                # at its kernel boundaries (dad_timing_start): per-kernel durations, live
